@@ -1,0 +1,197 @@
+/*
+ * subread_vote.h -- C ABI of the MI355X seed-and-vote read-alignment hot path.
+ *
+ * Drop-in boundary for the voting step of Subread v2.0.6 (subread-align /
+ * subjunc).  In the reference the step is the internal function
+ *     int do_voting(global_context_t*, thread_context_t*)        core.c:3049
+ * run once per pthread by run_in_thread(STEP_VOTING)             core.c:3366
+ * It pulls reads from fetch_next_read_pair (core.c:1121), probes the sorted
+ * hash table with gehash_go_X (sorted-hashtable.c:937), selects the top-K
+ * candidates with process_voting_junction_PE_topK (core-junction.c:2199) and
+ * writes up to multi_best mapping_result_t per read end into the bigtable
+ * (core-bigtable.c:127) -- plus subjunc_result_t and the big-margin records in
+ * subjunc mode.  svg_vote_batch() replaces that whole step for a batch of reads:
+ * reads (ASCII, exactly what fetch_next_read_pair hands to do_voting before the
+ * -S reversal) go in, the same bigtable records come out, byte for byte.
+ *
+ * Conventions (mirroring the reference): functions return 0 on success and a
+ * negative SVG_E_* code on failure; the text of the last error of the calling
+ * thread is available from svg_last_error().  The caller owns every host
+ * buffer; the library owns device memory and streams.  One handle per GPU;
+ * calls on one handle are serialised by the caller (one host thread).
+ *
+ * Nothing in this header depends on HIP or torch types.
+ */
+#ifndef SUBREAD_VOTE_H
+#define SUBREAD_VOTE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SVG_ABI_VERSION 1
+
+/* reference constants (subread.h:73,88,216-217; core-junction.c:3569) */
+#define SVG_MAX_READ_LENGTH       1210   /* MAX_READ_LENGTH == index padding */
+#define SVG_MAX_INDEL_SECTIONS    7
+#define SVG_VOTE_TABLE_SIZE       30     /* GENE_VOTE_TABLE_SIZE */
+#define SVG_VOTE_SPACE            24     /* GENE_VOTE_SPACE */
+#define SVG_BIG_MARGIN_WORDS      9      /* config.big_margin_record_size */
+#define SVG_NEGATIVE_STRAND_FLAG  8      /* CORE_IS_NEGATIVE_STRAND in result_flags */
+
+/* error codes */
+#define SVG_OK               0
+#define SVG_E_ARG          (-1)   /* bad argument / NULL pointer */
+#define SVG_E_IO           (-2)   /* index file missing / unreadable */
+#define SVG_E_FORMAT       (-3)   /* index file malformed */
+#define SVG_E_UNSUPPORTED  (-4)   /* configuration outside the drop-in contract */
+#define SVG_E_DEVICE       (-5)   /* HIP runtime failure */
+#define SVG_E_NOMEM        (-6)
+
+/* mapping_result_t, core.h:350-370 -- identical layout (68 bytes). */
+typedef struct svg_mapping_result {
+	uint32_t selected_position;
+	int16_t  result_flags;
+	int16_t  read_length;
+	int16_t  selected_votes;
+	int16_t  used_subreads_in_vote;
+	uint8_t  noninformative_subreads_in_vote;
+	int8_t   indels_in_confident_coverage;
+	int8_t   is_fully_covered;
+	uint8_t  _pad0;
+	int16_t  selected_indel_record[SVG_MAX_INDEL_SECTIONS * 3 + 1];
+	uint16_t confident_coverage_start;
+	uint16_t confident_coverage_end;
+	int16_t  subread_quality;
+	uint16_t _pad1;
+} svg_mapping_result;
+
+/* subjunc_result_t, core.h:397-410 -- identical layout (16 bytes). */
+typedef struct svg_subjunc_result {
+	int16_t  split_point;
+	int16_t  minor_votes;
+	int8_t   double_indel_offset;
+	int8_t   indel_at_junction;
+	int8_t   small_side_increasing_coordinate;
+	int8_t   large_side_increasing_coordinate;
+	uint32_t minor_position;
+	uint16_t minor_coverage_start;
+	uint16_t minor_coverage_end;
+} svg_subjunc_result;
+
+/*
+ * Voting parameters: the subset of configuration_t (core.h:128-253) the vote
+ * path reads.  svg_params_default() fills them exactly as the reference does:
+ * init_global_context (core-indel.c:4399-4538), then parse_opts_aligner /
+ * parse_opts_subjunc (core-interface-aligner.c:256, core-interface-subjunc.c:255),
+ * then the runtime overrides of load_global_context (core.c:4075-4094).
+ */
+typedef struct svg_params {
+	int32_t total_subreads;               /* -n                      (10 align, 14 subjunc) */
+	int32_t min_votes_first;              /* -m minimum_subread_for_first_read  (3 / 1)   */
+	int32_t min_votes_second;             /* -p minimum_subread_for_second_read (1)       */
+	int32_t max_indel_length;             /* -I  (voting uses min(16, I))        (5)      */
+	int32_t multi_best;                   /* multi_best_reads                    (3)      */
+	int32_t top_scores;                   /*                                     (3)      */
+	int32_t max_vote_simples;             /* 3 SE / 64 PE, max'ed with -B                 */
+	int32_t max_vote_combinations;        /* 3, max'ed with -B                            */
+	int32_t max_vote_number_cutoff;       /*                                     (2)      */
+	int32_t min_pair_distance;            /* -d                                  (50)     */
+	int32_t max_pair_distance;            /* -D                                  (600)    */
+	int32_t reverse_r1;                   /* is_first_read_reversed  (-S)        (0)      */
+	int32_t reverse_r2;                   /* is_second_read_reversed (-S)        (1)      */
+	int32_t do_breakpoint_detection;      /* subjunc                             (0 / 1)  */
+	int32_t do_big_margin_filtering_for_junctions; /* subjunc                    (0 / 1)  */
+	int32_t big_margin_record_size;       /*                                     (9)      */
+	int32_t maximum_intron_length;        /*                                     (500000) */
+	int32_t prefer_donor_receptor_junctions; /*                                  (1)      */
+	int32_t check_donor_at_junctions;     /*                                     (1)      */
+	int32_t max_insertion_at_junctions;   /*                                     (0)      */
+	int32_t more_accurate_fusions;        /*                                     (1)      */
+} svg_params;
+
+#define SVG_PROGRAM_ALIGN   0   /* subread-align */
+#define SVG_PROGRAM_SUBJUNC 1   /* subjunc */
+void svg_params_default(svg_params *p, int program, int paired_end);
+
+/*
+ * A batch of reads as ASCII text.  Read i is seq[offsets[i] .. offsets[i]+lens[i]).
+ * Reads are given as the FASTQ holds them (after trimming); the -S reversal
+ * (reverse_r1 / reverse_r2) is applied inside the library exactly like
+ * fetch_next_read_pair (core.c:1186-1198).  For paired-end input r1 and r2 hold
+ * the same number of reads.  Read numbering in a batch = array order.
+ */
+typedef struct svg_reads {
+	const char     *seq;
+	const uint64_t *offsets;
+	const uint16_t *lens;
+	uint64_t        n_reads;
+} svg_reads;
+
+/* opaque index handle: owns the HBM copy of <prefix>.00.b.tab / .array / .reads */
+typedef struct svg_index svg_index;
+
+typedef struct svg_index_info {
+	uint64_t items;              /* hashed 16-mers in the .tab                 */
+	uint32_t buckets;            /* buckets_number                             */
+	int32_t  index_gap;          /* 1 (-F full index) or 3 (gapped)            */
+	int32_t  padding;            /* 1210                                       */
+	uint32_t array_length;       /* .array length (bases incl. padding)        */
+	uint32_t n_chromosomes;
+	uint64_t device_bytes;       /* HBM held by the handle                     */
+	int32_t  device;             /* HIP device ordinal                         */
+} svg_index_info;
+
+/* Load "<prefix>.00.b.tab", "<prefix>.00.b.array", "<prefix>.reads" (single-block
+ * base-space index, as written by subread-buildindex) into HBM of `device`. */
+int  svg_index_open(const char *prefix, int device, svg_index **out);
+void svg_index_close(svg_index *idx);
+int  svg_index_get_info(const svg_index *idx, svg_index_info *out);
+
+/*
+ * Vote a batch.  Host buffers in, host buffers out (synchronous).
+ *   out   : n_reads * ends * multi_best records, index ((read*ends)+end)*multi_best+best
+ *   jout  : same shape, subjunc_result_t; required iff do_breakpoint_detection
+ *   big_margin : n_reads * ends * SVG_BIG_MARGIN_WORDS; required iff
+ *           do_big_margin_filtering_for_junctions (reference bigtable
+ *           big_margin_data, core.h:453)
+ * r2 == NULL means single-end.  Output buffers are fully overwritten (the
+ * reference zeroes the bigtable per chunk, core-bigtable.c:84-125).
+ */
+int svg_vote_batch(svg_index *idx, const svg_params *p,
+                   const svg_reads *r1, const svg_reads *r2,
+                   svg_mapping_result *out, svg_subjunc_result *jout,
+                   uint16_t *big_margin);
+
+/*
+ * Same computation on device-resident buffers, asynchronous on `hip_stream`
+ * (a hipStream_t passed as void*, NULL = the handle's own stream).  Every
+ * pointer in r1/r2 and the outputs is a device pointer.
+ */
+int svg_vote_batch_device(svg_index *idx, const svg_params *p,
+                          const svg_reads *r1, const svg_reads *r2,
+                          svg_mapping_result *out, svg_subjunc_result *jout,
+                          uint16_t *big_margin, void *hip_stream);
+
+/* Per-batch statistics of the last svg_vote_batch* call on this handle
+ * (filled only when the handle was opened with SVG_STATS=1 in the environment
+ * or after svg_set_stats(idx,1)); used for the algorithmic-byte roofline. */
+typedef struct svg_batch_stats {
+	uint64_t probes;             /* gehash_go_X calls                         */
+	uint64_t bucket_items;       /* sum of items in the probed buckets        */
+	uint64_t hits;               /* sum of equal-key run lengths              */
+	uint64_t results;            /* mapping records with selected_votes > 0   */
+} svg_batch_stats;
+int svg_set_stats(svg_index *idx, int enable);
+int svg_get_stats(const svg_index *idx, svg_batch_stats *out);
+
+const char *svg_last_error(void);
+int svg_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SUBREAD_VOTE_H */

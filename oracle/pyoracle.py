@@ -1,0 +1,89 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of the CPU restatement (oracle/svoracle.c).
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg -- as the checker, never as the thing measured or shipped.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from subread_amd.abi import MAPPING_DTYPE, SUBJUNC_DTYPE, BIG_MARGIN_WORDS
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "lib", "libsvoracle.so")
+REF_DIR = os.path.join(HERE, "_ref")
+
+_lib = None
+
+
+def build(quiet=True):
+    """Compile the restatement (and, when /root/reference exists, oracle/_ref)."""
+    out = subprocess.run(["make", "-C", HERE, "-j8"], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + out.stdout + out.stderr)
+    if not quiet:
+        print(out.stdout)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        L.svo_index_open.restype = ctypes.c_void_p
+        L.svo_index_open.argtypes = [ctypes.c_char_p]
+        L.svo_index_close.argtypes = [ctypes.c_void_p]
+        L.svo_index_info.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
+        L.svo_vote_batch.restype = ctypes.c_int
+        L.svo_vote_batch.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int, ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+class OracleIndex:
+    def __init__(self, prefix):
+        self.h = lib().svo_index_open(prefix.encode())
+        if not self.h:
+            raise IOError("oracle: cannot load index " + prefix)
+        nb, items, gap, pad, nchr = (ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_int(),
+                                     ctypes.c_int(), ctypes.c_uint32())
+        lib().svo_index_info(self.h, ctypes.byref(nb), ctypes.byref(items), ctypes.byref(gap),
+                             ctypes.byref(pad), ctypes.byref(nchr))
+        self.buckets, self.items, self.gap, self.padding, self.n_chr = (
+            nb.value, items.value, gap.value, pad.value, nchr.value)
+
+    def close(self):
+        if self.h:
+            lib().svo_index_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def vote(self, params, r1, r2=None, threads=None):
+        """-> (mapping[n, ends, multi_best], subjunc or None, big_margin or None, stats[3])"""
+        n = len(r1)
+        ends = 2 if r2 is not None else 1
+        mb = params.multi_best
+        out = np.zeros((n, ends, mb), dtype=MAPPING_DTYPE)
+        jout = np.zeros((n, ends, mb), dtype=SUBJUNC_DTYPE) if params.do_breakpoint_detection else None
+        bm = (np.zeros((n, ends, BIG_MARGIN_WORDS), dtype=np.uint16)
+              if params.do_big_margin_filtering_for_junctions else None)
+        st = np.zeros(3, dtype=np.uint64)
+        s1 = r1.struct()
+        s2 = r2.struct() if r2 is not None else None
+        rc = lib().svo_vote_batch(
+            self.h, ctypes.byref(params), ctypes.byref(s1),
+            ctypes.byref(s2) if s2 is not None else None,
+            out.ctypes.data, jout.ctypes.data if jout is not None else None,
+            bm.ctypes.data if bm is not None else None,
+            threads or os.cpu_count() or 1, st.ctypes.data)
+        if rc != 0:
+            raise RuntimeError("svo_vote_batch failed: %d" % rc)
+        return out, jout, bm, st

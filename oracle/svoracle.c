@@ -1,0 +1,923 @@
+/*
+ * svoracle.c -- TEST INFRASTRUCTURE ONLY (parity checker + cpu_baseline "port").
+ *
+ * A plain-C, single-read-at-a-time restatement of the Subread v2.0.6 voting
+ * step, written from the reference's behaviour and
+ * checked field-by-field against the reference itself (oracle/_ref, see
+ * tests/golden/make_golden.py).  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product (subread_amd/) never
+ * links or calls anything here.
+ *
+ * Reference anchors (all /root/reference/src):
+ *   driver            do_voting                     core.c:3049-3323
+ *   subread offsets   step / applied / offset       core.c:3117-3171
+ *   16-mer packing    genekey2int, base2int         input-files.c:1232-1251, subread.h:238
+ *   reverse strand    reverse_read + table          input-files.c:1111-1189
+ *   probe + tally     gehash_go_X                   sorted-hashtable.c:937-1123
+ *   vote-table reset  init_gene_vote                gene-algorithms.h:42
+ *   top-K / argmax    process_voting_junction_PE_topK core-junction.c:2199-2530
+ *                     update_top_three              core-junction.c:908-922
+ *                     merge_sort (<=11: selection)   core.c:4716-4760
+ *   record copy       copy_vote_to_alignment_res    core-junction.c:1058-1335
+ *                     indel_recorder_copy           sorted-hashtable.c:1144-1165
+ *   PE pair test      test_PE_and_same_chro         core.c:4819-4845
+ *                     locate_gene_position_max      gene-algorithms.c:441-511
+ *   subjunc           test_junction_minor           core-junction.c:889-906
+ *                     is_better_inner               core-junction.c:961-969
+ *                     donor_score                   core-junction.c:3675-3834
+ *                     insert_big_margin_record      core-junction.c:789-811
+ *                     match_chro / gvindex_get      gene-value-index.c:856-959, 96-107
+ *   index files       gehash_load                   sorted-hashtable.c:1390-1625
+ *                     gvindex_load                  gene-value-index.c:190-228
+ *                     load_offsets                  gene-algorithms.c:1293-1370
+ */
+#define _GNU_SOURCE
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdint.h>
+#include <pthread.h>
+#include "subread_vote.h"
+
+#define TAB_ROWS 30
+#define TAB_SPACE 24
+#define REC_LEN 21           /* MAX_INDEL_TOLERANCE*3 */
+#define SEG 5                /* INDEL_SEGMENT_SIZE */
+#define NEG_MASK 2048        /* IS_NEGATIVE_STRAND */
+#define LONG_READ 160        /* EXON_LONG_READ_LENGTH */
+#define JCW 17               /* JUNCTION_CONFIRM_WINDOW */
+
+/* ------------------------------------------------------------------ index */
+typedef struct {
+	uint32_t nb;
+	uint64_t items;
+	int gap, padding;
+	uint32_t *bstart;      /* nb+1 */
+	int16_t *keys;
+	uint32_t *vals;
+	/* .array */
+	uint32_t start_point, length, start_base_offset, values_bytes;
+	uint8_t *values;
+	/* .reads */
+	uint32_t n_chr;
+	uint32_t *chr_end;
+} svo_index;
+
+static int rd(FILE *fp, void *p, size_t n) { return fread(p, 1, n, fp) == n ? 0 : -1; }
+
+void svo_index_close(svo_index *ix)
+{
+	if (!ix) return;
+	free(ix->bstart); free(ix->keys); free(ix->vals); free(ix->values); free(ix->chr_end);
+	free(ix);
+}
+
+svo_index *svo_index_open(const char *prefix)
+{
+	char fn[4096];
+	svo_index *ix = calloc(1, sizeof(*ix));
+	FILE *fp;
+	char magic[8];
+	snprintf(fn, sizeof fn, "%s.00.b.tab", prefix);
+	fp = fopen(fn, "rb");
+	if (!fp) { free(ix); return NULL; }
+	if (rd(fp, magic, 8) || memcmp(magic, "2subindx", 8)) goto bad;
+	for (;;) {
+		int16_t k, l, v;
+		if (rd(fp, &k, 2)) goto bad;
+		if (!k) break;
+		if (rd(fp, &l, 2)) goto bad;
+		if (k == 0x0101 || k == 0x0102) {
+			if (rd(fp, &v, 2)) goto bad;
+			if (k == 0x0101) ix->gap = v; else ix->padding = v;
+		} else fseeko(fp, l, SEEK_CUR);
+	}
+	{
+		int64_t items; int32_t nb;
+		if (rd(fp, &items, 8) || rd(fp, &nb, 4)) goto bad;
+		ix->items = items; ix->nb = nb;
+	}
+	ix->bstart = malloc(sizeof(uint32_t) * ((size_t)ix->nb + 1));
+	ix->keys = malloc(2 * ix->items + 2);
+	ix->vals = malloc(4 * ix->items + 4);
+	{
+		uint64_t cur = 0; uint32_t b;
+		for (b = 0; b < ix->nb; b++) {
+			int32_t n, sp;
+			if (rd(fp, &n, 4) || rd(fp, &sp, 4)) goto bad;
+			ix->bstart[b] = (uint32_t)cur;
+			if (n) {
+				if (cur + n > ix->items) goto bad;
+				if (rd(fp, ix->keys + cur, 2 * (size_t)n) || rd(fp, ix->vals + cur, 4 * (size_t)n)) goto bad;
+			}
+			cur += n;
+		}
+		ix->bstart[ix->nb] = (uint32_t)cur;
+	}
+	fclose(fp);
+
+	snprintf(fn, sizeof fn, "%s.00.b.array", prefix);
+	fp = fopen(fn, "rb");
+	if (!fp) goto bad2;
+	if (rd(fp, &ix->start_point, 4) || rd(fp, &ix->length, 4)) goto bad;
+	ix->start_base_offset = ix->start_point - ix->start_point % 4;
+	{
+		uint32_t useful = (ix->length + ix->start_point - ix->start_base_offset) >> 2;
+		ix->values_bytes = useful + 1;
+		ix->values = calloc(ix->values_bytes + 8, 1);
+		if (fread(ix->values, 1, useful + 1, fp) < useful) goto bad;
+	}
+	fclose(fp);
+
+	snprintf(fn, sizeof fn, "%s.reads", prefix);
+	fp = fopen(fn, "r");
+	if (!fp) goto bad2;
+	{
+		char line[4096]; uint32_t cap = 64;
+		ix->chr_end = malloc(4 * cap);
+		while (fgets(line, sizeof line, fp)) {
+			if (strlen(line) < 2) continue;
+			if (ix->n_chr == cap) { cap *= 2; ix->chr_end = realloc(ix->chr_end, 4 * cap); }
+			ix->chr_end[ix->n_chr++] = (uint32_t)atoll(line);
+		}
+	}
+	fclose(fp);
+	return ix;
+bad:
+	fclose(fp);
+bad2:
+	svo_index_close(ix);
+	return NULL;
+}
+
+void svo_index_info(const svo_index *ix, uint32_t *nb, uint64_t *items, int *gap, int *padding, uint32_t *n_chr)
+{
+	*nb = ix->nb; *items = ix->items; *gap = ix->gap; *padding = ix->padding; *n_chr = ix->n_chr;
+}
+
+/* ------------------------------------------------------------------ read text */
+/* base2int, subread.h:238 */
+static inline uint32_t b2i(char c) { return c < 'G' ? (c == 'A' ? 0 : 2) : (c == 'G' ? 1 : 3); }
+/* reverse-complement table, input-files.c:1111 (ASCII part; everything else -> 'N') */
+static inline char comp(char c)
+{
+	switch (c) { case 'A': return 'T'; case 'C': return 'G'; case 'G': return 'C'; case 'T': return 'A'; case 'U': return 'A'; }
+	return 'N';
+}
+/* reverse_read, input-files.c:1113-1189 (base space): every char mapped once, order reversed */
+static void revcomp(char *s, int len)
+{
+	int i;
+	for (i = 0; i < len / 2; i++) {
+		char t = s[len - 1 - i];
+		s[len - 1 - i] = comp(s[i]);
+		s[i] = comp(t);
+	}
+	if (i * 2 == len - 1) s[i] = comp(s[i]);
+}
+/* genekey2int, input-files.c:1232 */
+static inline uint32_t pack16(const char *s)
+{
+	uint32_t k = 0; int i;
+	for (i = 0; i < 16; i++) k |= b2i(s[i]) << (30 - 2 * i);
+	return k;
+}
+
+/* ------------------------------------------------------------------ vote table (gene_vote_t subset) */
+typedef struct {
+	uint16_t items[TAB_ROWS];
+	int16_t max_vote;
+	int16_t noninf;
+	uint32_t pos[TAB_ROWS][TAB_SPACE];
+	int32_t masks[TAB_ROWS][TAB_SPACE];
+	uint8_t shift[TAB_ROWS][TAB_SPACE];
+	int16_t votes[TAB_ROWS][TAB_SPACE];
+	int16_t last[TAB_ROWS][TAB_SPACE];
+	int16_t rec[TAB_ROWS][TAB_SPACE][REC_LEN];
+	int8_t cursor[TAB_ROWS][TAB_SPACE];
+	int8_t toli[TAB_ROWS][TAB_SPACE];
+	int16_t cs[TAB_ROWS][TAB_SPACE], ce[TAB_ROWS][TAB_SPACE];
+} vtab_t;
+
+static inline void vt_reset(vtab_t *v)
+{
+	memset(v->items, 0, sizeof v->items);
+	v->max_vote = 0; v->noninf = 0;
+}
+
+static inline uint32_t vrow(uint32_t x) { return (x / SEG) % TAB_ROWS; }
+
+typedef struct {
+	uint64_t probes, bucket_items, hits;
+} probe_stats;
+
+/* gehash_go_X, sorted-hashtable.c:937-1123 */
+static void probe_X(const svo_index *ix, uint32_t key, int off, int strand, vtab_t *v, int tol, int subread_no,
+                    uint32_t low, uint32_t high, int round, uint32_t *shift_locs, uint32_t *shift_no, probe_stats *st)
+{
+	uint32_t b = key % ix->nb;
+	int16_t k16 = (int16_t)(key / ix->nb);
+	uint32_t first = ix->bstart[b];
+	int n = (int)(ix->bstart[b + 1] - first);
+	const int16_t *K = ix->keys + first;
+	const uint32_t *V = ix->vals + first;
+	int lo = 0, hi = n - 1, idx, start, back = 0;
+	int kP1 = subread_no + 1, ofp16 = off + 16, mask = strand ? NEG_MASK : 0;
+	int ii_end = SEG;
+	if (st) { st->probes++; st->bucket_items += n; }
+	if (!n) return;
+	for (;;) {
+		idx = (lo + hi) / 2;
+		if (K[idx] > k16) hi = idx - 1;
+		else if (K[idx] < k16) lo = idx + 1;
+		else break;
+		if (hi < lo) return;
+	}
+	if (tol > 5) ii_end = (tol % SEG) ? (tol - tol % SEG + SEG) : tol;
+	start = idx;
+	for (;;) {
+		uint32_t kv = V[idx] - (uint32_t)off;
+		uint32_t r0 = vrow(kv);
+		int n0 = v->items[r0];
+		int found = 0, iix;
+		if (st) st->hits++;
+		for (iix = 0; iix <= ii_end; iix = iix > 0 ? -iix : (-iix + SEG)) {
+			uint32_t r = r0; int cnt = n0, s;
+			if (iix) { r = vrow(kv + (uint32_t)iix); cnt = v->items[r]; }
+			if (!cnt) continue;
+			for (s = 0; s < cnt; s++) {
+				int d = (int)(kv - v->pos[r][s]);
+				int t = (round > 0 && v->shift[r][s]) ? 0 : tol;
+				int tl;
+				if (!(d >= -t && d <= t && mask == v->masks[r][s])) continue;
+				tl = v->toli[r][s];
+				if (round == 0 && tl > 0 && d == 0 && !v->shift[r][s]) {
+					v->shift[r][s] = 1;
+					shift_locs[(*shift_no)++] = v->pos[r][s];
+				}
+				if (kP1 == v->last[r][s] && tl > 0) {
+					int md = 0, nd;
+					if (tl >= 3) md = v->rec[r][s][tl - 1];
+					nd = md;
+					md -= v->rec[r][s][tl + 2];
+					nd -= d;
+					if (abs(md) > abs(nd)) {
+						tl -= 3;
+						v->toli[r][s] = tl;
+						v->last[r][s]--;
+						v->votes[r][s]--;
+					}
+				}
+				if (kP1 <= v->last[r][s]) continue;
+				{
+					int16_t nv = v->votes[r][s] + 1;
+					v->votes[r][s] = nv;
+					if (off + 16 > v->ce[r][s]) v->ce[r][s] = ofp16;
+					if (d == v->cursor[r][s]) v->rec[r][s][tl + 1] = kP1;
+					else {
+						tl += 3;
+						if (tl < REC_LEN) {
+							v->toli[r][s] = tl;
+							v->rec[r][s][tl] = kP1;
+							v->rec[r][s][tl + 1] = kP1;
+							v->rec[r][s][tl + 2] = d;
+							if (tl < REC_LEN - 3) v->rec[r][s][tl + 3] = 0;
+						}
+						v->cursor[r][s] = (int8_t)d;
+					}
+					v->last[r][s] = kP1;
+					if (v->max_vote < nv) v->max_vote = nv;
+				}
+				found = 1;
+				break;
+			}
+			if (found) break;
+		}
+		if (!found && kv >= low && kv <= high && n0 < TAB_SPACE) {
+			int s = n0;
+			v->items[r0]++;
+			v->pos[r0][s] = kv;
+			v->masks[r0][s] = mask;
+			v->votes[r0][s] = 1;
+			v->toli[r0][s] = 0;
+			v->shift[r0][s] = 0;
+			if (round > 0) {
+				uint32_t j;
+				for (j = 0; j < *shift_no; j++)
+					if (kv >= shift_locs[j] - (uint32_t)tol && kv <= shift_locs[j] + (uint32_t)tol) { v->shift[r0][s] = 1; break; }
+			}
+			v->rec[r0][s][0] = v->rec[r0][s][1] = kP1;
+			v->rec[r0][s][2] = 0;
+			v->rec[r0][s][3] = 0;
+			v->cursor[r0][s] = 0;
+			v->cs[r0][s] = off;
+			v->ce[r0][s] = ofp16;
+			v->last[r0][s] = kP1;
+			if (v->max_vote == 0) v->max_vote = 1;
+		}
+		if (!back) {
+			idx++;
+			if (idx == n || K[idx] != k16) { back = 1; idx = start; }
+		}
+		if (back) {
+			idx--;
+			if (idx < 0 || K[idx] != k16) break;
+		}
+	}
+}
+
+/* ------------------------------------------------------------------ .array access */
+static inline char gv_get(const svo_index *ix, uint32_t p)
+{
+	uint32_t byte = (p - ix->start_base_offset) >> 2, bit = p % 4 * 2;
+	if (byte >= ix->values_bytes - 1) return 'N';
+	return "AGCT"[(ix->values[byte] >> bit) & 3];
+}
+
+static int match_chro(const char *read, const svo_index *ix, uint32_t pos, int len)
+{
+	int ret = 0, i;
+	uint32_t byte, bit;
+	int8_t iv;
+	if ((uint32_t)(pos + len) >= ix->length + ix->start_point) return 0;
+	if (pos > 0xffff0000u) return 0;
+	byte = (pos - ix->start_base_offset) >> 2; bit = pos % 4 * 2;
+	if (byte >= ix->values_bytes) return 0;
+	iv = (int8_t)ix->values[byte];
+	for (i = 0; i < len; i++) {
+		int tt = (iv >> bit) & 3;
+		switch (read[i]) {
+		case 'A': ret += tt == 0; break;
+		case 'G': ret += tt == 1; break;
+		case 'C': ret += tt == 2; break;
+		case 0: break;
+		default: ret += tt == 3;
+		}
+		bit += 2;
+		if (bit == 8) {
+			byte++;
+			if (byte == ix->values_bytes) return 0;
+			iv = (int8_t)ix->values[byte];
+			bit = 0;
+		}
+	}
+	return ret;
+}
+
+/* ------------------------------------------------------------------ read context */
+typedef struct {
+	const svo_index *ix;
+	const svg_params *p;
+	int ends;
+	char text[2][SVG_MAX_READ_LENGTH + 1];
+	int rl[2];
+	vtab_t vt[2];
+	int applied[2];
+	svg_mapping_result res[2][3];   /* the read's bigtable slots */
+	svg_subjunc_result jres[2][3];
+	uint16_t bm[2][SVG_BIG_MARGIN_WORDS];
+	probe_stats st;
+} readctx;
+
+/* simple_mapping_t (core-junction.h) */
+typedef struct {
+	int is_vote;
+	int i, j;               /* table row/slot, or stored index in i */
+	int start_base;
+	uint32_t pos;
+	int votes;
+} simple_t;
+
+typedef struct { simple_t *r1, *r2; int score; } comb_t;
+
+/* update_top_three, core-junction.c:908 */
+static void top3(int *t, int ts, int v)
+{
+	int x1, x2;
+	if (v > t[ts - 1]) {
+		for (x1 = 0; x1 < ts; x1++) {
+			if (v > t[x1]) {
+				for (x2 = ts - 1; x2 > x1; x2--) t[x2] = t[x2 - 1];
+				t[x1] = v;
+				break;
+			} else if (v == t[x1]) break;
+		}
+	}
+}
+
+/* locate_gene_position_max(..., NULL, NULL, rl=0), gene-algorithms.c:441-511 */
+static int locate(const svo_index *ix, uint32_t linear, int *chr, int *pos)
+{
+	int n = 0, lo = 0, hi = (int)ix->n_chr;
+	*chr = -1; *pos = -1;
+	for (;;) {
+		int mid;
+		if (hi <= lo + 1) { n = lo - 2 > 0 ? lo - 2 : 0; break; }
+		mid = (lo + hi) / 2;
+		if (ix->chr_end[mid] > linear) hi = mid; else lo = mid + 1;
+	}
+	for (; n < (int)ix->n_chr; n++) {
+		if (ix->chr_end[n] > linear) {
+			*pos = n == 0 ? (int)linear : (int)(linear - ix->chr_end[n - 1]);
+			if (0u + linear > ix->chr_end[n] + 15u - (uint32_t)ix->padding) return 1;
+			if (*pos < ix->padding) return 1;
+			*pos -= ix->padding;
+			*chr = n;
+			return 0;
+		}
+	}
+	return -1;
+}
+
+/* test_PE_and_same_chro, core.c:4819-4845 */
+static void pe_test(const readctx *c, uint32_t p1, uint32_t p2, int *is_pe, int *same)
+{
+	int c1, c2, q1, q2;
+	int e1 = locate(c->ix, p1, &c1, &q1), e2 = locate(c->ix, p2, &c2, &q2);
+	*is_pe = 0; *same = 0;
+	if (e1 == 0 && e2 == 0) {
+		long long tl = q1; uint32_t tli;
+		tl -= q2;
+		tl = abs((int)tl);
+		tl += (q1 > q2) ? c->rl[0] : c->rl[1];
+		tli = (uint32_t)tl;
+		if (c1 == c2) {
+			*same = 1;
+			if (tli >= (uint32_t)c->p->min_pair_distance && tli <= (uint32_t)c->p->max_pair_distance) *is_pe = 1;
+		}
+	}
+}
+
+/* insert_big_margin_record, core-junction.c:789-811 */
+static void big_margin_insert(const svg_params *p, uint16_t *bm, unsigned char votes, short rs, short re, int rl, int neg)
+{
+	unsigned short s2 = neg ? rl - re : rs, e2 = neg ? rl - rs : re;
+	int x1, x2, size = p->big_margin_record_size;
+	if (size < 3) return;
+	for (x1 = 0; x1 < size / 3; x1++) if (votes >= bm[x1 * 3]) break;
+	if (x1 < size / 3) {
+		for (x2 = size - 4; x2 >= x1 * 3; x2--) bm[x2 + 3] = bm[x2];
+		bm[x1 * 3] = votes; bm[x1 * 3 + 1] = s2; bm[x1 * 3 + 2] = e2;
+	}
+}
+
+/* donor_score, core-junction.c:3675-3834 (no fusion / long-del; donor test on) */
+static int donor_score(const readctx *c, uint32_t left, uint32_t right, int lio, int rio, int normal,
+                       int gs, int ge, const char *read, int rl, int *split, int *gtag, int *found, int *ins,
+                       int *small_inc, int *large_inc)
+{
+	const svg_params *p = c->p;
+	const svo_index *ix = c->ix;
+	int need_donor = p->do_breakpoint_detection && p->check_donor_at_junctions;
+	int mid = (gs + ge) / 2, sel_sp = -1, sel_strand = -1, sel_ins = 0, best = -111111, non_ins_pref = 0;
+	int n = ge - gs, i;
+	int allow = p->more_accurate_fusions ? 0 : 1;
+	char dl[3] = {0, 0, 0}, dr[3] = {0, 0, 0};
+	*small_inc = !normal; *large_inc = normal;
+	for (i = 0; i < n; i++) {
+		int lm, rm = 0, ln = 0, rn = 0, ok = 0;
+		int sp = (i % 2) ? -((i + 1) / 2) : ((1 + i) / 2);
+		sp += mid;
+		if (sp > rl - JCW) continue;
+		if (sp < JCW) continue;
+		if (p->prefer_donor_receptor_junctions) {
+			if (normal) {
+				dl[0] = gv_get(ix, left + sp + lio); dl[1] = gv_get(ix, left + sp + lio + 1);
+				if ((dl[0] == 'G' && dl[1] == 'T') || (dl[0] == 'A' && dl[1] == 'G') || (dl[0] == 'A' && dl[1] == 'C') || (dl[0] == 'C' && dl[1] == 'T')) {
+					dr[0] = gv_get(ix, right + sp + rio - 2); dr[1] = gv_get(ix, right + sp + rio - 1);
+					if ((dr[0] == 'G' && dr[1] == 'T') || (dr[0] == 'A' && dr[1] == 'G') || (dr[0] == 'A' && dr[1] == 'C') || (dr[0] == 'C' && dr[1] == 'T'))
+						ok = ((dl[0] == 'G' && dl[1] == 'T' && dr[0] == 'A' && dr[1] == 'G') || (dl[0] == 'C' && dl[1] == 'T' && dr[0] == 'A' && dr[1] == 'C'))
+						     && ((dl[0] == 'C' && dl[1] == 'T') || (dl[0] == 'G' && dl[1] == 'T'));
+				}
+			} else {
+				dl[0] = gv_get(ix, right + sp + lio); dl[1] = gv_get(ix, right + sp + lio + 1);
+				dr[0] = gv_get(ix, left + sp + rio - 2); dr[1] = gv_get(ix, left + sp + rio - 1);
+				ok = ((dl[0] == 'G' && dl[1] == 'T') || (dl[0] == 'A' && dl[1] == 'G') || (dl[0] == 'A' && dl[1] == 'C') || (dl[0] == 'C' && dl[1] == 'T'))
+				     && ((dr[0] == 'G' && dr[1] == 'T') || (dr[0] == 'A' && dr[1] == 'G') || (dr[0] == 'A' && dr[1] == 'C') || (dr[0] == 'C' && dr[1] == 'T'))
+				     && ((dl[0] == 'G' && dl[1] == 'T' && dr[0] == 'A' && dr[1] == 'G') || (dl[0] == 'C' && dl[1] == 'T' && dr[0] == 'A' && dr[1] == 'C'))
+				     && ((dl[0] == 'C' && dl[1] == 'T') || (dl[0] == 'G' && dl[1] == 'T'));
+			}
+		}
+		if (!(ok || !need_donor)) continue;
+		if (normal) {
+			int ib;
+			lm = match_chro(read + sp - JCW, ix, left + sp - JCW + lio, JCW);
+			if (lm > JCW - (p->max_insertion_at_junctions ? 5 : 2)) {
+				for (ib = 0; ib <= p->max_insertion_at_junctions; ib++) {
+					rm = match_chro(read + sp + ib, ix, right + sp + rio + ib, JCW);
+					if (rm >= 2 * JCW - lm - allow) {
+						ln = match_chro(read + sp + ib, ix, left + sp + lio, JCW);
+						rn = match_chro(read + sp - JCW, ix, right + sp + rio - JCW + ib, JCW);
+						if (ln <= JCW - 5 && rn <= JCW - 5) {
+							int sc;
+							if (p->max_insertion_at_junctions)
+								sc = 100 * (ok * 3000 + lm + rm) - (ln + rn) - 20 * ib;
+							else
+								sc = 100 * (ok * 3000 + lm + rm - ln - rn);
+							if (sc > best) {
+								sel_strand = (dl[0] == 'G' || dr[1] == 'G');
+								sel_ins = ib; sel_sp = sp; best = sc;
+							}
+						}
+					}
+					if (p->max_insertion_at_junctions && 0 == ib && rm >= 2 * JCW - lm - 5) non_ins_pref = 1;
+				}
+			}
+		} else {
+			rm = match_chro(read + sp - JCW, ix, right + rio + sp - JCW, JCW);
+			lm = match_chro(read + sp, ix, left + sp + lio, JCW);
+			rn = match_chro(read + sp, ix, right + sp + rio, JCW);
+			ln = match_chro(read + sp - JCW, ix, left + lio + sp - JCW, JCW);
+			if (lm + rm >= 2 * JCW - allow && ln <= JCW - 5 && rn <= JCW - 5) {
+				int sc = 100 * (ok * 3000 + lm + rm - ln - rn);
+				if (sc > best) {
+					sel_strand = (dl[0] == 'G' || dr[1] == 'G');
+					sel_sp = sp; best = sc;
+				}
+			}
+		}
+	}
+	if (best > 0 && (0 == non_ins_pref || 0 == sel_ins)) {
+		*split = sel_sp; *found = best >= 290000; *gtag = sel_strand; *ins = sel_ins;
+		return (1 + best) / 100;
+	}
+	return 0;
+}
+
+static inline uint32_t abs32u(uint32_t x) { if (x > 0x7fffffffu) x = (0xffffffffu - x) + 1; return x; }
+
+/* indel_recorder_copy, sorted-hashtable.c:1144 */
+static int16_t rec_copy(int16_t *dst, const int16_t *src)
+{
+	int16_t all = 0; int i = 0;
+	while (src[i] && i < REC_LEN - 2) {
+		dst[i] = src[i]; i++;
+		dst[i] = src[i]; i++;
+		dst[i] = src[i]; all = dst[i]; i++;
+	}
+	dst[i] = 0;
+	return all;
+}
+
+/* copy_vote_to_alignment_res, core-junction.c:1058-1335 (non-fusion) */
+static void copy_vote(readctx *c, svg_mapping_result *a, svg_subjunc_result *J, int end, int vi, int vj)
+{
+	const svg_params *p = c->p;
+	vtab_t *v = &c->vt[end];
+	int rl = c->rl[end];
+	a->selected_position = v->pos[vi][vj];
+	a->selected_votes = v->votes[vi][vj];
+	a->indels_in_confident_coverage = (int8_t)rec_copy(a->selected_indel_record, v->rec[vi][vj]);
+	a->confident_coverage_end = v->ce[vi][vj];
+	a->confident_coverage_start = v->cs[vi][vj];
+	a->result_flags = (v->masks[vi][vj] & NEG_MASK) ? SVG_NEGATIVE_STRAND_FLAG : 0;
+	a->used_subreads_in_vote = c->applied[end];
+	a->noninformative_subreads_in_vote = (uint8_t)v->noninf;
+	a->is_fully_covered = 0;
+	if (!p->do_breakpoint_detection) return;
+	{
+		int i, j;
+		for (i = 0; i < TAB_ROWS; i++)
+			for (j = 0; j < v->items[i]; j++) {
+				long long dist;
+				int jumped, better, rep = 0, minor_off = 0, ins = 0, gtag = 0, found = 0, split = 0, major = 0, sinc = 0, linc = 0;
+				if (i == vi && j == vj) continue;
+				if (a->selected_votes < v->votes[i][j]) continue;
+				dist = v->pos[vi][vj]; dist -= v->pos[i][j];
+				jumped = (v->masks[vi][vj] & NEG_MASK) != (v->masks[i][j] & NEG_MASK);
+				/* test_junction_minor, core-junction.c:889-906 */
+				if (llabs(dist) > p->maximum_intron_length) continue;
+				if (v->cs[vi][vj] == v->cs[i][j]) continue;
+				if (v->ce[vi][vj] == v->ce[i][j]) continue;
+				if (v->cs[vi][vj] > v->cs[i][j]) { if (v->pos[vi][vj] < v->pos[i][j]) continue; }
+				else { if (v->pos[vi][vj] > v->pos[i][j]) continue; }
+				/* is_better_inner, core-junction.c:961 */
+				{
+					int old_intron = (int)abs32u(v->pos[vi][vj] - J->minor_position);
+					int vm = v->votes[i][j], cl = v->ce[i][j] - v->cs[i][j];
+					int intron = (int)abs32u(v->pos[vi][vj] - v->pos[i][j]);
+					better = vm > J->minor_votes || (vm == J->minor_votes && cl > J->minor_coverage_end - J->minor_coverage_start)
+					         || (vm == J->minor_votes && cl == J->minor_coverage_end - J->minor_coverage_start && intron < old_intron);
+				}
+				if (better) {
+					int ov, gs, ge, normal, lio = 0, rio = 0;
+					if (jumped) continue;   /* fusion detection off */
+					if (v->cs[vi][vj] > v->cs[i][j]) ov = v->ce[i][j] - v->cs[vi][vj];
+					else ov = v->ce[vi][vj] - v->cs[i][j];
+					if (ov > 14) continue;
+					if (abs((int)dist) < 6) continue;
+					gs = (v->cs[vi][vj] > v->cs[i][j]) ? (v->ce[i][j] - 8) : (v->ce[vi][vj] - 8);
+					ge = (v->cs[vi][vj] < v->cs[i][j]) ? (v->cs[i][j] + 8) : (v->cs[vi][vj] + 8);
+					normal = 1 != (v->cs[vi][vj] > v->cs[i][j]) + (v->pos[vi][vj] > v->pos[i][j]);
+					if (rl > LONG_READ) {
+						int kx;
+						for (kx = 0; kx < SVG_MAX_INDEL_SECTIONS; kx++) { if (!v->rec[vi][vj][kx * 3]) break; major += v->rec[vi][vj][kx * 3 + 2]; }
+						for (kx = 0; kx < SVG_MAX_INDEL_SECTIONS; kx++) { if (!v->rec[i][j][kx * 3]) break; minor_off += v->rec[i][j][kx * 3 + 2]; }
+						if (v->pos[vi][vj] < v->pos[i][j]) { lio = major; rio = minor_off; }
+						else { rio = major; lio = minor_off; }
+						rio = 0;
+					}
+					{
+						uint32_t pa = v->pos[vi][vj], pb = v->pos[i][j];
+						rep = donor_score(c, pa < pb ? pa : pb, pa > pb ? pa : pb, lio, rio, normal,
+						                  gs > 0 ? gs : 0, ge < rl ? ge : rl, c->text[end], rl,
+						                  &split, &gtag, &found, &ins, &sinc, &linc);
+					}
+					if (rep > 0) rep += v->votes[i][j] * 100000;
+				}
+				if (rep) {
+					J->minor_position = v->pos[i][j];
+					J->minor_votes = v->votes[i][j];
+					J->minor_coverage_start = v->cs[i][j];
+					J->minor_coverage_end = v->ce[i][j];
+					J->double_indel_offset = (int8_t)((minor_off & 0xf) | ((major & 0xf) << 4));
+					J->split_point = (int16_t)split;
+					J->small_side_increasing_coordinate = (int8_t)sinc;
+					J->large_side_increasing_coordinate = (int8_t)linc;
+					J->indel_at_junction = (int8_t)ins;
+					a->result_flags &= ~0x3;
+					if (!found || gtag > 2) a->result_flags |= 3;
+					else a->result_flags = gtag ? (a->result_flags | 1) : (a->result_flags & ~1);
+					a->result_flags = jumped ? (a->result_flags | 4) : (a->result_flags & ~4);
+				}
+			}
+		if (a->result_flags & 4) {
+			int t = J->minor_coverage_start;
+			J->minor_coverage_start = rl - J->minor_coverage_end;
+			J->minor_coverage_end = rl - t;
+			J->split_point = (a->result_flags & SVG_NEGATIVE_STRAND_FLAG) ? J->split_point : (rl - J->split_point);
+		}
+	}
+}
+
+/* process_voting_junction_PE_topK, core-junction.c:2199-2530 */
+static void topk(readctx *c)
+{
+	const svg_params *p = c->p;
+	int ends = c->ends, e, i, j, tk;
+	int top[2][9];
+	simple_t *simp[2];
+	int nsimp[2] = {0, 0};
+	comb_t comb[16];
+	int ncomb = 0;
+	svg_mapping_result tmp[2][3];
+	svg_subjunc_result jtmp[2][3];
+	int cur[2] = {0, 0};
+	simp[0] = alloca(sizeof(simple_t) * p->max_vote_simples);
+	simp[1] = alloca(sizeof(simple_t) * p->max_vote_simples);
+
+	for (e = 0; e < ends; e++) {
+		vtab_t *v = &c->vt[e];
+		memset(top[e], 0, sizeof(int) * p->top_scores);
+		for (i = 0; i < TAB_ROWS; i++)
+			for (j = 0; j < v->items[i]; j++) top3(top[e], p->top_scores, v->votes[i][j]);
+		for (i = 0; i < p->multi_best; i++)
+			if (c->res[e][i].selected_votes > 0) top3(top[e], p->top_scores, c->res[e][i].selected_votes);
+	}
+	for (e = 0; e < ends; e++) {
+		vtab_t *v = &c->vt[e];
+		int ns = 0;
+		for (tk = 0; tk < p->top_scores; tk++) {
+			int N = top[e][tk];
+			if (ns >= p->max_vote_simples) break;
+			if (N < 1 || (top[e][0] - N > p->max_vote_number_cutoff)) break;
+			for (i = 0; i < TAB_ROWS; i++) {
+				if (ns >= p->max_vote_simples) break;
+				for (j = 0; j < v->items[i]; j++) {
+					if (ns >= p->max_vote_simples) break;
+					if (p->do_big_margin_filtering_for_junctions && tk == 0 && v->votes[i][j] >= top[e][p->top_scores - 1])
+						big_margin_insert(p, c->bm[e], (unsigned char)v->votes[i][j], v->cs[i][j], v->ce[i][j], c->rl[e], (v->masks[i][j] & NEG_MASK) ? 1 : 0);
+					if (v->votes[i][j] == N && v->votes[i][j] >= p->min_votes_second) {
+						simple_t *s = &simp[e][ns++];
+						s->is_vote = 1; s->i = i; s->j = j;
+						s->start_base = v->cs[i][j]; s->pos = v->pos[i][j]; s->votes = N;
+					}
+				}
+			}
+			for (i = 0; i < p->multi_best; i++) {
+				if (ns >= p->max_vote_simples) break;
+				if (c->res[e][i].selected_votes == N) {
+					simple_t *s = &simp[e][ns++];
+					s->is_vote = 0; s->i = i; s->j = 0;
+					s->pos = c->res[e][i].selected_position;
+					s->votes = c->res[e][i].selected_votes;
+					s->start_base = c->res[e][i].confident_coverage_start;
+				}
+			}
+		}
+		nsimp[e] = ns;
+	}
+	if (ends == 2) {
+		for (i = 0; i < nsimp[0]; i++)
+			for (j = 0; j < nsimp[1]; j++) {
+				int pe, same, w, sc, t, mv;
+				simple_t *a = &simp[0][i], *b = &simp[1][j];
+				if ((a->votes > b->votes ? a->votes : b->votes) < p->min_votes_first) continue;
+				pe_test(c, a->pos, b->pos, &pe, &same);
+				if (!pe && (a->votes < b->votes ? a->votes : b->votes) < p->min_votes_first) continue;
+				w = pe ? 1300 : (same ? 1000 : 800);
+				sc = (a->votes + b->votes) * w;
+				for (t = 0; t < ncomb; t++) if (comb[t].score < sc) break;
+				if (t < p->max_vote_combinations) {
+					mv = ncomb < p->max_vote_combinations - 1 ? ncomb : p->max_vote_combinations - 1;
+					for (; mv > t; mv--) comb[mv] = comb[mv - 1];
+					comb[t].r1 = a; comb[t].r2 = b; comb[t].score = sc;
+					if (ncomb < p->max_vote_combinations) ncomb++;
+				}
+			}
+	}
+	memset(tmp, 0, sizeof tmp);
+	memset(jtmp, 0, sizeof jtmp);
+	if (ncomb > 0) {
+		/* merge_sort -> basic_sort_run for <= 11 items (core.c:4716-4729) */
+		if (ncomb > 11) abort();
+		for (i = 0; i < ncomb - 1; i++) {
+			int mj = i;
+			for (j = i + 1; j < ncomb; j++) if (comb[mj].score - comb[j].score > 0) mj = j;
+			if (i != mj) { comb_t t = comb[i]; comb[i] = comb[mj]; comb[mj] = t; }
+		}
+		for (e = 0; e < ends; e++) {
+			for (i = ncomb - 1; i >= 0; i--) {
+				simple_t *loc = e ? comb[i].r2 : comb[i].r1;
+				int ex = 0;
+				if (cur[e] >= p->multi_best) break;
+				for (j = 0; j < cur[e]; j++) if (tmp[e][j].selected_position == loc->pos) { ex = 1; break; }
+				if (ex) continue;
+				if (loc->is_vote) copy_vote(c, &tmp[e][cur[e]], &jtmp[e][cur[e]], e, loc->i, loc->j);
+				else { tmp[e][cur[e]] = c->res[e][loc->i]; jtmp[e][cur[e]] = c->jres[e][loc->i]; }
+				cur[e]++;
+			}
+		}
+	} else {
+		if (0 == nsimp[0]) c->res[0][0].noninformative_subreads_in_vote = (uint8_t)c->vt[0].noninf;
+		if (ends == 2 && 0 == nsimp[1]) c->res[1][0].noninformative_subreads_in_vote = (uint8_t)c->vt[1].noninf;
+		if (nsimp[0] > 0 || nsimp[1] > 0) {
+			for (e = 0; e < ends; e++)
+				for (i = 0; i < nsimp[e]; i++) {
+					simple_t *loc = &simp[e][i];
+					int ex = 0;
+					if (cur[e] >= p->multi_best) break;
+					if (loc->votes < p->min_votes_first) continue;
+					for (j = 0; j < cur[e]; j++) if (tmp[e][j].selected_position == loc->pos) { ex = 1; break; }
+					if (ex) continue;
+					if (loc->is_vote) copy_vote(c, &tmp[e][cur[e]], &jtmp[e][cur[e]], e, loc->i, loc->j);
+					else { tmp[e][cur[e]] = c->res[e][loc->i]; jtmp[e][cur[e]] = c->jres[e][loc->i]; }
+					cur[e]++;
+				}
+		}
+	}
+	for (e = 0; e < ends; e++)
+		for (i = 0; i < p->multi_best; i++) {
+			if (i < cur[e]) c->res[e][i] = tmp[e][i];
+			else c->res[e][i].selected_votes = 0;
+			if (p->do_breakpoint_detection) {
+				if (i < cur[e]) c->jres[e][i] = jtmp[e][i];
+				else c->jres[e][i].minor_votes = 0;
+			}
+		}
+}
+
+/* one read (pair): do_voting body, core.c:3091-3235 */
+static void vote_read(readctx *c)
+{
+	const svg_params *p = c->p;
+	const svo_index *ix = c->ix;
+	int strand, e, gap = ix->gap;
+	int tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
+	uint32_t low = ix->start_base_offset, high = ix->start_base_offset + ix->length;
+	static __thread uint32_t shift_locs[TAB_ROWS * TAB_SPACE];
+	memset(c->res, 0, sizeof c->res);
+	memset(c->jres, 0, sizeof c->jres);
+	memset(c->bm, 0, sizeof c->bm);
+	c->applied[0] = c->applied[1] = 0;
+	for (strand = 0; strand < 2; strand++) {
+		int applied = 0;
+		for (e = 0; e < c->ends; e++) {
+			vtab_t *v = &c->vt[e];
+			int rl = c->rl[e], step, cr, round, k, x;
+			uint32_t shift_no = 0, hb;
+			if (rl < 16) { vt_reset(v); continue; }   /* out of contract: reference reads a stale table */
+			cr = (rl - 15 - gap) << 16;
+			if (rl <= LONG_READ) {
+				step = cr / (p->total_subreads - 1);
+				if (step < (gap << 16)) step = gap << 16;
+			} else {
+				step = 6 << 16;
+				if (cr / step > 62) step = cr / 62;
+			}
+			applied = 1 + cr / step;
+			c->applied[e] = applied;
+			hb = high - (uint32_t)rl;
+			for (round = 0; round < 2; round++) {
+				vt_reset(v);
+				for (k = 0; k < applied; k++)
+					for (x = 0; x < gap; x++) {
+						int off = (int)(((int64_t)step * k) >> 16);
+						if (gap > 1) off -= off % gap - x;
+						probe_X(ix, pack16(c->text[e] + off), off, strand, v, tol, k, low, hb, round, shift_locs, &shift_no, &c->st);
+					}
+				if (shift_no == 0) break;
+			}
+		}
+		if (c->ends == 2) topk(c);
+		else if (c->vt[0].max_vote >= p->min_votes_first) topk(c);
+		else if (c->res[0][0].selected_votes < 1) {
+			c->res[0][0].noninformative_subreads_in_vote = 0;
+			if (applied > c->res[0][0].used_subreads_in_vote) c->res[0][0].used_subreads_in_vote = applied;
+			if (c->vt[0].noninf > c->res[0][0].noninformative_subreads_in_vote)
+				c->res[0][0].noninformative_subreads_in_vote = (uint8_t)c->vt[0].noninf;
+		}
+		if (strand == 0)
+			for (e = 0; e < c->ends; e++) revcomp(c->text[e], c->rl[e]);
+	}
+}
+
+/* ------------------------------------------------------------------ batch driver */
+typedef struct {
+	const svo_index *ix;
+	const svg_params *p;
+	const svg_reads *r1, *r2;
+	svg_mapping_result *out;
+	svg_subjunc_result *jout;
+	uint16_t *bm;
+	uint64_t next;
+	pthread_mutex_t lock;
+	probe_stats st;
+} batch_t;
+
+#define GRAIN 256
+
+static void *worker(void *arg)
+{
+	batch_t *b = arg;
+	readctx *c = malloc(sizeof(readctx));
+	int ends = b->r2 ? 2 : 1;
+	c->ix = b->ix; c->p = b->p; c->ends = ends;
+	memset(&c->st, 0, sizeof c->st);
+	for (;;) {
+		uint64_t s, r, n = b->r1->n_reads;
+		pthread_mutex_lock(&b->lock);
+		s = b->next; b->next += GRAIN;
+		pthread_mutex_unlock(&b->lock);
+		if (s >= n) break;
+		for (r = s; r < s + GRAIN && r < n; r++) {
+			int e, k;
+			for (e = 0; e < ends; e++) {
+				const svg_reads *rr = e ? b->r2 : b->r1;
+				int len = rr->lens[r];
+				int rev = e ? b->p->reverse_r2 : b->p->reverse_r1;
+				memcpy(c->text[e], rr->seq + rr->offsets[r], len);
+				c->text[e][len] = 0;
+				c->rl[e] = len;
+				if (rev) revcomp(c->text[e], len);
+			}
+			vote_read(c);
+			for (e = 0; e < ends; e++)
+				for (k = 0; k < b->p->multi_best; k++) {
+					size_t o = ((size_t)r * ends + e) * b->p->multi_best + k;
+					b->out[o] = c->res[e][k];
+					if (b->jout) b->jout[o] = c->jres[e][k];
+				}
+			if (b->bm)
+				for (e = 0; e < ends; e++)
+					memcpy(b->bm + ((size_t)r * ends + e) * SVG_BIG_MARGIN_WORDS, c->bm[e], sizeof(uint16_t) * SVG_BIG_MARGIN_WORDS);
+		}
+	}
+	pthread_mutex_lock(&b->lock);
+	b->st.probes += c->st.probes; b->st.bucket_items += c->st.bucket_items; b->st.hits += c->st.hits;
+	pthread_mutex_unlock(&b->lock);
+	free(c);
+	return NULL;
+}
+
+/* Vote a batch on the CPU with `threads` pthreads.  Returns 0 or SVG_E_*. */
+int svo_vote_batch(const svo_index *ix, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                   svg_mapping_result *out, svg_subjunc_result *jout, uint16_t *bm, int threads,
+                   uint64_t *stats3)
+{
+	batch_t b;
+	pthread_t th[256];
+	int t;
+	uint64_t i;
+	if (!ix || !p || !r1 || !out) return SVG_E_ARG;
+	if (r2 && r2->n_reads != r1->n_reads) return SVG_E_ARG;
+	if (p->multi_best < 1 || p->multi_best > 3 || p->top_scores < 1 || p->top_scores > 9) return SVG_E_UNSUPPORTED;
+	if (p->max_vote_combinations > 11 || p->max_vote_simples < 1) return SVG_E_UNSUPPORTED;
+	if (p->do_breakpoint_detection && !jout) return SVG_E_ARG;
+	if (p->do_big_margin_filtering_for_junctions && !bm) return SVG_E_ARG;
+	for (i = 0; i < r1->n_reads; i++) {
+		if (r1->lens[i] > SVG_MAX_READ_LENGTH) return SVG_E_UNSUPPORTED;
+		if (r2 && r2->lens[i] > SVG_MAX_READ_LENGTH) return SVG_E_UNSUPPORTED;
+		if (p->do_breakpoint_detection && (r1->lens[i] > LONG_READ || (r2 && r2->lens[i] > LONG_READ))) return SVG_E_UNSUPPORTED;
+	}
+	memset(&b, 0, sizeof b);
+	b.ix = ix; b.p = p; b.r1 = r1; b.r2 = r2; b.out = out; b.jout = jout; b.bm = bm;
+	pthread_mutex_init(&b.lock, NULL);
+	if (threads < 1) threads = 1;
+	if (threads > 256) threads = 256;
+	for (t = 0; t < threads; t++) pthread_create(&th[t], NULL, worker, &b);
+	for (t = 0; t < threads; t++) pthread_join(th[t], NULL);
+	pthread_mutex_destroy(&b.lock);
+	if (stats3) { stats3[0] = b.st.probes; stats3[1] = b.st.bucket_items; stats3[2] = b.st.hits; }
+	return 0;
+}

@@ -1,0 +1,203 @@
+"""ctypes mirror of include/subread_vote.h (the C ABI of the vote path).
+
+Record layouts are byte-identical to the reference's bigtable structs:
+mapping_result_t (core.h:350-370, 68 B) and subjunc_result_t (core.h:397-410,
+16 B).  Parameter defaults follow the reference's own order of precedence:
+init_global_context (core-indel.c:4399-4538), parse_opts_aligner /
+parse_opts_subjunc (core-interface-aligner.c:256-300, core-interface-subjunc.c:255-290,
+:671), then load_global_context's overrides (core.c:4075-4094).
+"""
+import ctypes
+import numpy as np
+
+MAX_READ_LENGTH = 1210
+BIG_MARGIN_WORDS = 9
+NEGATIVE_STRAND_FLAG = 8
+PROGRAM_ALIGN = 0
+PROGRAM_SUBJUNC = 1
+
+ERRORS = {0: "OK", -1: "SVG_E_ARG", -2: "SVG_E_IO", -3: "SVG_E_FORMAT",
+          -4: "SVG_E_UNSUPPORTED", -5: "SVG_E_DEVICE", -6: "SVG_E_NOMEM"}
+
+MAPPING_DTYPE = np.dtype([
+    ("selected_position", "<u4"),
+    ("result_flags", "<i2"),
+    ("read_length", "<i2"),
+    ("selected_votes", "<i2"),
+    ("used_subreads_in_vote", "<i2"),
+    ("noninformative_subreads_in_vote", "u1"),
+    ("indels_in_confident_coverage", "i1"),
+    ("is_fully_covered", "i1"),
+    ("_pad0", "u1"),
+    ("selected_indel_record", "<i2", (22,)),
+    ("confident_coverage_start", "<u2"),
+    ("confident_coverage_end", "<u2"),
+    ("subread_quality", "<i2"),
+    ("_pad1", "<u2"),
+])
+assert MAPPING_DTYPE.itemsize == 68
+
+SUBJUNC_DTYPE = np.dtype([
+    ("split_point", "<i2"),
+    ("minor_votes", "<i2"),
+    ("double_indel_offset", "i1"),
+    ("indel_at_junction", "i1"),
+    ("small_side_increasing_coordinate", "i1"),
+    ("large_side_increasing_coordinate", "i1"),
+    ("minor_position", "<u4"),
+    ("minor_coverage_start", "<u2"),
+    ("minor_coverage_end", "<u2"),
+])
+assert SUBJUNC_DTYPE.itemsize == 16
+
+_PARAM_FIELDS = [
+    "total_subreads", "min_votes_first", "min_votes_second", "max_indel_length",
+    "multi_best", "top_scores", "max_vote_simples", "max_vote_combinations",
+    "max_vote_number_cutoff", "min_pair_distance", "max_pair_distance",
+    "reverse_r1", "reverse_r2", "do_breakpoint_detection",
+    "do_big_margin_filtering_for_junctions", "big_margin_record_size",
+    "maximum_intron_length", "prefer_donor_receptor_junctions",
+    "check_donor_at_junctions", "max_insertion_at_junctions", "more_accurate_fusions",
+]
+
+
+class SvgParams(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_int32) for f in _PARAM_FIELDS]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f in _PARAM_FIELDS}
+
+
+class SvgReads(ctypes.Structure):
+    _fields_ = [
+        ("seq", ctypes.c_void_p),
+        ("offsets", ctypes.c_void_p),
+        ("lens", ctypes.c_void_p),
+        ("n_reads", ctypes.c_uint64),
+    ]
+
+
+class SvgIndexInfo(ctypes.Structure):
+    _fields_ = [
+        ("items", ctypes.c_uint64),
+        ("buckets", ctypes.c_uint32),
+        ("index_gap", ctypes.c_int32),
+        ("padding", ctypes.c_int32),
+        ("array_length", ctypes.c_uint32),
+        ("n_chromosomes", ctypes.c_uint32),
+        ("device_bytes", ctypes.c_uint64),
+        ("device", ctypes.c_int32),
+    ]
+
+
+class SvgBatchStats(ctypes.Structure):
+    _fields_ = [
+        ("probes", ctypes.c_uint64),
+        ("bucket_items", ctypes.c_uint64),
+        ("hits", ctypes.c_uint64),
+        ("results", ctypes.c_uint64),
+    ]
+
+
+def default_params(program=PROGRAM_ALIGN, paired=False, **overrides):
+    """Python mirror of svg_params_default() (same values, same precedence)."""
+    p = SvgParams()
+    # init_global_context, core-indel.c:4399-4538
+    p.total_subreads = 10
+    p.min_votes_first = 3
+    p.min_votes_second = 1
+    p.max_indel_length = 5
+    p.top_scores = 3
+    p.min_pair_distance = 50
+    p.max_pair_distance = 600
+    p.reverse_r1 = 0
+    p.reverse_r2 = 1
+    p.do_breakpoint_detection = 0
+    p.do_big_margin_filtering_for_junctions = 0
+    p.big_margin_record_size = 9
+    p.maximum_intron_length = 500000
+    p.prefer_donor_receptor_junctions = 1
+    p.check_donor_at_junctions = 1
+    p.max_insertion_at_junctions = 0
+    p.more_accurate_fusions = 1
+    if program == PROGRAM_SUBJUNC:
+        # parse_opts_subjunc, core-interface-subjunc.c:268-282
+        p.do_breakpoint_detection = 1
+        p.total_subreads = 14
+        p.min_votes_first = 1
+        p.min_votes_second = 1
+        p.do_big_margin_filtering_for_junctions = 1
+    # more_accurate_fusions only survives with fusion / long-del detection
+    # (core-interface-aligner.c:648, core-interface-subjunc.c:671)
+    p.more_accurate_fusions = 0
+    # load_global_context overrides, core.c:4075-4084 (reported_multi_best_reads = 1)
+    p.max_vote_combinations = 3
+    p.multi_best = 3
+    p.max_vote_simples = 64 if paired else 3
+    p.max_vote_number_cutoff = 2
+    for k, v in overrides.items():
+        setattr(p, k, int(v))
+    return p
+
+
+class ReadBatch:
+    """Concatenated ASCII reads + offsets + lengths, kept alive for ctypes."""
+
+    def __init__(self, seq, offsets, lens):
+        self.seq = np.ascontiguousarray(seq, dtype=np.uint8)
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        assert self.offsets.shape == self.lens.shape
+
+    @classmethod
+    def from_list(cls, reads):
+        reads = [r.encode() if isinstance(r, str) else bytes(r) for r in reads]
+        lens = np.array([len(r) for r in reads], dtype=np.uint16)
+        offs = np.zeros(len(reads), dtype=np.uint64)
+        if len(reads) > 1:
+            offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        seq = np.frombuffer(b"".join(reads), dtype=np.uint8) if reads else np.zeros(0, np.uint8)
+        return cls(seq, offs, lens)
+
+    @classmethod
+    def fixed(cls, seq2d):
+        """Reads of one length: seq2d is an (n, L) uint8 array."""
+        seq2d = np.ascontiguousarray(seq2d, dtype=np.uint8)
+        n, L = seq2d.shape
+        return cls(seq2d.reshape(-1), np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint16))
+
+    def __len__(self):
+        return int(self.lens.shape[0])
+
+    def slice(self, a, b):
+        return ReadBatch(self.seq, self.offsets[a:b], self.lens[a:b])
+
+    def read(self, i):
+        o = int(self.offsets[i])
+        return bytes(self.seq[o:o + int(self.lens[i])])
+
+    def struct(self):
+        s = SvgReads()
+        s.seq = self.seq.ctypes.data
+        s.offsets = self.offsets.ctypes.data
+        s.lens = self.lens.ctypes.data
+        s.n_reads = len(self)
+        return s
+
+
+def read_fastq(path):
+    """Minimal FASTQ reader (plain or .gz) -> (names, ReadBatch)."""
+    import gzip
+    op = gzip.open if str(path).endswith(".gz") else open
+    names, reads = [], []
+    with op(path, "rb") as f:
+        while True:
+            h = f.readline()
+            if not h:
+                break
+            s = f.readline().rstrip(b"\r\n")
+            f.readline()
+            f.readline()
+            names.append(h[1:].split()[0].decode())
+            reads.append(s)
+    return names, ReadBatch.from_list(reads)
