@@ -191,6 +191,25 @@ int svg_get_stats(const svg_index *idx, svg_batch_stats *out);
 const char *svg_last_error(void);
 int svg_abi_version(void);
 
+/*
+ * Index builder (replaces subread-buildindex for a single-block index,
+ * index-builder.c:1014-1306): writes <prefix>.00.b.tab/.00.b.array/.reads/
+ * .files/.log byte-identical (tab/array/reads) to the reference.
+ *   gap 1 = full index (-F), 3 = gapped (default); memory_mb = -M (8000);
+ *   force_one_block = -B; repeat_threshold = -f (100).
+ */
+int svg_build_index(const char *fasta, const char *prefix, int gap, int memory_mb,
+                    int force_one_block, int repeat_threshold);
+
+/* Seeded synthetic data for tests/benchmarks (genRandomReads counterpart). */
+void svg_sim_genome(char *out, uint64_t length, uint64_t seed);
+void svg_sim_repeats(char *genome, uint64_t length, uint64_t n_copies, uint32_t element_len,
+                     uint32_t n_families, double divergence, uint64_t seed);
+int  svg_sim_reads(const char *genome, const uint64_t *ctg_start, const uint32_t *ctg_len,
+                   uint32_t n_ctg, uint64_t first, uint64_t n_reads, int len, double sub,
+                   double indel_frac, double n_rate, uint64_t seed, char *seq,
+                   uint32_t *truth_ctg, uint32_t *truth_pos, uint8_t *truth_strand, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,158 @@
+"""subread_amd -- MI355X-native seed-and-vote hot path of Subread (subread-align / subjunc).
+
+The product is the C-ABI shared library ``subread_amd/lib/libsubread_amd.so``
+(include/subread_vote.h): host C (index loader, format-exact index builder,
+read simulator) + hand-written HIP kernels for gfx950.  This module is a thin
+ctypes wrapper used by the CLI front end, the tests and bench.py.
+
+There is no CPU fallback anywhere in this package: if the library is missing,
+or the GPU is missing when a vote is requested, the call raises.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from .abi import (MAPPING_DTYPE, SUBJUNC_DTYPE, BIG_MARGIN_WORDS, ERRORS, PROGRAM_ALIGN,
+                  PROGRAM_SUBJUNC, SvgParams, SvgReads, SvgIndexInfo, SvgBatchStats, ReadBatch,
+                  default_params, read_fastq)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libsubread_amd.so")
+CSRC = os.path.join(HERE, "csrc")
+
+# every symbol include/subread_vote.h declares
+EXPORTS = [
+    "svg_params_default", "svg_index_open", "svg_index_close", "svg_index_get_info",
+    "svg_vote_batch", "svg_vote_batch_device", "svg_set_stats", "svg_get_stats",
+    "svg_last_error", "svg_abi_version", "svg_build_index", "svg_sim_genome",
+    "svg_sim_repeats", "svg_sim_reads",
+]
+
+_lib = None
+
+
+class SvgError(RuntimeError):
+    pass
+
+
+def build(arch="gfx950", quiet=True):
+    """Compile libsubread_amd.so in-tree (hipcc --offload-arch=gfx950)."""
+    r = subprocess.run(["make", "-C", CSRC, "ARCH=" + arch, "-j8"], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise SvgError("build of libsubread_amd.so failed:\n" + r.stdout[-4000:] + r.stderr[-4000:])
+    if not quiet:
+        print(r.stdout)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SvgError("libsubread_amd.so not built (run __graft_entry__.build() or make -C subread_amd/csrc)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64
+        L.svg_params_default.argtypes = [vp, i32, i32]
+        L.svg_index_open.argtypes = [ctypes.c_char_p, i32, ctypes.POINTER(vp)]
+        L.svg_index_open.restype = i32
+        L.svg_index_close.argtypes = [vp]
+        L.svg_index_get_info.argtypes = [vp, vp]
+        L.svg_vote_batch.argtypes = [vp] * 7
+        L.svg_vote_batch.restype = i32
+        L.svg_vote_batch_device.argtypes = [vp] * 8
+        L.svg_vote_batch_device.restype = i32
+        L.svg_set_stats.argtypes = [vp, i32]
+        L.svg_get_stats.argtypes = [vp, vp]
+        L.svg_last_error.restype = ctypes.c_char_p
+        L.svg_build_index.argtypes = [ctypes.c_char_p, ctypes.c_char_p, i32, i32, i32, i32]
+        L.svg_build_index.restype = i32
+        L.svg_sim_genome.argtypes = [vp, u64, u64]
+        L.svg_sim_repeats.argtypes = [vp, u64, u64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, u64]
+        L.svg_sim_reads.argtypes = [vp, vp, vp, ctypes.c_uint32, u64, u64, i32, ctypes.c_double,
+                                    ctypes.c_double, ctypes.c_double, u64, vp, vp, vp, vp, i32]
+        L.svg_sim_reads.restype = i32
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = lib().svg_last_error().decode(errors="replace")
+        raise SvgError("%s failed: %s (%s)" % (what, ERRORS.get(rc, rc), msg))
+
+
+def params_default(program=PROGRAM_ALIGN, paired=False):
+    p = SvgParams()
+    lib().svg_params_default(ctypes.byref(p), program, 1 if paired else 0)
+    return p
+
+
+def build_index(fasta, prefix, gap=3, memory_mb=8000, force_one_block=False, repeat_threshold=100):
+    """Format-exact subread-buildindex (single block): -F => gap=1, -B => force_one_block."""
+    rc = lib().svg_build_index(str(fasta).encode(), str(prefix).encode(), gap, memory_mb,
+                               1 if force_one_block else 0, repeat_threshold)
+    _check(rc, "svg_build_index")
+
+
+class VoteIndex:
+    """An index resident in HBM of one GPU (svg_index_open)."""
+
+    def __init__(self, prefix, device=0):
+        h = ctypes.c_void_p()
+        _check(lib().svg_index_open(str(prefix).encode(), device, ctypes.byref(h)), "svg_index_open")
+        self.h = h
+        info = SvgIndexInfo()
+        lib().svg_index_get_info(self.h, ctypes.byref(info))
+        self.info = info
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().svg_index_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stats(self, on=True):
+        lib().svg_set_stats(self.h, 1 if on else 0)
+
+    def stats(self):
+        s = SvgBatchStats()
+        lib().svg_get_stats(self.h, ctypes.byref(s))
+        return {"probes": s.probes, "bucket_items": s.bucket_items, "hits": s.hits, "results": s.results}
+
+    def vote(self, params, r1, r2=None):
+        """Host buffers in, host records out: (mapping[n,ends,mb], subjunc|None, big_margin|None)."""
+        n = len(r1)
+        ends = 2 if r2 is not None else 1
+        mb = params.multi_best
+        out = np.zeros((n, ends, mb), dtype=MAPPING_DTYPE)
+        jout = np.zeros((n, ends, mb), dtype=SUBJUNC_DTYPE) if params.do_breakpoint_detection else None
+        bm = (np.zeros((n, ends, BIG_MARGIN_WORDS), dtype=np.uint16)
+              if params.do_big_margin_filtering_for_junctions else None)
+        s1 = r1.struct()
+        s2 = r2.struct() if r2 is not None else None
+        rc = lib().svg_vote_batch(self.h, ctypes.byref(params), ctypes.byref(s1),
+                                  ctypes.byref(s2) if s2 is not None else None,
+                                  out.ctypes.data, jout.ctypes.data if jout is not None else None,
+                                  bm.ctypes.data if bm is not None else None)
+        _check(rc, "svg_vote_batch")
+        return out, jout, bm
+
+    def vote_device(self, params, r1_ptrs, r2_ptrs, out_ptr, jout_ptr=None, bm_ptr=None, stream=None):
+        """Device pointers in/out, async on `stream` (int handle or None).
+        r*_ptrs = (seq_ptr, offsets_ptr, lens_ptr, n_reads)."""
+        def mk(t):
+            s = SvgReads()
+            s.seq, s.offsets, s.lens, s.n_reads = t
+            return s
+        s1 = mk(r1_ptrs)
+        s2 = mk(r2_ptrs) if r2_ptrs is not None else None
+        rc = lib().svg_vote_batch_device(self.h, ctypes.byref(params), ctypes.byref(s1),
+                                         ctypes.byref(s2) if s2 is not None else None,
+                                         out_ptr, jout_ptr, bm_ptr, stream)
+        _check(rc, "svg_vote_batch_device")

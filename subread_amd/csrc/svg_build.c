@@ -1,0 +1,315 @@
+/*
+ * svg_build.c -- format-exact builder of the Subread base-space index
+ * (<prefix>.00.b.tab / .00.b.array / .reads / .files / .log), single block.
+ *
+ * Replaces subread-buildindex (index-builder.c:1014-1306) for the one-block
+ * case: the bytes of .tab/.array/.reads equal the reference's (md5 known
+ * answers in tests/golden/index_md5.json).  The reference builds the table by
+ * per-bucket insertion + selection sort at dump time; here the same total order
+ * is produced with two LSD radix sorts:
+ *   1. FASTA normalisation     check_and_convert_FastA   index-builder.c:789-992
+ *      (a/c/g/t any case -> upper, everything else -> 'A'; contigs <=16 bp dropped)
+ *   2. coordinates             build_gene_index          index-builder.c:113-420
+ *      (first contig at PAD=1210, next at +L-16+2*PAD; .reads = O+L-16+PAD)
+ *   3. sampled 16-mers every `gap` bases, key = genekey2int (input-files.c:1232)
+ *   4. repeat exclusion        scan_gene_index           index-builder.c:472-684
+ *      (keys occurring > threshold times over the sampled windows are dropped)
+ *   5. bucket count            calculate_buckets_by_size sorted-hashtable.c:42-75
+ *   6. .tab layout + in-bucket order  gehash_dump / is_1_greater_than_2
+ *                                      sorted-hashtable.c:1689-1908
+ *   7. .array 2-bit LSB-first  gvindex_set / gvindex_dump gene-value-index.c:135-187
+ */
+#define _GNU_SOURCE
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdint.h>
+#include <ctype.h>
+#include <zlib.h>
+#include "subread_vote.h"
+#include "svg_internal.h"
+
+#define PAD 1210
+#define NAME_MAX_LEN 200
+
+typedef struct {
+	char name[NAME_MAX_LEN];
+	uint64_t start;   /* into base buffer */
+	uint32_t len;
+} contig_t;
+
+typedef struct {
+	char *bases;      /* normalised, concatenated */
+	uint64_t nbases, cap;
+	contig_t *ctg;
+	uint32_t nctg, ctg_cap;
+} genome_t;
+
+static void g_push(genome_t *g, const char *s, size_t n)
+{
+	if (g->nbases + n > g->cap) {
+		g->cap = (g->nbases + n) * 2 + (1 << 20);
+		g->bases = realloc(g->bases, g->cap);
+	}
+	memcpy(g->bases + g->nbases, s, n);
+	g->nbases += n;
+}
+
+/* check_and_convert_FastA semantics (index-builder.c:789-992) */
+static int read_fasta(const char *path, genome_t *g)
+{
+	gzFile fp = gzopen(path, "rb");
+	char *line = malloc(1 << 16);
+	int have = 0;
+	if (!fp) { free(line); svg_set_error("cannot open FASTA '%s'", path); return SVG_E_IO; }
+	while (gzgets(fp, line, 1 << 16)) {
+		size_t L = strlen(line);
+		while (L && (line[L - 1] == '\n' || line[L - 1] == '\r')) line[--L] = 0;
+		if (!L) continue;
+		if (line[0] == '>') {
+			contig_t *c;
+			uint32_t i;
+			if (have && g->ctg[g->nctg - 1].len <= 16) {  /* short contig: drop entirely */
+				g->nbases = g->ctg[g->nctg - 1].start;
+				g->nctg--;
+			}
+			if (g->nctg == g->ctg_cap) {
+				g->ctg_cap = g->ctg_cap ? g->ctg_cap * 2 : 64;
+				g->ctg = realloc(g->ctg, sizeof(contig_t) * g->ctg_cap);
+			}
+			c = &g->ctg[g->nctg++];
+			memset(c, 0, sizeof *c);
+			/* .reads name: up to ' ', '\t' or end, at most NAME_MAX_LEN-1 chars
+			 * (build_gene_index, index-builder.c:266-270, '|' kept) */
+			for (i = 0; line[i + 1] && line[i + 1] != ' ' && line[i + 1] != '\t' && i < NAME_MAX_LEN - 1; i++)
+				c->name[i] = line[i + 1];
+			c->name[i] = 0;
+			/* duplicate names are an error in the reference */
+			{
+				uint32_t k;
+				char key[NAME_MAX_LEN]; size_t kl = 0;
+				for (kl = 0; line[kl + 1] && line[kl + 1] != ' ' && line[kl + 1] != '|' && line[kl + 1] != '\t' && kl < NAME_MAX_LEN - 1; kl++) key[kl] = line[kl + 1];
+				key[kl] = 0;
+				for (k = 0; k + 1 < g->nctg; k++) {
+					char k2[NAME_MAX_LEN]; size_t j;
+					for (j = 0; g->ctg[k].name[j] && g->ctg[k].name[j] != '|' && j < NAME_MAX_LEN - 1; j++) k2[j] = g->ctg[k].name[j];
+					k2[j] = 0;
+					if (!strcmp(k2, key)) { gzclose(fp); free(line); svg_set_error("repeated chromosome name '%s'", key); return SVG_E_FORMAT; }
+				}
+			}
+			c->start = g->nbases;
+			have = 1;
+		} else if (have) {
+			size_t i;
+			for (i = 0; i < L; i++) {
+				int ch = line[i], lo = tolower(ch);
+				if (lo == 'a' || lo == 'c' || lo == 'g' || lo == 't') line[i] = (char)toupper(ch);
+				else line[i] = 'A';
+			}
+			g_push(g, line, L);
+			g->ctg[g->nctg - 1].len += (uint32_t)L;
+		}
+	}
+	if (have && g->ctg[g->nctg - 1].len <= 16) { g->nbases = g->ctg[g->nctg - 1].start; g->nctg--; }
+	gzclose(fp);
+	free(line);
+	if (!g->nctg) { svg_set_error("no contig of >16 bases in '%s'", path); return SVG_E_FORMAT; }
+	return 0;
+}
+
+/* calculate_buckets_by_size, sorted-hashtable.c:42-75 (VER2) */
+uint32_t svg_bucket_count(uint64_t expected_items, int gap)
+{
+	int64_t nb = (int64_t)(expected_items / 31);
+	if (gap >= 3) nb /= 3;
+	if (nb <= 0x3ffff) nb = 0x3ffff + 4;
+	for (;; nb++) {
+		int j, ok = 1;
+		for (j = 2; j <= 13; j++) if (nb % j == 0) ok = 0;
+		if (ok) break;
+	}
+	return (uint32_t)nb;
+}
+
+static inline uint32_t b2i(char c) { return c < 'G' ? (c == 'A' ? 0 : 2) : (c == 'G' ? 1 : 3); }
+
+/* LSD radix sort of 64-bit keys, 16-bit digits, skipping constant digits */
+static void radix64(uint64_t *a, uint64_t *tmp, uint64_t n)
+{
+	int pass;
+	uint64_t *cnt = malloc(sizeof(uint64_t) * 65536);
+	for (pass = 0; pass < 4; pass++) {
+		int sh = pass * 16;
+		uint64_t i, s = 0;
+		memset(cnt, 0, sizeof(uint64_t) * 65536);
+		for (i = 0; i < n; i++) cnt[(a[i] >> sh) & 0xffff]++;
+		for (i = 0; i < 65536; i++) if (cnt[i] == n) break;
+		if (i < 65536) continue;   /* digit constant -> already ordered */
+		for (i = 0; i < 65536; i++) { uint64_t c = cnt[i]; cnt[i] = s; s += c; }
+		for (i = 0; i < n; i++) tmp[cnt[(a[i] >> sh) & 0xffff]++] = a[i];
+		memcpy(a, tmp, n * sizeof(uint64_t));
+	}
+	free(cnt);
+}
+
+static int write_all(FILE *fp, const void *p, size_t n) { return fwrite(p, 1, n, fp) == n ? 0 : -1; }
+
+int svg_build_index(const char *fasta, const char *prefix, int gap, int memory_mb, int force_one_block, int repeat_threshold)
+{
+	genome_t g;
+	uint64_t *O = NULL, nwin = 0, i, nkeep = 0;
+	uint64_t *items = NULL, *tmp = NULL;
+	uint32_t c, nb;
+	uint64_t budget;
+	char fn[4096];
+	FILE *fp;
+	int rc = 0;
+	memset(&g, 0, sizeof g);
+	if (!fasta || !prefix || (gap != 1 && gap != 3)) { svg_set_error("svg_build_index: bad argument"); return SVG_E_ARG; }
+	if (repeat_threshold < 1) repeat_threshold = 100;
+	rc = read_fasta(fasta, &g);
+	if (rc) goto out;
+
+	/* 2. coordinates */
+	O = malloc(sizeof(uint64_t) * g.nctg);
+	{
+		uint64_t off = PAD;
+		for (c = 0; c < g.nctg; c++) {
+			O[c] = off;
+			nwin += (g.ctg[c].len - 16) / gap + 1;
+			off += (uint64_t)g.ctg[c].len - 16 + 2 * PAD;
+		}
+		if (O[g.nctg - 1] + g.ctg[g.nctg - 1].len + PAD >= 0xffffffffull) { rc = SVG_E_UNSUPPORTED; svg_set_error("genome too long for 32-bit coordinates"); goto out; }
+	}
+
+	/* 5. bucket count */
+	if (force_one_block) memory_mb = gap == 1 ? 22000 : 11500;
+	else if (memory_mb > 12000 && gap > 2) memory_mb = 12000;
+	budget = (uint32_t)(memory_mb * 1024.0 / 8.) * 1024;
+	nb = svg_bucket_count(budget, gap);
+
+	/* 3+4. windows, sorted by (key, in-run order) */
+	items = malloc(sizeof(uint64_t) * (nwin + 1));
+	tmp = malloc(sizeof(uint64_t) * (nwin + 1));
+	if (!items || !tmp) { rc = SVG_E_NOMEM; svg_set_error("out of memory (%llu windows)", (unsigned long long)nwin); goto out; }
+	{
+		uint64_t w = 0;
+		for (c = 0; c < g.nctg; c++) {
+			const char *b = g.bases + g.ctg[c].start;
+			uint32_t t, nt = (g.ctg[c].len - 16) / gap + 1;
+			for (t = 0; t < nt; t++) {
+				uint32_t key = 0, pos = (uint32_t)(O[c] + (uint64_t)t * gap), pa; int k;
+				for (k = 0; k < 16; k++) key |= b2i(b[(uint64_t)t * gap + k]) << (30 - 2 * k);
+				/* is_1_greater_than_2: equal keys ascending by pos if key%791 even, else descending */
+				pa = ((key % 791) % 2 == 0) ? pos : ~pos;
+				items[w++] = ((uint64_t)key << 32) | pa;
+			}
+		}
+	}
+	radix64(items, tmp, nwin);
+	/* drop keys occurring more than repeat_threshold times */
+	for (i = 0; i < nwin;) {
+		uint64_t j = i;
+		uint32_t key = (uint32_t)(items[i] >> 32);
+		while (j < nwin && (uint32_t)(items[j] >> 32) == key) j++;
+		if (j - i <= (uint64_t)repeat_threshold) {
+			uint64_t k;
+			for (k = i; k < j; k++) items[nkeep++] = items[k];
+		}
+		i = j;
+	}
+	if (!force_one_block && nkeep >= budget) { rc = SVG_E_UNSUPPORTED; svg_set_error("index would need more than one block; use force_one_block"); goto out; }
+	if (nkeep > 0xffffffffull) { rc = SVG_E_UNSUPPORTED; svg_set_error("more than 2^32-1 items"); goto out; }
+
+	/* 6. stable counting sort by bucket (within a bucket, key order == key_hi order) */
+	{
+		uint32_t *bstart = calloc((size_t)nb + 1, sizeof(uint32_t));
+		int16_t *keys = malloc(2 * nkeep + 2);
+		uint32_t *vals = malloc(4 * nkeep + 4);
+		char *buf;
+		size_t bufsz = 1 << 24, bl = 0;
+		if (!bstart || !keys || !vals) { free(bstart); free(keys); free(vals); rc = SVG_E_NOMEM; goto out; }
+		for (i = 0; i < nkeep; i++) bstart[(uint32_t)(items[i] >> 32) % nb + 1]++;
+		for (c = 0; c < nb; c++) bstart[c + 1] += bstart[c];
+		{
+			uint32_t *cur = malloc(sizeof(uint32_t) * nb);
+			memcpy(cur, bstart, sizeof(uint32_t) * nb);
+			for (i = 0; i < nkeep; i++) {
+				uint32_t key = (uint32_t)(items[i] >> 32), pa = (uint32_t)items[i];
+				uint32_t b = key % nb, d = cur[b]++;
+				keys[d] = (int16_t)(key / nb);
+				vals[d] = ((key % 791) % 2 == 0) ? pa : ~pa;
+			}
+			free(cur);
+		}
+		snprintf(fn, sizeof fn, "%s.00.b.tab", prefix);
+		fp = fopen(fn, "wb");
+		if (!fp) { free(bstart); free(keys); free(vals); rc = SVG_E_IO; svg_set_error("cannot write '%s'", fn); goto out; }
+		buf = malloc(bufsz);
+		{
+			int16_t opt[7] = {0x0102, 2, PAD, 0x0101, 2, (int16_t)gap, 0};
+			int64_t nit = (int64_t)nkeep; int32_t nbs = (int32_t)nb;
+			memcpy(buf + bl, "2subindx", 8); bl += 8;
+			memcpy(buf + bl, opt, sizeof opt); bl += sizeof opt;
+			memcpy(buf + bl, &nit, 8); bl += 8;
+			memcpy(buf + bl, &nbs, 4); bl += 4;
+		}
+		for (c = 0; c < nb && !rc; c++) {
+			int32_t n = (int32_t)(bstart[c + 1] - bstart[c]);
+			size_t need = 8 + 6 * (size_t)n;
+			if (bl + need > bufsz) {
+				if (write_all(fp, buf, bl)) rc = SVG_E_IO;
+				bl = 0;
+				if (need > bufsz) { bufsz = need * 2; buf = realloc(buf, bufsz); }
+			}
+			memcpy(buf + bl, &n, 4); memcpy(buf + bl + 4, &n, 4); bl += 8;
+			memcpy(buf + bl, keys + bstart[c], 2 * (size_t)n); bl += 2 * (size_t)n;
+			memcpy(buf + bl, vals + bstart[c], 4 * (size_t)n); bl += 4 * (size_t)n;
+		}
+		buf[bl++] = 0;
+		if (!rc && write_all(fp, buf, bl)) rc = SVG_E_IO;
+		if (fclose(fp)) rc = SVG_E_IO;
+		free(buf); free(bstart); free(keys); free(vals);
+		if (rc) { svg_set_error("write error on '%s'", fn); goto out; }
+	}
+
+	/* 7. .array */
+	{
+		uint32_t last = g.nctg - 1;
+		uint32_t length = (uint32_t)(O[last] + g.ctg[last].len - 16 + 16 + PAD), start = 0;
+		size_t nbytes = (length >> 2) + 1;
+		uint8_t *arr = calloc(nbytes + 8, 1);
+		for (c = 0; c < g.nctg; c++) {
+			const char *b = g.bases + g.ctg[c].start;
+			uint32_t k;
+			for (k = 0; k < g.ctg[c].len; k++) {
+				uint64_t p = O[c] + k;
+				arr[p >> 2] |= (uint8_t)(b2i(b[k]) << (2 * (p & 3)));
+			}
+		}
+		snprintf(fn, sizeof fn, "%s.00.b.array", prefix);
+		fp = fopen(fn, "wb");
+		if (!fp) { free(arr); rc = SVG_E_IO; svg_set_error("cannot write '%s'", fn); goto out; }
+		if (write_all(fp, &start, 4) || write_all(fp, &length, 4) || write_all(fp, arr, nbytes)) rc = SVG_E_IO;
+		fclose(fp);
+		free(arr);
+		if (rc) goto out;
+	}
+
+	/* .reads / .files / .log */
+	snprintf(fn, sizeof fn, "%s.reads", prefix);
+	fp = fopen(fn, "wb");
+	if (!fp) { rc = SVG_E_IO; goto out; }
+	for (c = 0; c < g.nctg; c++) fprintf(fp, "%u\t%s\n", (uint32_t)(O[c] + g.ctg[c].len - 16 + PAD), g.ctg[c].name);
+	fclose(fp);
+	snprintf(fn, sizeof fn, "%s.files", prefix);
+	fp = fopen(fn, "wb");
+	if (fp) { for (c = 0; c < g.nctg; c++) fprintf(fp, "%s\t%s\t0\n", g.ctg[c].name, fasta); fclose(fp); }
+	snprintf(fn, sizeof fn, "%s.log", prefix);
+	fp = fopen(fn, "wb");
+	if (fp) { fprintf(fp, "svg_build_index: %u contigs, %llu windows, %llu items, %u buckets, gap %d\n", g.nctg, (unsigned long long)nwin, (unsigned long long)nkeep, nb, gap); fclose(fp); }
+out:
+	free(items); free(tmp); free(O);
+	free(g.bases); free(g.ctg);
+	return rc;
+}

@@ -1,0 +1,230 @@
+/*
+ * svg_host.c -- host C side of the vote path: error text, parameter defaults,
+ * and the loader that turns the reference's on-disk index into the flat
+ * arrays uploaded to HBM.
+ *
+ *   .tab   gehash_load      sorted-hashtable.c:1390-1625   ("2subindx", option
+ *          TLVs 0x0101 gap / 0x0102 padding, i64 items, i32 nb, then per bucket
+ *          i32 n, i32 space, i16 keys[n], u32 values[n], then u8 is_small)
+ *   .array gvindex_load     gene-value-index.c:190-228
+ *   .reads load_offsets     gene-algorithms.c:1293-1370
+ *
+ * The .tab is mmap'ed; one sequential pass over the bucket headers yields the
+ * bucket offsets, then worker threads copy disjoint bucket ranges.
+ */
+#define _GNU_SOURCE
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdarg.h>
+#include <pthread.h>
+#include <fcntl.h>
+#include <unistd.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include "svg_internal.h"
+
+static __thread char g_err[1024];
+
+void svg_set_error(const char *fmt, ...)
+{
+	va_list ap;
+	va_start(ap, fmt);
+	vsnprintf(g_err, sizeof g_err, fmt, ap);
+	va_end(ap);
+}
+
+const char *svg_last_error(void) { return g_err; }
+int svg_abi_version(void) { return SVG_ABI_VERSION; }
+
+/* init_global_context (core-indel.c:4399-4538) -> parse_opts_* -> load_global_context (core.c:4075-4094) */
+void svg_params_default(svg_params *p, int program, int paired_end)
+{
+	memset(p, 0, sizeof *p);
+	p->total_subreads = 10;
+	p->min_votes_first = 3;
+	p->min_votes_second = 1;
+	p->max_indel_length = 5;
+	p->top_scores = 3;
+	p->min_pair_distance = 50;
+	p->max_pair_distance = 600;
+	p->reverse_r1 = 0;
+	p->reverse_r2 = 1;
+	p->big_margin_record_size = 9;
+	p->maximum_intron_length = 500000;
+	p->prefer_donor_receptor_junctions = 1;
+	p->check_donor_at_junctions = 1;
+	p->max_insertion_at_junctions = 0;
+	if (program == SVG_PROGRAM_SUBJUNC) {          /* core-interface-subjunc.c:268-282 */
+		p->do_breakpoint_detection = 1;
+		p->total_subreads = 14;
+		p->min_votes_first = 1;
+		p->min_votes_second = 1;
+		p->do_big_margin_filtering_for_junctions = 1;
+	}
+	p->more_accurate_fusions = 0;                  /* no fusion/long-del: core-interface-*.c:648/671 */
+	p->max_vote_combinations = 3;                  /* core.c:4075-4084 */
+	p->multi_best = 3;
+	p->max_vote_simples = paired_end ? 64 : 3;
+	p->max_vote_number_cutoff = 2;
+}
+
+/* ------------------------------------------------------------------ index loader */
+typedef struct {
+	const uint8_t *base;
+	const uint64_t *hdr_off;   /* file offset of each bucket header */
+	svg_host_index *ix;
+	uint32_t b0, b1;
+} copy_job;
+
+static void *copy_worker(void *arg)
+{
+	copy_job *j = arg;
+	uint32_t b;
+	for (b = j->b0; b < j->b1; b++) {
+		uint32_t n = j->ix->bstart[b + 1] - j->ix->bstart[b];
+		const uint8_t *h = j->base + j->hdr_off[b] + 8;
+		if (!n) continue;
+		memcpy(j->ix->keys + j->ix->bstart[b], h, 2 * (size_t)n);
+		memcpy(j->ix->vals + j->ix->bstart[b], h + 2 * (size_t)n, 4 * (size_t)n);
+	}
+	return NULL;
+}
+
+void svg_host_index_free(svg_host_index *ix)
+{
+	if (!ix) return;
+	free(ix->bstart); free(ix->keys); free(ix->vals); free(ix->values);
+	free(ix->chr_end); free(ix->chr_name);
+	if (ix->map) munmap(ix->map, ix->map_len);
+	memset(ix, 0, sizeof *ix);
+}
+
+static int load_tab(const char *fn, svg_host_index *ix, int threads)
+{
+	int fd = open(fn, O_RDONLY);
+	struct stat st;
+	const uint8_t *m, *p, *end;
+	uint64_t *hdr = NULL, cur = 0;
+	uint32_t b;
+	if (fd < 0) { svg_set_error("index table '%s' not found", fn); return SVG_E_IO; }
+	if (fstat(fd, &st) || st.st_size < 32) { close(fd); svg_set_error("index table '%s' unreadable", fn); return SVG_E_IO; }
+	ix->map_len = st.st_size;
+	ix->map = mmap(NULL, ix->map_len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+	close(fd);
+	if (ix->map == MAP_FAILED) { ix->map = NULL; svg_set_error("mmap of '%s' failed", fn); return SVG_E_IO; }
+	m = ix->map; end = m + ix->map_len;
+	if (memcmp(m, "2subindx", 8)) { svg_set_error("'%s' is not a v2 subread index (magic)", fn); return SVG_E_FORMAT; }
+	p = m + 8;
+	for (;;) {
+		int16_t k, l;
+		if (p + 2 > end) return SVG_E_FORMAT;
+		memcpy(&k, p, 2); p += 2;
+		if (!k) break;
+		memcpy(&l, p, 2); p += 2;
+		if (k == 0x0101) { int16_t v; memcpy(&v, p, 2); ix->gap = v; }
+		else if (k == 0x0102) { int16_t v; memcpy(&v, p, 2); ix->padding = v; }
+		p += l;
+	}
+	{
+		int64_t items; int32_t nb;
+		memcpy(&items, p, 8); p += 8;
+		memcpy(&nb, p, 4); p += 4;
+		if (items < 1 || (uint64_t)items > 0xffffffffull || nb < 1) { svg_set_error("'%s': bad item/bucket count", fn); return SVG_E_FORMAT; }
+		ix->items = items; ix->nb = nb;
+	}
+	if (ix->gap < 1) { svg_set_error("'%s': no index gap option", fn); return SVG_E_FORMAT; }
+	ix->bstart = malloc(sizeof(uint32_t) * ((size_t)ix->nb + 1));
+	hdr = malloc(sizeof(uint64_t) * ix->nb);
+	ix->keys = malloc(2 * ix->items + 64);
+	ix->vals = malloc(4 * ix->items + 64);
+	if (!ix->bstart || !hdr || !ix->keys || !ix->vals) { free(hdr); svg_set_error("out of host memory loading index"); return SVG_E_NOMEM; }
+	for (b = 0; b < ix->nb; b++) {
+		int32_t n;
+		if (p + 8 > end) { free(hdr); svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT; }
+		memcpy(&n, p, 4);
+		hdr[b] = (uint64_t)(p - m);
+		ix->bstart[b] = (uint32_t)cur;
+		cur += (uint32_t)n;
+		p += 8 + 6 * (size_t)(uint32_t)n;
+	}
+	ix->bstart[ix->nb] = (uint32_t)cur;
+	if (cur != ix->items || p > end) { free(hdr); svg_set_error("'%s': bucket sizes do not add up", fn); return SVG_E_FORMAT; }
+	{
+		int t, nt = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
+		pthread_t th[64];
+		copy_job jb[64];
+		for (t = 0; t < nt; t++) {
+			jb[t].base = m; jb[t].hdr_off = hdr; jb[t].ix = ix;
+			jb[t].b0 = (uint32_t)((uint64_t)ix->nb * t / nt);
+			jb[t].b1 = (uint32_t)((uint64_t)ix->nb * (t + 1) / nt);
+			pthread_create(&th[t], NULL, copy_worker, &jb[t]);
+		}
+		for (t = 0; t < nt; t++) pthread_join(th[t], NULL);
+	}
+	free(hdr);
+	munmap(ix->map, ix->map_len);
+	ix->map = NULL;
+	return 0;
+}
+
+int svg_host_index_load(const char *prefix, svg_host_index *ix, int threads)
+{
+	char fn[4096];
+	FILE *fp;
+	int rc;
+	memset(ix, 0, sizeof *ix);
+	snprintf(fn, sizeof fn, "%s.00.b.tab", prefix);
+	{
+		char fn1[4096];
+		snprintf(fn1, sizeof fn1, "%s.01.b.tab", prefix);
+		if (access(fn1, F_OK) == 0) { svg_set_error("multi-block index '%s' is outside the drop-in contract", prefix); return SVG_E_UNSUPPORTED; }
+	}
+	rc = load_tab(fn, ix, threads);
+	if (rc) { svg_host_index_free(ix); return rc; }
+
+	snprintf(fn, sizeof fn, "%s.00.b.array", prefix);
+	fp = fopen(fn, "rb");
+	if (!fp) { svg_host_index_free(ix); svg_set_error("'%s' not found", fn); return SVG_E_IO; }
+	if (fread(&ix->start_point, 4, 1, fp) != 1 || fread(&ix->length, 4, 1, fp) != 1) {
+		fclose(fp); svg_host_index_free(ix); svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT;
+	}
+	ix->start_base_offset = ix->start_point - ix->start_point % 4;
+	{
+		uint32_t useful = (ix->length + ix->start_point - ix->start_base_offset) >> 2;
+		ix->values_bytes = useful + 1;
+		ix->values = calloc((size_t)ix->values_bytes + 64, 1);
+		if (fread(ix->values, 1, useful + 1, fp) < useful) {
+			fclose(fp); svg_host_index_free(ix); svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT;
+		}
+	}
+	fclose(fp);
+
+	snprintf(fn, sizeof fn, "%s.reads", prefix);
+	fp = fopen(fn, "r");
+	if (!fp) { svg_host_index_free(ix); svg_set_error("'%s' not found", fn); return SVG_E_IO; }
+	{
+		char line[4096];
+		uint32_t cap = 64;
+		ix->chr_end = malloc(4 * cap);
+		ix->chr_name = malloc(sizeof(*ix->chr_name) * cap);
+		while (fgets(line, sizeof line, fp)) {
+			char *tab;
+			size_t L = strlen(line);
+			while (L && (line[L - 1] == '\n' || line[L - 1] == '\r')) line[--L] = 0;
+			if (L < 2) continue;
+			if (ix->n_chr == cap) {
+				cap *= 2;
+				ix->chr_end = realloc(ix->chr_end, 4 * cap);
+				ix->chr_name = realloc(ix->chr_name, sizeof(*ix->chr_name) * cap);
+			}
+			ix->chr_end[ix->n_chr] = (uint32_t)atoll(line);
+			tab = strchr(line, '\t');
+			snprintf(ix->chr_name[ix->n_chr], 200, "%s", tab ? tab + 1 : "");
+			ix->n_chr++;
+		}
+	}
+	fclose(fp);
+	if (!ix->n_chr) { svg_host_index_free(ix); svg_set_error("'%s' is empty", fn); return SVG_E_FORMAT; }
+	return 0;
+}

@@ -1,0 +1,1073 @@
+// svg_vote.hip -- MI355X (gfx950) seed-and-vote kernel + the C ABI of include/subread_vote.h
+//
+// One wavefront (64 lanes) owns one read (SE) or one read pair (PE) at a time
+// and walks the reference's voting step for it:
+//
+//   phase P  (lanes = probes)    every 16-mer of both strands of every end is
+//            packed from the read text in LDS (genekey2int, input-files.c:1232),
+//            hashed to its bucket (key % nb) and binary-searched in HBM exactly
+//            like gehash_go_X (sorted-hashtable.c:947-981); each lane keeps the
+//            search midpoint and the length of the equal-key run on both sides.
+//            All probes of a read are in flight together, so the dependent
+//            HBM chain (bucket bounds -> keys -> run) is paid once per read.
+//   phase G  (lanes = candidates) the hit values of one (strand, end) are
+//            gathered into an LDS queue in the reference's visiting order:
+//            subread_no, then xk1, then mid..last, then mid-1..first
+//            (sorted-hashtable.c:1109-1119).
+//   phase V  (lanes = vote slots) the queue is replayed in order.  For each
+//            candidate the lanes test the <=24 slots of the rows (kv+iix)/5 %30,
+//            iix = 0,+5,-5 (sorted-hashtable.c:995-1001) in parallel; a ballot
+//            finds, in row/slot order, every slot within the indel tolerance,
+//            each matched lane applies its own shift-indel mark and toli
+//            roll-back (sorted-hashtable.c:1021-1039) up to the first slot that
+//            actually takes the vote, and that lane votes (:1041-1068).  With
+//            no taker a new slot is opened in row kv/5 %30 (:1071-1106).
+//   phase K  (lanes = slots / pairs) top-3 distinct vote values, candidate
+//            lists, PE pair scoring and the final <=multi_best records
+//            (process_voting_junction_PE_topK, core-junction.c:2199-2530).
+//
+// The vote table keeps the reference's geometry (30 rows x 24 slots, first
+// match wins, 24-slot cap) so that overflow and tie behaviour are identical.
+// Hot slot state (position + packed votes/last/toli/shift/cursor) lives in LDS;
+// the cold part (coverage start/end, 21-entry indel recorder) lives in a
+// per-wave HBM scratch that stays L2-resident.  Integer work only: no MFMA.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdlib.h>
+#include <stdio.h>
+#include "subread_vote.h"
+#include "svg_internal.h"
+
+#define ROWS 30
+#define SPACE 24
+#define NSLOT (ROWS * SPACE)
+#define REC_LEN 21
+#define COLD_WORDS 8          // per slot: cs|ce<<16, rec[21] as bytes, pad
+#define JCW 17
+
+// ---------------------------------------------------------------------------------------------
+// device-side index
+struct DevIndex {
+	const uint32_t *bstart;   // nb+1
+	const int16_t *keys;
+	const uint32_t *vals;
+	const uint8_t *values;    // .array
+	const uint32_t *chr_end;  // .reads offsets
+	uint32_t nb, n_chr;
+	uint32_t start_point, length, start_base_offset, values_bytes;
+	int32_t gap, padding;
+};
+
+// kernel parameters (passed by value)
+struct KParams {
+	svg_params p;
+	DevIndex ix;
+	const char *seq1, *seq2;
+	const uint64_t *off1, *off2;
+	const uint16_t *len1, *len2;
+	uint64_t n_reads;
+	uint8_t *out;             // mapping records
+	uint8_t *jout;            // subjunc records
+	uint16_t *bm_out;
+	uint32_t *scratch;        // per-wave cold state
+	unsigned long long *stats; // probes, bucket_items, hits, results (may be NULL)
+	int tol, ii_end;
+	uint32_t low, high;
+};
+
+// ---------------------------------------------------------------------------------------------
+// LDS layout of one wave
+template <int ENDS, int MAXL, int MAXP>
+struct WaveLDS {
+	uint32_t pos[ENDS][NSLOT];            // slot positions, [row*24+slot]
+	uint32_t meta[ENDS][NSLOT];           // votes | last<<8 | (toli | shift<<7)<<16 | (u8)cursor<<24
+	uint32_t pmid[ENDS][2][MAXP];         // probe: binary-search midpoint (absolute item index)
+	uint16_t pfwd[ENDS][2][MAXP];         // equal-key items at mid..last
+	uint16_t pbwd[ENDS][2][MAXP];         // equal-key items at first..mid-1
+	uint32_t pcum[MAXP + 1];              // candidate prefix of the (strand,end) being replayed
+	uint32_t cand[512];                   // kv of queued candidates
+	uint8_t cand_p[512];                  // probe index of queued candidates
+	uint32_t res[ENDS][3][17];            // the read's stored mapping_result_t (68 B)
+	uint32_t tmp[ENDS][3][17];            // top-K output under construction
+	uint32_t jres[ENDS][3][4];            // subjunc_result_t
+	uint32_t jtmp[ENDS][3][4];
+	uint32_t simp_pos[ENDS][64];          // simple_mapping_t: position
+	uint16_t simp_slot[ENDS][64];         // slot index, or 0x8000|stored index
+	uint16_t simp_votes[ENDS][64];
+	uint16_t bm[ENDS][10];
+	uint16_t rowstart[ENDS][32];
+	char text[ENDS][2][MAXL];             // strand 0 form / strand 1 (reversed) form
+	uint8_t items[ENDS][32];
+	int32_t max_vote[ENDS];
+	int32_t nshift[ENDS];
+	int32_t comb_i[4], comb_j[4], comb_s[4];
+};
+
+// ---------------------------------------------------------------------------------------------
+// wave helpers
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int lanes_below(unsigned long long m) { return __popcll(m & ((1ull << lane_id()) - 1ull)); }
+__device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
+__device__ __forceinline__ int wave_max(int v)
+{
+	for (int o = 32; o; o >>= 1) { int t = __shfl_xor(v, o); v = t > v ? t : v; }
+	return v;
+}
+__device__ __forceinline__ int wave_min(int v)
+{
+	for (int o = 32; o; o >>= 1) { int t = __shfl_xor(v, o); v = t < v ? t : v; }
+	return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+	for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+	return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+	int l = lane_id();
+	for (int o = 1; o < 64; o <<= 1) { uint32_t t = __shfl_up(v, o); if (l >= o) v += t; }
+	return v;
+}
+
+// base2int, subread.h:238
+__device__ __forceinline__ uint32_t b2i(char c) { return c < 'G' ? (c == 'A' ? 0u : 2u) : (c == 'G' ? 1u : 3u); }
+// reverse_read table, input-files.c:1111 (ASCII; everything else -> 'N')
+__device__ __forceinline__ char comp(char c)
+{
+	return c == 'A' ? 'T' : c == 'C' ? 'G' : c == 'G' ? 'C' : (c == 'T' || c == 'U') ? 'A' : 'N';
+}
+
+// meta packing
+__device__ __forceinline__ int m_votes(uint32_t m) { return m & 0xff; }
+__device__ __forceinline__ int m_last(uint32_t m) { return (m >> 8) & 0xff; }
+__device__ __forceinline__ int m_toli(uint32_t m) { return (m >> 16) & 0x7f; }
+__device__ __forceinline__ int m_shift(uint32_t m) { return (m >> 23) & 1; }
+__device__ __forceinline__ int m_cursor(uint32_t m) { return (int)(int8_t)(m >> 24); }
+__device__ __forceinline__ uint32_t m_pack(int votes, int last, int toli, int shift, int cursor)
+{
+	return (uint32_t)(votes & 0xff) | ((uint32_t)(last & 0xff) << 8) | ((uint32_t)((toli & 0x7f) | (shift << 7)) << 16) |
+	       ((uint32_t)(uint8_t)(int8_t)cursor << 24);
+}
+
+// record field offsets in mapping_result_t (byte offsets)
+#define MR_POS 0
+#define MR_FLAGS 4
+#define MR_VOTES 8
+#define MR_USED 10
+#define MR_NONINF 12
+#define MR_INDELS 13
+#define MR_REC 16
+#define MR_CS 60
+#define MR_CE 62
+
+__device__ __forceinline__ int16_t rec_votes(const uint32_t *r) { return (int16_t)(r[2] & 0xffff); }
+__device__ __forceinline__ uint32_t rec_pos(const uint32_t *r) { return r[0]; }
+__device__ __forceinline__ void rec_set_votes(uint32_t *r, int v) { r[2] = (r[2] & 0xffff0000u) | ((uint32_t)v & 0xffff); }
+__device__ __forceinline__ int rec_used(const uint32_t *r) { return (int16_t)(r[2] >> 16); }
+__device__ __forceinline__ void rec_set_used(uint32_t *r, int v) { r[2] = (r[2] & 0xffffu) | ((uint32_t)v << 16); }
+__device__ __forceinline__ int rec_noninf(const uint32_t *r) { return r[3] & 0xff; }
+__device__ __forceinline__ void rec_set_noninf(uint32_t *r, int v) { r[3] = (r[3] & 0xffffff00u) | ((uint32_t)v & 0xff); }
+__device__ __forceinline__ int rec_cs(const uint32_t *r) { return r[15] & 0xffff; }
+
+// ---------------------------------------------------------------------------------------------
+// cold per-slot state in HBM scratch: word 0 = cs | ce<<16, bytes 4..24 = indel recorder
+__device__ __forceinline__ uint32_t *cold_slot(uint32_t *cold, int slot) { return cold + slot * COLD_WORDS; }
+__device__ __forceinline__ int cold_rec(const uint32_t *cs, int i) { return (int)((const int8_t *)(cs + 1))[i]; }
+__device__ __forceinline__ void cold_set_rec(uint32_t *cs, int i, int v) { ((int8_t *)(cs + 1))[i] = (int8_t)v; }
+
+// ---------------------------------------------------------------------------------------------
+// per-read context (registers, wave-uniform values)
+struct ReadCtx {
+	int rl[2];
+	int applied[2];
+	int step[2];
+	int np[2];          // probes per strand for each end (applied*gap)
+};
+
+template <int ENDS, int MAXL, int MAXP>
+struct Wave {
+	WaveLDS<ENDS, MAXL, MAXP> *L;
+	uint32_t *cold[2];      // [ENDS] cold slot state
+	uint32_t *shift_locs[2];
+	const KParams *kp;
+	ReadCtx rc;
+	unsigned long long st_probes, st_items, st_hits;
+
+	// ---------------------------------------------------------------- probe offset of probe p
+	__device__ __forceinline__ int probe_off(int e, int p) const
+	{
+		int gap = kp->ix.gap;
+		int k = p / gap, x = p - k * gap;
+		int off = (int)(((int64_t)rc.step[e] * k) >> 16);
+		if (gap > 1) off -= off % gap - x;
+		return off;
+	}
+
+	// ---------------------------------------------------------------- phase P: all probes of the read
+	__device__ void probe_all()
+	{
+		const DevIndex &ix = kp->ix;
+		int total = 0;
+		int base[2][2];
+		for (int e = 0; e < ENDS; e++)
+			for (int s = 0; s < 2; s++) { base[e][s] = total; total += (rc.rl[e] >= 16) ? rc.np[e] : 0; }
+		for (int p0 = 0; p0 < total; p0 += 64) {
+			int id = p0 + lane_id();
+			if (id < total) {
+				int e = 0, s = 0;
+				for (int ee = 0; ee < ENDS; ee++)
+					for (int ss = 0; ss < 2; ss++)
+						if (rc.rl[ee] >= 16 && id >= base[ee][ss]) { e = ee; s = ss; }
+				int p = id - base[e][s];
+				int off = probe_off(e, p);
+				const char *t = L->text[e][s] + off;
+				uint32_t key = 0;
+#pragma unroll
+				for (int i = 0; i < 16; i++) key |= b2i(t[i]) << (30 - 2 * i);
+				uint32_t b = key % ix.nb;
+				int16_t k16 = (int16_t)(key / ix.nb);
+				uint32_t first = ix.bstart[b];
+				int n = (int)(ix.bstart[b + 1] - first);
+				uint32_t mid = 0;
+				int fwd = 0, bwd = 0;
+				st_items += n;
+				if (n > 0) {
+					const int16_t *K = ix.keys + first;
+					int lo = 0, hi = n - 1, m;
+					bool hit = false;
+					for (;;) {
+						m = (lo + hi) >> 1;
+						int16_t kk = K[m];
+						if (kk > k16) hi = m - 1;
+						else if (kk < k16) lo = m + 1;
+						else { hit = true; break; }
+						if (hi < lo) break;
+					}
+					if (hit) {
+						mid = first + m;
+						int q = m + 1;
+						while (q < n && K[q] == k16) q++;
+						fwd = q - m;
+						q = m - 1;
+						while (q >= 0 && K[q] == k16) q--;
+						bwd = m - 1 - q;
+					}
+				}
+				L->pmid[e][s][p] = mid;
+				L->pfwd[e][s][p] = (uint16_t)fwd;
+				L->pbwd[e][s][p] = (uint16_t)bwd;
+				st_hits += fwd + bwd;
+			}
+		}
+		st_probes += total;
+		wsync();
+	}
+
+	// ---------------------------------------------------------------- vote-table reset (init_gene_vote)
+	__device__ __forceinline__ void table_reset(int e)
+	{
+		if (lane_id() < 32) L->items[e][lane_id()] = 0;
+		if (lane_id() == 0) L->max_vote[e] = 0;
+		wsync();
+	}
+
+	// ---------------------------------------------------------------- phase V: one candidate
+	__device__ void vote_one(int e, uint32_t kv, int k, int off, int round, uint32_t high_b)
+	{
+		const int lane = lane_id();
+		const int kP1 = k + 1;
+		const int tol = kp->tol;
+		const uint32_t r0 = (kv / 5u) % ROWS;
+		const int n0 = L->items[e][r0];
+		uint32_t *cold = this->cold[e];
+		bool found = false;
+		for (int iix = 0; iix <= kp->ii_end; iix = iix > 0 ? -iix : (-iix + 5)) {
+			uint32_t r = iix ? ((kv + (uint32_t)iix) / 5u) % ROWS : r0;
+			int cnt = iix ? (int)L->items[e][r] : n0;
+			if (!cnt) continue;
+			int slot = (int)r * SPACE + lane;
+			bool valid = lane < cnt;
+			uint32_t P = valid ? L->pos[e][slot] : 0u;
+			uint32_t M = valid ? L->meta[e][slot] : 0u;
+			int d = (int)(kv - P);
+			int sh = m_shift(M);
+			int t = (round > 0 && sh) ? 0 : tol;
+			bool match = valid && d >= -t && d <= t;
+			unsigned long long mm = ballot(match);
+			if (!mm) continue;
+			int votes = m_votes(M), last = m_last(M), tl = m_toli(M), cur = m_cursor(M);
+			bool sev = match && round == 0 && tl > 0 && d == 0 && !sh;
+			bool rb = false;
+			if (match && last == kP1 && tl > 0) {
+				const uint32_t *cs = cold_slot(cold, slot);
+				int md = tl >= 3 ? cold_rec(cs, tl - 1) : 0;
+				int nd = md - d;
+				md -= cold_rec(cs, tl + 2);
+				rb = abs(md) > abs(nd);
+			}
+			int last2 = rb ? last - 1 : last;
+			bool wv = match && !(kP1 <= last2);
+			unsigned long long wm = ballot(wv);
+			int wl = wm ? (__ffsll((long long)wm) - 1) : 64;
+			bool apply = match && lane <= wl;
+			unsigned long long smask = ballot(apply && sev);
+			if (apply && sev) {
+				int at = L->nshift[e] + lanes_below(smask);
+				this->shift_locs[e][at] = P;
+			}
+			if (apply) {
+				int nvotes = votes, nlast = last, ntl = tl, nsh = sh | (sev ? 1 : 0), ncur = cur;
+				if (rb) { ntl -= 3; nlast -= 1; nvotes -= 1; }
+				if (lane == wl) {
+					uint32_t *cs = cold_slot(cold, slot);
+					nvotes += 1;
+					// coverage_end = max(coverage_end, off+16): off rises strictly along the probe
+					// order of a round (step >= gap<<16), so the new value is always off+16
+					((uint16_t *)cs)[1] = (uint16_t)(off + 16);
+					if (d == ncur) cold_set_rec(cs, ntl + 1, kP1);
+					else {
+						int t2 = ntl + 3;
+						if (t2 < REC_LEN) {
+							ntl = t2;
+							cold_set_rec(cs, t2, kP1);
+							cold_set_rec(cs, t2 + 1, kP1);
+							cold_set_rec(cs, t2 + 2, d);
+							if (t2 < REC_LEN - 3) cold_set_rec(cs, t2 + 3, 0);
+						}
+						ncur = (int)(int8_t)d;
+					}
+					nlast = kP1;
+					if (L->max_vote[e] < nvotes) L->max_vote[e] = nvotes;
+				}
+				L->meta[e][slot] = m_pack(nvotes, nlast, ntl, nsh, ncur);
+			}
+			wsync();
+			if (lane == 0) L->nshift[e] += __popcll(smask);
+			wsync();
+			if (wm) { found = true; break; }
+		}
+		if (!found && kv >= kp->low && kv <= high_b && n0 < SPACE) {
+			int sh = 0;
+			if (round > 0) {
+				int ns = L->nshift[e];
+				bool any = false;
+				for (int j = lane; j < ns; j += 64) {
+					uint32_t loc = this->shift_locs[e][j];
+					if (kv >= loc - (uint32_t)tol && kv <= loc + (uint32_t)tol) any = true;
+				}
+				sh = ballot(any) ? 1 : 0;
+			}
+			if (lane == 0) {
+				int slot = (int)r0 * SPACE + n0;
+				uint32_t *cs = cold_slot(cold, slot);
+				L->items[e][r0] = (uint8_t)(n0 + 1);
+				L->pos[e][slot] = kv;
+				L->meta[e][slot] = m_pack(1, kP1, 0, sh, 0);
+				cs[0] = (uint32_t)(uint16_t)off | ((uint32_t)(uint16_t)(off + 16) << 16);
+				cold_set_rec(cs, 0, kP1);
+				cold_set_rec(cs, 1, kP1);
+				cold_set_rec(cs, 2, 0);
+				cold_set_rec(cs, 3, 0);
+				if (L->max_vote[e] == 0) L->max_vote[e] = 1;
+			}
+			wsync();
+		}
+	}
+
+	// ---------------------------------------------------------------- phases G+V for one (strand, end, round)
+	__device__ void replay(int e, int s, int round)
+	{
+		const int lane = lane_id();
+		const int np = rc.np[e];
+		const int gap = kp->ix.gap;
+		const uint32_t high_b = kp->high - (uint32_t)rc.rl[e];
+		// candidate prefix over probes (probe order = subread_no, xk1)
+		uint32_t total = 0;
+		for (int p0 = 0; p0 < np; p0 += 64) {
+			int p = p0 + lane;
+			uint32_t h = p < np ? (uint32_t)L->pfwd[e][s][p] + L->pbwd[e][s][p] : 0u;
+			uint32_t inc = wave_incl_scan(h);
+			if (p < np) L->pcum[p + 1] = total + inc;
+			total += __shfl(inc, 63);
+		}
+		if (lane == 0) L->pcum[0] = 0;
+		wsync();
+		for (uint32_t c0 = 0; c0 < total; c0 += 512) {
+			uint32_t cn = total - c0 < 512 ? total - c0 : 512;
+			// gather
+			for (uint32_t c = lane; c < cn; c += 64) {
+				uint32_t cc = c0 + c;
+				int lo = 0, hi = np - 1;   // find probe p with pcum[p] <= cc < pcum[p+1]
+				while (lo < hi) { int m = (lo + hi + 1) >> 1; if (L->pcum[m] <= cc) lo = m; else hi = m - 1; }
+				int p = lo;
+				uint32_t j = cc - L->pcum[p];
+				uint32_t fwd = L->pfwd[e][s][p];
+				uint32_t mid = L->pmid[e][s][p];
+				uint32_t item = j < fwd ? mid + j : mid - 1 - (j - fwd);
+				uint32_t off = (uint32_t)probe_off(e, p);
+				L->cand[c] = kp->ix.vals[item] - off;
+				L->cand_p[c] = (uint8_t)p;
+			}
+			wsync();
+			for (uint32_t c = 0; c < cn; c++) {
+				uint32_t kv = L->cand[c];
+				int p = L->cand_p[c];
+				int k = p / gap;
+				vote_one(e, kv, k, probe_off(e, p), round, high_b);
+			}
+			wsync();
+		}
+	}
+
+	// ---------------------------------------------------------------- record helpers
+	__device__ void rec_zero(uint32_t *r) { if (lane_id() < 17) r[lane_id()] = 0; }
+
+	// copy_vote_to_alignment_res (core-junction.c:1058-1071) for slot -> tmp record r
+	__device__ void copy_vote(int e, int slot, uint32_t *r)
+	{
+		const int lane = lane_id();
+		const uint32_t *cs = cold_slot(cold[e], slot);
+		// indel_recorder_copy (sorted-hashtable.c:1144): triples while rec[3t] != 0 and 3t < 19
+		int v = lane < REC_LEN ? cold_rec(cs, lane) : 0;
+		unsigned long long z = ballot(lane < 21 && (lane % 3) == 0 && (v == 0 || lane >= 19));
+		int T = z ? (__ffsll((long long)z) - 1) / 3 : 7;   // number of triples copied
+		int nrec = 3 * T;
+		int last_ind = __shfl(v, nrec > 0 ? nrec - 1 : 0);
+		int16_t rv = lane < nrec ? (int16_t)v : (int16_t)0;
+		// records are zeroed before; write the 22 shorts of selected_indel_record as 11 dwords
+		int16_t rv_hi = __shfl(rv, (2 * lane + 1) & 63);
+		int16_t rv_lo = __shfl(rv, (2 * lane) & 63);
+		if (lane < 11) r[MR_REC / 4 + lane] = (uint32_t)(uint16_t)rv_lo | ((uint32_t)(uint16_t)rv_hi << 16);
+		if (lane == 0) {
+			uint32_t M = L->meta[e][slot];
+			uint32_t cw = cs[0];
+			int negative = 0;   // masks: every slot of a (strand) table carries that strand
+			r[0] = L->pos[e][slot];
+			(void)negative;
+			r[2] = (uint32_t)(uint16_t)m_votes(M) | ((uint32_t)(uint16_t)rc.applied[e] << 16);
+			r[3] = (uint32_t)(uint8_t)(int8_t)(nrec > 0 ? last_ind : 0) << 8;   // noninf 0, indels
+			r[15] = cw;   // confident_coverage_start | confident_coverage_end << 16
+			r[16] = 0;
+		}
+	}
+
+	// locate_gene_position_max(..., NULL, NULL, rl = 0), gene-algorithms.c:441-511
+	__device__ int locate(uint32_t linear, int *chr, int *pos) const
+	{
+		const uint32_t *ce = kp->ix.chr_end;
+		int ntot = (int)kp->ix.n_chr, lo = 0, hi = ntot, n;
+		*chr = -1; *pos = -1;
+		for (;;) {
+			if (hi <= lo + 1) { n = lo - 2 > 0 ? lo - 2 : 0; break; }
+			int mid = (lo + hi) / 2;
+			if (ce[mid] > linear) hi = mid; else lo = mid + 1;
+		}
+		for (; n < ntot; n++) {
+			if (ce[n] > linear) {
+				*pos = n == 0 ? (int)linear : (int)(linear - ce[n - 1]);
+				if (linear > ce[n] + 15u - (uint32_t)kp->ix.padding) return 1;
+				if (*pos < kp->ix.padding) return 1;
+				*pos -= kp->ix.padding;
+				*chr = n;
+				return 0;
+			}
+		}
+		return -1;
+	}
+
+	// ---------------------------------------------------------------- phase K
+	__device__ void topk(int strand)
+	{
+		const svg_params &p = kp->p;
+		const int lane = lane_id();
+		int top[2][3] = {{0, 0, 0}, {0, 0, 0}};
+		int nsimp[2] = {0, 0};
+		const int TS = p.top_scores;   // 3 (validated on the host)
+		for (int e = 0; e < ENDS; e++) {
+			// row prefix of used slots
+			int it = lane < ROWS ? L->items[e][lane] : 0;
+			int inc = (int)wave_incl_scan((uint32_t)it);
+			if (lane < ROWS) L->rowstart[e][lane + 1] = (uint16_t)inc;
+			if (lane == 0) L->rowstart[e][0] = 0;
+		}
+		wsync();
+		for (int e = 0; e < ENDS; e++) {
+			int U = L->rowstart[e][ROWS];
+			// top-3 distinct over table votes and stored results (update_top_three)
+			int bound = 0x7fffffff;
+			for (int t = 0; t < TS; t++) {
+				int best = 0;
+				for (int f0 = 0; f0 < U; f0 += 64) {
+					int f = f0 + lane;
+					if (f < U) {
+						int r = 0;
+						while (L->rowstart[e][r + 1] <= f) r++;
+						int v = m_votes(L->meta[e][r * SPACE + (f - L->rowstart[e][r])]);
+						if (v < bound && v > best) best = v;
+					}
+				}
+				if (lane < p.multi_best) {
+					int v = rec_votes(L->res[e][lane]);
+					if (v > 0 && v < bound && v > best) best = v;
+				}
+				best = wave_max(best);
+				top[e][t] = best;
+				bound = best > 0 ? best : 0;
+				if (best == 0) bound = 0;
+			}
+		}
+		// candidate lists (simples)
+		for (int e = 0; e < ENDS; e++) {
+			int U = L->rowstart[e][ROWS];
+			int ns = 0;
+			for (int t = 0; t < TS; t++) {
+				int N = top[e][t];
+				if (ns >= p.max_vote_simples) break;
+				if (N < 1 || (top[e][0] - N > p.max_vote_number_cutoff)) break;
+				for (int f0 = 0; f0 < U && ns < p.max_vote_simples; f0 += 64) {
+					int f = f0 + lane;
+					int slot = 0, v = -1;
+					if (f < U) {
+						int r = 0;
+						while (L->rowstart[e][r + 1] <= f) r++;
+						slot = r * SPACE + (f - L->rowstart[e][r]);
+						v = m_votes(L->meta[e][slot]);
+					}
+					bool sel = f < U && v == N && v >= p.min_votes_second;
+					unsigned long long sm = ballot(sel);
+					int at = ns + lanes_below(sm);
+					if (sel && at < p.max_vote_simples) {
+						L->simp_pos[e][at] = L->pos[e][slot];
+						L->simp_slot[e][at] = (uint16_t)slot;
+						L->simp_votes[e][at] = (uint16_t)v;
+					}
+					ns += __popcll(sm);
+					if (ns > p.max_vote_simples) ns = p.max_vote_simples;
+				}
+				for (int i = 0; i < p.multi_best; i++) {
+					if (ns >= p.max_vote_simples) break;
+					if (rec_votes(L->res[e][i]) == N) {
+						if (lane == 0) {
+							L->simp_pos[e][ns] = rec_pos(L->res[e][i]);
+							L->simp_slot[e][ns] = (uint16_t)(0x8000 | i);
+							L->simp_votes[e][ns] = (uint16_t)N;
+						}
+						ns++;
+					}
+				}
+			}
+			nsimp[e] = ns;
+		}
+		wsync();
+		// tmp records
+		for (int e = 0; e < ENDS; e++)
+			for (int i = 0; i < 3; i++) rec_zero(L->tmp[e][i]);
+		wsync();
+		int cur[2] = {0, 0};
+		int ncomb = 0;
+		if (ENDS == 2) {
+			// all valid pairs, keep the first 3 by (score desc, pair order asc)
+			int n0 = nsimp[0], n1 = nsimp[1];
+			int npairs = n0 * n1;
+			int bs[3] = {-1, -1, -1}, bidx[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff};
+			for (int q0 = 0; q0 < npairs; q0 += 64) {
+				int q = q0 + lane;
+				int sc = -1;
+				if (q < npairs) {
+					int i = q / n1, j = q - i * n1;
+					int va = L->simp_votes[0][i], vb = L->simp_votes[1][j];
+					int mx = va > vb ? va : vb, mn = va < vb ? va : vb;
+					if (mx >= p.min_votes_first) {
+						int c1, c2, q1, q2, pe = 0, same = 0;
+						int e1 = locate(L->simp_pos[0][i], &c1, &q1), e2 = locate(L->simp_pos[1][j], &c2, &q2);
+						if (e1 == 0 && e2 == 0) {
+							long long tlen = (long long)q1 - q2;
+							tlen = abs((int)tlen);
+							tlen += (q1 > q2) ? rc.rl[0] : rc.rl[1];
+							uint32_t tli = (uint32_t)tlen;
+							if (c1 == c2) {
+								same = 1;
+								if (tli >= (uint32_t)p.min_pair_distance && tli <= (uint32_t)p.max_pair_distance) pe = 1;
+							}
+						}
+						if (pe || mn >= p.min_votes_first) sc = (va + vb) * (pe ? 1300 : (same ? 1000 : 800));
+					}
+				}
+				// merge lane candidates into the running top-3
+				for (int r = 0; r < 3; r++) {
+					int m = wave_max(sc);
+					if (m < 0) break;
+					int qi = wave_min(sc == m ? q : 0x7fffffff);
+					// insert (m, qi) into bs/bidx ordered by score desc, index asc
+					int pos3 = 3;
+					for (int t = 0; t < 3; t++) {
+						if (bs[t] < m || (bs[t] == m && bidx[t] > qi)) { pos3 = t; break; }
+					}
+					if (pos3 < 3) {
+						for (int t = 2; t > pos3; t--) { bs[t] = bs[t - 1]; bidx[t] = bidx[t - 1]; }
+						bs[pos3] = m; bidx[pos3] = qi;
+					}
+					if (q == qi) sc = -1;
+				}
+			}
+			for (int t = 0; t < 3 && t < p.max_vote_combinations; t++)
+				if (bs[t] >= 0) ncomb++;
+			int ci[3], cj[3], cs3[3];
+			for (int t = 0; t < ncomb; t++) { ci[t] = bidx[t] / n1; cj[t] = bidx[t] % n1; cs3[t] = bs[t]; }
+			// merge_sort -> selection sort ascending by score (core.c:4716-4729), unstable
+			for (int i = 0; i < ncomb - 1; i++) {
+				int mj = i;
+				for (int j = i + 1; j < ncomb; j++) if (cs3[mj] - cs3[j] > 0) mj = j;
+				if (i != mj) {
+					int t1 = ci[i], t2 = cj[i], t3 = cs3[i];
+					ci[i] = ci[mj]; cj[i] = cj[mj]; cs3[i] = cs3[mj];
+					ci[mj] = t1; cj[mj] = t2; cs3[mj] = t3;
+				}
+			}
+			if (ncomb > 0) {
+				for (int e = 0; e < 2; e++) {
+					for (int i = ncomb - 1; i >= 0; i--) {
+						if (cur[e] >= p.multi_best) break;
+						int si = e ? cj[i] : ci[i];
+						uint32_t ps = L->simp_pos[e][si];
+						bool ex = false;
+						for (int j = 0; j < cur[e]; j++) if (rec_pos(L->tmp[e][j]) == ps) ex = true;
+						if (ex) continue;
+						emit(e, si, cur[e]);
+						cur[e]++;
+					}
+				}
+			}
+		}
+		if (ncomb == 0) {
+			if (nsimp[0] == 0 && lane == 0) rec_set_noninf(L->res[0][0], 0);
+			if (ENDS == 2 && nsimp[ENDS - 1] == 0 && lane == 0) rec_set_noninf(L->res[ENDS - 1][0], 0);
+			wsync();
+			for (int e = 0; e < ENDS; e++)
+				for (int i = 0; i < nsimp[e]; i++) {
+					if (cur[e] >= p.multi_best) break;
+					if ((int)L->simp_votes[e][i] < p.min_votes_first) continue;
+					uint32_t ps = L->simp_pos[e][i];
+					bool ex = false;
+					for (int j = 0; j < cur[e]; j++) if (rec_pos(L->tmp[e][j]) == ps) ex = true;
+					if (ex) continue;
+					emit(e, i, cur[e]);
+					cur[e]++;
+				}
+		}
+		wsync();
+		for (int e = 0; e < ENDS; e++)
+			for (int i = 0; i < p.multi_best; i++) {
+				if (i < cur[e]) { if (lane < 17) L->res[e][i][lane] = L->tmp[e][i][lane]; }
+				else if (lane == 0) rec_set_votes(L->res[e][i], 0);
+			}
+		wsync();
+	}
+
+	// write simple si of end e as tmp record slot c
+	__device__ void emit(int e, int si, int c)
+	{
+		int sl = L->simp_slot[e][si];
+		if (sl & 0x8000) {
+			if (lane_id() < 17) L->tmp[e][c][lane_id()] = L->res[e][sl & 3][lane_id()];
+		} else {
+			copy_vote(e, sl, L->tmp[e][c]);
+			if (lane_id() == 0) {
+				// result_flags: IS_NEGATIVE_STRAND mask of the slot (the table's strand)
+				L->tmp[e][c][1] = cur_strand ? (uint32_t)SVG_NEGATIVE_STRAND_FLAG : 0u;
+			}
+		}
+		wsync();
+	}
+
+	int cur_strand;
+
+	// ---------------------------------------------------------------- one read
+	__device__ void run_read(uint64_t r)
+	{
+		const svg_params &p = kp->p;
+		const int lane = lane_id();
+		const int gap = kp->ix.gap;
+		// load text (fetch_next_read_pair: -S reversal), both strands
+		for (int e = 0; e < ENDS; e++) {
+			const char *seq = e ? kp->seq2 : kp->seq1;
+			uint64_t o = e ? kp->off2[r] : kp->off1[r];
+			int len = e ? kp->len2[r] : kp->len1[r];
+			int rev = e ? p.reverse_r2 : p.reverse_r1;
+			rc.rl[e] = len;
+			for (int i = lane; i < len; i += 64) {
+				char c = seq[o + i];
+				char c2 = seq[o + (len - 1 - i)];
+				char s0 = rev ? comp(c2) : c;
+				char s1 = rev ? comp(comp(c)) : comp(c2);
+				L->text[e][0][i] = s0;
+				L->text[e][1][i] = s1;
+			}
+			if (len >= 16) {
+				int cr = (len - 15 - gap) << 16, step;
+				if (len <= 160) {
+					step = cr / (p.total_subreads - 1);
+					if (step < (gap << 16)) step = gap << 16;
+				} else {
+					step = 6 << 16;
+					if (cr / step > 62) step = cr / 62;
+				}
+				rc.step[e] = step;
+				rc.applied[e] = 1 + cr / step;
+				rc.np[e] = rc.applied[e] * gap;
+			} else {
+				rc.step[e] = 0; rc.applied[e] = 0; rc.np[e] = 0;
+			}
+		}
+		for (int e = 0; e < ENDS; e++) {
+			for (int i = 0; i < 3; i++) rec_zero(L->res[e][i]);
+			if (lane < 12) L->jres[e][lane / 4][lane % 4] = 0;
+			if (lane < 10) L->bm[e][lane] = 0;
+		}
+		wsync();
+		probe_all();
+		for (int strand = 0; strand < 2; strand++) {
+			cur_strand = strand;
+			for (int e = 0; e < ENDS; e++) {
+				if (lane == 0) L->nshift[e] = 0;
+				wsync();
+				if (rc.rl[e] < 16) { table_reset(e); continue; }
+				for (int round = 0; round < 2; round++) {
+					table_reset(e);
+					replay(e, strand, round);
+					if (L->nshift[e] == 0) break;
+				}
+			}
+			if (ENDS == 2) topk(strand);
+			else if (L->max_vote[0] >= p.min_votes_first) topk(strand);
+			else if (rec_votes(L->res[0][0]) < 1) {
+				if (lane == 0) {
+					uint32_t *r0 = L->res[0][0];
+					rec_set_noninf(r0, 0);
+					if (rc.applied[0] > rec_used(r0)) rec_set_used(r0, rc.applied[0]);
+				}
+				wsync();
+			}
+		}
+		// write the read's records
+		for (int e = 0; e < ENDS; e++) {
+			uint32_t *dst = (uint32_t *)(kp->out + ((r * ENDS + e) * (uint64_t)p.multi_best) * 68);
+			for (int w = lane; w < 17 * p.multi_best; w += 64) dst[w] = L->res[e][w / 17][w % 17];
+		}
+		if (kp->stats) {
+			int nres = 0;
+			for (int e = 0; e < ENDS; e++)
+				for (int i = 0; i < p.multi_best; i++) nres += rec_votes(L->res[e][i]) > 0;
+			if (lane == 0) atomicAdd(&kp->stats[3], (unsigned long long)nres);
+		}
+		wsync();
+	}
+};
+
+template <int ENDS, int MAXL, int MAXP, int WPB>
+__global__ void __launch_bounds__(64 * WPB) vote_kernel(KParams kp)
+{
+	extern __shared__ __align__(16) uint8_t lds_raw[];
+	typedef WaveLDS<ENDS, MAXL, MAXP> LT;
+	const int wib = threadIdx.x >> 6;
+	const uint64_t gw = (uint64_t)blockIdx.x * WPB + wib;
+	const uint64_t nw = (uint64_t)gridDim.x * WPB;
+	Wave<ENDS, MAXL, MAXP> W;
+	W.L = reinterpret_cast<LT *>(lds_raw + (size_t)wib * ((sizeof(LT) + 15) & ~(size_t)15));
+	W.kp = &kp;
+	const size_t per_end = (size_t)NSLOT * COLD_WORDS + NSLOT;   // cold + shift_locs
+	uint32_t *base = kp.scratch + gw * per_end * ENDS;
+	for (int e = 0; e < ENDS; e++) {
+		W.cold[e] = base + e * per_end;
+		W.shift_locs[e] = base + e * per_end + (size_t)NSLOT * COLD_WORDS;
+	}
+	W.st_probes = W.st_items = W.st_hits = 0;
+	for (uint64_t r = gw; r < kp.n_reads; r += nw) W.run_read(r);
+	if (kp.stats) {
+		unsigned long long a = W.st_items, h = W.st_hits;
+		for (int o = 32; o; o >>= 1) { a += __shfl_xor(a, o); h += __shfl_xor(h, o); }
+		if (lane_id() == 0) {
+			atomicAdd(&kp.stats[0], W.st_probes);
+			atomicAdd(&kp.stats[1], a);
+			atomicAdd(&kp.stats[2], h);
+		}
+	}
+}
+
+// =============================================================================================
+// host side: handle, upload, launch
+// =============================================================================================
+struct svg_index {
+	int device;
+	hipStream_t stream;
+	svg_host_index host;
+	DevIndex dix;
+	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr;
+	uint32_t *d_scratch;
+	size_t scratch_words;
+	unsigned long long *d_stats;
+	int stats_on;
+	svg_batch_stats last_stats;
+	uint64_t device_bytes;
+	int n_cu;
+	// staging for svg_vote_batch (host buffers)
+	void *d_in; size_t d_in_cap;
+	void *d_out; size_t d_out_cap;
+};
+
+#define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) { svg_set_error("HIP error %s at %s:%d", hipGetErrorString(_e), __FILE__, __LINE__); return SVG_E_DEVICE; } } while (0)
+
+static int dmalloc(svg_index *h, void **p, size_t n)
+{
+	hipError_t e = hipMalloc(p, n ? n : 16);
+	if (e != hipSuccess) { svg_set_error("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e)); return SVG_E_NOMEM; }
+	h->device_bytes += n;
+	return 0;
+}
+
+extern "C" int svg_index_open(const char *prefix, int device, svg_index **out)
+{
+	if (!prefix || !out) { svg_set_error("svg_index_open: NULL argument"); return SVG_E_ARG; }
+	*out = NULL;
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { svg_set_error("no HIP device visible"); return SVG_E_DEVICE; }
+	if (device < 0 || device >= ndev) { svg_set_error("device %d out of range (%d visible)", device, ndev); return SVG_E_ARG; }
+	HIPCHK(hipSetDevice(device));
+	svg_index *h = (svg_index *)calloc(1, sizeof(svg_index));
+	h->device = device;
+	int rc = svg_host_index_load(prefix, &h->host, 16);
+	if (rc) { free(h); return rc; }
+	svg_host_index *x = &h->host;
+	if ((rc = dmalloc(h, &h->d_bstart, 4 * ((size_t)x->nb + 1))) || (rc = dmalloc(h, &h->d_keys, 2 * x->items + 64)) ||
+	    (rc = dmalloc(h, &h->d_vals, 4 * x->items + 64)) || (rc = dmalloc(h, &h->d_values, (size_t)x->values_bytes + 64)) ||
+	    (rc = dmalloc(h, &h->d_chr, 4 * (size_t)x->n_chr + 64))) {
+		svg_index_close(h);
+		return rc;
+	}
+	HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+	HIPCHK(hipMemcpy(h->d_bstart, x->bstart, 4 * ((size_t)x->nb + 1), hipMemcpyHostToDevice));
+	HIPCHK(hipMemcpy(h->d_keys, x->keys, 2 * x->items, hipMemcpyHostToDevice));
+	HIPCHK(hipMemcpy(h->d_vals, x->vals, 4 * x->items, hipMemcpyHostToDevice));
+	HIPCHK(hipMemcpy(h->d_values, x->values, x->values_bytes, hipMemcpyHostToDevice));
+	HIPCHK(hipMemcpy(h->d_chr, x->chr_end, 4 * (size_t)x->n_chr, hipMemcpyHostToDevice));
+	// the flat key/value arrays now live in HBM; keep only the small host parts
+	free(x->bstart); x->bstart = NULL;
+	free(x->keys); x->keys = NULL;
+	free(x->vals); x->vals = NULL;
+	h->dix.bstart = (const uint32_t *)h->d_bstart;
+	h->dix.keys = (const int16_t *)h->d_keys;
+	h->dix.vals = (const uint32_t *)h->d_vals;
+	h->dix.values = (const uint8_t *)h->d_values;
+	h->dix.chr_end = (const uint32_t *)h->d_chr;
+	h->dix.nb = x->nb;
+	h->dix.n_chr = x->n_chr;
+	h->dix.start_point = x->start_point;
+	h->dix.length = x->length;
+	h->dix.start_base_offset = x->start_base_offset;
+	h->dix.values_bytes = x->values_bytes;
+	h->dix.gap = x->gap;
+	h->dix.padding = x->padding;
+	hipDeviceProp_t prop;
+	HIPCHK(hipGetDeviceProperties(&prop, device));
+	h->n_cu = prop.multiProcessorCount;
+	if ((rc = dmalloc(h, (void **)&h->d_stats, 8 * sizeof(unsigned long long)))) { svg_index_close(h); return rc; }
+	const char *se = getenv("SVG_STATS");
+	h->stats_on = se && se[0] == '1';
+	*out = h;
+	return 0;
+}
+
+extern "C" void svg_index_close(svg_index *h)
+{
+	if (!h) return;
+	hipSetDevice(h->device);
+	if (h->stream) hipStreamSynchronize(h->stream);
+	hipFree(h->d_bstart); hipFree(h->d_keys); hipFree(h->d_vals); hipFree(h->d_values); hipFree(h->d_chr);
+	hipFree(h->d_scratch); hipFree(h->d_stats); hipFree(h->d_in); hipFree(h->d_out);
+	if (h->stream) hipStreamDestroy(h->stream);
+	svg_host_index_free(&h->host);
+	free(h);
+}
+
+extern "C" int svg_index_get_info(const svg_index *h, svg_index_info *o)
+{
+	if (!h || !o) { svg_set_error("svg_index_get_info: NULL argument"); return SVG_E_ARG; }
+	o->items = h->host.items;
+	o->buckets = h->host.nb;
+	o->index_gap = h->host.gap;
+	o->padding = h->host.padding;
+	o->array_length = h->host.length;
+	o->n_chromosomes = h->host.n_chr;
+	o->device_bytes = h->device_bytes;
+	o->device = h->device;
+	return 0;
+}
+
+extern "C" int svg_set_stats(svg_index *h, int enable)
+{
+	if (!h) return SVG_E_ARG;
+	h->stats_on = enable ? 1 : 0;
+	return 0;
+}
+
+extern "C" int svg_get_stats(const svg_index *h, svg_batch_stats *o)
+{
+	if (!h || !o) return SVG_E_ARG;
+	*o = h->last_stats;
+	return 0;
+}
+
+static int check_params(const svg_index *h, const svg_params *p)
+{
+	if (p->multi_best < 1 || p->multi_best > 3) { svg_set_error("multi_best must be 1..3"); return SVG_E_UNSUPPORTED; }
+	if (p->top_scores != 3) { svg_set_error("top_scores must be 3 (reference runtime value)"); return SVG_E_UNSUPPORTED; }
+	if (p->max_vote_combinations < 1 || p->max_vote_combinations > 3) { svg_set_error("max_vote_combinations must be 1..3"); return SVG_E_UNSUPPORTED; }
+	if (p->max_vote_simples < 1 || p->max_vote_simples > 64) { svg_set_error("max_vote_simples must be 1..64"); return SVG_E_UNSUPPORTED; }
+	if (p->total_subreads < 2 || p->total_subreads > 64) { svg_set_error("total_subreads must be 2..64"); return SVG_E_UNSUPPORTED; }
+	if (p->max_indel_length < 0) { svg_set_error("max_indel_length < 0"); return SVG_E_ARG; }
+	if (p->do_breakpoint_detection) { svg_set_error("subjunc mode is not available in this build"); return SVG_E_UNSUPPORTED; }
+	(void)h;
+	return 0;
+}
+
+template <int ENDS, int MAXL, int MAXP, int WPB>
+static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
+{
+	typedef WaveLDS<ENDS, MAXL, MAXP> LT;
+	size_t lds = (size_t)WPB * ((sizeof(LT) + 15) & ~(size_t)15);
+	int per_cu = (int)(160 * 1024 / lds);
+	if (per_cu < 1) { svg_set_error("kernel LDS too large"); return SVG_E_DEVICE; }
+	if (per_cu > 16) per_cu = 16;
+	uint64_t blocks = (uint64_t)h->n_cu * per_cu;
+	uint64_t need = (kp.n_reads + WPB - 1) / WPB;
+	if (blocks > need) blocks = need;
+	if (blocks < 1) blocks = 1;
+	size_t per_end = (size_t)NSLOT * COLD_WORDS + NSLOT;
+	size_t words = blocks * WPB * ENDS * per_end;
+	if (words > h->scratch_words) {
+		hipFree(h->d_scratch);
+		h->d_scratch = NULL;
+		h->scratch_words = 0;
+		if (dmalloc(h, (void **)&h->d_scratch, words * 4)) return SVG_E_NOMEM;
+		h->scratch_words = words;
+	}
+	kp.scratch = h->d_scratch;
+	hipLaunchKernelGGL((vote_kernel<ENDS, MAXL, MAXP, WPB>), dim3((unsigned)blocks), dim3(64 * WPB), lds, st, kp);
+	HIPCHK(hipGetLastError());
+	return 0;
+}
+
+extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                                     svg_mapping_result *out, svg_subjunc_result *jout, uint16_t *big_margin, void *stream)
+{
+	if (!h || !p || !r1 || !out) { svg_set_error("svg_vote_batch_device: NULL argument"); return SVG_E_ARG; }
+	if (r2 && r2->n_reads != r1->n_reads) { svg_set_error("R1/R2 read counts differ"); return SVG_E_ARG; }
+	int rc = check_params(h, p);
+	if (rc) return rc;
+	HIPCHK(hipSetDevice(h->device));
+	hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+	if (r1->n_reads == 0) return 0;
+	KParams kp;
+	memset(&kp, 0, sizeof kp);
+	kp.p = *p;
+	kp.ix = h->dix;
+	kp.seq1 = r1->seq; kp.off1 = r1->offsets; kp.len1 = r1->lens;
+	if (r2) { kp.seq2 = r2->seq; kp.off2 = r2->offsets; kp.len2 = r2->lens; }
+	kp.n_reads = r1->n_reads;
+	kp.out = (uint8_t *)out;
+	kp.jout = (uint8_t *)jout;
+	kp.bm_out = big_margin;
+	kp.tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
+	kp.ii_end = 5;
+	if (kp.tol > 5) kp.ii_end = (kp.tol % 5) ? (kp.tol - kp.tol % 5 + 5) : kp.tol;
+	kp.low = h->dix.start_base_offset;
+	kp.high = h->dix.start_base_offset + h->dix.length;
+	if (h->stats_on) {
+		HIPCHK(hipMemsetAsync(h->d_stats, 0, 8 * sizeof(unsigned long long), st));
+		kp.stats = h->d_stats;
+	}
+	if (r2) rc = launch_t<2, 256, 64, 2>(h, kp, st);
+	else rc = launch_t<1, 256, 64, 2>(h, kp, st);
+	if (rc) return rc;
+	if (h->stats_on) {
+		unsigned long long s[4];
+		HIPCHK(hipMemcpyAsync(s, h->d_stats, sizeof s, hipMemcpyDeviceToHost, st));
+		HIPCHK(hipStreamSynchronize(st));
+		h->last_stats.probes = s[0];
+		h->last_stats.bucket_items = s[1];
+		h->last_stats.hits = s[2];
+		h->last_stats.results = s[3];
+	}
+	return 0;
+}
+
+static int ensure(svg_index *h, void **p, size_t *cap, size_t need)
+{
+	if (need <= *cap) return 0;
+	hipFree(*p);
+	*p = NULL;
+	*cap = 0;
+	if (dmalloc(h, p, need)) return SVG_E_NOMEM;
+	*cap = need;
+	return 0;
+}
+
+// host buffers in/out: stage through HBM
+extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                              svg_mapping_result *out, svg_subjunc_result *jout, uint16_t *big_margin)
+{
+	if (!h || !p || !r1 || !out) { svg_set_error("svg_vote_batch: NULL argument"); return SVG_E_ARG; }
+	if (r2 && r2->n_reads != r1->n_reads) { svg_set_error("R1/R2 read counts differ"); return SVG_E_ARG; }
+	int rc = check_params(h, p);
+	if (rc) return rc;
+	uint64_t n = r1->n_reads;
+	if (!n) return 0;
+	int ends = r2 ? 2 : 1;
+	HIPCHK(hipSetDevice(h->device));
+	// total sequence span per end
+	uint64_t span[2] = {0, 0}, lo[2] = {0, 0};
+	for (int e = 0; e < ends; e++) {
+		const svg_reads *rr = e ? r2 : r1;
+		uint64_t mn = ~0ull, mx = 0;
+		for (uint64_t i = 0; i < n; i++) {
+			if (rr->lens[i] > 256) { svg_set_error("read %llu longer than 256 bases (long-read kernel not built)", (unsigned long long)i); return SVG_E_UNSUPPORTED; }
+			if (rr->offsets[i] < mn) mn = rr->offsets[i];
+			if (rr->offsets[i] + rr->lens[i] > mx) mx = rr->offsets[i] + rr->lens[i];
+		}
+		lo[e] = mn; span[e] = mx - mn;
+	}
+	size_t in_bytes = 0, o_seq[2], o_off[2], o_len[2];
+	for (int e = 0; e < ends; e++) {
+		o_seq[e] = in_bytes; in_bytes += (span[e] + 15) & ~15ull;
+		o_off[e] = in_bytes; in_bytes += 8 * n;
+		o_len[e] = in_bytes; in_bytes += (2 * n + 15) & ~15ull;
+	}
+	size_t out_bytes = (size_t)n * ends * p->multi_best * 68;
+	if ((rc = ensure(h, &h->d_in, &h->d_in_cap, in_bytes))) return rc;
+	if ((rc = ensure(h, &h->d_out, &h->d_out_cap, out_bytes))) return rc;
+	uint8_t *din = (uint8_t *)h->d_in;
+	uint64_t *tmpoff = (uint64_t *)malloc(8 * n);
+	svg_reads dr[2];
+	for (int e = 0; e < ends; e++) {
+		const svg_reads *rr = e ? r2 : r1;
+		for (uint64_t i = 0; i < n; i++) tmpoff[i] = rr->offsets[i] - lo[e];
+		HIPCHK(hipMemcpyAsync(din + o_seq[e], rr->seq + lo[e], span[e], hipMemcpyHostToDevice, h->stream));
+		HIPCHK(hipMemcpyAsync(din + o_off[e], tmpoff, 8 * n, hipMemcpyHostToDevice, h->stream));
+		HIPCHK(hipMemcpyAsync(din + o_len[e], rr->lens, 2 * n, hipMemcpyHostToDevice, h->stream));
+		HIPCHK(hipStreamSynchronize(h->stream));
+		dr[e].seq = (const char *)(din + o_seq[e]);
+		dr[e].offsets = (const uint64_t *)(din + o_off[e]);
+		dr[e].lens = (const uint16_t *)(din + o_len[e]);
+		dr[e].n_reads = n;
+	}
+	free(tmpoff);
+	rc = svg_vote_batch_device(h, p, &dr[0], r2 ? &dr[1] : NULL, (svg_mapping_result *)h->d_out, NULL, NULL, h->stream);
+	if (rc) return rc;
+	HIPCHK(hipMemcpyAsync(out, h->d_out, out_bytes, hipMemcpyDeviceToHost, h->stream));
+	HIPCHK(hipStreamSynchronize(h->stream));
+	(void)jout; (void)big_margin;
+	return 0;
+}

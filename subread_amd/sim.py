@@ -1,0 +1,113 @@
+"""Seeded synthetic genomes / reads (wrappers over svg_sim_* in libsubread_amd.so).
+
+Workloads of BASELINE.json:
+  C2  1,000,000 bp i.i.d. genome (seed 901), full one-block index, 100 bp SE reads,
+      1% substitutions, 0.1% reads with one 1-5 bp indel, seed 20261015.
+  C3  3.0 Gbp, 24 contigs with GRCh38-like lengths (seed 3000) + injected repeat
+      families, full one-block index, 100 bp SE reads.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import lib, ReadBatch
+
+# GRCh38 primary chromosome lengths (chr1..22, X, Y), scaled to 3.0 Gbp for C3
+GRCH38_LENGTHS = [248956422, 242193529, 198295559, 190214555, 181538259, 170805979, 159345973,
+                  145138636, 138394717, 133797422, 135086622, 133275309, 114364328, 107043718,
+                  101991189, 90338345, 83257441, 80373285, 58617616, 64444167, 46709983, 50818468,
+                  156040895, 57227415]
+
+
+class Genome:
+    def __init__(self, names, seqs):
+        self.names = list(names)
+        self.seqs = [np.ascontiguousarray(s, dtype=np.uint8) for s in seqs]
+        self.flat = np.concatenate(self.seqs) if len(self.seqs) > 1 else self.seqs[0]
+        lens = np.array([len(s) for s in self.seqs], dtype=np.uint64)
+        self.starts = np.zeros(len(lens), dtype=np.uint64)
+        if len(lens) > 1:
+            self.starts[1:] = np.cumsum(lens[:-1])
+        self.lens = lens.astype(np.uint32)
+
+    @property
+    def length(self):
+        return int(self.lens.astype(np.uint64).sum())
+
+    def write_fasta(self, path, width=70):
+        with open(path, "wb") as f:
+            for n, s in zip(self.names, self.seqs):
+                f.write(b">" + n.encode() + b"\n")
+                b = s.tobytes()
+                for i in range(0, len(b), width):
+                    f.write(b[i:i + width] + b"\n")
+
+    @classmethod
+    def read_fasta(cls, path):
+        import gzip
+        op = gzip.open if str(path).endswith(".gz") else open
+        names, seqs, cur = [], [], []
+        with op(path, "rb") as f:
+            for line in f:
+                line = line.rstrip(b"\r\n")
+                if not line:
+                    continue
+                if line[:1] == b">":
+                    if names:
+                        seqs.append(np.frombuffer(b"".join(cur), dtype=np.uint8))
+                    names.append(line[1:].split()[0].decode())
+                    cur = []
+                else:
+                    cur.append(line.upper())
+            if names:
+                seqs.append(np.frombuffer(b"".join(cur), dtype=np.uint8))
+        return cls(names, seqs)
+
+
+def random_genome(lengths, seed, names=None, repeats=None):
+    """i.i.d. ACGT contigs; repeats = (n_copies, element_len, n_families, divergence)."""
+    seqs = []
+    for i, L in enumerate(lengths):
+        a = np.empty(int(L), dtype=np.uint8)
+        lib().svg_sim_genome(a.ctypes.data, int(L), int(seed) * 1000003 + i)
+        if repeats:
+            n_copies, elen, nfam, div = repeats
+            share = int(n_copies * L / max(1, sum(lengths)))
+            lib().svg_sim_repeats(a.ctypes.data, int(L), share, int(elen), int(nfam), float(div),
+                                  int(seed) * 7 + i)
+        seqs.append(a)
+    if names is None:
+        names = ["chr%d" % (i + 1) for i in range(len(lengths))] if len(lengths) > 1 else ["chrS%d" % seed]
+    return Genome(names, seqs)
+
+
+def c3_lengths(total=3_000_000_000):
+    s = sum(GRCH38_LENGTHS)
+    return [int(round(L * total / s)) for L in GRCH38_LENGTHS]
+
+
+def simulate_reads(genome, n, length=100, seed=20261015, first=0, sub=0.01, indel=0.001, nrate=0.0,
+                   threads=None, truth=False):
+    """-> ReadBatch (fixed length), optionally (ReadBatch, ctg, pos, strand)."""
+    seq = np.empty((n, length), dtype=np.uint8)
+    tc = np.empty(n, dtype=np.uint32) if truth else None
+    tp = np.empty(n, dtype=np.uint32) if truth else None
+    ts = np.empty(n, dtype=np.uint8) if truth else None
+    rc = lib().svg_sim_reads(genome.flat.ctypes.data, genome.starts.ctypes.data, genome.lens.ctypes.data,
+                             len(genome.lens), int(first), int(n), int(length), float(sub), float(indel),
+                             float(nrate), int(seed), seq.ctypes.data,
+                             tc.ctypes.data if truth else None, tp.ctypes.data if truth else None,
+                             ts.ctypes.data if truth else None, threads or min(16, os.cpu_count() or 1))
+    if rc != 0:
+        raise RuntimeError("svg_sim_reads failed %d" % rc)
+    rb = ReadBatch.fixed(seq)
+    return (rb, tc, tp, ts) if truth else rb
+
+
+def write_fastq(path, batch, names=None):
+    with open(path, "wb") as f:
+        for i in range(len(batch)):
+            s = batch.read(i)
+            nm = names[i] if names is not None else "r%d" % i
+            f.write(b"@" + nm.encode() + b"\n" + s + b"\n+\n" + b"I" * len(s) + b"\n")
