@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""bench.py -- throughput of the MI355X vote path (BASELINE.json metric).
+
+A "step" = one svg_vote_batch_device pass over one batch of synthetic reads
+resident in HBM (reads in, mapping_result_t[3] per read out).  Workloads
+(SURVEY.md §8(d)):
+  c2 (default): 10M x 100 bp SE reads per GPU vs a chr901-scale 1,000,000 bp
+      i.i.d. genome (seed 901), full one-block index (subread-buildindex -F -B),
+      1% substitutions, 0.1% reads with a 1-5 bp indel, read seed 20261015.
+  c3: 50M x 100 bp SE reads per GPU vs a 3.0 Gbp 24-contig genome with repeat
+      families, full one-block index.
+Multi-GPU (torchrun): one process per GPU, index replicated, reads sharded by
+rank (disjoint read-stream ranges), no collective on the data path; the only
+communication is the timing barrier / max.  scaling = "weak".
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "Mreads/s aligned, 100bp SE vs 3Gbp index; 1/2/4/8-GPU scaling + HBM GB/s"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def workload(name):
+    if name == "c2":
+        return dict(lengths=[1_000_000], gseed=901, repeats=None, reads=10_000_000, read_len=100,
+                    desc="C2: 10M x 100bp SE reads vs chr901-scale 1 Mbp genome, full one-block index")
+    if name == "c3":
+        from subread_amd.sim import c3_lengths
+        return dict(lengths=c3_lengths(), gseed=3000, repeats=(1_000_000, 300, 200, 0.12), reads=50_000_000,
+                    read_len=100, desc="C3: 50M x 100bp SE reads vs 3.0 Gbp 24-contig genome, full one-block index")
+    raise SystemExit("unknown workload " + name)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default=os.environ.get("SVG_WORKLOAD", "c2"))
+    ap.add_argument("--reads", type=int, default=0, help="reads per GPU per step (default: workload size)")
+    ap.add_argument("--workdir", default=os.environ.get("SVG_BENCH_DIR", ""))
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import subread_amd as sa
+    from subread_amd.abi import default_params, PROGRAM_ALIGN, MAPPING_DTYPE
+    from subread_amd.sim import random_genome, simulate_reads
+
+    W = workload(args.workload)
+    n = args.reads or W["reads"]
+    L = W["read_len"]
+    wd = args.workdir or os.path.join(tempfile.gettempdir(), "svg_bench_%s" % args.workload)
+    os.makedirs(wd, exist_ok=True)
+    prefix = os.path.join(wd, "genome_full")
+    t0 = time.time()
+    genome = random_genome(W["lengths"], W["gseed"], repeats=W["repeats"])
+    if rank == 0 and not os.path.exists(prefix + ".00.b.tab"):
+        fa = os.path.join(wd, "genome.fa")
+        genome.write_fasta(fa)
+        sa.build_index(fa, prefix, gap=1, force_one_block=True)
+        log("[bench] built index in %.1fs" % (time.time() - t0))
+    if dist is not None:
+        dist.barrier()
+    t1 = time.time()
+    ix = sa.VoteIndex(prefix, device=local)
+    log("[bench] index in HBM (%.1f GB) in %.1fs" % (ix.info.device_bytes / 1e9, time.time() - t1))
+
+    # this rank's shard of the read stream: reads rank*n .. rank*n+n-1
+    t1 = time.time()
+    rb = simulate_reads(genome, n, L, seed=20261015, first=rank * n, sub=0.01, indel=0.001)
+    log("[bench] simulated %d reads in %.1fs" % (n, time.time() - t1))
+    dev = torch.device("cuda", local)
+    d_seq = torch.from_numpy(rb.seq).to(dev)
+    d_off = torch.from_numpy(rb.offsets.view(np.int64)).to(dev)
+    d_len = torch.from_numpy(rb.lens.view(np.int16)).to(dev)
+    p = default_params(PROGRAM_ALIGN, False)
+    rec_bytes = MAPPING_DTYPE.itemsize * p.multi_best
+    d_out = torch.empty(n * rec_bytes, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    r1 = (d_seq.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n)
+
+    def step():
+        ix.vote_device(p, r1, None, d_out.data_ptr(), stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # algorithmic bytes from the kernel's own counters, outside the timed region
+    ix.set_stats(True)
+    step()
+    torch.cuda.synchronize()
+    st = ix.stats()
+    ix.set_stats(False)
+    in_bytes = n * (L + 8 + 2)                       # ASCII read + offset + length
+    probe_bytes = 8 * st["probes"] + 2 * st["bucket_items"] + 4 * st["hits"]
+    out_bytes = n * rec_bytes
+    algo_bytes = in_bytes + probe_bytes + out_bytes
+    avg_kern_s = float(np.mean(kern_ms)) / 1e3
+    achieved = algo_bytes / avg_kern_s / 1e9
+
+    check = None
+    if rank == 0 and not args.no_check:
+        # parity spot check against the oracle restatement (outside the timed region)
+        from oracle.pyoracle import OracleIndex
+        m = min(n, 20000)
+        got = d_out[: m * rec_bytes].cpu().numpy().reshape(m, -1)
+        oi = OracleIndex(prefix)
+        ref, _, _, _ = oi.vote(p, rb.slice(0, m), threads=args.cpu_threads)
+        check = bool((ref.view(np.uint8).reshape(m, -1) == got).all())
+        log("[bench] parity spot check on %d reads: %s" % (m, "IDENTICAL" if check else "MISMATCH"))
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        from oracle.pyoracle import OracleIndex
+        oi = OracleIndex(prefix)
+        ms = min(n, args.cpu_sample)
+        sample = rb.slice(0, ms)
+        t1 = time.perf_counter()
+        oi.vote(p, sample, threads=args.cpu_threads)
+        cs = time.perf_counter() - t1
+        cpu = {"value": round(ms / cs / 1e6, 4), "unit": "Mreads/s", "cores": args.cpu_threads, "kind": "port",
+               "sample": "%d of the same reads, oracle/svoracle.c restatement, %d pthreads, %.1f s" % (
+                   ms, args.cpu_threads, cs)}
+
+    total_reads = n * world * args.steps
+    value = total_reads / elapsed / 1e6
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mreads/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": W["desc"], "reads_per_gpu_per_step": n, "read_len": L,
+                       "index": "full one-block (gap 1), %d buckets, %d items" % (ix.info.buckets, ix.info.items),
+                       "parallelism": "reads sharded across %d GPU(s), index replicated, no collective" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "algorithmic_bytes_per_read": round(algo_bytes / n, 1),
+                         "kernel_ms": round(avg_kern_s * 1e3, 3)},
+            "cpu_baseline": cpu,
+            "parity_check": check,
+        }
+        print(json.dumps(line), flush=True)
+    ix.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

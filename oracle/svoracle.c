@@ -796,7 +796,9 @@ static void vote_read(readctx *c)
 			vtab_t *v = &c->vt[e];
 			int rl = c->rl[e], step, cr, round, k, x;
 			uint32_t shift_no = 0, hb;
-			if (rl < 16) { vt_reset(v); continue; }   /* out of contract: reference reads a stale table */
+			/* out of contract: rl < 16 (reference votes on a stale table, core.c:3116) and, for a
+			 * gapped index, rl < 18 (subreads run past the read end): treated as "no hits" */
+			if (rl < 15 + gap) { vt_reset(v); continue; }
 			cr = (rl - 15 - gap) << 16;
 			if (rl <= LONG_READ) {
 				step = cr / (p->total_subreads - 1);

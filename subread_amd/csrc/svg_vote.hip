@@ -213,14 +213,14 @@ struct Wave {
 		int total = 0;
 		int base[2][2];
 		for (int e = 0; e < ENDS; e++)
-			for (int s = 0; s < 2; s++) { base[e][s] = total; total += (rc.rl[e] >= 16) ? rc.np[e] : 0; }
+			for (int s = 0; s < 2; s++) { base[e][s] = total; total += rc.np[e]; }
 		for (int p0 = 0; p0 < total; p0 += 64) {
 			int id = p0 + lane_id();
 			if (id < total) {
 				int e = 0, s = 0;
 				for (int ee = 0; ee < ENDS; ee++)
 					for (int ss = 0; ss < 2; ss++)
-						if (rc.rl[ee] >= 16 && id >= base[ee][ss]) { e = ee; s = ss; }
+						if (rc.np[ee] > 0 && id >= base[ee][ss]) { e = ee; s = ss; }
 				int p = id - base[e][s];
 				int off = probe_off(e, p);
 				const char *t = L->text[e][s] + off;
@@ -431,8 +431,9 @@ struct Wave {
 		const int lane = lane_id();
 		const uint32_t *cs = cold_slot(cold[e], slot);
 		// indel_recorder_copy (sorted-hashtable.c:1144): triples while rec[3t] != 0 and 3t < 19
-		int v = lane < REC_LEN ? cold_rec(cs, lane) : 0;
-		unsigned long long z = ballot(lane < 21 && (lane % 3) == 0 && (v == 0 || lane >= 19));
+		int v = 0;
+		if (lane < REC_LEN) v = cold_rec(cs, lane);
+		unsigned long long z = ballot(lane < 19 && (lane % 3) == 0 && v == 0);
 		int T = z ? (__ffsll((long long)z) - 1) / 3 : 7;   // number of triples copied
 		int nrec = 3 * T;
 		int last_ind = __shfl(v, nrec > 0 ? nrec - 1 : 0);
@@ -485,7 +486,7 @@ struct Wave {
 		const int lane = lane_id();
 		int top[2][3] = {{0, 0, 0}, {0, 0, 0}};
 		int nsimp[2] = {0, 0};
-		const int TS = p.top_scores;   // 3 (validated on the host)
+		constexpr int TS = 3;   // p.top_scores, validated == 3 on the host
 		for (int e = 0; e < ENDS; e++) {
 			// row prefix of used slots
 			int it = lane < ROWS ? L->items[e][lane] : 0;
@@ -698,6 +699,11 @@ struct Wave {
 			int len = e ? kp->len2[r] : kp->len1[r];
 			int rev = e ? p.reverse_r2 : p.reverse_r1;
 			rc.rl[e] = len;
+			if (len > MAXL) {   // host-validated; never index LDS past the text buffer
+				if (lane == 0 && kp->stats) atomicOr((unsigned long long *)&kp->stats[7], 1ull);
+				len = 0;
+				rc.rl[e] = 0;
+			}
 			for (int i = lane; i < len; i += 64) {
 				char c = seq[o + i];
 				char c2 = seq[o + (len - 1 - i)];
@@ -706,7 +712,7 @@ struct Wave {
 				L->text[e][0][i] = s0;
 				L->text[e][1][i] = s1;
 			}
-			if (len >= 16) {
+			if (len >= 15 + gap) {   // shorter reads: out of contract, no hits (see oracle)
 				int cr = (len - 15 - gap) << 16, step;
 				if (len <= 160) {
 					step = cr / (p.total_subreads - 1);
@@ -718,6 +724,10 @@ struct Wave {
 				rc.step[e] = step;
 				rc.applied[e] = 1 + cr / step;
 				rc.np[e] = rc.applied[e] * gap;
+				if (rc.np[e] > MAXP) {   // host-validated; keep LDS probe tables in bounds
+					if (lane == 0 && kp->stats) atomicOr((unsigned long long *)&kp->stats[7], 2ull);
+					rc.np[e] = 0; rc.applied[e] = 0;
+				}
 			} else {
 				rc.step[e] = 0; rc.applied[e] = 0; rc.np[e] = 0;
 			}
@@ -734,7 +744,7 @@ struct Wave {
 			for (int e = 0; e < ENDS; e++) {
 				if (lane == 0) L->nshift[e] = 0;
 				wsync();
-				if (rc.rl[e] < 16) { table_reset(e); continue; }
+				if (rc.np[e] == 0) { table_reset(e); continue; }
 				for (int round = 0; round < 2; round++) {
 					table_reset(e);
 					replay(e, strand, round);
@@ -951,7 +961,7 @@ static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 		hipFree(h->d_scratch);
 		h->d_scratch = NULL;
 		h->scratch_words = 0;
-		if (dmalloc(h, (void **)&h->d_scratch, words * 4)) return SVG_E_NOMEM;
+		if (dmalloc(h, (void **)&h->d_scratch, words * 4 + 65536)) return SVG_E_NOMEM;
 		h->scratch_words = words;
 	}
 	kp.scratch = h->d_scratch;
@@ -1033,7 +1043,14 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 		const svg_reads *rr = e ? r2 : r1;
 		uint64_t mn = ~0ull, mx = 0;
 		for (uint64_t i = 0; i < n; i++) {
-			if (rr->lens[i] > 256) { svg_set_error("read %llu longer than 256 bases (long-read kernel not built)", (unsigned long long)i); return SVG_E_UNSUPPORTED; }
+			int len = rr->lens[i];
+			if (len > 256) { svg_set_error("read %llu longer than 256 bases (long-read kernel not built)", (unsigned long long)i); return SVG_E_UNSUPPORTED; }
+			if (len >= 15 + h->dix.gap) {
+				int cr = (len - 15 - h->dix.gap) << 16, step;
+				if (len <= 160) { step = cr / (p->total_subreads - 1); if (step < (h->dix.gap << 16)) step = h->dix.gap << 16; }
+				else { step = 6 << 16; if (cr / step > 62) step = cr / 62; }
+				if ((1 + cr / step) * h->dix.gap > 64) { svg_set_error("read %llu needs %d probes per strand (> 64; long-read kernel not built)", (unsigned long long)i, (1 + cr / step) * h->dix.gap); return SVG_E_UNSUPPORTED; }
+			}
 			if (rr->offsets[i] < mn) mn = rr->offsets[i];
 			if (rr->offsets[i] + rr->lens[i] > mx) mx = rr->offsets[i] + rr->lens[i];
 		}

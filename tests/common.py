@@ -1,0 +1,137 @@
+"""Shared helpers for the parity tests: golden fixtures, index cache, record comparison."""
+import glob
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+
+from subread_amd.abi import (MAPPING_DTYPE, SUBJUNC_DTYPE, ReadBatch, SvgParams, PROGRAM_ALIGN,
+                             PROGRAM_SUBJUNC)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def ensure_built():
+    """Build the product library and the oracle restatement if missing (CPU-only compile)."""
+    lib = os.path.join(ROOT, "subread_amd", "lib", "libsubread_amd.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "subread_amd", "csrc"), "-j8"], check=True,
+                       capture_output=True)
+    olib = os.path.join(ROOT, "oracle", "lib", "libsvoracle.so")
+    if not os.path.exists(olib):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "port"], check=True, capture_output=True)
+
+
+def golden_names():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "*.npz")))
+
+
+def index_md5():
+    with open(os.path.join(GOLD, "index_md5.json")) as f:
+        return json.load(f)
+
+
+def md5(p):
+    h = hashlib.md5()
+    with open(p, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 24), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+class IndexCache:
+    """Builds the fixture indexes with OUR builder and checks them against the
+    reference's md5 known answers before anything votes on them."""
+
+    def __init__(self, root):
+        self.root = root
+        self.built = {}
+
+    def genome_fasta(self, gname):
+        if gname == "chr901":
+            path = os.path.join(self.root, "chr901.fa")
+            if not os.path.exists(path):
+                with gzip.open(os.path.join(GOLD, "chr901.fa.gz"), "rb") as f, open(path, "wb") as o:
+                    o.write(f.read())
+            return path
+        if gname == "synth4242":
+            from subread_amd.sim import random_genome
+            path = os.path.join(self.root, "synth4242.fa")
+            if not os.path.exists(path):
+                random_genome([300000, 250000, 17, 200000, 120000], 4242,
+                              repeats=(2500, 300, 16, 0.04)).write_fasta(path)
+            return path
+        raise KeyError(gname)
+
+    def get(self, key):
+        if key in self.built:
+            return self.built[key]
+        import subread_amd as sa
+        gname, mode = key.rsplit("_", 1)
+        fa = self.genome_fasta(gname)
+        pre = os.path.join(self.root, key)
+        if mode == "full":
+            sa.build_index(fa, pre, gap=1, memory_mb=100, force_one_block=True)
+        else:
+            sa.build_index(fa, pre, gap=3, memory_mb=8000, force_one_block=False)
+        want = index_md5()["md5"][key]
+        for suf, m in want.items():
+            got = md5(pre + suf)
+            assert got == m, "index %s%s md5 %s != reference %s" % (key, suf, got, m)
+        self.built[key] = pre
+        return pre
+
+
+class Case:
+    def __init__(self, name):
+        self.name = name
+        with open(os.path.join(GOLD, name + ".json")) as f:
+            self.meta = json.load(f)
+        z = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+        self.r1 = ReadBatch(z["r1_seq"], z["r1_off"], z["r1_len"])
+        self.r2 = ReadBatch(z["r2_seq"], z["r2_off"], z["r2_len"]) if "r2_seq" in z else None
+        self.expected = z["expected"]
+        p = SvgParams()
+        for (f, _), v in zip(p._fields_, z["params"]):
+            setattr(p, f, int(v))
+        self.params = p
+        self.ends = 2 if self.r2 is not None else 1
+
+    @property
+    def index_key(self):
+        return self.meta["index"]
+
+
+def pack_records(out, jout, bm):
+    n = out.shape[0]
+    parts = [out.view(np.uint8).reshape(n, -1)]
+    if jout is not None:
+        parts.append(jout.view(np.uint8).reshape(n, -1))
+    if bm is not None:
+        parts.append(bm.view(np.uint8).reshape(n, -1))
+    return np.concatenate(parts, 1)
+
+
+def describe_mismatch(got, want, ends, mb, limit=5):
+    """Human-readable first mismatches: read, end, best, field."""
+    bad = np.nonzero((got != want).any(1))[0]
+    lines = ["%d of %d reads differ" % (len(bad), got.shape[0])]
+    names = MAPPING_DTYPE.names
+    for i in bad[:limit]:
+        d = np.nonzero(got[i] != want[i])[0]
+        msgs = []
+        for b in d[:6]:
+            if b < ends * mb * 68:
+                rec, off = divmod(int(b), 68)
+                fld = [n for n in names if MAPPING_DTYPE.fields[n][1] <= off][-1]
+                msgs.append("end%d best%d %s" % (rec // mb, rec % mb, fld))
+            else:
+                msgs.append("byte %d" % b)
+        g = got[i, :ends * mb * 68].copy().view(MAPPING_DTYPE)
+        w = want[i, :ends * mb * 68].copy().view(MAPPING_DTYPE)
+        lines.append("read %d: %s\n  got  %s\n  want %s" % (i, ", ".join(msgs), g, w))
+    return "\n".join(lines)

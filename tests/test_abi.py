@@ -1,0 +1,63 @@
+"""CPU: the C-ABI library loads, exports every symbol include/subread_vote.h
+declares, and its host-side pieces behave (no GPU compute here)."""
+import ctypes
+import re
+import os
+
+import numpy as np
+
+import subread_amd as sa
+from subread_amd.abi import default_params, PROGRAM_ALIGN, PROGRAM_SUBJUNC, MAPPING_DTYPE, SUBJUNC_DTYPE
+from tests.common import ROOT, ensure_built
+
+ensure_built()
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "subread_vote.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(svg_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    L = ctypes.CDLL(sa.LIB_PATH)
+    syms = header_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(sa.EXPORTS) == set(syms)
+    assert L.svg_abi_version() == 1
+
+
+def test_struct_sizes_match_reference():
+    assert MAPPING_DTYPE.itemsize == 68      # sizeof(mapping_result_t), core.h:350-370
+    assert SUBJUNC_DTYPE.itemsize == 16      # sizeof(subjunc_result_t), core.h:397-410
+    assert MAPPING_DTYPE.fields["selected_indel_record"][1] == 16
+    assert MAPPING_DTYPE.fields["confident_coverage_start"][1] == 60
+
+
+def test_params_default_c_equals_python():
+    for prog in (PROGRAM_ALIGN, PROGRAM_SUBJUNC):
+        for paired in (False, True):
+            assert sa.params_default(prog, paired).as_dict() == default_params(prog, paired).as_dict()
+    p = default_params(PROGRAM_SUBJUNC, True)
+    assert (p.total_subreads, p.min_votes_first, p.max_vote_simples, p.do_breakpoint_detection) == (14, 1, 64, 1)
+
+
+def test_simulator_deterministic_across_threads():
+    from subread_amd.sim import random_genome, simulate_reads
+    g = random_genome([50000, 30000], 5)
+    a = simulate_reads(g, 3000, 100, seed=9, threads=1)
+    b = simulate_reads(g, 3000, 100, seed=9, threads=7)
+    assert (a.seq == b.seq).all()
+    c = simulate_reads(g, 1000, 100, seed=9, first=2000, threads=3)
+    assert (c.seq == a.seq[2000 * 100:]).all()
+
+
+def test_index_open_without_gpu_fails_loudly(tmp_path):
+    # in the CPU container there is no HIP device: the product must refuse, not fall back
+    import subprocess, sys
+    code = ("import subread_amd as sa\n"
+            "try:\n sa.VoteIndex('/nonexistent/x')\nexcept sa.SvgError as e:\n print('ERR', e)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT)
+    assert "ERR" in r.stdout
