@@ -143,6 +143,7 @@ typedef struct svg_index_info {
 	uint32_t n_chromosomes;
 	uint64_t device_bytes;       /* HBM held by the handle                     */
 	int32_t  device;             /* HIP device ordinal                         */
+	uint32_t array_values_bytes; /* bytes of the packed .array image           */
 } svg_index_info;
 
 /* Load "<prefix>.00.b.tab", "<prefix>.00.b.array", "<prefix>.reads" (single-block
@@ -150,6 +151,21 @@ typedef struct svg_index_info {
 int  svg_index_open(const char *prefix, int device, svg_index **out);
 void svg_index_close(svg_index *idx);
 int  svg_index_get_info(const svg_index *idx, svg_index_info *out);
+
+/*
+ * Build a single-block index straight into HBM (same bytes as svg_build_index /
+ * subread-buildindex), from a FASTA file or from in-memory contigs; when
+ * save_prefix is not NULL the reference-format files are also written there.
+ */
+int  svg_index_build(const char *fasta, int gap, int memory_mb, int force_one_block,
+                     int repeat_threshold, int device, const char *save_prefix, svg_index **out);
+int  svg_index_build_mem(const char *const *names, const char *const *seqs, const uint64_t *lens,
+                         uint32_t n_contigs, int gap, int memory_mb, int force_one_block,
+                         int repeat_threshold, int device, const char *save_prefix, svg_index **out);
+/* Copy the index back to host arrays (any pointer may be NULL): bstart[buckets+1],
+ * keys[items], vals[items], values[array_values_bytes], chr_end[n_chromosomes]. */
+int  svg_index_export(const svg_index *idx, uint32_t *bstart, int16_t *keys, uint32_t *vals,
+                      uint8_t *values, uint32_t *chr_end);
 
 /*
  * Vote a batch.  Host buffers in, host buffers out (synchronous).

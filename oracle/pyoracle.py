@@ -37,6 +37,10 @@ def lib():
         L.svo_index_open.argtypes = [ctypes.c_char_p]
         L.svo_index_close.argtypes = [ctypes.c_void_p]
         L.svo_index_info.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
+        L.svo_index_from_arrays.restype = ctypes.c_void_p
+        L.svo_index_from_arrays.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
         L.svo_vote_batch.restype = ctypes.c_int
         L.svo_vote_batch.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int, ctypes.c_void_p]
         _lib = L
@@ -44,10 +48,19 @@ def lib():
 
 
 class OracleIndex:
-    def __init__(self, prefix):
-        self.h = lib().svo_index_open(prefix.encode())
+    def __init__(self, prefix=None, arrays=None):
+        self._keep = None
+        if arrays is not None:
+            a = arrays
+            self._keep = a
+            self.h = lib().svo_index_from_arrays(
+                a["buckets"], a["items"], a["gap"], a["padding"], a["bstart"].ctypes.data, a["keys"].ctypes.data,
+                a["vals"].ctypes.data, a["length"], a["values_bytes"], a["values"].ctypes.data,
+                a["n_chr"], a["chr_end"].ctypes.data)
+        else:
+            self.h = lib().svo_index_open(prefix.encode())
         if not self.h:
-            raise IOError("oracle: cannot load index " + prefix)
+            raise IOError("oracle: cannot load index %s" % prefix)
         nb, items, gap, pad, nchr = (ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_int(),
                                      ctypes.c_int(), ctypes.c_uint32())
         lib().svo_index_info(self.h, ctypes.byref(nb), ctypes.byref(items), ctypes.byref(gap),

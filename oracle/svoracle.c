@@ -61,6 +61,7 @@ typedef struct {
 	/* .reads */
 	uint32_t n_chr;
 	uint32_t *chr_end;
+	int borrowed;          /* arrays owned by the caller (svo_index_from_arrays) */
 } svo_index;
 
 static int rd(FILE *fp, void *p, size_t n) { return fread(p, 1, n, fp) == n ? 0 : -1; }
@@ -68,7 +69,7 @@ static int rd(FILE *fp, void *p, size_t n) { return fread(p, 1, n, fp) == n ? 0 
 void svo_index_close(svo_index *ix)
 {
 	if (!ix) return;
-	free(ix->bstart); free(ix->keys); free(ix->vals); free(ix->values); free(ix->chr_end);
+	if (!ix->borrowed) { free(ix->bstart); free(ix->keys); free(ix->vals); free(ix->values); free(ix->chr_end); }
 	free(ix);
 }
 
@@ -148,6 +149,20 @@ bad:
 bad2:
 	svo_index_close(ix);
 	return NULL;
+}
+
+/* wrap caller-owned arrays of an index that was never written to disk (bench C3) */
+svo_index *svo_index_from_arrays(uint32_t nb, uint64_t items, int gap, int padding, uint32_t *bstart, int16_t *keys,
+                                 uint32_t *vals, uint32_t length, uint32_t values_bytes, uint8_t *values,
+                                 uint32_t n_chr, uint32_t *chr_end)
+{
+	svo_index *ix = calloc(1, sizeof(*ix));
+	ix->nb = nb; ix->items = items; ix->gap = gap; ix->padding = padding;
+	ix->bstart = bstart; ix->keys = keys; ix->vals = vals;
+	ix->start_point = 0; ix->start_base_offset = 0; ix->length = length; ix->values_bytes = values_bytes;
+	ix->values = values; ix->n_chr = n_chr; ix->chr_end = chr_end;
+	ix->borrowed = 1;
+	return ix;
 }
 
 void svo_index_info(const svo_index *ix, uint32_t *nb, uint64_t *items, int *gap, int *padding, uint32_t *n_chr)

@@ -27,7 +27,7 @@ EXPORTS = [
     "svg_params_default", "svg_index_open", "svg_index_close", "svg_index_get_info",
     "svg_vote_batch", "svg_vote_batch_device", "svg_set_stats", "svg_get_stats",
     "svg_last_error", "svg_abi_version", "svg_build_index", "svg_sim_genome",
-    "svg_sim_repeats", "svg_sim_reads",
+    "svg_sim_repeats", "svg_sim_reads", "svg_index_build", "svg_index_build_mem", "svg_index_export",
 ]
 
 _lib = None
@@ -65,6 +65,13 @@ def lib():
         L.svg_set_stats.argtypes = [vp, i32]
         L.svg_get_stats.argtypes = [vp, vp]
         L.svg_last_error.restype = ctypes.c_char_p
+        L.svg_index_build.argtypes = [ctypes.c_char_p, i32, i32, i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
+        L.svg_index_build.restype = i32
+        L.svg_index_build_mem.argtypes = [vp, vp, vp, ctypes.c_uint32, i32, i32, i32, i32, i32, ctypes.c_char_p,
+                                          ctypes.POINTER(vp)]
+        L.svg_index_build_mem.restype = i32
+        L.svg_index_export.argtypes = [vp] * 6
+        L.svg_index_export.restype = i32
         L.svg_build_index.argtypes = [ctypes.c_char_p, ctypes.c_char_p, i32, i32, i32, i32]
         L.svg_build_index.restype = i32
         L.svg_sim_genome.argtypes = [vp, u64, u64]
@@ -96,15 +103,54 @@ def build_index(fasta, prefix, gap=3, memory_mb=8000, force_one_block=False, rep
 
 
 class VoteIndex:
-    """An index resident in HBM of one GPU (svg_index_open)."""
+    """An index resident in HBM of one GPU (svg_index_open / svg_index_build*)."""
 
-    def __init__(self, prefix, device=0):
-        h = ctypes.c_void_p()
-        _check(lib().svg_index_open(str(prefix).encode(), device, ctypes.byref(h)), "svg_index_open")
-        self.h = h
+    def __init__(self, prefix=None, device=0, _handle=None):
+        if _handle is None:
+            h = ctypes.c_void_p()
+            _check(lib().svg_index_open(str(prefix).encode(), device, ctypes.byref(h)), "svg_index_open")
+            _handle = h
+        self.h = _handle
         info = SvgIndexInfo()
         lib().svg_index_get_info(self.h, ctypes.byref(info))
         self.info = info
+
+    @classmethod
+    def build(cls, fasta, gap=1, memory_mb=8000, force_one_block=True, repeat_threshold=100, device=0,
+              save_prefix=None):
+        """Build the index in HBM (GPU builder); optionally also write the reference files."""
+        h = ctypes.c_void_p()
+        _check(lib().svg_index_build(str(fasta).encode(), gap, memory_mb, 1 if force_one_block else 0,
+                                     repeat_threshold, device, save_prefix.encode() if save_prefix else None,
+                                     ctypes.byref(h)), "svg_index_build")
+        return cls(_handle=h)
+
+    @classmethod
+    def build_genome(cls, genome, gap=1, memory_mb=8000, force_one_block=True, repeat_threshold=100, device=0,
+                     save_prefix=None):
+        """Build from a subread_amd.sim.Genome (in-memory contigs)."""
+        n = len(genome.seqs)
+        names = (ctypes.c_char_p * n)(*[x.encode() for x in genome.names])
+        seqs = (ctypes.c_void_p * n)(*[s.ctypes.data for s in genome.seqs])
+        lens = np.array([len(s) for s in genome.seqs], dtype=np.uint64)
+        h = ctypes.c_void_p()
+        _check(lib().svg_index_build_mem(names, seqs, lens.ctypes.data, n, gap, memory_mb,
+                                         1 if force_one_block else 0, repeat_threshold, device,
+                                         save_prefix.encode() if save_prefix else None, ctypes.byref(h)),
+               "svg_index_build_mem")
+        return cls(_handle=h)
+
+    def export(self):
+        """Host copy of the index arrays (dict usable by the oracle's from_arrays)."""
+        i = self.info
+        a = dict(buckets=i.buckets, items=i.items, gap=i.index_gap, padding=i.padding, length=i.array_length,
+                 values_bytes=i.array_values_bytes, n_chr=i.n_chromosomes,
+                 bstart=np.empty(i.buckets + 1, np.uint32), keys=np.empty(max(1, i.items), np.int16),
+                 vals=np.empty(max(1, i.items), np.uint32), values=np.empty(i.array_values_bytes + 64, np.uint8),
+                 chr_end=np.empty(max(1, i.n_chromosomes), np.uint32))
+        _check(lib().svg_index_export(self.h, a["bstart"].ctypes.data, a["keys"].ctypes.data, a["vals"].ctypes.data,
+                                      a["values"].ctypes.data, a["chr_end"].ctypes.data), "svg_index_export")
+        return a
 
     def close(self):
         if getattr(self, "h", None):

@@ -87,6 +87,7 @@ class SvgIndexInfo(ctypes.Structure):
         ("n_chromosomes", ctypes.c_uint32),
         ("device_bytes", ctypes.c_uint64),
         ("device", ctypes.c_int32),
+        ("array_values_bytes", ctypes.c_uint32),
     ]
 
 

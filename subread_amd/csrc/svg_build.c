@@ -32,18 +32,8 @@
 #define PAD 1210
 #define NAME_MAX_LEN 200
 
-typedef struct {
-	char name[NAME_MAX_LEN];
-	uint64_t start;   /* into base buffer */
-	uint32_t len;
-} contig_t;
-
-typedef struct {
-	char *bases;      /* normalised, concatenated */
-	uint64_t nbases, cap;
-	contig_t *ctg;
-	uint32_t nctg, ctg_cap;
-} genome_t;
+typedef svg_contig contig_t;
+typedef svg_genome genome_t;
 
 static void g_push(genome_t *g, const char *s, size_t n)
 {
@@ -56,7 +46,7 @@ static void g_push(genome_t *g, const char *s, size_t n)
 }
 
 /* check_and_convert_FastA semantics (index-builder.c:789-992) */
-static int read_fasta(const char *path, genome_t *g)
+int svg_genome_read_fasta(const char *path, genome_t *g)
 {
 	gzFile fp = gzopen(path, "rb");
 	char *line = malloc(1 << 16);
@@ -154,6 +144,159 @@ static void radix64(uint64_t *a, uint64_t *tmp, uint64_t n)
 
 static int write_all(FILE *fp, const void *p, size_t n) { return fwrite(p, 1, n, fp) == n ? 0 : -1; }
 
+void svg_genome_free(genome_t *g)
+{
+	free(g->bases); free(g->ctg);
+	memset(g, 0, sizeof *g);
+}
+
+/* in-memory contigs -> normalised genome (same rules as the FASTA path) */
+int svg_genome_from_mem(const char *const *names, const char *const *seqs, const uint64_t *lens, uint32_t n, genome_t *g)
+{
+	uint32_t c;
+	memset(g, 0, sizeof *g);
+	for (c = 0; c < n; c++) {
+		uint64_t i;
+		contig_t *ct;
+		if (lens[c] <= 16) continue;
+		if (lens[c] > 0xffffffffull) { svg_set_error("contig longer than 2^32"); return SVG_E_UNSUPPORTED; }
+		if (g->nctg == g->ctg_cap) {
+			g->ctg_cap = g->ctg_cap ? g->ctg_cap * 2 : 64;
+			g->ctg = realloc(g->ctg, sizeof(contig_t) * g->ctg_cap);
+		}
+		ct = &g->ctg[g->nctg++];
+		memset(ct, 0, sizeof *ct);
+		snprintf(ct->name, NAME_MAX_LEN, "%s", names[c]);
+		ct->start = g->nbases;
+		ct->len = (uint32_t)lens[c];
+		if (g->nbases + lens[c] > g->cap) {
+			g->cap = g->nbases + lens[c] + (1 << 20);
+			g->bases = realloc(g->bases, g->cap);
+		}
+		for (i = 0; i < lens[c]; i++) {
+			int ch = seqs[c][i], lo = tolower(ch);
+			g->bases[g->nbases + i] = (lo == 'a' || lo == 'c' || lo == 'g' || lo == 't') ? (char)toupper(ch) : 'A';
+		}
+		g->nbases += lens[c];
+	}
+	if (!g->nctg) { svg_set_error("no contig of >16 bases"); return SVG_E_FORMAT; }
+	return 0;
+}
+
+void svg_genome_layout(const genome_t *g, int gap, uint64_t *O, uint64_t *nwin)
+{
+	uint64_t off = PAD;
+	uint32_t c;
+	*nwin = 0;
+	for (c = 0; c < g->nctg; c++) {
+		O[c] = off;
+		*nwin += (g->ctg[c].len - 16) / gap + 1;
+		off += (uint64_t)g->ctg[c].len - 16 + 2 * PAD;
+	}
+}
+
+uint64_t svg_items_budget(int gap, int memory_mb, int force_one_block)
+{
+	if (force_one_block) memory_mb = gap == 1 ? 22000 : 11500;
+	else if (memory_mb > 12000 && gap > 2) memory_mb = 12000;
+	return (uint32_t)(memory_mb * 1024.0 / 8.) * 1024;
+}
+
+int svg_write_tab(const char *prefix, uint32_t nb, uint64_t items, int gap, const uint32_t *bstart,
+                  const int16_t *keys, const uint32_t *vals)
+{
+	char fn[4096];
+	FILE *fp;
+	char *buf;
+	size_t bufsz = 1 << 24, bl = 0;
+	uint32_t c;
+	int rc = 0;
+	snprintf(fn, sizeof fn, "%s.00.b.tab", prefix);
+	fp = fopen(fn, "wb");
+	if (!fp) { svg_set_error("cannot write '%s'", fn); return SVG_E_IO; }
+	buf = malloc(bufsz);
+	{
+		int16_t opt[7] = {0x0102, 2, PAD, 0x0101, 2, (int16_t)gap, 0};
+		int64_t nit = (int64_t)items; int32_t nbs = (int32_t)nb;
+		memcpy(buf + bl, "2subindx", 8); bl += 8;
+		memcpy(buf + bl, opt, sizeof opt); bl += sizeof opt;
+		memcpy(buf + bl, &nit, 8); bl += 8;
+		memcpy(buf + bl, &nbs, 4); bl += 4;
+	}
+	for (c = 0; c < nb && !rc; c++) {
+		int32_t n = (int32_t)(bstart[c + 1] - bstart[c]);
+		size_t need = 8 + 6 * (size_t)n;
+		if (bl + need > bufsz) {
+			if (write_all(fp, buf, bl)) rc = SVG_E_IO;
+			bl = 0;
+			if (need > bufsz) { bufsz = need * 2; buf = realloc(buf, bufsz); }
+		}
+		memcpy(buf + bl, &n, 4); memcpy(buf + bl + 4, &n, 4); bl += 8;
+		memcpy(buf + bl, keys + bstart[c], 2 * (size_t)n); bl += 2 * (size_t)n;
+		memcpy(buf + bl, vals + bstart[c], 4 * (size_t)n); bl += 4 * (size_t)n;
+	}
+	buf[bl++] = 0;
+	if (!rc && write_all(fp, buf, bl)) rc = SVG_E_IO;
+	if (fclose(fp)) rc = SVG_E_IO;
+	free(buf);
+	if (rc) svg_set_error("write error on '%s'", fn);
+	return rc;
+}
+
+uint8_t *svg_pack_array(const genome_t *g, const uint64_t *O, uint32_t *length_out, uint32_t *vbytes_out)
+{
+	uint32_t last = g->nctg - 1, c;
+	uint32_t length = (uint32_t)(O[last] + g->ctg[last].len - 16 + 16 + PAD);
+	size_t nbytes = (length >> 2) + 1;
+	uint8_t *arr = calloc(nbytes + 64, 1);
+	if (!arr) return NULL;
+	for (c = 0; c < g->nctg; c++) {
+		const char *b = g->bases + g->ctg[c].start;
+		uint32_t k;
+		for (k = 0; k < g->ctg[c].len; k++) {
+			uint64_t p = O[c] + k;
+			arr[p >> 2] |= (uint8_t)(b2i(b[k]) << (2 * (p & 3)));
+		}
+	}
+	*length_out = length;
+	*vbytes_out = (uint32_t)nbytes;
+	return arr;
+}
+
+int svg_write_array_reads(const char *prefix, const genome_t *g, const uint64_t *O, int gap, uint64_t nwin,
+                          uint64_t items, uint32_t nb, const char *source)
+{
+	char fn[4096];
+	FILE *fp;
+	uint32_t c, length, vb, start = 0;
+	int rc = 0;
+	uint8_t *arr = svg_pack_array(g, O, &length, &vb);
+	if (!arr) { svg_set_error("out of memory packing .array"); return SVG_E_NOMEM; }
+	snprintf(fn, sizeof fn, "%s.00.b.array", prefix);
+	fp = fopen(fn, "wb");
+	if (!fp) { free(arr); svg_set_error("cannot write '%s'", fn); return SVG_E_IO; }
+	if (write_all(fp, &start, 4) || write_all(fp, &length, 4) || write_all(fp, arr, vb)) rc = SVG_E_IO;
+	fclose(fp);
+	free(arr);
+	if (rc) { svg_set_error("write error on '%s'", fn); return rc; }
+	snprintf(fn, sizeof fn, "%s.reads", prefix);
+	fp = fopen(fn, "wb");
+	if (!fp) { svg_set_error("cannot write '%s'", fn); return SVG_E_IO; }
+	for (c = 0; c < g->nctg; c++) fprintf(fp, "%u\t%s\n", (uint32_t)(O[c] + g->ctg[c].len - 16 + PAD), g->ctg[c].name);
+	fclose(fp);
+	snprintf(fn, sizeof fn, "%s.files", prefix);
+	fp = fopen(fn, "wb");
+	if (fp) { for (c = 0; c < g->nctg; c++) fprintf(fp, "%s\t%s\t0\n", g->ctg[c].name, source); fclose(fp); }
+	snprintf(fn, sizeof fn, "%s.log", prefix);
+	fp = fopen(fn, "wb");
+	if (fp) {
+		fprintf(fp, "svg index: %u contigs, %llu windows, %llu items, %u buckets, gap %d\n", g->nctg,
+		        (unsigned long long)nwin, (unsigned long long)items, nb, gap);
+		fclose(fp);
+	}
+	return 0;
+}
+
 int svg_build_index(const char *fasta, const char *prefix, int gap, int memory_mb, int force_one_block, int repeat_threshold)
 {
 	genome_t g;
@@ -161,31 +304,20 @@ int svg_build_index(const char *fasta, const char *prefix, int gap, int memory_m
 	uint64_t *items = NULL, *tmp = NULL;
 	uint32_t c, nb;
 	uint64_t budget;
-	char fn[4096];
-	FILE *fp;
 	int rc = 0;
 	memset(&g, 0, sizeof g);
 	if (!fasta || !prefix || (gap != 1 && gap != 3)) { svg_set_error("svg_build_index: bad argument"); return SVG_E_ARG; }
 	if (repeat_threshold < 1) repeat_threshold = 100;
-	rc = read_fasta(fasta, &g);
+	rc = svg_genome_read_fasta(fasta, &g);
 	if (rc) goto out;
 
 	/* 2. coordinates */
 	O = malloc(sizeof(uint64_t) * g.nctg);
-	{
-		uint64_t off = PAD;
-		for (c = 0; c < g.nctg; c++) {
-			O[c] = off;
-			nwin += (g.ctg[c].len - 16) / gap + 1;
-			off += (uint64_t)g.ctg[c].len - 16 + 2 * PAD;
-		}
-		if (O[g.nctg - 1] + g.ctg[g.nctg - 1].len + PAD >= 0xffffffffull) { rc = SVG_E_UNSUPPORTED; svg_set_error("genome too long for 32-bit coordinates"); goto out; }
-	}
+	svg_genome_layout(&g, gap, O, &nwin);
+	if (O[g.nctg - 1] + g.ctg[g.nctg - 1].len + PAD >= 0xffffffffull) { rc = SVG_E_UNSUPPORTED; svg_set_error("genome too long for 32-bit coordinates"); goto out; }
 
 	/* 5. bucket count */
-	if (force_one_block) memory_mb = gap == 1 ? 22000 : 11500;
-	else if (memory_mb > 12000 && gap > 2) memory_mb = 12000;
-	budget = (uint32_t)(memory_mb * 1024.0 / 8.) * 1024;
+	budget = svg_items_budget(gap, memory_mb, force_one_block);
 	nb = svg_bucket_count(budget, gap);
 
 	/* 3+4. windows, sorted by (key, in-run order) */
@@ -226,8 +358,6 @@ int svg_build_index(const char *fasta, const char *prefix, int gap, int memory_m
 		uint32_t *bstart = calloc((size_t)nb + 1, sizeof(uint32_t));
 		int16_t *keys = malloc(2 * nkeep + 2);
 		uint32_t *vals = malloc(4 * nkeep + 4);
-		char *buf;
-		size_t bufsz = 1 << 24, bl = 0;
 		if (!bstart || !keys || !vals) { free(bstart); free(keys); free(vals); rc = SVG_E_NOMEM; goto out; }
 		for (i = 0; i < nkeep; i++) bstart[(uint32_t)(items[i] >> 32) % nb + 1]++;
 		for (c = 0; c < nb; c++) bstart[c + 1] += bstart[c];
@@ -242,74 +372,15 @@ int svg_build_index(const char *fasta, const char *prefix, int gap, int memory_m
 			}
 			free(cur);
 		}
-		snprintf(fn, sizeof fn, "%s.00.b.tab", prefix);
-		fp = fopen(fn, "wb");
-		if (!fp) { free(bstart); free(keys); free(vals); rc = SVG_E_IO; svg_set_error("cannot write '%s'", fn); goto out; }
-		buf = malloc(bufsz);
-		{
-			int16_t opt[7] = {0x0102, 2, PAD, 0x0101, 2, (int16_t)gap, 0};
-			int64_t nit = (int64_t)nkeep; int32_t nbs = (int32_t)nb;
-			memcpy(buf + bl, "2subindx", 8); bl += 8;
-			memcpy(buf + bl, opt, sizeof opt); bl += sizeof opt;
-			memcpy(buf + bl, &nit, 8); bl += 8;
-			memcpy(buf + bl, &nbs, 4); bl += 4;
-		}
-		for (c = 0; c < nb && !rc; c++) {
-			int32_t n = (int32_t)(bstart[c + 1] - bstart[c]);
-			size_t need = 8 + 6 * (size_t)n;
-			if (bl + need > bufsz) {
-				if (write_all(fp, buf, bl)) rc = SVG_E_IO;
-				bl = 0;
-				if (need > bufsz) { bufsz = need * 2; buf = realloc(buf, bufsz); }
-			}
-			memcpy(buf + bl, &n, 4); memcpy(buf + bl + 4, &n, 4); bl += 8;
-			memcpy(buf + bl, keys + bstart[c], 2 * (size_t)n); bl += 2 * (size_t)n;
-			memcpy(buf + bl, vals + bstart[c], 4 * (size_t)n); bl += 4 * (size_t)n;
-		}
-		buf[bl++] = 0;
-		if (!rc && write_all(fp, buf, bl)) rc = SVG_E_IO;
-		if (fclose(fp)) rc = SVG_E_IO;
-		free(buf); free(bstart); free(keys); free(vals);
-		if (rc) { svg_set_error("write error on '%s'", fn); goto out; }
-	}
-
-	/* 7. .array */
-	{
-		uint32_t last = g.nctg - 1;
-		uint32_t length = (uint32_t)(O[last] + g.ctg[last].len - 16 + 16 + PAD), start = 0;
-		size_t nbytes = (length >> 2) + 1;
-		uint8_t *arr = calloc(nbytes + 8, 1);
-		for (c = 0; c < g.nctg; c++) {
-			const char *b = g.bases + g.ctg[c].start;
-			uint32_t k;
-			for (k = 0; k < g.ctg[c].len; k++) {
-				uint64_t p = O[c] + k;
-				arr[p >> 2] |= (uint8_t)(b2i(b[k]) << (2 * (p & 3)));
-			}
-		}
-		snprintf(fn, sizeof fn, "%s.00.b.array", prefix);
-		fp = fopen(fn, "wb");
-		if (!fp) { free(arr); rc = SVG_E_IO; svg_set_error("cannot write '%s'", fn); goto out; }
-		if (write_all(fp, &start, 4) || write_all(fp, &length, 4) || write_all(fp, arr, nbytes)) rc = SVG_E_IO;
-		fclose(fp);
-		free(arr);
+		free(items); items = NULL;
+		free(tmp); tmp = NULL;
+		rc = svg_write_tab(prefix, nb, nkeep, gap, bstart, keys, vals);
+		free(bstart); free(keys); free(vals);
 		if (rc) goto out;
 	}
-
-	/* .reads / .files / .log */
-	snprintf(fn, sizeof fn, "%s.reads", prefix);
-	fp = fopen(fn, "wb");
-	if (!fp) { rc = SVG_E_IO; goto out; }
-	for (c = 0; c < g.nctg; c++) fprintf(fp, "%u\t%s\n", (uint32_t)(O[c] + g.ctg[c].len - 16 + PAD), g.ctg[c].name);
-	fclose(fp);
-	snprintf(fn, sizeof fn, "%s.files", prefix);
-	fp = fopen(fn, "wb");
-	if (fp) { for (c = 0; c < g.nctg; c++) fprintf(fp, "%s\t%s\t0\n", g.ctg[c].name, fasta); fclose(fp); }
-	snprintf(fn, sizeof fn, "%s.log", prefix);
-	fp = fopen(fn, "wb");
-	if (fp) { fprintf(fp, "svg_build_index: %u contigs, %llu windows, %llu items, %u buckets, gap %d\n", g.nctg, (unsigned long long)nwin, (unsigned long long)nkeep, nb, gap); fclose(fp); }
+	rc = svg_write_array_reads(prefix, &g, O, gap, nwin, nkeep, nb, fasta);
 out:
 	free(items); free(tmp); free(O);
-	free(g.bases); free(g.ctg);
+	svg_genome_free(&g);
 	return rc;
 }

@@ -39,6 +39,32 @@ void svg_host_index_free(svg_host_index *ix);
 
 uint32_t svg_bucket_count(uint64_t expected_items, int gap);
 
+/* normalised genome (check_and_convert_FastA semantics, index-builder.c:789-992) */
+typedef struct svg_contig {
+	char name[200];
+	uint64_t start;      /* into bases */
+	uint32_t len;
+} svg_contig;
+typedef struct svg_genome {
+	char *bases;         /* A/C/G/T only, contigs concatenated */
+	uint64_t nbases, cap;
+	svg_contig *ctg;
+	uint32_t nctg, ctg_cap;
+} svg_genome;
+int  svg_genome_read_fasta(const char *path, svg_genome *g);
+int  svg_genome_from_mem(const char *const *names, const char *const *seqs, const uint64_t *lens, uint32_t n, svg_genome *g);
+void svg_genome_free(svg_genome *g);
+/* linear coordinates: O[c] (first base of contig c), windows per contig, index budget */
+void svg_genome_layout(const svg_genome *g, int gap, uint64_t *O, uint64_t *nwin);
+uint64_t svg_items_budget(int gap, int memory_mb, int force_one_block);
+/* writers of the reference on-disk format */
+int svg_write_tab(const char *prefix, uint32_t nb, uint64_t items, int gap, const uint32_t *bstart,
+                  const int16_t *keys, const uint32_t *vals);
+int svg_write_array_reads(const char *prefix, const svg_genome *g, const uint64_t *O, int gap,
+                          uint64_t nwin, uint64_t items, uint32_t nb, const char *source);
+/* 2-bit LSB-first .array image (gvindex_set), length/values_bytes as gvindex_load sees them */
+uint8_t *svg_pack_array(const svg_genome *g, const uint64_t *O, uint32_t *length, uint32_t *values_bytes);
+
 #ifdef __cplusplus
 }
 #endif

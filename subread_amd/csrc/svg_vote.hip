@@ -38,6 +38,7 @@
 #include <stdio.h>
 #include "subread_vote.h"
 #include "svg_internal.h"
+#include "svg_device.h"
 
 #define ROWS 30
 #define SPACE 24
@@ -45,19 +46,6 @@
 #define REC_LEN 21
 #define COLD_WORDS 8          // per slot: cs|ce<<16, rec[21] as bytes, pad
 #define JCW 17
-
-// ---------------------------------------------------------------------------------------------
-// device-side index
-struct DevIndex {
-	const uint32_t *bstart;   // nb+1
-	const int16_t *keys;
-	const uint32_t *vals;
-	const uint8_t *values;    // .array
-	const uint32_t *chr_end;  // .reads offsets
-	uint32_t nb, n_chr;
-	uint32_t start_point, length, start_base_offset, values_bytes;
-	int32_t gap, padding;
-};
 
 // kernel parameters (passed by value)
 struct KParams {
@@ -810,31 +798,39 @@ __global__ void __launch_bounds__(64 * WPB) vote_kernel(KParams kp)
 // =============================================================================================
 // host side: handle, upload, launch
 // =============================================================================================
-struct svg_index {
-	int device;
-	hipStream_t stream;
-	svg_host_index host;
-	DevIndex dix;
-	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr;
-	uint32_t *d_scratch;
-	size_t scratch_words;
-	unsigned long long *d_stats;
-	int stats_on;
-	svg_batch_stats last_stats;
-	uint64_t device_bytes;
-	int n_cu;
-	// staging for svg_vote_batch (host buffers)
-	void *d_in; size_t d_in_cap;
-	void *d_out; size_t d_out_cap;
-};
 
-#define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) { svg_set_error("HIP error %s at %s:%d", hipGetErrorString(_e), __FILE__, __LINE__); return SVG_E_DEVICE; } } while (0)
-
-static int dmalloc(svg_index *h, void **p, size_t n)
+// common tail of svg_index_open / svg_index_build*: d_bstart/d_keys/d_vals already in HBM,
+// host part holds .array and the chromosome table
+int svg_index_finish_device(svg_index *h)
 {
-	hipError_t e = hipMalloc(p, n ? n : 16);
-	if (e != hipSuccess) { svg_set_error("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e)); return SVG_E_NOMEM; }
-	h->device_bytes += n;
+	svg_host_index *x = &h->host;
+	int rc;
+	HIPCHK(hipSetDevice(h->device));
+	if ((rc = dmalloc(h, &h->d_values, (size_t)x->values_bytes + 64)) || (rc = dmalloc(h, &h->d_chr, 4 * (size_t)x->n_chr + 64)))
+		return rc;
+	HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+	HIPCHK(hipMemcpy(h->d_values, x->values, x->values_bytes, hipMemcpyHostToDevice));
+	HIPCHK(hipMemcpy(h->d_chr, x->chr_end, 4 * (size_t)x->n_chr, hipMemcpyHostToDevice));
+	h->dix.bstart = (const uint32_t *)h->d_bstart;
+	h->dix.keys = (const int16_t *)h->d_keys;
+	h->dix.vals = (const uint32_t *)h->d_vals;
+	h->dix.values = (const uint8_t *)h->d_values;
+	h->dix.chr_end = (const uint32_t *)h->d_chr;
+	h->dix.nb = x->nb;
+	h->dix.n_chr = x->n_chr;
+	h->dix.start_point = x->start_point;
+	h->dix.length = x->length;
+	h->dix.start_base_offset = x->start_base_offset;
+	h->dix.values_bytes = x->values_bytes;
+	h->dix.gap = x->gap;
+	h->dix.padding = x->padding;
+	hipDeviceProp_t prop;
+	HIPCHK(hipGetDeviceProperties(&prop, h->device));
+	h->n_cu = prop.multiProcessorCount;
+	if ((rc = dmalloc(h, (void **)&h->d_stats, 8 * sizeof(unsigned long long)))) return rc;
+	HIPCHK(hipMemset(h->d_stats, 0, 8 * sizeof(unsigned long long)));
+	const char *se = getenv("SVG_STATS");
+	h->stats_on = se && se[0] == '1';
 	return 0;
 }
 
@@ -852,41 +848,36 @@ extern "C" int svg_index_open(const char *prefix, int device, svg_index **out)
 	if (rc) { free(h); return rc; }
 	svg_host_index *x = &h->host;
 	if ((rc = dmalloc(h, &h->d_bstart, 4 * ((size_t)x->nb + 1))) || (rc = dmalloc(h, &h->d_keys, 2 * x->items + 64)) ||
-	    (rc = dmalloc(h, &h->d_vals, 4 * x->items + 64)) || (rc = dmalloc(h, &h->d_values, (size_t)x->values_bytes + 64)) ||
-	    (rc = dmalloc(h, &h->d_chr, 4 * (size_t)x->n_chr + 64))) {
+	    (rc = dmalloc(h, &h->d_vals, 4 * x->items + 64))) {
 		svg_index_close(h);
 		return rc;
 	}
-	HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-	HIPCHK(hipMemcpy(h->d_bstart, x->bstart, 4 * ((size_t)x->nb + 1), hipMemcpyHostToDevice));
-	HIPCHK(hipMemcpy(h->d_keys, x->keys, 2 * x->items, hipMemcpyHostToDevice));
-	HIPCHK(hipMemcpy(h->d_vals, x->vals, 4 * x->items, hipMemcpyHostToDevice));
-	HIPCHK(hipMemcpy(h->d_values, x->values, x->values_bytes, hipMemcpyHostToDevice));
-	HIPCHK(hipMemcpy(h->d_chr, x->chr_end, 4 * (size_t)x->n_chr, hipMemcpyHostToDevice));
+	if (hipMemcpy(h->d_bstart, x->bstart, 4 * ((size_t)x->nb + 1), hipMemcpyHostToDevice) != hipSuccess ||
+	    hipMemcpy(h->d_keys, x->keys, 2 * x->items, hipMemcpyHostToDevice) != hipSuccess ||
+	    hipMemcpy(h->d_vals, x->vals, 4 * x->items, hipMemcpyHostToDevice) != hipSuccess) {
+		svg_set_error("upload of the index to HBM failed");
+		svg_index_close(h);
+		return SVG_E_DEVICE;
+	}
 	// the flat key/value arrays now live in HBM; keep only the small host parts
 	free(x->bstart); x->bstart = NULL;
 	free(x->keys); x->keys = NULL;
 	free(x->vals); x->vals = NULL;
-	h->dix.bstart = (const uint32_t *)h->d_bstart;
-	h->dix.keys = (const int16_t *)h->d_keys;
-	h->dix.vals = (const uint32_t *)h->d_vals;
-	h->dix.values = (const uint8_t *)h->d_values;
-	h->dix.chr_end = (const uint32_t *)h->d_chr;
-	h->dix.nb = x->nb;
-	h->dix.n_chr = x->n_chr;
-	h->dix.start_point = x->start_point;
-	h->dix.length = x->length;
-	h->dix.start_base_offset = x->start_base_offset;
-	h->dix.values_bytes = x->values_bytes;
-	h->dix.gap = x->gap;
-	h->dix.padding = x->padding;
-	hipDeviceProp_t prop;
-	HIPCHK(hipGetDeviceProperties(&prop, device));
-	h->n_cu = prop.multiProcessorCount;
-	if ((rc = dmalloc(h, (void **)&h->d_stats, 8 * sizeof(unsigned long long)))) { svg_index_close(h); return rc; }
-	const char *se = getenv("SVG_STATS");
-	h->stats_on = se && se[0] == '1';
+	if ((rc = svg_index_finish_device(h))) { svg_index_close(h); return rc; }
 	*out = h;
+	return 0;
+}
+
+extern "C" int svg_index_export(const svg_index *h, uint32_t *bstart, int16_t *keys, uint32_t *vals, uint8_t *values,
+                                uint32_t *chr_end)
+{
+	if (!h) { svg_set_error("svg_index_export: NULL handle"); return SVG_E_ARG; }
+	HIPCHK(hipSetDevice(h->device));
+	if (bstart) HIPCHK(hipMemcpy(bstart, h->d_bstart, 4 * ((size_t)h->host.nb + 1), hipMemcpyDeviceToHost));
+	if (keys) HIPCHK(hipMemcpy(keys, h->d_keys, 2 * h->host.items, hipMemcpyDeviceToHost));
+	if (vals) HIPCHK(hipMemcpy(vals, h->d_vals, 4 * h->host.items, hipMemcpyDeviceToHost));
+	if (values) memcpy(values, h->host.values, h->host.values_bytes);
+	if (chr_end) memcpy(chr_end, h->host.chr_end, 4 * (size_t)h->host.n_chr);
 	return 0;
 }
 
@@ -913,6 +904,7 @@ extern "C" int svg_index_get_info(const svg_index *h, svg_index_info *o)
 	o->n_chromosomes = h->host.n_chr;
 	o->device_bytes = h->device_bytes;
 	o->device = h->device;
+	o->array_values_bytes = h->host.values_bytes;
 	return 0;
 }
 
