@@ -4,10 +4,10 @@
 A "step" = one svg_vote_batch_device pass over one batch of synthetic reads
 resident in HBM (reads in, mapping_result_t[3] per read out).  Workloads
 (SURVEY.md §8(d)):
-  c2 (default): 10M x 100 bp SE reads per GPU vs a chr901-scale 1,000,000 bp
+  c2: 10M x 100 bp SE reads per GPU vs a chr901-scale 1,000,000 bp
       i.i.d. genome (seed 901), full one-block index (subread-buildindex -F -B),
       1% substitutions, 0.1% reads with a 1-5 bp indel, read seed 20261015.
-  c3: 50M x 100 bp SE reads per GPU vs a 3.0 Gbp 24-contig genome with repeat
+  c3 (default, the BASELINE.json metric): 50M x 100 bp SE reads per GPU vs a 3.0 Gbp 24-contig genome with repeat
       families, full one-block index.
 Multi-GPU (torchrun): one process per GPU, index replicated, reads sharded by
 rank (disjoint read-stream ranges), no collective on the data path; the only
@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default=os.environ.get("SVG_WORKLOAD", "c2"))
+    ap.add_argument("--workload", default=os.environ.get("SVG_WORKLOAD", "c3"))
     ap.add_argument("--reads", type=int, default=0, help="reads per GPU per step (default: workload size)")
     ap.add_argument("--workdir", default=os.environ.get("SVG_BENCH_DIR", ""))
     ap.add_argument("--cpu-sample", type=int, default=20_000_000)
