@@ -19,7 +19,7 @@ from .abi import (MAPPING_DTYPE, SUBJUNC_DTYPE, BIG_MARGIN_WORDS, ERRORS, PROGRA
                   default_params, read_fastq)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libsubread_amd.so")
+LIB_PATH = os.environ.get("SVG_LIB") or os.path.join(HERE, "lib", "libsubread_amd.so")
 CSRC = os.path.join(HERE, "csrc")
 
 # every symbol include/subread_vote.h declares

@@ -175,8 +175,17 @@ struct ReadCtx {
 	int np[2];          // probes per strand for each end (applied*gap)
 };
 
+#ifdef SVG_STAMPS
+#define STAMP(k) do { unsigned long long _t = __builtin_amdgcn_s_memtime(); acc[k] += _t - t_last; t_last = _t; } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
 template <int ENDS, int MAXL, int MAXP>
 struct Wave {
+#ifdef SVG_STAMPS
+	unsigned long long t_last, acc[8];
+#endif
 	WaveLDS<ENDS, MAXL, MAXP> *L;
 	uint32_t *cold[2];      // [ENDS] cold slot state
 	uint32_t *shift_locs[2];
@@ -383,6 +392,7 @@ struct Wave {
 		}
 		if (lane == 0) L->pcum[0] = 0;
 		wsync();
+		STAMP(2);
 		for (uint32_t c0 = 0; c0 < total; c0 += 512) {
 			uint32_t cn = total - c0 < 512 ? total - c0 : 512;
 			// gather
@@ -400,6 +410,7 @@ struct Wave {
 				L->cand_p[c] = (uint8_t)p;
 			}
 			wsync();
+			STAMP(2);
 			for (uint32_t c = 0; c < cn; c++) {
 				uint32_t kv = L->cand[c];
 				int p = L->cand_p[c];
@@ -407,6 +418,7 @@ struct Wave {
 				vote_one(e, kv, k, probe_off(e, p), round, high_b);
 			}
 			wsync();
+			STAMP(3);
 		}
 	}
 
@@ -726,7 +738,9 @@ struct Wave {
 			if (lane < 10) L->bm[e][lane] = 0;
 		}
 		wsync();
+		STAMP(0);
 		probe_all();
+		STAMP(1);
 		for (int strand = 0; strand < 2; strand++) {
 			cur_strand = strand;
 			for (int e = 0; e < ENDS; e++) {
@@ -739,6 +753,7 @@ struct Wave {
 					if (L->nshift[e] == 0) break;
 				}
 			}
+			STAMP(3);
 			if (ENDS == 2) topk(strand);
 			else if (L->max_vote[0] >= p.min_votes_first) topk(strand);
 			else if (rec_votes(L->res[0][0]) < 1) {
@@ -749,6 +764,7 @@ struct Wave {
 				}
 				wsync();
 			}
+			STAMP(4);
 		}
 		// write the read's records
 		for (int e = 0; e < ENDS; e++) {
@@ -782,8 +798,21 @@ __global__ void __launch_bounds__(64 * WPB) vote_kernel(KParams kp)
 		W.cold[e] = base + e * per_end;
 		W.shift_locs[e] = base + e * per_end + (size_t)NSLOT * COLD_WORDS;
 	}
+#ifdef SVG_STAMPS
+	for (int k = 0; k < 8; k++) W.acc[k] = 0;
+	W.t_last = __builtin_amdgcn_s_memtime();
+#endif
 	W.st_probes = W.st_items = W.st_hits = 0;
-	for (uint64_t r = gw; r < kp.n_reads; r += nw) W.run_read(r);
+	for (uint64_t r = gw; r < kp.n_reads; r += nw) {
+		W.run_read(r);
+#ifdef SVG_STAMPS
+		{ unsigned long long _t = __builtin_amdgcn_s_memtime(); W.acc[5] += _t - W.t_last; W.t_last = _t; }
+#endif
+	}
+#ifdef SVG_STAMPS
+	if (kp.stats && lane_id() == 0)
+		for (int k = 0; k < 8; k++) atomicAdd(&kp.stats[8 + k], W.acc[k]);
+#endif
 	if (kp.stats) {
 		unsigned long long a = W.st_items, h = W.st_hits;
 		for (int o = 32; o; o >>= 1) { a += __shfl_xor(a, o); h += __shfl_xor(h, o); }
@@ -827,8 +856,8 @@ int svg_index_finish_device(svg_index *h)
 	hipDeviceProp_t prop;
 	HIPCHK(hipGetDeviceProperties(&prop, h->device));
 	h->n_cu = prop.multiProcessorCount;
-	if ((rc = dmalloc(h, (void **)&h->d_stats, 8 * sizeof(unsigned long long)))) return rc;
-	HIPCHK(hipMemset(h->d_stats, 0, 8 * sizeof(unsigned long long)));
+	if ((rc = dmalloc(h, (void **)&h->d_stats, 16 * sizeof(unsigned long long)))) return rc;
+	HIPCHK(hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
 	const char *se = getenv("SVG_STATS");
 	h->stats_on = se && se[0] == '1';
 	return 0;
@@ -915,6 +944,14 @@ extern "C" int svg_set_stats(svg_index *h, int enable)
 	return 0;
 }
 
+// debug: raw device counters (16 words; 8..15 = per-phase wave cycles in SVG_STAMPS builds)
+extern "C" int svg_debug_counters(svg_index *h, unsigned long long *out16)
+{
+	if (!h || !out16) return SVG_E_ARG;
+	HIPCHK(hipMemcpy(out16, h->d_stats, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+	return 0;
+}
+
 extern "C" int svg_get_stats(const svg_index *h, svg_batch_stats *o)
 {
 	if (!h || !o) return SVG_E_ARG;
@@ -988,7 +1025,7 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	kp.low = h->dix.start_base_offset;
 	kp.high = h->dix.start_base_offset + h->dix.length;
 	if (h->stats_on) {
-		HIPCHK(hipMemsetAsync(h->d_stats, 0, 8 * sizeof(unsigned long long), st));
+		HIPCHK(hipMemsetAsync(h->d_stats, 0, 16 * sizeof(unsigned long long), st));
 		kp.stats = h->d_stats;
 	}
 	if (r2) rc = launch_t<2, 256, 64, 2>(h, kp, st);

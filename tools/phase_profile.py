@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase share of wave cycles of the vote kernel (SVG_STAMPS build).
+Run with SVG_LIB=subread_amd/lib/libsubread_amd_stamps.so.  Shares only -- the
+stamp build's run time is not a benchmark number."""
+import ctypes
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import subread_amd as sa  # noqa: E402
+from subread_amd.abi import default_params  # noqa: E402
+from subread_amd.sim import random_genome, simulate_reads, c3_lengths  # noqa: E402
+
+
+def main():
+    wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 5_000_000
+    paired = len(sys.argv) > 3 and sys.argv[3] == "pe"
+    if wl == "c3":
+        g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))
+    else:
+        g = random_genome([1_000_000], 901)
+    ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True)
+    r1 = simulate_reads(g, n, 100, seed=20261015)
+    r2 = simulate_reads(g, n, 100, seed=7) if paired else None
+    p = default_params(paired=paired)
+    ix.vote(p, r1, r2)
+    ix.set_stats(True)
+    t = time.time()
+    ix.vote(p, r1, r2)
+    dt = time.time() - t
+    c = (ctypes.c_ulonglong * 16)()
+    sa.lib().svg_debug_counters(ix.h, c)
+    names = ["text+init", "probe", "gather", "vote", "topk", "output", "-", "-"]
+    tot = sum(c[8 + k] for k in range(6))
+    print("workload %s reads %d paired %s wall %.3fs probes %d items %d hits %d results %d" % (
+        wl, n, paired, dt, c[0], c[1], c[2], c[3]))
+    for k in range(6):
+        print("  %-10s %6.2f%%  %8.0f cycles/read" % (names[k], 100.0 * c[8 + k] / max(1, tot), c[8 + k] / n))
+
+
+if __name__ == "__main__":
+    main()
