@@ -65,7 +65,9 @@ struct KParams {
 };
 
 // ---------------------------------------------------------------------------------------------
-// LDS layout of one wave
+// LDS layout of one wave.  Row occupancy (items[30]) and max_vote live in
+// registers (lane 32*end+row holds items[row]); only slot state is in LDS.
+#define CAND_CAP 256
 template <int ENDS, int MAXL, int MAXP>
 struct WaveLDS {
 	uint32_t pos[ENDS][NSLOT];            // slot positions, [row*24+slot]
@@ -74,8 +76,8 @@ struct WaveLDS {
 	uint16_t pfwd[ENDS][2][MAXP];         // equal-key items at mid..last
 	uint16_t pbwd[ENDS][2][MAXP];         // equal-key items at first..mid-1
 	uint32_t pcum[MAXP + 1];              // candidate prefix of the (strand,end) being replayed
-	uint32_t cand[512];                   // kv of queued candidates
-	uint8_t cand_p[512];                  // probe index of queued candidates
+	uint32_t cand[CAND_CAP];              // kv of queued candidates
+	uint32_t cand_ko[CAND_CAP];           // subread_no | offset << 8
 	uint32_t res[ENDS][3][17];            // the read's stored mapping_result_t (68 B)
 	uint32_t tmp[ENDS][3][17];            // top-K output under construction
 	uint32_t jres[ENDS][3][4];            // subjunc_result_t
@@ -84,12 +86,7 @@ struct WaveLDS {
 	uint16_t simp_slot[ENDS][64];         // slot index, or 0x8000|stored index
 	uint16_t simp_votes[ENDS][64];
 	uint16_t bm[ENDS][10];
-	uint16_t rowstart[ENDS][32];
 	char text[ENDS][2][MAXL];             // strand 0 form / strand 1 (reversed) form
-	uint8_t items[ENDS][32];
-	int32_t max_vote[ENDS];
-	int32_t nshift[ENDS];
-	int32_t comb_i[4], comb_j[4], comb_s[4];
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -192,6 +189,12 @@ struct Wave {
 	const KParams *kp;
 	ReadCtx rc;
 	unsigned long long st_probes, st_items, st_hits;
+	int items_v;            // lane 32*e + r: items[r] of table e (gene_vote_t.items)
+	int max_vote[2];        // gene_vote_t.max_vote per table (wave-uniform)
+	int nshift[2];          // shift_indel_NO per table (wave-uniform)
+	int cur_strand;
+
+	__device__ __forceinline__ static int rd(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 	// ---------------------------------------------------------------- probe offset of probe p
 	__device__ __forceinline__ int probe_off(int e, int p) const
@@ -264,128 +267,147 @@ struct Wave {
 	}
 
 	// ---------------------------------------------------------------- vote-table reset (init_gene_vote)
-	__device__ __forceinline__ void table_reset(int e)
+	template <int E>
+	__device__ __forceinline__ void table_reset()
 	{
-		if (lane_id() < 32) L->items[e][lane_id()] = 0;
-		if (lane_id() == 0) L->max_vote[e] = 0;
-		wsync();
+		if ((lane_id() >> 5) == E) items_v = 0;
+		max_vote[E] = 0;
 	}
 
-	// ---------------------------------------------------------------- phase V: one candidate
-	__device__ void vote_one(int e, uint32_t kv, int k, int off, int round, uint32_t high_b)
+	// one group of <= 64 candidate slots, lanes in the reference's scan order
+	// (rows iix = 0,+5,-5,..., slots ascending).  Returns true when a slot took the vote.
+	template <int E>
+	__device__ __forceinline__ bool vote_group(bool valid, int slot, uint32_t kv, int kP1, int off, int round)
 	{
 		const int lane = lane_id();
-		const int kP1 = k + 1;
+		const int tol = kp->tol;
+		uint32_t P = 0u, M = 0u;
+		if (valid) { P = L->pos[E][slot]; M = L->meta[E][slot]; }
+		int d = (int)(kv - P);
+		int sh = m_shift(M);
+		int t = (round > 0 && sh) ? 0 : tol;
+		bool match = valid && d >= -t && d <= t;
+		unsigned long long mm = ballot(match);
+		if (!mm) return false;
+		int votes = m_votes(M), last = m_last(M), tl = m_toli(M), cur = m_cursor(M);
+		bool sev = match && round == 0 && tl > 0 && d == 0 && !sh;
+		bool rb = false;
+		if (match && last == kP1 && tl > 0) {    // roll-back test (sorted-hashtable.c:1027-1039)
+			const uint32_t *cs = cold_slot(cold[E], slot);
+			int md = tl >= 3 ? cold_rec(cs, tl - 1) : 0;
+			int nd = md - d;
+			md -= cold_rec(cs, tl + 2);
+			rb = abs(md) > abs(nd);
+		}
+		int last2 = rb ? last - 1 : last;
+		bool wv = match && !(kP1 <= last2);
+		unsigned long long wm = ballot(wv);
+		int wl = wm ? (__ffsll((long long)wm) - 1) : 64;
+		bool apply = match && lane <= wl;
+		unsigned long long smask = ballot(apply && sev);
+		if (apply && sev) shift_locs[E][nshift[E] + lanes_below(smask)] = P;
+		nshift[E] += __popcll(smask);
+		int nvotes = votes;
+		if (apply) {
+			int nlast = last, ntl = tl, nsh = sh | (sev ? 1 : 0), ncur = cur;
+			if (rb) { ntl -= 3; nlast -= 1; nvotes -= 1; }
+			if (lane == wl) {
+				uint32_t *cs = cold_slot(cold[E], slot);
+				nvotes += 1;
+				// coverage_end = max(coverage_end, off+16): off rises strictly along the probe
+				// order of a round (step >= gap<<16), so the new value is always off+16
+				((uint16_t *)cs)[1] = (uint16_t)(off + 16);
+				if (d == ncur) cold_set_rec(cs, ntl + 1, kP1);
+				else {
+					int t2 = ntl + 3;
+					if (t2 < REC_LEN) {
+						ntl = t2;
+						cold_set_rec(cs, t2, kP1);
+						cold_set_rec(cs, t2 + 1, kP1);
+						cold_set_rec(cs, t2 + 2, d);
+						if (t2 < REC_LEN - 3) cold_set_rec(cs, t2 + 3, 0);
+					}
+					ncur = (int)(int8_t)d;
+				}
+				nlast = kP1;
+			}
+			L->meta[E][slot] = m_pack(nvotes, nlast, ntl, nsh, ncur);
+		}
+		wsync();
+		if (wm) {
+			int nv = rd(nvotes, wl);
+			if (max_vote[E] < nv) max_vote[E] = nv;
+			return true;
+		}
+		return false;
+	}
+
+	// ---------------------------------------------------------------- phase V: one candidate (gehash_go_X body)
+	template <int E>
+	__device__ void vote_one(uint32_t kv, int kP1, int off, int round, uint32_t high_b)
+	{
+		const int lane = lane_id();
 		const int tol = kp->tol;
 		const uint32_t r0 = (kv / 5u) % ROWS;
-		const int n0 = L->items[e][r0];
-		uint32_t *cold = this->cold[e];
+		const int n0 = rd(items_v, E * 32 + (int)r0);
 		bool found = false;
-		for (int iix = 0; iix <= kp->ii_end; iix = iix > 0 ? -iix : (-iix + 5)) {
-			uint32_t r = iix ? ((kv + (uint32_t)iix) / 5u) % ROWS : r0;
-			int cnt = iix ? (int)L->items[e][r] : n0;
-			if (!cnt) continue;
-			int slot = (int)r * SPACE + lane;
-			bool valid = lane < cnt;
-			uint32_t P = valid ? L->pos[e][slot] : 0u;
-			uint32_t M = valid ? L->meta[e][slot] : 0u;
-			int d = (int)(kv - P);
-			int sh = m_shift(M);
-			int t = (round > 0 && sh) ? 0 : tol;
-			bool match = valid && d >= -t && d <= t;
-			unsigned long long mm = ballot(match);
-			if (!mm) continue;
-			int votes = m_votes(M), last = m_last(M), tl = m_toli(M), cur = m_cursor(M);
-			bool sev = match && round == 0 && tl > 0 && d == 0 && !sh;
-			bool rb = false;
-			if (match && last == kP1 && tl > 0) {
-				const uint32_t *cs = cold_slot(cold, slot);
-				int md = tl >= 3 ? cold_rec(cs, tl - 1) : 0;
-				int nd = md - d;
-				md -= cold_rec(cs, tl + 2);
-				rb = abs(md) > abs(nd);
+		if (kp->ii_end == 5) {
+			// the three rows r0, r0+1, r0-1 (iix = 0, +5, -5) fetched in one LDS round trip
+			const uint32_t rp = ((kv + 5u) / 5u) % ROWS, rm = ((kv - 5u) / 5u) % ROWS;
+			const int np_ = rd(items_v, E * 32 + (int)rp), nm = rd(items_v, E * 32 + (int)rm);
+			const int T = n0 + np_ + nm;
+			for (int f0 = 0; f0 < T && !found; f0 += 64) {
+				int f = f0 + lane;
+				int seg = (f >= n0) + (f >= n0 + np_);
+				int s = f - (seg == 0 ? 0 : (seg == 1 ? n0 : n0 + np_));
+				uint32_t r = seg == 0 ? r0 : (seg == 1 ? rp : rm);
+				found = vote_group<E>(f < T, (int)r * SPACE + s, kv, kP1, off, round);
 			}
-			int last2 = rb ? last - 1 : last;
-			bool wv = match && !(kP1 <= last2);
-			unsigned long long wm = ballot(wv);
-			int wl = wm ? (__ffsll((long long)wm) - 1) : 64;
-			bool apply = match && lane <= wl;
-			unsigned long long smask = ballot(apply && sev);
-			if (apply && sev) {
-				int at = L->nshift[e] + lanes_below(smask);
-				this->shift_locs[e][at] = P;
+		} else {
+			for (int iix = 0; iix <= kp->ii_end && !found; iix = iix > 0 ? -iix : (-iix + 5)) {
+				uint32_t r = iix ? ((kv + (uint32_t)iix) / 5u) % ROWS : r0;
+				int cnt = iix ? rd(items_v, E * 32 + (int)r) : n0;
+				if (!cnt) continue;
+				found = vote_group<E>(lane < cnt, (int)r * SPACE + lane, kv, kP1, off, round);
 			}
-			if (apply) {
-				int nvotes = votes, nlast = last, ntl = tl, nsh = sh | (sev ? 1 : 0), ncur = cur;
-				if (rb) { ntl -= 3; nlast -= 1; nvotes -= 1; }
-				if (lane == wl) {
-					uint32_t *cs = cold_slot(cold, slot);
-					nvotes += 1;
-					// coverage_end = max(coverage_end, off+16): off rises strictly along the probe
-					// order of a round (step >= gap<<16), so the new value is always off+16
-					((uint16_t *)cs)[1] = (uint16_t)(off + 16);
-					if (d == ncur) cold_set_rec(cs, ntl + 1, kP1);
-					else {
-						int t2 = ntl + 3;
-						if (t2 < REC_LEN) {
-							ntl = t2;
-							cold_set_rec(cs, t2, kP1);
-							cold_set_rec(cs, t2 + 1, kP1);
-							cold_set_rec(cs, t2 + 2, d);
-							if (t2 < REC_LEN - 3) cold_set_rec(cs, t2 + 3, 0);
-						}
-						ncur = (int)(int8_t)d;
-					}
-					nlast = kP1;
-					if (L->max_vote[e] < nvotes) L->max_vote[e] = nvotes;
-				}
-				L->meta[e][slot] = m_pack(nvotes, nlast, ntl, nsh, ncur);
-			}
-			wsync();
-			if (lane == 0) L->nshift[e] += __popcll(smask);
-			wsync();
-			if (wm) { found = true; break; }
 		}
 		if (!found && kv >= kp->low && kv <= high_b && n0 < SPACE) {
 			int sh = 0;
 			if (round > 0) {
-				int ns = L->nshift[e];
 				bool any = false;
-				for (int j = lane; j < ns; j += 64) {
-					uint32_t loc = this->shift_locs[e][j];
+				for (int j = lane; j < nshift[E]; j += 64) {
+					uint32_t loc = shift_locs[E][j];
 					if (kv >= loc - (uint32_t)tol && kv <= loc + (uint32_t)tol) any = true;
 				}
 				sh = ballot(any) ? 1 : 0;
 			}
 			if (lane == 0) {
 				int slot = (int)r0 * SPACE + n0;
-				uint32_t *cs = cold_slot(cold, slot);
-				L->items[e][r0] = (uint8_t)(n0 + 1);
-				L->pos[e][slot] = kv;
-				L->meta[e][slot] = m_pack(1, kP1, 0, sh, 0);
+				uint32_t *cs = cold_slot(cold[E], slot);
+				L->pos[E][slot] = kv;
+				L->meta[E][slot] = m_pack(1, kP1, 0, sh, 0);
 				cs[0] = (uint32_t)(uint16_t)off | ((uint32_t)(uint16_t)(off + 16) << 16);
-				cold_set_rec(cs, 0, kP1);
-				cold_set_rec(cs, 1, kP1);
-				cold_set_rec(cs, 2, 0);
-				cold_set_rec(cs, 3, 0);
-				if (L->max_vote[e] == 0) L->max_vote[e] = 1;
+				cs[1] = (uint32_t)(uint8_t)kP1 | ((uint32_t)(uint8_t)kP1 << 8);   // rec[0..3] = k+1, k+1, 0, 0
 			}
+			if (lane == E * 32 + (int)r0) items_v = n0 + 1;
+			if (max_vote[E] == 0) max_vote[E] = 1;
 			wsync();
 		}
 	}
 
 	// ---------------------------------------------------------------- phases G+V for one (strand, end, round)
-	__device__ void replay(int e, int s, int round)
+	template <int E>
+	__device__ void replay(int s, int round)
 	{
 		const int lane = lane_id();
-		const int np = rc.np[e];
+		const int np = rc.np[E];
 		const int gap = kp->ix.gap;
-		const uint32_t high_b = kp->high - (uint32_t)rc.rl[e];
+		const uint32_t high_b = kp->high - (uint32_t)rc.rl[E];
 		// candidate prefix over probes (probe order = subread_no, xk1)
 		uint32_t total = 0;
 		for (int p0 = 0; p0 < np; p0 += 64) {
 			int p = p0 + lane;
-			uint32_t h = p < np ? (uint32_t)L->pfwd[e][s][p] + L->pbwd[e][s][p] : 0u;
+			uint32_t h = p < np ? (uint32_t)L->pfwd[E][s][p] + L->pbwd[E][s][p] : 0u;
 			uint32_t inc = wave_incl_scan(h);
 			if (p < np) L->pcum[p + 1] = total + inc;
 			total += __shfl(inc, 63);
@@ -393,29 +415,33 @@ struct Wave {
 		if (lane == 0) L->pcum[0] = 0;
 		wsync();
 		STAMP(2);
-		for (uint32_t c0 = 0; c0 < total; c0 += 512) {
-			uint32_t cn = total - c0 < 512 ? total - c0 : 512;
-			// gather
+		for (uint32_t c0 = 0; c0 < total; c0 += CAND_CAP) {
+			uint32_t cn = total - c0 < CAND_CAP ? total - c0 : CAND_CAP;
+			// gather in visiting order: probe p, then mid..last, then mid-1..first
 			for (uint32_t c = lane; c < cn; c += 64) {
 				uint32_t cc = c0 + c;
-				int lo = 0, hi = np - 1;   // find probe p with pcum[p] <= cc < pcum[p+1]
+				int lo = 0, hi = np - 1;   // probe p with pcum[p] <= cc < pcum[p+1]
 				while (lo < hi) { int m = (lo + hi + 1) >> 1; if (L->pcum[m] <= cc) lo = m; else hi = m - 1; }
 				int p = lo;
 				uint32_t j = cc - L->pcum[p];
-				uint32_t fwd = L->pfwd[e][s][p];
-				uint32_t mid = L->pmid[e][s][p];
+				uint32_t fwd = L->pfwd[E][s][p];
+				uint32_t mid = L->pmid[E][s][p];
 				uint32_t item = j < fwd ? mid + j : mid - 1 - (j - fwd);
-				uint32_t off = (uint32_t)probe_off(e, p);
-				L->cand[c] = kp->ix.vals[item] - off;
-				L->cand_p[c] = (uint8_t)p;
+				int off = probe_off(E, p);
+				L->cand[c] = kp->ix.vals[item] - (uint32_t)off;
+				L->cand_ko[c] = (uint32_t)(p / gap) | ((uint32_t)off << 8);
 			}
 			wsync();
 			STAMP(2);
-			for (uint32_t c = 0; c < cn; c++) {
-				uint32_t kv = L->cand[c];
-				int p = L->cand_p[c];
-				int k = p / gap;
-				vote_one(e, kv, k, probe_off(e, p), round, high_b);
+			for (uint32_t cb = 0; cb < cn; cb += 64) {
+				int kvv = (int)L->cand[cb + (lane & (CAND_CAP - 1))];
+				int kov = (int)L->cand_ko[cb + (lane & (CAND_CAP - 1))];
+				int m = cn - cb < 64 ? (int)(cn - cb) : 64;
+				for (int j = 0; j < m; j++) {
+					uint32_t kv = (uint32_t)rd(kvv, j);
+					uint32_t ko = (uint32_t)rd(kov, j);
+					vote_one<E>(kv, (int)(ko & 255) + 1, (int)(ko >> 8), round, high_b);
+				}
 			}
 			wsync();
 			STAMP(3);
@@ -425,7 +451,7 @@ struct Wave {
 	// ---------------------------------------------------------------- record helpers
 	__device__ void rec_zero(uint32_t *r) { if (lane_id() < 17) r[lane_id()] = 0; }
 
-	// copy_vote_to_alignment_res (core-junction.c:1058-1071) for slot -> tmp record r
+	// copy_vote_to_alignment_res (core-junction.c:1058-1071) for slot -> record r (pre-zeroed)
 	__device__ void copy_vote(int e, int slot, uint32_t *r)
 	{
 		const int lane = lane_id();
@@ -438,19 +464,15 @@ struct Wave {
 		int nrec = 3 * T;
 		int last_ind = __shfl(v, nrec > 0 ? nrec - 1 : 0);
 		int16_t rv = lane < nrec ? (int16_t)v : (int16_t)0;
-		// records are zeroed before; write the 22 shorts of selected_indel_record as 11 dwords
 		int16_t rv_hi = __shfl(rv, (2 * lane + 1) & 63);
 		int16_t rv_lo = __shfl(rv, (2 * lane) & 63);
 		if (lane < 11) r[MR_REC / 4 + lane] = (uint32_t)(uint16_t)rv_lo | ((uint32_t)(uint16_t)rv_hi << 16);
 		if (lane == 0) {
 			uint32_t M = L->meta[e][slot];
-			uint32_t cw = cs[0];
-			int negative = 0;   // masks: every slot of a (strand) table carries that strand
 			r[0] = L->pos[e][slot];
-			(void)negative;
 			r[2] = (uint32_t)(uint16_t)m_votes(M) | ((uint32_t)(uint16_t)rc.applied[e] << 16);
 			r[3] = (uint32_t)(uint8_t)(int8_t)(nrec > 0 ? last_ind : 0) << 8;   // noninf 0, indels
-			r[15] = cw;   // confident_coverage_start | confident_coverage_end << 16
+			r[15] = cs[0];   // confident_coverage_start | confident_coverage_end << 16
 			r[16] = 0;
 		}
 	}
@@ -479,6 +501,18 @@ struct Wave {
 		return -1;
 	}
 
+	// flattened (row-major) used-slot index f -> slot, given the inclusive row prefix rs_v
+	// (lane 32*e+r holds items[0..r] of table e)
+	__device__ __forceinline__ int slot_of(int e, int rs_v, int f) const
+	{
+		int row = 0;
+#pragma unroll
+		for (int r = 0; r < ROWS - 1; r++) row += (rd(rs_v, e * 32 + r) <= f);
+		int start = __shfl(rs_v, (e * 32 + row - 1) & 63);
+		if (row == 0) start = 0;
+		return row * SPACE + (f - start);
+	}
+
 	// ---------------------------------------------------------------- phase K
 	__device__ void topk(int strand)
 	{
@@ -487,26 +521,27 @@ struct Wave {
 		int top[2][3] = {{0, 0, 0}, {0, 0, 0}};
 		int nsimp[2] = {0, 0};
 		constexpr int TS = 3;   // p.top_scores, validated == 3 on the host
-		for (int e = 0; e < ENDS; e++) {
-			// row prefix of used slots
-			int it = lane < ROWS ? L->items[e][lane] : 0;
-			int inc = (int)wave_incl_scan((uint32_t)it);
-			if (lane < ROWS) L->rowstart[e][lane + 1] = (uint16_t)inc;
-			if (lane == 0) L->rowstart[e][0] = 0;
+		// inclusive row prefix of used slots per table
+		int mine = ((lane & 31) < ROWS) ? items_v : 0;
+		int rs_v = 0;
+		{
+			int lo = lane & 31;
+			int v = mine;
+			for (int o = 1; o < 32; o <<= 1) { int t = __shfl_up(v, o); if (lo >= o) v += t; }
+			rs_v = v;
 		}
-		wsync();
+		int U[2];
+		U[0] = rd(rs_v, ROWS - 1);
+		U[1] = ENDS == 2 ? rd(rs_v, 32 + ROWS - 1) : 0;
 		for (int e = 0; e < ENDS; e++) {
-			int U = L->rowstart[e][ROWS];
 			// top-3 distinct over table votes and stored results (update_top_three)
 			int bound = 0x7fffffff;
 			for (int t = 0; t < TS; t++) {
 				int best = 0;
-				for (int f0 = 0; f0 < U; f0 += 64) {
+				for (int f0 = 0; f0 < U[e]; f0 += 64) {
 					int f = f0 + lane;
-					if (f < U) {
-						int r = 0;
-						while (L->rowstart[e][r + 1] <= f) r++;
-						int v = m_votes(L->meta[e][r * SPACE + (f - L->rowstart[e][r])]);
+					if (f < U[e]) {
+						int v = m_votes(L->meta[e][slot_of(e, rs_v, f)]);
 						if (v < bound && v > best) best = v;
 					}
 				}
@@ -516,28 +551,24 @@ struct Wave {
 				}
 				best = wave_max(best);
 				top[e][t] = best;
-				bound = best > 0 ? best : 0;
-				if (best == 0) bound = 0;
+				bound = best;
 			}
 		}
 		// candidate lists (simples)
 		for (int e = 0; e < ENDS; e++) {
-			int U = L->rowstart[e][ROWS];
 			int ns = 0;
 			for (int t = 0; t < TS; t++) {
 				int N = top[e][t];
 				if (ns >= p.max_vote_simples) break;
 				if (N < 1 || (top[e][0] - N > p.max_vote_number_cutoff)) break;
-				for (int f0 = 0; f0 < U && ns < p.max_vote_simples; f0 += 64) {
+				for (int f0 = 0; f0 < U[e] && ns < p.max_vote_simples; f0 += 64) {
 					int f = f0 + lane;
 					int slot = 0, v = -1;
-					if (f < U) {
-						int r = 0;
-						while (L->rowstart[e][r + 1] <= f) r++;
-						slot = r * SPACE + (f - L->rowstart[e][r]);
+					if (f < U[e]) {
+						slot = slot_of(e, rs_v, f);
 						v = m_votes(L->meta[e][slot]);
 					}
-					bool sel = f < U && v == N && v >= p.min_votes_second;
+					bool sel = f < U[e] && v == N && v >= p.min_votes_second;
 					unsigned long long sm = ballot(sel);
 					int at = ns + lanes_below(sm);
 					if (sel && at < p.max_vote_simples) {
@@ -563,7 +594,6 @@ struct Wave {
 			nsimp[e] = ns;
 		}
 		wsync();
-		// tmp records
 		for (int e = 0; e < ENDS; e++)
 			for (int i = 0; i < 3; i++) rec_zero(L->tmp[e][i]);
 		wsync();
@@ -597,12 +627,10 @@ struct Wave {
 						if (pe || mn >= p.min_votes_first) sc = (va + vb) * (pe ? 1300 : (same ? 1000 : 800));
 					}
 				}
-				// merge lane candidates into the running top-3
 				for (int r = 0; r < 3; r++) {
 					int m = wave_max(sc);
 					if (m < 0) break;
 					int qi = wave_min(sc == m ? q : 0x7fffffff);
-					// insert (m, qi) into bs/bidx ordered by score desc, index asc
 					int pos3 = 3;
 					for (int t = 0; t < 3; t++) {
 						if (bs[t] < m || (bs[t] == m && bidx[t] > qi)) { pos3 = t; break; }
@@ -676,15 +704,24 @@ struct Wave {
 			if (lane_id() < 17) L->tmp[e][c][lane_id()] = L->res[e][sl & 3][lane_id()];
 		} else {
 			copy_vote(e, sl, L->tmp[e][c]);
-			if (lane_id() == 0) {
-				// result_flags: IS_NEGATIVE_STRAND mask of the slot (the table's strand)
-				L->tmp[e][c][1] = cur_strand ? (uint32_t)SVG_NEGATIVE_STRAND_FLAG : 0u;
-			}
+			// result_flags: IS_NEGATIVE_STRAND mask of the slot (every slot of a table has the table's strand)
+			if (lane_id() == 0) L->tmp[e][c][1] = cur_strand ? (uint32_t)SVG_NEGATIVE_STRAND_FLAG : 0u;
 		}
 		wsync();
 	}
 
-	int cur_strand;
+	// voting of one end for one strand: init_gene_vote + subread loop + shift-indel round
+	template <int E>
+	__device__ void vote_end(int strand)
+	{
+		nshift[E] = 0;
+		if (rc.np[E] == 0) { table_reset<E>(); return; }
+		for (int round = 0; round < 2; round++) {
+			table_reset<E>();
+			replay<E>(strand, round);
+			if (nshift[E] == 0) break;
+		}
+	}
 
 	// ---------------------------------------------------------------- one read
 	__device__ void run_read(uint64_t r)
@@ -743,19 +780,11 @@ struct Wave {
 		STAMP(1);
 		for (int strand = 0; strand < 2; strand++) {
 			cur_strand = strand;
-			for (int e = 0; e < ENDS; e++) {
-				if (lane == 0) L->nshift[e] = 0;
-				wsync();
-				if (rc.np[e] == 0) { table_reset(e); continue; }
-				for (int round = 0; round < 2; round++) {
-					table_reset(e);
-					replay(e, strand, round);
-					if (L->nshift[e] == 0) break;
-				}
-			}
+			vote_end<0>(strand);
+			if constexpr (ENDS == 2) vote_end<1>(strand);
 			STAMP(3);
 			if (ENDS == 2) topk(strand);
-			else if (L->max_vote[0] >= p.min_votes_first) topk(strand);
+			else if (max_vote[0] >= p.min_votes_first) topk(strand);
 			else if (rec_votes(L->res[0][0]) < 1) {
 				if (lane == 0) {
 					uint32_t *r0 = L->res[0][0];
