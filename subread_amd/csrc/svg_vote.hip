@@ -502,7 +502,8 @@ struct Wave {
 	}
 
 	// flattened (row-major) used-slot index f -> slot, given the inclusive row prefix rs_v
-	// (lane 32*e+r holds items[0..r] of table e)
+	// (lane 32*e+r holds items[0..r] of table e).  Must run with every lane active: the
+	// cross-lane read (ds_bpermute) returns nothing useful from inactive source lanes.
 	__device__ __forceinline__ int slot_of(int e, int rs_v, int f) const
 	{
 		int row = 0;
@@ -540,8 +541,9 @@ struct Wave {
 				int best = 0;
 				for (int f0 = 0; f0 < U[e]; f0 += 64) {
 					int f = f0 + lane;
+					int sl = slot_of(e, rs_v, f);   // all lanes active: slot_of shuffles
 					if (f < U[e]) {
-						int v = m_votes(L->meta[e][slot_of(e, rs_v, f)]);
+						int v = m_votes(L->meta[e][sl]);
 						if (v < bound && v > best) best = v;
 					}
 				}
@@ -563,11 +565,8 @@ struct Wave {
 				if (N < 1 || (top[e][0] - N > p.max_vote_number_cutoff)) break;
 				for (int f0 = 0; f0 < U[e] && ns < p.max_vote_simples; f0 += 64) {
 					int f = f0 + lane;
-					int slot = 0, v = -1;
-					if (f < U[e]) {
-						slot = slot_of(e, rs_v, f);
-						v = m_votes(L->meta[e][slot]);
-					}
+					int slot = slot_of(e, rs_v, f), v = -1;   // all lanes active: slot_of shuffles
+					if (f < U[e]) v = m_votes(L->meta[e][slot]);
 					bool sel = f < U[e] && v == N && v >= p.min_votes_second;
 					unsigned long long sm = ballot(sel);
 					int at = ns + lanes_below(sm);
