@@ -67,7 +67,7 @@ struct KParams {
 // ---------------------------------------------------------------------------------------------
 // LDS layout of one wave.  Row occupancy (items[30]) and max_vote live in
 // registers (lane 32*end+row holds items[row]); only slot state is in LDS.
-#define QCAP 128
+#define CAND_CAP 256
 template <int ENDS, int MAXL, int MAXP>
 struct WaveLDS {
 	uint32_t pos[ENDS][NSLOT];            // slot positions, [row*24+slot]
@@ -75,10 +75,9 @@ struct WaveLDS {
 	uint32_t pmid[ENDS][2][MAXP];         // probe: binary-search midpoint (absolute item index)
 	uint16_t pfwd[ENDS][2][MAXP];         // equal-key items at mid..last
 	uint16_t pbwd[ENDS][2][MAXP];         // equal-key items at first..mid-1
-	uint32_t pcum[MAXP + 1];              // candidate prefix (fallback gather only)
-	uint32_t qkv[ENDS][2][QCAP];          // candidate queue per (end, strand): kv in visiting order
-	uint8_t qp[ENDS][2][QCAP];            // ... and the probe it came from
-	int32_t qn[ENDS][2];                  // queue length, or -1: replay through the fallback gather
+	uint32_t pcum[MAXP + 1];              // candidate prefix of the (strand,end) being replayed
+	uint32_t cand[CAND_CAP];              // kv of queued candidates
+	uint32_t cand_ko[CAND_CAP];           // subread_no | offset << 8
 	uint32_t res[ENDS][3][17];            // the read's stored mapping_result_t (68 B)
 	uint32_t tmp[ENDS][3][17];            // top-K output under construction
 	uint32_t jres[ENDS][3][4];            // subjunc_result_t
@@ -208,143 +207,60 @@ struct Wave {
 	}
 
 	// ---------------------------------------------------------------- phase P: all probes of the read
-	// Stage 1 (lanes = probes): pack the 16-mer, hash it, read the bucket bounds.
-	// Stage 2 (8 probes in flight): the wave loads each bucket whole (keys and values,
-	// lane l = item l), replays gehash_go_X's binary search on the keys with readlane,
-	// takes the equal-key run from a ballot (keys are sorted, so the run is contiguous)
-	// and appends kv = value - offset to the (end, strand) queue in visiting order
-	// mid..last, mid-1..first (sorted-hashtable.c:947-1119).  Buckets of more than 64
-	// items, or queues over QCAP, switch that (end, strand) to the fallback gather.
 	__device__ void probe_all()
 	{
 		const DevIndex &ix = kp->ix;
-		const int lane = lane_id();
 		int total = 0;
 		int base[2][2];
 		for (int e = 0; e < ENDS; e++)
 			for (int s = 0; s < 2; s++) { base[e][s] = total; total += rc.np[e]; }
-		if (lane < ENDS * 2) L->qn[lane >> 1][lane & 1] = 0;
-		wsync();
 		for (int p0 = 0; p0 < total; p0 += 64) {
-			const int id = p0 + lane;
-			int e = 0, s = 0;
-			for (int ee = 0; ee < ENDS; ee++)
-				for (int ss = 0; ss < 2; ss++)
-					if (rc.np[ee] > 0 && id >= base[ee][ss]) { e = ee; s = ss; }
-			const int p = id - base[e][s];
-			int k16 = 0, n = 0;
-			uint32_t first = 0;
+			int id = p0 + lane_id();
 			if (id < total) {
+				int e = 0, s = 0;
+				for (int ee = 0; ee < ENDS; ee++)
+					for (int ss = 0; ss < 2; ss++)
+						if (rc.np[ee] > 0 && id >= base[ee][ss]) { e = ee; s = ss; }
+				int p = id - base[e][s];
 				int off = probe_off(e, p);
 				const char *t = L->text[e][s] + off;
 				uint32_t key = 0;
 #pragma unroll
 				for (int i = 0; i < 16; i++) key |= b2i(t[i]) << (30 - 2 * i);
 				uint32_t b = key % ix.nb;
-				k16 = (int16_t)(key / ix.nb);
-				first = ix.bstart[b];
-				n = (int)(ix.bstart[b + 1] - first);
-				st_items += n;
-			}
-			const int cnt = total - p0 < 64 ? total - p0 : 64;
-			bool slow = false;   // this lane's probe needs the per-lane search (bucket > 64 items)
-			for (int j0 = 0; j0 < cnt; j0 += 8) {
-				int K[8];
-				uint32_t V[8];
-#pragma unroll
-				for (int j = 0; j < 8; j++) {
-					int q = j0 + j < cnt ? j0 + j : cnt - 1;
-					int nj = rd(n, q);
-					uint32_t fj = (uint32_t)rd((int)first, q);
-					K[j] = 0x7fffffff;
-					V[j] = 0;
-					if (lane < nj && nj <= 64) { K[j] = ix.keys[fj + lane]; V[j] = ix.vals[fj + lane]; }
-				}
-#pragma unroll
-				for (int j = 0; j < 8; j++) {
-					const int q = j0 + j;
-					if (q >= cnt) break;
-					const int nj = rd(n, q), kq = rd(k16, q);
-					const int qid = p0 + q;
-					int qe = 0, qs = 0;
-					for (int ee = 0; ee < ENDS; ee++)
-						for (int ss = 0; ss < 2; ss++)
-							if (rc.np[ee] > 0 && qid >= base[ee][ss]) { qe = ee; qs = ss; }
-					const int qp_ = qid - base[qe][qs];
-					int fwd = 0, bwd = 0, mid = 0;
-					if (nj > 64) {
-						if (lane == q) slow = true;
-						continue;
-					}
-					if (nj > 0) {
-						int lo = 0, hi = nj - 1, m = 0;
-						bool hit = false;
-						for (;;) {
-							m = (lo + hi) >> 1;
-							int kk = rd(K[j], m);
-							if (kk > kq) hi = m - 1;
-							else if (kk < kq) lo = m + 1;
-							else { hit = true; break; }
-							if (hi < lo) break;
-						}
-						if (hit) {
-							unsigned long long eq = ballot(lane < nj && K[j] == kq);
-							int fr = __ffsll((long long)eq) - 1, lr = 63 - __clzll((long long)eq);
-							fwd = lr - m + 1;
-							bwd = m - fr;
-							mid = m;
-							int h = fwd + bwd;
-							int qb = L->qn[qe][qs];
-							if (qb >= 0) {
-								if (qb + h <= QCAP) {
-									if (lane >= fr && lane <= lr) {
-										int idx = lane >= m ? lane - m : fwd + (m - 1 - lane);
-										L->qkv[qe][qs][qb + idx] = V[j] - (uint32_t)probe_off(qe, qp_);
-										L->qp[qe][qs][qb + idx] = (uint8_t)qp_;
-									}
-									if (lane == 0) L->qn[qe][qs] = qb + h;
-								} else if (lane == 0) L->qn[qe][qs] = -1;
-							}
-							wsync();
-						}
-					}
-					if (lane == 0) {
-						L->pmid[qe][qs][qp_] = (uint32_t)rd((int)first, q) + (uint32_t)mid;
-						L->pfwd[qe][qs][qp_] = (uint16_t)fwd;
-						L->pbwd[qe][qs][qp_] = (uint16_t)bwd;
-					}
-					st_hits += (lane == 0) ? (unsigned long long)(fwd + bwd) : 0ull;
-				}
-			}
-			// buckets of more than 64 items: the lane-serial gehash_go_X search
-			if (slow) {
-				const int16_t *Kp = ix.keys + first;
-				int lo = 0, hi = n - 1, m;
-				bool hit = false;
+				int16_t k16 = (int16_t)(key / ix.nb);
+				uint32_t first = ix.bstart[b];
+				int n = (int)(ix.bstart[b + 1] - first);
+				uint32_t mid = 0;
 				int fwd = 0, bwd = 0;
-				for (;;) {
-					m = (lo + hi) >> 1;
-					int16_t kk = Kp[m];
-					if (kk > (int16_t)k16) hi = m - 1;
-					else if (kk < (int16_t)k16) lo = m + 1;
-					else { hit = true; break; }
-					if (hi < lo) break;
+				st_items += n;
+				if (n > 0) {
+					const int16_t *K = ix.keys + first;
+					int lo = 0, hi = n - 1, m;
+					bool hit = false;
+					for (;;) {
+						m = (lo + hi) >> 1;
+						int16_t kk = K[m];
+						if (kk > k16) hi = m - 1;
+						else if (kk < k16) lo = m + 1;
+						else { hit = true; break; }
+						if (hi < lo) break;
+					}
+					if (hit) {
+						mid = first + m;
+						int q = m + 1;
+						while (q < n && K[q] == k16) q++;
+						fwd = q - m;
+						q = m - 1;
+						while (q >= 0 && K[q] == k16) q--;
+						bwd = m - 1 - q;
+					}
 				}
-				if (hit) {
-					int q = m + 1;
-					while (q < n && Kp[q] == (int16_t)k16) q++;
-					fwd = q - m;
-					q = m - 1;
-					while (q >= 0 && Kp[q] == (int16_t)k16) q--;
-					bwd = m - 1 - q;
-				}
-				L->pmid[e][s][p] = first + (hit ? m : 0);
+				L->pmid[e][s][p] = mid;
 				L->pfwd[e][s][p] = (uint16_t)fwd;
 				L->pbwd[e][s][p] = (uint16_t)bwd;
-				L->qn[e][s] = -1;
 				st_hits += fwd + bwd;
 			}
-			wsync();
 		}
 		st_probes += total;
 		wsync();
@@ -487,27 +403,7 @@ struct Wave {
 		const int np = rc.np[E];
 		const int gap = kp->ix.gap;
 		const uint32_t high_b = kp->high - (uint32_t)rc.rl[E];
-		// per-probe (subread_no, offset), lane = probe
-		int ko_v = 0;
-		if (lane < np) ko_v = (lane / gap) | (probe_off(E, lane) << 8);
-		const int qn = L->qn[E][s];
-		STAMP(2);
-		if (qn >= 0) {
-			for (int cb = 0; cb < qn; cb += 64) {
-				int kvv = (int)L->qkv[E][s][(cb + lane) & (QCAP - 1)];
-				int pv = (int)L->qp[E][s][(cb + lane) & (QCAP - 1)];
-				int m = qn - cb < 64 ? qn - cb : 64;
-				for (int j = 0; j < m; j++) {
-					uint32_t kv = (uint32_t)rd(kvv, j);
-					uint32_t ko = (uint32_t)rd(ko_v, rd(pv, j));
-					vote_one<E>(kv, (int)(ko & 255) + 1, (int)(ko >> 8), round, high_b);
-				}
-			}
-			wsync();
-			STAMP(3);
-			return;
-		}
-		// fallback: candidate prefix over probes, then gather QCAP at a time
+		// candidate prefix over probes (probe order = subread_no, xk1)
 		uint32_t total = 0;
 		for (int p0 = 0; p0 < np; p0 += 64) {
 			int p = p0 + lane;
@@ -518,8 +414,10 @@ struct Wave {
 		}
 		if (lane == 0) L->pcum[0] = 0;
 		wsync();
-		for (uint32_t c0 = 0; c0 < total; c0 += QCAP) {
-			uint32_t cn = total - c0 < QCAP ? total - c0 : QCAP;
+		STAMP(2);
+		for (uint32_t c0 = 0; c0 < total; c0 += CAND_CAP) {
+			uint32_t cn = total - c0 < CAND_CAP ? total - c0 : CAND_CAP;
+			// gather in visiting order: probe p, then mid..last, then mid-1..first
 			for (uint32_t c = lane; c < cn; c += 64) {
 				uint32_t cc = c0 + c;
 				int lo = 0, hi = np - 1;   // probe p with pcum[p] <= cc < pcum[p+1]
@@ -529,18 +427,19 @@ struct Wave {
 				uint32_t fwd = L->pfwd[E][s][p];
 				uint32_t mid = L->pmid[E][s][p];
 				uint32_t item = j < fwd ? mid + j : mid - 1 - (j - fwd);
-				L->qkv[E][s][c] = kp->ix.vals[item] - (uint32_t)probe_off(E, p);
-				L->qp[E][s][c] = (uint8_t)p;
+				int off = probe_off(E, p);
+				L->cand[c] = kp->ix.vals[item] - (uint32_t)off;
+				L->cand_ko[c] = (uint32_t)(p / gap) | ((uint32_t)off << 8);
 			}
 			wsync();
 			STAMP(2);
 			for (uint32_t cb = 0; cb < cn; cb += 64) {
-				int kvv = (int)L->qkv[E][s][(cb + lane) & (QCAP - 1)];
-				int pv = (int)L->qp[E][s][(cb + lane) & (QCAP - 1)];
+				int kvv = (int)L->cand[cb + (lane & (CAND_CAP - 1))];
+				int kov = (int)L->cand_ko[cb + (lane & (CAND_CAP - 1))];
 				int m = cn - cb < 64 ? (int)(cn - cb) : 64;
 				for (int j = 0; j < m; j++) {
 					uint32_t kv = (uint32_t)rd(kvv, j);
-					uint32_t ko = (uint32_t)rd(ko_v, rd(pv, j));
+					uint32_t ko = (uint32_t)rd(kov, j);
 					vote_one<E>(kv, (int)(ko & 255) + 1, (int)(ko >> 8), round, high_b);
 				}
 			}
