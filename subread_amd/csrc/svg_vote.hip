@@ -67,9 +67,10 @@ struct KParams {
 // ---------------------------------------------------------------------------------------------
 // LDS layout of one wave.  Row occupancy (items[30]) and max_vote live in
 // registers (lane 32*end+row holds items[row]); only slot state is in LDS.
-#define CAND_CAP 256
+#define CAND_CAP 128
 template <int ENDS, int MAXL, int MAXP>
 struct WaveLDS {
+	static constexpr int MAXS = ENDS == 1 ? 16 : 64;   // max_vote_simples capacity
 	uint32_t pos[ENDS][NSLOT];            // slot positions, [row*24+slot]
 	uint32_t meta[ENDS][NSLOT];           // votes | last<<8 | (toli | shift<<7)<<16 | (u8)cursor<<24
 	uint32_t pmid[ENDS][2][MAXP];         // probe: binary-search midpoint (absolute item index)
@@ -82,9 +83,9 @@ struct WaveLDS {
 	uint32_t tmp[ENDS][3][17];            // top-K output under construction
 	uint32_t jres[ENDS][3][4];            // subjunc_result_t
 	uint32_t jtmp[ENDS][3][4];
-	uint32_t simp_pos[ENDS][64];          // simple_mapping_t: position
-	uint16_t simp_slot[ENDS][64];         // slot index, or 0x8000|stored index
-	uint16_t simp_votes[ENDS][64];
+	uint32_t simp_pos[ENDS][MAXS];        // simple_mapping_t: position
+	uint16_t simp_slot[ENDS][MAXS];       // slot index, or 0x8000|stored index
+	uint16_t simp_votes[ENDS][MAXS];
 	uint16_t bm[ENDS][10];
 	char text[ENDS][2][MAXL];             // strand 0 form / strand 1 (reversed) form
 };
@@ -534,6 +535,10 @@ struct Wave {
 		int U[2];
 		U[0] = rd(rs_v, ROWS - 1);
 		U[1] = ENDS == 2 ? rd(rs_v, 32 + ROWS - 1) : 0;
+		// slot of flattened index f = lane (first 64 used slots), computed once per table
+		int sl0[2];
+		sl0[0] = slot_of(0, rs_v, lane);
+		sl0[1] = ENDS == 2 ? slot_of(1, rs_v, lane) : 0;
 		for (int e = 0; e < ENDS; e++) {
 			// top-3 distinct over table votes and stored results (update_top_three)
 			int bound = 0x7fffffff;
@@ -541,7 +546,7 @@ struct Wave {
 				int best = 0;
 				for (int f0 = 0; f0 < U[e]; f0 += 64) {
 					int f = f0 + lane;
-					int sl = slot_of(e, rs_v, f);   // all lanes active: slot_of shuffles
+					int sl = f0 == 0 ? (e ? sl0[1] : sl0[0]) : slot_of(e, rs_v, f);   // all lanes active
 					if (f < U[e]) {
 						int v = m_votes(L->meta[e][sl]);
 						if (v < bound && v > best) best = v;
@@ -565,7 +570,7 @@ struct Wave {
 				if (N < 1 || (top[e][0] - N > p.max_vote_number_cutoff)) break;
 				for (int f0 = 0; f0 < U[e] && ns < p.max_vote_simples; f0 += 64) {
 					int f = f0 + lane;
-					int slot = slot_of(e, rs_v, f), v = -1;   // all lanes active: slot_of shuffles
+					int slot = f0 == 0 ? (e ? sl0[1] : sl0[0]) : slot_of(e, rs_v, f), v = -1;   // all lanes active
 					if (f < U[e]) v = m_votes(L->meta[e][slot]);
 					bool sel = f < U[e] && v == N && v >= p.min_votes_second;
 					unsigned long long sm = ballot(sel);
@@ -810,7 +815,7 @@ struct Wave {
 };
 
 template <int ENDS, int MAXL, int MAXP, int WPB>
-__global__ void __launch_bounds__(64 * WPB) vote_kernel(KParams kp)
+__global__ void __launch_bounds__(64 * WPB, 4) vote_kernel(KParams kp)
 {
 	extern __shared__ __align__(16) uint8_t lds_raw[];
 	typedef WaveLDS<ENDS, MAXL, MAXP> LT;
@@ -987,12 +992,13 @@ extern "C" int svg_get_stats(const svg_index *h, svg_batch_stats *o)
 	return 0;
 }
 
-static int check_params(const svg_index *h, const svg_params *p)
+static int check_params(const svg_index *h, const svg_params *p, int paired)
 {
 	if (p->multi_best < 1 || p->multi_best > 3) { svg_set_error("multi_best must be 1..3"); return SVG_E_UNSUPPORTED; }
 	if (p->top_scores != 3) { svg_set_error("top_scores must be 3 (reference runtime value)"); return SVG_E_UNSUPPORTED; }
 	if (p->max_vote_combinations < 1 || p->max_vote_combinations > 3) { svg_set_error("max_vote_combinations must be 1..3"); return SVG_E_UNSUPPORTED; }
 	if (p->max_vote_simples < 1 || p->max_vote_simples > 64) { svg_set_error("max_vote_simples must be 1..64"); return SVG_E_UNSUPPORTED; }
+	if (p->max_vote_simples > 16 && !paired) { svg_set_error("single-end max_vote_simples must be <= 16"); return SVG_E_UNSUPPORTED; }
 	if (p->total_subreads < 2 || p->total_subreads > 64) { svg_set_error("total_subreads must be 2..64"); return SVG_E_UNSUPPORTED; }
 	if (p->max_indel_length < 0) { svg_set_error("max_indel_length < 0"); return SVG_E_ARG; }
 	if (p->do_breakpoint_detection) { svg_set_error("subjunc mode is not available in this build"); return SVG_E_UNSUPPORTED; }
@@ -1032,7 +1038,7 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 {
 	if (!h || !p || !r1 || !out) { svg_set_error("svg_vote_batch_device: NULL argument"); return SVG_E_ARG; }
 	if (r2 && r2->n_reads != r1->n_reads) { svg_set_error("R1/R2 read counts differ"); return SVG_E_ARG; }
-	int rc = check_params(h, p);
+	int rc = check_params(h, p, r2 != NULL);
 	if (rc) return rc;
 	HIPCHK(hipSetDevice(h->device));
 	hipStream_t st = stream ? (hipStream_t)stream : h->stream;
@@ -1088,7 +1094,7 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 {
 	if (!h || !p || !r1 || !out) { svg_set_error("svg_vote_batch: NULL argument"); return SVG_E_ARG; }
 	if (r2 && r2->n_reads != r1->n_reads) { svg_set_error("R1/R2 read counts differ"); return SVG_E_ARG; }
-	int rc = check_params(h, p);
+	int rc = check_params(h, p, r2 != NULL);
 	if (rc) return rc;
 	uint64_t n = r1->n_reads;
 	if (!n) return 0;
