@@ -202,6 +202,12 @@ typedef struct svg_batch_stats {
 	uint64_t results;            /* mapping records with selected_votes > 0   */
 } svg_batch_stats;
 int svg_set_stats(svg_index *idx, int enable);
+
+/* Upper bound of read lengths passed to svg_vote_batch_device on this handle
+ * (default 256; svg_vote_batch measures its own batch).  A tighter bound lets
+ * the library pick a kernel variant with smaller probe tables and higher
+ * occupancy; reads beyond the bound are rejected. */
+int svg_set_max_read_length(svg_index *idx, int max_len);
 int svg_get_stats(const svg_index *idx, svg_batch_stats *out);
 
 const char *svg_last_error(void);

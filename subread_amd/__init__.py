@@ -28,6 +28,7 @@ EXPORTS = [
     "svg_vote_batch", "svg_vote_batch_device", "svg_set_stats", "svg_get_stats",
     "svg_last_error", "svg_abi_version", "svg_build_index", "svg_sim_genome",
     "svg_sim_repeats", "svg_sim_reads", "svg_index_build", "svg_index_build_mem", "svg_index_export",
+    "svg_set_max_read_length",
 ]
 
 _lib = None
@@ -64,6 +65,8 @@ def lib():
         L.svg_vote_batch_device.restype = i32
         L.svg_set_stats.argtypes = [vp, i32]
         L.svg_get_stats.argtypes = [vp, vp]
+        L.svg_set_max_read_length.argtypes = [vp, i32]
+        L.svg_set_max_read_length.restype = i32
         L.svg_last_error.restype = ctypes.c_char_p
         L.svg_index_build.argtypes = [ctypes.c_char_p, i32, i32, i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
         L.svg_index_build.restype = i32
@@ -162,6 +165,9 @@ class VoteIndex:
             self.close()
         except Exception:
             pass
+
+    def set_max_read_length(self, n):
+        _check(lib().svg_set_max_read_length(self.h, int(n)), "svg_set_max_read_length")
 
     def set_stats(self, on=True):
         lib().svg_set_stats(self.h, 1 if on else 0)

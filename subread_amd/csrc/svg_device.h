@@ -32,6 +32,7 @@ struct svg_index {
 	svg_batch_stats last_stats;
 	uint64_t device_bytes;
 	int n_cu;
+	int max_read_len;        // announced read-length bound (svg_set_max_read_length), picks the kernel variant
 	// staging for svg_vote_batch (host buffers)
 	void *d_in; size_t d_in_cap;
 	void *d_out; size_t d_out_cap;

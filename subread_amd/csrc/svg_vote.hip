@@ -67,7 +67,7 @@ struct KParams {
 // ---------------------------------------------------------------------------------------------
 // LDS layout of one wave.  Row occupancy (items[30]) and max_vote live in
 // registers (lane 32*end+row holds items[row]); only slot state is in LDS.
-#define CAND_CAP 128
+#define CAND_CAP 64
 template <int ENDS, int MAXL, int MAXP>
 struct WaveLDS {
 	static constexpr int MAXS = ENDS == 1 ? 16 : 64;   // max_vote_simples capacity
@@ -87,8 +87,7 @@ struct WaveLDS {
 	uint16_t simp_slot[ENDS][MAXS];       // slot index, or 0x8000|stored index
 	uint16_t simp_votes[ENDS][MAXS];
 	uint16_t bm[ENDS][10];
-	char text[2][ENDS][MAXL];             // strand-0 form of each end, double-buffered across reads
-	char traw[MAXL];                      // raw read bytes while applying the -S reversal
+	char text[ENDS][MAXL];                // strand-0 form (strand 1 = reverse_read of it)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -172,19 +171,6 @@ struct ReadCtx {
 	int applied[2];
 	int step[2];
 	int np[2];          // probes per strand for each end (applied*gap)
-	int buf;            // LDS text buffer holding this read
-};
-
-// prefetched raw text of one read: lane l holds bytes 4l..4l+3 of each end
-struct TextRegs {
-	uint32_t w[2];
-	int len[2];
-};
-
-// bucket bounds of the first 64 probes of a read (lane = probe id)
-struct Stage1 {
-	int k16, n;
-	uint32_t first;
 };
 
 #ifdef SVG_STAMPS
@@ -212,112 +198,77 @@ struct Wave {
 	__device__ __forceinline__ static int rd(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 	// ---------------------------------------------------------------- probe offset of probe p
-	// (subread offsets, core.c:3159-3167)
-	__device__ __forceinline__ int probe_off_x(const ReadCtx &c, int e, int p) const
+	__device__ __forceinline__ int probe_off(int e, int p) const
 	{
 		int gap = kp->ix.gap;
 		int k = p / gap, x = p - k * gap;
-		int off = (int)(((int64_t)c.step[e] * k) >> 16);
+		int off = (int)(((int64_t)rc.step[e] * k) >> 16);
 		if (gap > 1) off -= off % gap - x;
 		return off;
 	}
-	__device__ __forceinline__ int probe_off(int e, int p) const { return probe_off_x(rc, e, p); }
 
 	// ---------------------------------------------------------------- phase P: all probes of the read
-	// probe id -> (end, strand, probe) for a read context
-	__device__ __forceinline__ static void probe_owner(const ReadCtx &x, int id, int *e, int *s, int *p)
-	{
-		int base = 0, ee = 0, ss = 0, b = 0;
-		for (int ex = 0; ex < ENDS; ex++)
-			for (int sx = 0; sx < 2; sx++) {
-				if (x.np[ex] > 0 && id >= base) { ee = ex; ss = sx; b = base; }
-				base += x.np[ex];
-			}
-		*e = ee; *s = ss; *p = id - b;
-	}
-
-	// stage 1 (lanes = probes p0..p0+63): pack the 16-mer (genekey2int) from the strand-0
-	// text in LDS -- strand 1 is reverse_read of it, comp(t0[L-1-i]) -- hash it and load
-	// the bucket bounds.  The loads stay in flight until stage 2 reads the registers.
-	__device__ Stage1 stage1(const ReadCtx &x, int p0)
+	__device__ void probe_all()
 	{
 		const DevIndex &ix = kp->ix;
-		Stage1 r;
-		r.k16 = 0; r.n = 0; r.first = 0;
-		const int total = 2 * (x.np[0] + (ENDS == 2 ? x.np[1] : 0));
-		const int id = p0 + lane_id();
-		if (id < total) {
-			int e, s, p;
-			probe_owner(x, id, &e, &s, &p);
-			int off = probe_off_x(x, e, p);
-			const char *t = L->text[x.buf][e];
-			uint32_t key = 0;
-			if (s == 0) {
+		int total = 0;
+		int base[2][2];
+		for (int e = 0; e < ENDS; e++)
+			for (int s = 0; s < 2; s++) { base[e][s] = total; total += rc.np[e]; }
+		for (int p0 = 0; p0 < total; p0 += 64) {
+			int id = p0 + lane_id();
+			if (id < total) {
+				int e = 0, s = 0;
+				for (int ee = 0; ee < ENDS; ee++)
+					for (int ss = 0; ss < 2; ss++)
+						if (rc.np[ee] > 0 && id >= base[ee][ss]) { e = ee; s = ss; }
+				int p = id - base[e][s];
+				int off = probe_off(e, p);
+				uint32_t key = 0;
+				if (s == 0) {
+					const char *t = L->text[e] + off;
 #pragma unroll
-				for (int i = 0; i < 16; i++) key |= b2i(t[off + i]) << (30 - 2 * i);
-			} else {
-				const char *tr = t + x.rl[e] - 1 - off;
+					for (int i = 0; i < 16; i++) key |= b2i(t[i]) << (30 - 2 * i);
+				} else {   // strand 1: reverse_read (input-files.c:1113) of the strand-0 text
+					const char *t = L->text[e] + rc.rl[e] - 1 - off;
 #pragma unroll
-				for (int i = 0; i < 16; i++) key |= b2i(comp(tr[-i])) << (30 - 2 * i);
-			}
-			uint32_t b = key % ix.nb;
-			r.k16 = (int16_t)(key / ix.nb);
-			r.first = ix.bstart[b];
-			r.n = (int)(ix.bstart[b + 1] - r.first);
-		}
-		return r;
-	}
-
-	// stage 2: gehash_go_X's binary search (sorted-hashtable.c:947-981) and the equal-key
-	// run around the midpoint, lane-serial over the bucket's i16 keys
-	__device__ void stage2(const Stage1 &r, int p0)
-	{
-		const DevIndex &ix = kp->ix;
-		const int total = 2 * (rc.np[0] + (ENDS == 2 ? rc.np[1] : 0));
-		const int id = p0 + lane_id();
-		if (id < total) {
-			int e, s, p;
-			probe_owner(rc, id, &e, &s, &p);
-			const int n = r.n;
-			const int16_t k16 = (int16_t)r.k16;
-			uint32_t mid = 0;
-			int fwd = 0, bwd = 0;
-			st_items += n;
-			if (n > 0) {
-				const int16_t *K = ix.keys + r.first;
-				int lo = 0, hi = n - 1, m;
-				bool hit = false;
-				for (;;) {
-					m = (lo + hi) >> 1;
-					int16_t kk = K[m];
-					if (kk > k16) hi = m - 1;
-					else if (kk < k16) lo = m + 1;
-					else { hit = true; break; }
-					if (hi < lo) break;
+					for (int i = 0; i < 16; i++) key |= b2i(comp(t[-i])) << (30 - 2 * i);
 				}
-				if (hit) {
-					mid = r.first + m;
-					int q = m + 1;
-					while (q < n && K[q] == k16) q++;
-					fwd = q - m;
-					q = m - 1;
-					while (q >= 0 && K[q] == k16) q--;
-					bwd = m - 1 - q;
+				uint32_t b = key % ix.nb;
+				int16_t k16 = (int16_t)(key / ix.nb);
+				uint32_t first = ix.bstart[b];
+				int n = (int)(ix.bstart[b + 1] - first);
+				uint32_t mid = 0;
+				int fwd = 0, bwd = 0;
+				st_items += n;
+				if (n > 0) {
+					const int16_t *K = ix.keys + first;
+					int lo = 0, hi = n - 1, m;
+					bool hit = false;
+					for (;;) {
+						m = (lo + hi) >> 1;
+						int16_t kk = K[m];
+						if (kk > k16) hi = m - 1;
+						else if (kk < k16) lo = m + 1;
+						else { hit = true; break; }
+						if (hi < lo) break;
+					}
+					if (hit) {
+						mid = first + m;
+						int q = m + 1;
+						while (q < n && K[q] == k16) q++;
+						fwd = q - m;
+						q = m - 1;
+						while (q >= 0 && K[q] == k16) q--;
+						bwd = m - 1 - q;
+					}
 				}
+				L->pmid[e][s][p] = mid;
+				L->pfwd[e][s][p] = (uint16_t)fwd;
+				L->pbwd[e][s][p] = (uint16_t)bwd;
+				st_hits += fwd + bwd;
 			}
-			L->pmid[e][s][p] = mid;
-			L->pfwd[e][s][p] = (uint16_t)fwd;
-			L->pbwd[e][s][p] = (uint16_t)bwd;
-			st_hits += fwd + bwd;
 		}
-	}
-
-	// all probes of the current read; the first 64 had their stage 1 issued one read ahead
-	__device__ void probe_all(const Stage1 &pre)
-	{
-		const int total = 2 * (rc.np[0] + (ENDS == 2 ? rc.np[1] : 0));
-		stage2(pre, 0);
-		for (int p0 = 64; p0 < total; p0 += 64) stage2(stage1(rc, p0), p0);
 		st_probes += total;
 		wsync();
 	}
@@ -782,53 +733,29 @@ struct Wave {
 		}
 	}
 
-	// ---------------------------------------------------------------- read intake (pipelined)
-	// stage A: issue the raw text loads of read r into registers (lane l: bytes 4l..4l+3)
-	__device__ TextRegs text_fetch(uint64_t r)
-	{
-		TextRegs t;
-		const int lane = lane_id();
-		for (int e = 0; e < ENDS; e++) {
-			const char *seq = e ? kp->seq2 : kp->seq1;
-			uint64_t o = e ? kp->off2[r] : kp->off1[r];
-			int len = e ? kp->len2[r] : kp->len1[r];
-			if (len > MAXL) {   // host-validated; never index LDS past the text buffer
-				if (lane == 0 && kp->stats) atomicOr((unsigned long long *)&kp->stats[7], 1ull);
-				len = 0;
-			}
-			t.len[e] = len;
-			uint32_t w = 0;
-			const int i0 = 4 * lane;
-#pragma unroll
-			for (int j = 0; j < 4; j++)
-				if (i0 + j < len) w |= (uint32_t)(uint8_t)seq[o + i0 + j] << (8 * j);
-			t.w[e] = w;
-		}
-		return t;
-	}
-
-	// stage B: text registers -> LDS buffer `buf` in strand-0 form (fetch_next_read_pair's
-	// -S reversal, core.c:1186-1198) and the read's subread geometry (core.c:3117-3129)
-	__device__ ReadCtx text_install(const TextRegs &t, int buf)
+	// ---------------------------------------------------------------- one read
+	__device__ void run_read(uint64_t r)
 	{
 		const svg_params &p = kp->p;
 		const int lane = lane_id();
 		const int gap = kp->ix.gap;
-		ReadCtx x;
-		x.buf = buf;
+		// load text (fetch_next_read_pair: -S reversal), both strands
 		for (int e = 0; e < ENDS; e++) {
-			const int len = t.len[e];
-			const int rev = e ? p.reverse_r2 : p.reverse_r1;
-			char *dst = L->text[buf][e];
-			if (!rev) {
-				if (4 * lane < len) *(uint32_t *)(dst + 4 * lane) = t.w[e];
-			} else {
-				if (4 * lane < len) *(uint32_t *)(L->traw + 4 * lane) = t.w[e];
-				wsync();
-				for (int i = lane; i < len; i += 64) dst[i] = comp(L->traw[len - 1 - i]);
-				wsync();
+			const char *seq = e ? kp->seq2 : kp->seq1;
+			uint64_t o = e ? kp->off2[r] : kp->off1[r];
+			int len = e ? kp->len2[r] : kp->len1[r];
+			int rev = e ? p.reverse_r2 : p.reverse_r1;
+			rc.rl[e] = len;
+			if (len > MAXL) {   // host-validated; never index LDS past the text buffer
+				if (lane == 0 && kp->stats) atomicOr((unsigned long long *)&kp->stats[7], 1ull);
+				len = 0;
+				rc.rl[e] = 0;
 			}
-			x.rl[e] = len;
+			for (int i = lane; i < len; i += 64) {
+				char c = seq[o + i];
+				char c2 = seq[o + (len - 1 - i)];
+				L->text[e][i] = rev ? comp(c2) : c;
+			}
 			if (len >= 15 + gap) {   // shorter reads: out of contract, no hits (see oracle)
 				int cr = (len - 15 - gap) << 16, step;
 				if (len <= 160) {
@@ -838,27 +765,17 @@ struct Wave {
 					step = 6 << 16;
 					if (cr / step > 62) step = cr / 62;
 				}
-				x.step[e] = step;
-				x.applied[e] = 1 + cr / step;
-				x.np[e] = x.applied[e] * gap;
-				if (x.np[e] > MAXP) {   // host-validated; keep LDS probe tables in bounds
+				rc.step[e] = step;
+				rc.applied[e] = 1 + cr / step;
+				rc.np[e] = rc.applied[e] * gap;
+				if (rc.np[e] > MAXP) {   // host-validated; keep LDS probe tables in bounds
 					if (lane == 0 && kp->stats) atomicOr((unsigned long long *)&kp->stats[7], 2ull);
-					x.np[e] = 0; x.applied[e] = 0;
+					rc.np[e] = 0; rc.applied[e] = 0;
 				}
 			} else {
-				x.step[e] = 0; x.applied[e] = 0; x.np[e] = 0;
+				rc.step[e] = 0; rc.applied[e] = 0; rc.np[e] = 0;
 			}
 		}
-		if (ENDS == 1) { x.rl[1] = 0; x.step[1] = 0; x.applied[1] = 0; x.np[1] = 0; }
-		wsync();
-		return x;
-	}
-
-	// ---------------------------------------------------------------- one read (rc installed, stage 1 in `pre`)
-	__device__ void run_read(uint64_t r, const Stage1 &pre)
-	{
-		const svg_params &p = kp->p;
-		const int lane = lane_id();
 		for (int e = 0; e < ENDS; e++) {
 			for (int i = 0; i < 3; i++) rec_zero(L->res[e][i]);
 			if (lane < 12) L->jres[e][lane / 4][lane % 4] = 0;
@@ -866,7 +783,7 @@ struct Wave {
 		}
 		wsync();
 		STAMP(0);
-		probe_all(pre);
+		probe_all();
 		STAMP(1);
 		for (int strand = 0; strand < 2; strand++) {
 			cur_strand = strand;
@@ -900,8 +817,8 @@ struct Wave {
 	}
 };
 
-template <int ENDS, int MAXL, int MAXP, int WPB>
-__global__ void __launch_bounds__(64 * WPB, 4) vote_kernel(KParams kp)
+template <int ENDS, int MAXL, int MAXP, int WPB, int OCC>
+__global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 {
 	extern __shared__ __align__(16) uint8_t lds_raw[];
 	typedef WaveLDS<ENDS, MAXL, MAXP> LT;
@@ -922,28 +839,11 @@ __global__ void __launch_bounds__(64 * WPB, 4) vote_kernel(KParams kp)
 	W.t_last = __builtin_amdgcn_s_memtime();
 #endif
 	W.st_probes = W.st_items = W.st_hits = 0;
-	// software pipeline over this wave's reads r, r+nw, r+2nw: while read r votes, the
-	// bucket bounds of r+nw and the text of r+2nw are in flight
-	if (gw < kp.n_reads) {
-		TextRegs tnext = W.text_fetch(gw);
-		W.rc = W.text_install(tnext, 0);
-		Stage1 s_cur = W.stage1(W.rc, 0);
-		if (gw + nw < kp.n_reads) tnext = W.text_fetch(gw + nw);
-		for (uint64_t r = gw; r < kp.n_reads; r += nw) {
-			ReadCtx rc_next = W.rc;
-			Stage1 s_next = s_cur;
-			if (r + nw < kp.n_reads) {
-				rc_next = W.text_install(tnext, W.rc.buf ^ 1);
-				s_next = W.stage1(rc_next, 0);
-				if (r + 2 * nw < kp.n_reads) tnext = W.text_fetch(r + 2 * nw);
-			}
-			W.run_read(r, s_cur);
-			W.rc = rc_next;
-			s_cur = s_next;
+	for (uint64_t r = gw; r < kp.n_reads; r += nw) {
+		W.run_read(r);
 #ifdef SVG_STAMPS
-			{ unsigned long long _t = __builtin_amdgcn_s_memtime(); W.acc[5] += _t - W.t_last; W.t_last = _t; }
+		{ unsigned long long _t = __builtin_amdgcn_s_memtime(); W.acc[5] += _t - W.t_last; W.t_last = _t; }
 #endif
-		}
 	}
 #ifdef SVG_STAMPS
 	if (kp.stats && lane_id() == 0)
@@ -996,6 +896,7 @@ int svg_index_finish_device(svg_index *h)
 	HIPCHK(hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
 	const char *se = getenv("SVG_STATS");
 	h->stats_on = se && se[0] == '1';
+	h->max_read_len = 256;
 	return 0;
 }
 
@@ -1095,6 +996,27 @@ extern "C" int svg_get_stats(const svg_index *h, svg_batch_stats *o)
 	return 0;
 }
 
+// largest applied_subreads * gap over read lengths 15+gap..max_len (core.c:3117-3129)
+static int svg_probe_bound(int max_len, int gap, int n)
+{
+	int best = 0;
+	for (int len = 15 + gap; len <= max_len; len++) {
+		int cr = (len - 15 - gap) << 16, step;
+		if (len <= 160) { step = cr / (n - 1); if (step < (gap << 16)) step = gap << 16; }
+		else { step = 6 << 16; if (cr / step > 62) step = cr / 62; }
+		int np = (1 + cr / step) * gap;
+		if (np > best) best = np;
+	}
+	return best;
+}
+
+extern "C" int svg_set_max_read_length(svg_index *h, int max_len)
+{
+	if (!h || max_len < 1 || max_len > SVG_MAX_READ_LENGTH) { svg_set_error("svg_set_max_read_length: bad argument"); return SVG_E_ARG; }
+	h->max_read_len = max_len;
+	return 0;
+}
+
 static int check_params(const svg_index *h, const svg_params *p, int paired)
 {
 	if (p->multi_best < 1 || p->multi_best > 3) { svg_set_error("multi_best must be 1..3"); return SVG_E_UNSUPPORTED; }
@@ -1109,14 +1031,14 @@ static int check_params(const svg_index *h, const svg_params *p, int paired)
 	return 0;
 }
 
-template <int ENDS, int MAXL, int MAXP, int WPB>
+template <int ENDS, int MAXL, int MAXP, int WPB, int OCC>
 static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 {
 	typedef WaveLDS<ENDS, MAXL, MAXP> LT;
 	size_t lds = (size_t)WPB * ((sizeof(LT) + 15) & ~(size_t)15);
 	int per_cu = (int)(160 * 1024 / lds);
 	if (per_cu < 1) { svg_set_error("kernel LDS too large"); return SVG_E_DEVICE; }
-	if (per_cu > 16) per_cu = 16;
+	if (per_cu > 4 * OCC / WPB) per_cu = 4 * OCC / WPB;   // 4 SIMDs x OCC waves
 	uint64_t blocks = (uint64_t)h->n_cu * per_cu;
 	uint64_t need = (kp.n_reads + WPB - 1) / WPB;
 	if (blocks > need) blocks = need;
@@ -1131,7 +1053,7 @@ static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 		h->scratch_words = words;
 	}
 	kp.scratch = h->d_scratch;
-	hipLaunchKernelGGL((vote_kernel<ENDS, MAXL, MAXP, WPB>), dim3((unsigned)blocks), dim3(64 * WPB), lds, st, kp);
+	hipLaunchKernelGGL((vote_kernel<ENDS, MAXL, MAXP, WPB, OCC>), dim3((unsigned)blocks), dim3(64 * WPB), lds, st, kp);
 	HIPCHK(hipGetLastError());
 	return 0;
 }
@@ -1165,8 +1087,10 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 		HIPCHK(hipMemsetAsync(h->d_stats, 0, 16 * sizeof(unsigned long long), st));
 		kp.stats = h->d_stats;
 	}
-	if (r2) rc = launch_t<2, 256, 64, 2>(h, kp, st);
-	else rc = launch_t<1, 256, 64, 2>(h, kp, st);
+	// probes per strand are bounded by the read lengths the caller announced
+	int npmax = svg_probe_bound(h->max_read_len, h->dix.gap, p->total_subreads);
+	if (r2) rc = npmax <= 32 ? launch_t<2, 256, 32, 2, 4>(h, kp, st) : launch_t<2, 256, 64, 2, 4>(h, kp, st);
+	else rc = npmax <= 32 ? launch_t<1, 256, 32, 2, 5>(h, kp, st) : launch_t<1, 256, 64, 2, 4>(h, kp, st);
 	if (rc) return rc;
 	if (h->stats_on) {
 		unsigned long long s[4];
@@ -1222,6 +1146,11 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 		}
 		lo[e] = mn; span[e] = mx - mn;
 	}
+	int saved_len = h->max_read_len, batch_max = 16;
+	for (int e = 0; e < ends; e++) {
+		const svg_reads *rr = e ? r2 : r1;
+		for (uint64_t i = 0; i < n; i++) if (rr->lens[i] > batch_max) batch_max = rr->lens[i];
+	}
 	size_t in_bytes = 0, o_seq[2], o_off[2], o_len[2];
 	for (int e = 0; e < ends; e++) {
 		o_seq[e] = in_bytes; in_bytes += (span[e] + 15) & ~15ull;
@@ -1247,7 +1176,9 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 		dr[e].n_reads = n;
 	}
 	free(tmpoff);
+	h->max_read_len = batch_max;
 	rc = svg_vote_batch_device(h, p, &dr[0], r2 ? &dr[1] : NULL, (svg_mapping_result *)h->d_out, NULL, NULL, h->stream);
+	h->max_read_len = saved_len;
 	if (rc) return rc;
 	HIPCHK(hipMemcpyAsync(out, h->d_out, out_bytes, hipMemcpyDeviceToHost, h->stream));
 	HIPCHK(hipStreamSynchronize(h->stream));

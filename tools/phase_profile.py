@@ -27,6 +27,7 @@ def main():
     r1 = simulate_reads(g, n, 100, seed=20261015)
     r2 = simulate_reads(g, n, 100, seed=7) if paired else None
     p = default_params(paired=paired)
+    ix.set_max_read_length(100)
     ix.vote(p, r1, r2)
     ix.set_stats(True)
     t = time.time()
