@@ -87,7 +87,7 @@ struct WaveLDS {
 	uint16_t simp_slot[ENDS][MAXS];       // slot index, or 0x8000|stored index
 	uint16_t simp_votes[ENDS][MAXS];
 	uint16_t bm[ENDS][10];
-	char text[ENDS][MAXL];                // strand-0 form (strand 1 = reverse_read of it)
+	char text[ENDS][2][MAXL];             // strand 0 form / strand 1 (reverse_read) form
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -224,16 +224,10 @@ struct Wave {
 						if (rc.np[ee] > 0 && id >= base[ee][ss]) { e = ee; s = ss; }
 				int p = id - base[e][s];
 				int off = probe_off(e, p);
+				const char *t = L->text[e][s] + off;
 				uint32_t key = 0;
-				if (s == 0) {
-					const char *t = L->text[e] + off;
 #pragma unroll
-					for (int i = 0; i < 16; i++) key |= b2i(t[i]) << (30 - 2 * i);
-				} else {   // strand 1: reverse_read (input-files.c:1113) of the strand-0 text
-					const char *t = L->text[e] + rc.rl[e] - 1 - off;
-#pragma unroll
-					for (int i = 0; i < 16; i++) key |= b2i(comp(t[-i])) << (30 - 2 * i);
-				}
+				for (int i = 0; i < 16; i++) key |= b2i(t[i]) << (30 - 2 * i);
 				uint32_t b = key % ix.nb;
 				int16_t k16 = (int16_t)(key / ix.nb);
 				uint32_t first = ix.bstart[b];
@@ -754,7 +748,8 @@ struct Wave {
 			for (int i = lane; i < len; i += 64) {
 				char c = seq[o + i];
 				char c2 = seq[o + (len - 1 - i)];
-				L->text[e][i] = rev ? comp(c2) : c;
+				L->text[e][0][i] = rev ? comp(c2) : c;
+				L->text[e][1][i] = rev ? comp(comp(c)) : comp(c2);   // reverse_read of strand 0
 			}
 			if (len >= 15 + gap) {   // shorter reads: out of contract, no hits (see oracle)
 				int cr = (len - 15 - gap) << 16, step;
@@ -1090,7 +1085,7 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	// probes per strand are bounded by the read lengths the caller announced
 	int npmax = svg_probe_bound(h->max_read_len, h->dix.gap, p->total_subreads);
 	if (r2) rc = npmax <= 32 ? launch_t<2, 256, 32, 2, 4>(h, kp, st) : launch_t<2, 256, 64, 2, 4>(h, kp, st);
-	else rc = npmax <= 32 ? launch_t<1, 256, 32, 2, 5>(h, kp, st) : launch_t<1, 256, 64, 2, 4>(h, kp, st);
+	else rc = npmax <= 32 ? launch_t<1, 256, 32, 2, 4>(h, kp, st) : launch_t<1, 256, 64, 2, 4>(h, kp, st);
 	if (rc) return rc;
 	if (h->stats_on) {
 		unsigned long long s[4];
