@@ -112,7 +112,7 @@ def main():
     p = default_params(PROGRAM_ALIGN, False)
     rec_bytes = MAPPING_DTYPE.itemsize * p.multi_best
     d_out = torch.empty(n * rec_bytes, dtype=torch.uint8, device=dev)
-    ix.set_max_read_length(L)
+    ix.set_max_read_length(int(os.environ.get("SVG_BENCH_MAXLEN", L)))
     stream = torch.cuda.Stream(device=dev)
     r1 = (d_seq.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n)
 

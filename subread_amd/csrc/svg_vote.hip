@@ -745,11 +745,22 @@ struct Wave {
 				len = 0;
 				rc.rl[e] = 0;
 			}
-			for (int i = lane; i < len; i += 64) {
-				char c = seq[o + i];
-				char c2 = seq[o + (len - 1 - i)];
-				L->text[e][0][i] = rev ? comp(c2) : c;
-				L->text[e][1][i] = rev ? comp(comp(c)) : comp(c2);   // reverse_read of strand 0
+			// all MAXL/64 chunk loads are issued before the first LDS write, so the
+			// read costs one HBM latency, not one per 64 bases (measured: -11% when
+			// the compiler kept this as a rolled loop)
+			char c[MAXL / 64], c2[MAXL / 64];
+#pragma unroll
+			for (int k = 0; k < MAXL / 64; k++) {
+				int i = lane + 64 * k;
+				if (i < len) { c[k] = seq[o + i]; c2[k] = seq[o + (len - 1 - i)]; }
+			}
+#pragma unroll
+			for (int k = 0; k < MAXL / 64; k++) {
+				int i = lane + 64 * k;
+				if (i < len) {
+					L->text[e][0][i] = rev ? comp(c2[k]) : c[k];
+					L->text[e][1][i] = rev ? comp(comp(c[k])) : comp(c2[k]);   // reverse_read of strand 0
+				}
 			}
 			if (len >= 15 + gap) {   // shorter reads: out of contract, no hits (see oracle)
 				int cr = (len - 15 - gap) << 16, step;
