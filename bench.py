@@ -155,6 +155,17 @@ def main():
     avg_kern_s = float(np.mean(kern_ms)) / 1e3
     achieved = algo_bytes / avg_kern_s / 1e9
 
+    # HBM traffic from the committed PMC passes of this workload (tools/pmc_traffic.py;
+    # rocprofv3 cannot run inside this process), scaled to this launch's read count
+    traffic, traffic_src = None, None
+    import glob
+    tj = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_traffic.json" % args.workload)))
+    if tj:
+        t = json.load(open(tj[-1]))
+        traffic = round(t["traffic_bytes_per_read"] * n / 1e9, 3)
+        traffic_src = "%s (FETCH_SIZE+WRITE_SIZE, %.0f B/read, GB per launch)" % (
+            os.path.relpath(tj[-1], ROOT), t["traffic_bytes_per_read"])
+
     check = None
     oi = None
     if rank == 0 and not (args.no_check and args.no_cpu):
@@ -195,7 +206,8 @@ def main():
                            "reference-format files via svg_index_open" if prefix else "built in HBM by svg_index_build_mem"),
                        "parallelism": "reads sharded across %d GPU(s), index replicated, no collective" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_unit": "GB per launch", "traffic_source": traffic_src,
                          "algorithmic_bytes_per_read": round(algo_bytes / n, 1),
                          "kernel_ms": round(avg_kern_s * 1e3, 3)},
             "cpu_baseline": cpu,
