@@ -149,6 +149,7 @@ __device__ __forceinline__ uint32_t m_pack(int votes, int last, int toli, int sh
 #define MR_CS 60
 #define MR_CE 62
 
+__device__ __forceinline__ uint32_t abs32u(uint32_t x) { return x > 0x7fffffffu ? (0xffffffffu - x) + 1 : x; }
 __device__ __forceinline__ int16_t rec_votes(const uint32_t *r) { return (int16_t)(r[2] & 0xffff); }
 __device__ __forceinline__ uint32_t rec_pos(const uint32_t *r) { return r[0]; }
 __device__ __forceinline__ void rec_set_votes(uint32_t *r, int v) { r[2] = (r[2] & 0xffff0000u) | ((uint32_t)v & 0xffff); }
@@ -179,7 +180,7 @@ struct ReadCtx {
 #define STAMP(k) do { } while (0)
 #endif
 
-template <int ENDS, int MAXL, int MAXP>
+template <int ENDS, int MAXL, int MAXP, bool SJ>
 struct Wave {
 #ifdef SVG_STAMPS
 	unsigned long long t_last, acc[8];
@@ -502,6 +503,210 @@ struct Wave {
 		return -1;
 	}
 
+	// ---------------------------------------------------------------- subjunc helpers (SJ variant)
+	// gvindex_get (gene-value-index.c:1118-1136 via gvindex_get_string): 'N' past the array
+	__device__ __forceinline__ char gv_get(uint32_t pos) const
+	{
+		const DevIndex &ix = kp->ix;
+		uint32_t byte = (pos - ix.start_base_offset) >> 2, bit = pos % 4 * 2;
+		if (byte >= ix.values_bytes - 1) return 'N';
+		return "AGCT"[(ix.values[byte] >> bit) & 3];
+	}
+
+	// match_chro (gene-value-index.c:856-959, space_type = base): matched bases of
+	// read[0..len) against the array at pos; 0 whenever the walk reaches the array end
+	__device__ int match_chro(const char *read, int read_len, int at, uint32_t pos, int len) const
+	{
+		const DevIndex &ix = kp->ix;
+		if ((uint32_t)(pos + len) >= ix.length + ix.start_point) return 0;
+		if (pos > 0xffff0000u) return 0;
+		uint32_t byte = (pos - ix.start_base_offset) >> 2, bit = pos % 4 * 2;
+		if (byte >= ix.values_bytes) return 0;
+		if (byte + (bit / 2 + len) / 4 >= ix.values_bytes) return 0;   // the walk would hit the end
+		int ret = 0;
+		int iv = (int8_t)ix.values[byte];
+		for (int i = 0; i < len; i++) {
+			int tt = (iv >> bit) & 3;
+			int q = at + i;
+			char c = q < read_len ? read[q] : 0;   // the reference's read buffer is NUL-terminated
+			ret += c == 'A' ? tt == 0 : c == 'G' ? tt == 1 : c == 'C' ? tt == 2 : c == 0 ? 0 : tt == 3;
+			bit += 2;
+			if (bit == 8) { byte++; iv = (int8_t)ix.values[byte]; bit = 0; }
+		}
+		return ret;
+	}
+
+	__device__ static bool donor_pair(char a, char b)
+	{
+		return (a == 'G' && b == 'T') || (a == 'A' && b == 'G') || (a == 'A' && b == 'C') || (a == 'C' && b == 'T');
+	}
+
+	// donor_score (core-junction.c:3675-3834; no fusion/long-del, max_insertion_at_junctions 0),
+	// lanes = tested split points.  The reference keeps the first split point (in its
+	// mid-outward visiting order) with the strictly best score, so the wave takes the
+	// maximum score and, among equal scores, the lowest visiting index.  Returns
+	// (1+best)/100 or 0 and the split point / GT-AG strand / found flag.
+	__device__ int donor(int e, uint32_t left, uint32_t right, int normal, int gs, int ge, int *split, int *gtag, int *found)
+	{
+		const svg_params &p = kp->p;
+		const int lane = lane_id();
+		const char *read = L->text[e][cur_strand];
+		const int rl = rc.rl[e];
+		const bool need_donor = p.check_donor_at_junctions != 0;
+		const int allow = p.more_accurate_fusions ? 0 : 1;
+		const int mid = (gs + ge) / 2, n = ge - gs;
+		int best = -111111, bi = 0x7fffffff, bstrand = -1, bsp = -1;
+		int carry_dr1 = 0;   // dr[1] left by the last earlier split point that fetched it (normal branch)
+		for (int i0 = 0; i0 < n; i0 += 64) {
+			int i = i0 + lane;
+			int sc = -0x7fffffff, sp = 0;
+			bool cand = false, dr_set = false;
+			char dl0 = 0, dl1 = 0, dr0 = 0, dr1 = 0;
+			if (i < n) {
+				sp = mid + ((i % 2) ? -((i + 1) / 2) : ((1 + i) / 2));
+				if (sp <= rl - JCW && sp >= JCW) {
+					bool ok = false;
+					if (p.prefer_donor_receptor_junctions) {
+						if (normal) {
+							dl0 = gv_get(left + sp); dl1 = gv_get(left + sp + 1);
+							if (donor_pair(dl0, dl1)) {
+								dr0 = gv_get(right + sp - 2); dr1 = gv_get(right + sp - 1);
+								dr_set = true;
+								if (donor_pair(dr0, dr1))
+									ok = ((dl0 == 'G' && dl1 == 'T' && dr0 == 'A' && dr1 == 'G') || (dl0 == 'C' && dl1 == 'T' && dr0 == 'A' && dr1 == 'C'))
+									     && ((dl0 == 'C' && dl1 == 'T') || (dl0 == 'G' && dl1 == 'T'));
+							}
+						} else {
+							dl0 = gv_get(right + sp); dl1 = gv_get(right + sp + 1);
+							dr0 = gv_get(left + sp - 2); dr1 = gv_get(left + sp - 1);
+							dr_set = true;
+							ok = donor_pair(dl0, dl1) && donor_pair(dr0, dr1)
+							     && ((dl0 == 'G' && dl1 == 'T' && dr0 == 'A' && dr1 == 'G') || (dl0 == 'C' && dl1 == 'T' && dr0 == 'A' && dr1 == 'C'))
+							     && ((dl0 == 'C' && dl1 == 'T') || (dl0 == 'G' && dl1 == 'T'));
+						}
+					}
+					if (ok || !need_donor) {
+						int lm, rm, ln, rn;
+						if (normal) {
+							lm = match_chro(read, rl, sp - JCW, left + sp - JCW, JCW);
+							if (lm > JCW - 2) {
+								rm = match_chro(read, rl, sp, right + sp, JCW);
+								if (rm >= 2 * JCW - lm - allow) {
+									ln = match_chro(read, rl, sp, left + sp, JCW);
+									rn = match_chro(read, rl, sp - JCW, right + sp - JCW, JCW);
+									if (ln <= JCW - 5 && rn <= JCW - 5) { sc = 100 * ((ok ? 3000 : 0) + lm + rm - ln - rn); cand = true; }
+								}
+							}
+						} else {
+							rm = match_chro(read, rl, sp - JCW, right + sp - JCW, JCW);
+							lm = match_chro(read, rl, sp, left + sp, JCW);
+							rn = match_chro(read, rl, sp, right + sp, JCW);
+							ln = match_chro(read, rl, sp - JCW, left + sp - JCW, JCW);
+							if (lm + rm >= 2 * JCW - allow && ln <= JCW - 5 && rn <= JCW - 5) { sc = 100 * ((ok ? 3000 : 0) + lm + rm - ln - rn); cand = true; }
+						}
+					}
+				}
+			}
+			// the strand test uses the dr[] the reference's loop holds at that point: this split
+			// point's when fetched, else the last earlier fetch (only reachable without the donor test)
+			unsigned long long dm = ballot(dr_set);
+			unsigned long long below = dm & ((1ull << lane) - 1ull);
+			int prev_dr1 = below ? __shfl((int)dr1, 63 - __clzll(below)) : carry_dr1;
+			int use_dr1 = dr_set ? (int)dr1 : prev_dr1;
+			if (dm) carry_dr1 = __shfl((int)dr1, 63 - __clzll(dm));
+			int strand = (dl0 == 'G' || use_dr1 == 'G') ? 1 : 0;
+			int cmax = wave_max(cand ? sc : -0x7fffffff);
+			unsigned long long wm = ballot(cand && sc == cmax);
+			if (wm && cmax > best) {
+				int w = __ffsll((long long)wm) - 1;   // lowest visiting index in this chunk
+				best = cmax;
+				bi = i0 + w;
+				bsp = __shfl(sp, w);
+				bstrand = __shfl(strand, w);
+			}
+		}
+		(void)bi;
+		if (best > 0) {
+			*split = bsp; *found = best >= 290000; *gtag = bstrand;
+			return (1 + best) / 100;
+		}
+		return 0;
+	}
+
+	// junction part of copy_vote_to_alignment_res (core-junction.c:1073-1334, no fusion):
+	// every other used slot of the table is a minor-half candidate.  The J-independent
+	// filters run lane-parallel; the is_better chain and donor scoring run in slot order.
+	__device__ void junction(int e, int ms, uint32_t *r, uint32_t *J, int rs_v, int U)
+	{
+		const svg_params &p = kp->p;
+		const int lane = lane_id();
+		const uint32_t Mpos = L->pos[e][ms];
+		const int Mv = m_votes(L->meta[e][ms]);
+		const uint32_t mw = cold_slot(cold[e], ms)[0];
+		const int Mcs = (int)(mw & 0xffff), Mce = (int)(mw >> 16);
+		const int rl = rc.rl[e];
+		int Jv = 0, Jcs = 0, Jce = 0, Jsplit = 0, Jnormal = 0;
+		uint32_t Jpos = 0;
+		int flags = (int)(r[1] & 0xffff);
+		bool upd = false;
+		for (int f0 = 0; f0 < U; f0 += 64) {
+			int f = f0 + lane;
+			int sl = slot_of(e, rs_v, f);   // all lanes active
+			bool ok = f < U && sl != ms;
+			uint32_t P = 0;
+			int V = 0, cs = 0, ce = 0;
+			if (ok) {
+				P = L->pos[e][sl];
+				V = m_votes(L->meta[e][sl]);
+				uint32_t w = cold_slot(cold[e], sl)[0];
+				cs = (int)(w & 0xffff); ce = (int)(w >> 16);
+				long long dist = (long long)Mpos - (long long)P;
+				ok = Mv >= V && (dist < 0 ? -dist : dist) <= (long long)p.maximum_intron_length && cs != Mcs && ce != Mce;
+				if (ok) ok = (Mcs > cs) ? (Mpos >= P) : (Mpos <= P);   // test_junction_minor
+				if (ok) {
+					int ov = (Mcs > cs) ? ce - Mcs : Mce - cs;
+					ok = ov <= 14 && abs((int)dist) >= 6;
+				}
+			}
+			unsigned long long m = ballot(ok);
+			while (m) {
+				int b = __ffsll((long long)m) - 1;
+				m &= m - 1;
+				uint32_t Pb = (uint32_t)rd((int)P, b);
+				int Vb = rd(V, b), csb = rd(cs, b), ceb = rd(ce, b);
+				// is_better_inner, core-junction.c:961
+				int old_intron = (int)abs32u(Mpos - Jpos), intron = (int)abs32u(Mpos - Pb);
+				int cl = ceb - csb, jl = Jce - Jcs;
+				bool better = Vb > Jv || (Vb == Jv && cl > jl) || (Vb == Jv && cl == jl && intron < old_intron);
+				if (!better) continue;
+				int gs = (Mcs > csb) ? ceb - 8 : Mce - 8;
+				int ge = (Mcs < csb) ? csb + 8 : Mcs + 8;
+				int normal = 1 != (int)(Mcs > csb) + (int)(Mpos > Pb);
+				int split = 0, gtag = 0, found = 0;
+				int sc = donor(e, Mpos < Pb ? Mpos : Pb, Mpos > Pb ? Mpos : Pb, normal, gs > 0 ? gs : 0, ge < rl ? ge : rl,
+				               &split, &gtag, &found);
+				if (sc > 0) {
+					Jpos = Pb; Jv = Vb; Jcs = csb; Jce = ceb; Jsplit = split; Jnormal = normal;
+					flags &= ~0x3;
+					if (!found || gtag > 2) flags |= 3;
+					else flags = gtag ? (flags | 1) : (flags & ~1);
+					flags &= ~4;
+					upd = true;
+				}
+			}
+		}
+		if (upd && lane == 0) {
+			// subjunc_result_t: split_point, minor_votes | double_indel_offset 0, indel_at_junction 0,
+			// small/large_side_increasing_coordinate = !normal / normal of the last update
+			J[0] = (uint32_t)(uint16_t)Jsplit | ((uint32_t)(uint16_t)Jv << 16);
+			J[1] = ((uint32_t)(Jnormal ? 0 : 1) << 16) | ((uint32_t)(Jnormal ? 1 : 0) << 24);
+			J[2] = Jpos;
+			J[3] = (uint32_t)(uint16_t)Jcs | ((uint32_t)(uint16_t)Jce << 16);
+			r[1] = (r[1] & 0xffff0000u) | (uint32_t)(uint16_t)flags;
+		}
+		wsync();
+	}
+
 	// flattened (row-major) used-slot index f -> slot, given the inclusive row prefix rs_v
 	// (lane 32*e+r holds items[0..r] of table e).  Must run with every lane active: the
 	// cross-lane read (ds_bpermute) returns nothing useful from inactive source lanes.
@@ -575,6 +780,20 @@ struct Wave {
 					bool sel = f < U[e] && v == N && v >= p.min_votes_second;
 					unsigned long long sm = ballot(sel);
 					int at = ns + lanes_below(sm);
+					if constexpr (SJ) {
+						// insert_big_margin_record (core-junction.c:2276-2277,789) for every slot the
+						// reference's scan visits before max_vote_simples is reached, first value only
+						if (t == 0 && p.do_big_margin_filtering_for_junctions) {
+							unsigned long long bmm = ballot(f < U[e] && at < p.max_vote_simples && v >= top[e][TS - 1]);
+							while (bmm) {
+								int b = __ffsll((long long)bmm) - 1;
+								bmm &= bmm - 1;
+								int bs = rd(slot, b), bv = rd(v, b);
+								if (lane == 0) big_margin_insert(e, bv, bs);
+								wsync();
+							}
+						}
+					}
 					if (sel && at < p.max_vote_simples) {
 						L->simp_pos[e][at] = L->pos[e][slot];
 						L->simp_slot[e][at] = (uint16_t)slot;
@@ -598,8 +817,10 @@ struct Wave {
 			nsimp[e] = ns;
 		}
 		wsync();
-		for (int e = 0; e < ENDS; e++)
+		for (int e = 0; e < ENDS; e++) {
 			for (int i = 0; i < 3; i++) rec_zero(L->tmp[e][i]);
+			if constexpr (SJ) { if (lane < 12) L->jtmp[e][lane / 4][lane % 4] = 0; }
+		}
 		wsync();
 		int cur[2] = {0, 0};
 		int ncomb = 0;
@@ -669,7 +890,7 @@ struct Wave {
 						bool ex = false;
 						for (int j = 0; j < cur[e]; j++) if (rec_pos(L->tmp[e][j]) == ps) ex = true;
 						if (ex) continue;
-						emit(e, si, cur[e]);
+						emit(e, si, cur[e], rs_v, U[e]);
 						cur[e]++;
 					}
 				}
@@ -687,7 +908,7 @@ struct Wave {
 					bool ex = false;
 					for (int j = 0; j < cur[e]; j++) if (rec_pos(L->tmp[e][j]) == ps) ex = true;
 					if (ex) continue;
-					emit(e, i, cur[e]);
+					emit(e, i, cur[e], rs_v, U[e]);
 					cur[e]++;
 				}
 		}
@@ -696,22 +917,53 @@ struct Wave {
 			for (int i = 0; i < p.multi_best; i++) {
 				if (i < cur[e]) { if (lane < 17) L->res[e][i][lane] = L->tmp[e][i][lane]; }
 				else if (lane == 0) rec_set_votes(L->res[e][i], 0);
+				if constexpr (SJ) {
+					if (p.do_breakpoint_detection) {
+						if (i < cur[e]) { if (lane < 4) L->jres[e][i][lane] = L->jtmp[e][i][lane]; }
+						else if (lane == 0) L->jres[e][i][0] &= 0xffffu;   // minor_votes = 0
+					}
+				}
 			}
 		wsync();
 	}
 
 	// write simple si of end e as tmp record slot c
-	__device__ void emit(int e, int si, int c)
+	__device__ void emit(int e, int si, int c, int rs_v, int U)
 	{
 		int sl = L->simp_slot[e][si];
 		if (sl & 0x8000) {
 			if (lane_id() < 17) L->tmp[e][c][lane_id()] = L->res[e][sl & 3][lane_id()];
+			if constexpr (SJ) { if (lane_id() < 4) L->jtmp[e][c][lane_id()] = L->jres[e][sl & 3][lane_id()]; }
 		} else {
 			copy_vote(e, sl, L->tmp[e][c]);
 			// result_flags: IS_NEGATIVE_STRAND mask of the slot (every slot of a table has the table's strand)
 			if (lane_id() == 0) L->tmp[e][c][1] = cur_strand ? (uint32_t)SVG_NEGATIVE_STRAND_FLAG : 0u;
+			if constexpr (SJ) {
+				if (kp->p.do_breakpoint_detection) {
+					wsync();
+					junction(e, sl, L->tmp[e][c], L->jtmp[e][c], rs_v, U);
+				}
+			}
 		}
 		wsync();
+	}
+
+	// insert_big_margin_record, core-junction.c:789-811 (lane 0)
+	__device__ void big_margin_insert(int e, int votes, int slot)
+	{
+		const int size = kp->p.big_margin_record_size;
+		if (size < 3) return;
+		const uint32_t w = cold_slot(cold[e], slot)[0];
+		const int rs = (int)(w & 0xffff), re = (int)(w >> 16), rl = rc.rl[e];
+		uint16_t *bm = L->bm[e];
+		uint16_t s2 = cur_strand ? (uint16_t)(rl - re) : (uint16_t)rs, e2 = cur_strand ? (uint16_t)(rl - rs) : (uint16_t)re;
+		unsigned char vv = (unsigned char)votes;
+		int x1;
+		for (x1 = 0; x1 < size / 3; x1++) if (vv >= bm[x1 * 3]) break;
+		if (x1 < size / 3) {
+			for (int x2 = size - 4; x2 >= x1 * 3; x2--) bm[x2 + 3] = bm[x2];
+			bm[x1 * 3] = vv; bm[x1 * 3 + 1] = s2; bm[x1 * 3 + 2] = e2;
+		}
 	}
 
 	// voting of one end for one strand: init_gene_vote + subread loop + shift-indel round
@@ -813,6 +1065,18 @@ struct Wave {
 			uint32_t *dst = (uint32_t *)(kp->out + ((r * ENDS + e) * (uint64_t)p.multi_best) * 68);
 			for (int w = lane; w < 17 * p.multi_best; w += 64) dst[w] = L->res[e][w / 17][w % 17];
 		}
+		if constexpr (SJ) {
+			for (int e = 0; e < ENDS; e++) {
+				if (p.do_breakpoint_detection) {
+					uint32_t *jd = (uint32_t *)(kp->jout + ((r * ENDS + e) * (uint64_t)p.multi_best) * 16);
+					if (lane < 4 * p.multi_best) jd[lane] = L->jres[e][lane / 4][lane % 4];
+				}
+				if (p.do_big_margin_filtering_for_junctions) {
+					uint16_t *bd = kp->bm_out + (r * ENDS + e) * (uint64_t)SVG_BIG_MARGIN_WORDS;
+					if (lane < SVG_BIG_MARGIN_WORDS) bd[lane] = L->bm[e][lane];
+				}
+			}
+		}
 		if (kp->stats) {
 			int nres = 0;
 			for (int e = 0; e < ENDS; e++)
@@ -823,7 +1087,7 @@ struct Wave {
 	}
 };
 
-template <int ENDS, int MAXL, int MAXP, int WPB, int OCC>
+template <int ENDS, int MAXL, int MAXP, int WPB, int OCC, bool SJ>
 __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 {
 	extern __shared__ __align__(16) uint8_t lds_raw[];
@@ -831,7 +1095,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	const int wib = threadIdx.x >> 6;
 	const uint64_t gw = (uint64_t)blockIdx.x * WPB + wib;
 	const uint64_t nw = (uint64_t)gridDim.x * WPB;
-	Wave<ENDS, MAXL, MAXP> W;
+	Wave<ENDS, MAXL, MAXP, SJ> W;
 	W.L = reinterpret_cast<LT *>(lds_raw + (size_t)wib * ((sizeof(LT) + 15) & ~(size_t)15));
 	W.kp = &kp;
 	const size_t per_end = (size_t)NSLOT * COLD_WORDS + NSLOT;   // cold + shift_locs
@@ -1032,12 +1296,17 @@ static int check_params(const svg_index *h, const svg_params *p, int paired)
 	if (p->max_vote_simples > 16 && !paired) { svg_set_error("single-end max_vote_simples must be <= 16"); return SVG_E_UNSUPPORTED; }
 	if (p->total_subreads < 2 || p->total_subreads > 64) { svg_set_error("total_subreads must be 2..64"); return SVG_E_UNSUPPORTED; }
 	if (p->max_indel_length < 0) { svg_set_error("max_indel_length < 0"); return SVG_E_ARG; }
-	if (p->do_breakpoint_detection) { svg_set_error("subjunc mode is not available in this build"); return SVG_E_UNSUPPORTED; }
+	if (p->do_big_margin_filtering_for_junctions && (p->big_margin_record_size < 0 || p->big_margin_record_size > SVG_BIG_MARGIN_WORDS)) {
+		svg_set_error("big_margin_record_size must be 0..%d", SVG_BIG_MARGIN_WORDS); return SVG_E_UNSUPPORTED;
+	}
+	if (p->do_breakpoint_detection && p->max_insertion_at_junctions != 0) {
+		svg_set_error("max_insertion_at_junctions > 0 reads past the read end in the reference; not supported"); return SVG_E_UNSUPPORTED;
+	}
 	(void)h;
 	return 0;
 }
 
-template <int ENDS, int MAXL, int MAXP, int WPB, int OCC>
+template <int ENDS, int MAXL, int MAXP, int WPB, int OCC, bool SJ>
 static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 {
 	typedef WaveLDS<ENDS, MAXL, MAXP> LT;
@@ -1059,7 +1328,7 @@ static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 		h->scratch_words = words;
 	}
 	kp.scratch = h->d_scratch;
-	hipLaunchKernelGGL((vote_kernel<ENDS, MAXL, MAXP, WPB, OCC>), dim3((unsigned)blocks), dim3(64 * WPB), lds, st, kp);
+	hipLaunchKernelGGL((vote_kernel<ENDS, MAXL, MAXP, WPB, OCC, SJ>), dim3((unsigned)blocks), dim3(64 * WPB), lds, st, kp);
 	HIPCHK(hipGetLastError());
 	return 0;
 }
@@ -1071,6 +1340,12 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	if (r2 && r2->n_reads != r1->n_reads) { svg_set_error("R1/R2 read counts differ"); return SVG_E_ARG; }
 	int rc = check_params(h, p, r2 != NULL);
 	if (rc) return rc;
+	if (p->do_breakpoint_detection && !jout) { svg_set_error("do_breakpoint_detection needs jout"); return SVG_E_ARG; }
+	if (p->do_big_margin_filtering_for_junctions && !big_margin) { svg_set_error("big-margin filtering needs big_margin"); return SVG_E_ARG; }
+	// reads > 160 bp use fragile junction voting (gehash_go_q, core-junction.c:5205) in subjunc mode
+	if ((p->do_breakpoint_detection || p->do_big_margin_filtering_for_junctions) && h->max_read_len > 160) {
+		svg_set_error("subjunc mode supports reads up to 160 bp (announce with svg_set_max_read_length)"); return SVG_E_UNSUPPORTED;
+	}
 	HIPCHK(hipSetDevice(h->device));
 	hipStream_t st = stream ? (hipStream_t)stream : h->stream;
 	if (r1->n_reads == 0) return 0;
@@ -1095,8 +1370,16 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	}
 	// probes per strand are bounded by the read lengths the caller announced
 	int npmax = svg_probe_bound(h->max_read_len, h->dix.gap, p->total_subreads);
-	if (r2) rc = npmax <= 32 ? launch_t<2, 256, 32, 2, 4>(h, kp, st) : launch_t<2, 256, 64, 2, 4>(h, kp, st);
-	else rc = npmax <= 32 ? launch_t<1, 256, 32, 2, 4>(h, kp, st) : launch_t<1, 256, 64, 2, 4>(h, kp, st);
+	// subjunc (junction minor search, donor scoring, big-margin records) is a separate
+	// variant so the plain-align kernels carry none of its registers
+	const bool sj = p->do_breakpoint_detection || p->do_big_margin_filtering_for_junctions;
+	if (sj) {
+		if (r2) rc = npmax <= 32 ? launch_t<2, 256, 32, 2, 4, true>(h, kp, st) : launch_t<2, 256, 64, 2, 4, true>(h, kp, st);
+		else rc = npmax <= 32 ? launch_t<1, 256, 32, 2, 4, true>(h, kp, st) : launch_t<1, 256, 64, 2, 4, true>(h, kp, st);
+	} else {
+		if (r2) rc = npmax <= 32 ? launch_t<2, 256, 32, 2, 4, false>(h, kp, st) : launch_t<2, 256, 64, 2, 4, false>(h, kp, st);
+		else rc = npmax <= 32 ? launch_t<1, 256, 32, 2, 4, false>(h, kp, st) : launch_t<1, 256, 64, 2, 4, false>(h, kp, st);
+	}
 	if (rc) return rc;
 	if (h->stats_on) {
 		unsigned long long s[4];
@@ -1164,8 +1447,13 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 		o_len[e] = in_bytes; in_bytes += (2 * n + 15) & ~15ull;
 	}
 	size_t out_bytes = (size_t)n * ends * p->multi_best * 68;
+	size_t j_bytes = p->do_breakpoint_detection ? (size_t)n * ends * p->multi_best * 16 : 0;
+	size_t bm_bytes = p->do_big_margin_filtering_for_junctions ? (size_t)n * ends * SVG_BIG_MARGIN_WORDS * 2 : 0;
+	size_t o_j = (out_bytes + 255) & ~(size_t)255, o_bm = (o_j + j_bytes + 255) & ~(size_t)255;
+	if (p->do_breakpoint_detection && !jout) { svg_set_error("do_breakpoint_detection needs jout"); return SVG_E_ARG; }
+	if (p->do_big_margin_filtering_for_junctions && !big_margin) { svg_set_error("big-margin filtering needs big_margin"); return SVG_E_ARG; }
 	if ((rc = ensure(h, &h->d_in, &h->d_in_cap, in_bytes))) return rc;
-	if ((rc = ensure(h, &h->d_out, &h->d_out_cap, out_bytes))) return rc;
+	if ((rc = ensure(h, &h->d_out, &h->d_out_cap, o_bm + bm_bytes))) return rc;
 	uint8_t *din = (uint8_t *)h->d_in;
 	uint64_t *tmpoff = (uint64_t *)malloc(8 * n);
 	svg_reads dr[2];
@@ -1183,11 +1471,15 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 	}
 	free(tmpoff);
 	h->max_read_len = batch_max;
-	rc = svg_vote_batch_device(h, p, &dr[0], r2 ? &dr[1] : NULL, (svg_mapping_result *)h->d_out, NULL, NULL, h->stream);
+	uint8_t *dout = (uint8_t *)h->d_out;
+	rc = svg_vote_batch_device(h, p, &dr[0], r2 ? &dr[1] : NULL, (svg_mapping_result *)dout,
+	                           j_bytes ? (svg_subjunc_result *)(dout + o_j) : NULL,
+	                           bm_bytes ? (uint16_t *)(dout + o_bm) : NULL, h->stream);
 	h->max_read_len = saved_len;
 	if (rc) return rc;
-	HIPCHK(hipMemcpyAsync(out, h->d_out, out_bytes, hipMemcpyDeviceToHost, h->stream));
+	HIPCHK(hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, h->stream));
+	if (j_bytes) HIPCHK(hipMemcpyAsync(jout, dout + o_j, j_bytes, hipMemcpyDeviceToHost, h->stream));
+	if (bm_bytes) HIPCHK(hipMemcpyAsync(big_margin, dout + o_bm, bm_bytes, hipMemcpyDeviceToHost, h->stream));
 	HIPCHK(hipStreamSynchronize(h->stream));
-	(void)jout; (void)big_margin;
 	return 0;
 }

@@ -105,6 +105,70 @@ def simulate_reads(genome, n, length=100, seed=20261015, first=0, sub=0.01, inde
     return (rb, tc, tp, ts) if truth else rb
 
 
+def simulate_spliced_reads(genome, n, length=100, seed=5, spliced=0.3, sub=0.005, min_intron=60,
+                           max_intron=50_000):
+    """RNA-seq-like reads for subjunc (config C5): a fraction `spliced` of the reads
+    spans one GT..AG intron of the genome (donor 'GT' right after the first exon
+    part, acceptor 'AG' right before the second), the rest are contiguous.  Exon
+    part lengths are uniform in [10, length-10]; intron lengths log-uniform in
+    [min_intron, max_intron] rounded up to the next AG.  Substitutions at rate
+    `sub`; strand 50/50.  Deterministic in (seed, n).  -> ReadBatch."""
+    rng = np.random.default_rng(seed)
+    g = genome.flat
+    starts = genome.starts.astype(np.int64)
+    ends = starts + genome.lens.astype(np.int64)
+    L = int(length)
+    out = np.empty((n, L), dtype=np.uint8)
+    n_sp = int(n * spliced)
+    # contiguous reads
+    n_ct = n - n_sp
+    if n_ct:
+        usable = np.maximum(genome.lens.astype(np.int64) - L - 1, 0)
+        cum = np.concatenate([[0], np.cumsum(usable)])
+        u = rng.integers(0, cum[-1], n_ct)
+        c = np.searchsorted(cum, u, side="right") - 1
+        pos = starts[c] + (u - cum[c])
+        out[:n_ct] = g[pos[:, None] + np.arange(L)[None, :]]
+    if n_sp:
+        gt = np.flatnonzero((g[:-1] == ord("G")) & (g[1:] == ord("T"))).astype(np.int64)
+        ag_end = np.flatnonzero((g[:-1] == ord("A")) & (g[1:] == ord("G"))).astype(np.int64) + 2
+        got = 0
+        while got < n_sp:
+            m = (n_sp - got) * 2
+            x = gt[rng.integers(0, len(gt), m)]                     # exon 1 ends at x (x = 'G' of GT)
+            a = rng.integers(10, L - 9, m)
+            d = np.exp(rng.uniform(np.log(min_intron), np.log(max_intron), m)).astype(np.int64)
+            k = np.searchsorted(ag_end, x + d)
+            ok = k < len(ag_end)
+            y = np.where(ok, ag_end[np.minimum(k, len(ag_end) - 1)], 0)   # exon 2 starts at y
+            c = np.searchsorted(ends, x, side="right")
+            ok &= c < len(ends)
+            cc = np.minimum(c, len(ends) - 1)
+            ok &= (x - a >= starts[cc]) & (y + (L - a) <= ends[cc]) & (y - x <= max_intron * 2)
+            x, a, y = x[ok], a[ok], y[ok]
+            take = min(len(x), n_sp - got)
+            j = np.arange(L)[None, :]
+            for c0 in range(0, take, 1 << 18):
+                c1 = min(take, c0 + (1 << 18))
+                xa, aa, ya = x[c0:c1, None], a[c0:c1, None], y[c0:c1, None]
+                out[n_ct + got + c0:n_ct + got + c1] = g[np.where(j < aa, xa - aa + j, ya + j - aa)]
+            got += take
+        perm = rng.permutation(n)
+        out = out[perm]
+    # substitutions and strand
+    if sub > 0:
+        hit = rng.random((n, L)) < sub
+        alt = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, (n, L))]
+        out = np.where(hit, alt, out)
+    rev = rng.random(n) < 0.5
+    comp = np.zeros(256, dtype=np.uint8)
+    comp[:] = ord("N")
+    for a_, b_ in (("A", "T"), ("C", "G"), ("G", "C"), ("T", "A")):
+        comp[ord(a_)] = ord(b_)
+    out[rev] = comp[out[rev][:, ::-1]]
+    return ReadBatch.fixed(out)
+
+
 def write_fastq(path, batch, names=None):
     with open(path, "wb") as f:
         for i in range(len(batch)):

@@ -11,7 +11,7 @@ from tests.common import Case, golden_names, ensure_built, pack_records, describ
 ensure_built()
 pytestmark = pytest.mark.gpu
 
-GPU_CASES = [n for n in golden_names() if not n.startswith("sj_")]
+GPU_CASES = golden_names()
 
 
 @pytest.fixture(scope="module")
@@ -52,6 +52,27 @@ def test_gpu_matches_oracle_simulated(key, paired, n, gpu_indexes, index_cache):
     ref, _, _, _ = OracleIndex(pre).vote(p, r1, r2, threads=16)
     got = pack_records(out, None, None)
     want = pack_records(ref, None, None)
+    assert (got == want).all(), describe_mismatch(got, want, 2 if paired else 1, 3)
+
+
+@pytest.mark.parametrize("key,paired,n", [("chr901_full", False, 60000), ("synth4242_gapped", True, 20000),
+                                          ("chr901_gapped", True, 20000)])
+def test_gpu_subjunc_matches_oracle_spliced(key, paired, n, gpu_indexes, index_cache):
+    """Subjunc mode (junction minor search, donor scoring, big-margin records) on
+    spliced reads: ~30% of reads span a GT..AG intron of the genome."""
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.abi import default_params, PROGRAM_SUBJUNC
+    from subread_amd.sim import Genome, simulate_spliced_reads
+    pre = index_cache.get(key)
+    g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
+    r1 = simulate_spliced_reads(g, n, 100, seed=11)
+    r2 = simulate_spliced_reads(g, n, 100, seed=12) if paired else None
+    p = default_params(PROGRAM_SUBJUNC, paired)
+    out, jout, bm = gpu_indexes(key).vote(p, r1, r2)
+    ref, rj, rbm, _ = OracleIndex(pre).vote(p, r1, r2, threads=16)
+    assert (rj["minor_votes"] > 0).sum() > n // 20      # the case exercises junctions
+    got = pack_records(out, jout, bm)
+    want = pack_records(ref, rj, rbm)
     assert (got == want).all(), describe_mismatch(got, want, 2 if paired else 1, 3)
 
 
