@@ -9,6 +9,10 @@ resident in HBM (reads in, mapping_result_t[3] per read out).  Workloads
       1% substitutions, 0.1% reads with a 1-5 bp indel, read seed 20261015.
   c3 (default, the BASELINE.json metric): 50M x 100 bp SE reads per GPU vs a 3.0 Gbp 24-contig genome with repeat
       families, full one-block index.
+  c4: 150 bp PE vs the C3 index, 25M pairs per GPU (400M reads over 8 GPUs); fragments N(300,50)
+      clipped to [150,600], R2 reverse complement.  value counts reads (2 per pair).
+  c5: subjunc mode, 50M x 100 bp RNA-seq-like reads per GPU vs the C3 index, 30% spanning one
+      GT..AG intron (60 bp-50 kbp); outputs mapping + subjunc + big-margin records.
 Multi-GPU (torchrun): one process per GPU, index replicated, reads sharded by
 rank (disjoint read-stream ranges), no collective on the data path; the only
 communication is the timing barrier / max.  scaling = "weak".
@@ -36,12 +40,19 @@ def log(*a):
 
 def workload(name):
     if name == "c2":
-        return dict(lengths=[1_000_000], gseed=901, repeats=None, reads=10_000_000, read_len=100,
+        return dict(lengths=[1_000_000], gseed=901, repeats=None, reads=10_000_000, read_len=100, kind="se",
                     desc="C2: 10M x 100bp SE reads vs chr901-scale 1 Mbp genome, full one-block index")
+    from subread_amd.sim import c3_lengths
+    c3 = dict(lengths=c3_lengths(), gseed=3000, repeats=(1_000_000, 300, 200, 0.12))
     if name == "c3":
-        from subread_amd.sim import c3_lengths
-        return dict(lengths=c3_lengths(), gseed=3000, repeats=(1_000_000, 300, 200, 0.12), reads=50_000_000,
-                    read_len=100, desc="C3: 50M x 100bp SE reads vs 3.0 Gbp 24-contig genome, full one-block index")
+        return dict(c3, reads=50_000_000, read_len=100, kind="se",
+                    desc="C3: 50M x 100bp SE reads vs 3.0 Gbp 24-contig genome, full one-block index")
+    if name == "c4":
+        return dict(c3, reads=25_000_000, read_len=150, kind="pe",
+                    desc="C4: 25M x 2 x 150bp PE pairs per GPU vs the C3 3.0 Gbp index (400M reads on 8 GPUs)")
+    if name == "c5":
+        return dict(c3, reads=50_000_000, read_len=100, kind="sj",
+                    desc="C5: subjunc, 50M x 100bp spliced RNA-seq reads (30% span a GT..AG intron) vs the C3 index")
     raise SystemExit("unknown workload " + name)
 
 
@@ -70,8 +81,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import subread_amd as sa
-    from subread_amd.abi import default_params, PROGRAM_ALIGN, MAPPING_DTYPE
-    from subread_amd.sim import random_genome, simulate_reads
+    from subread_amd.abi import default_params, PROGRAM_ALIGN, PROGRAM_SUBJUNC, MAPPING_DTYPE, BIG_MARGIN_WORDS
+    from subread_amd.sim import random_genome, simulate_reads, simulate_pairs, simulate_spliced_reads
 
     W = workload(args.workload)
     n = args.reads or W["reads"]
@@ -101,23 +112,40 @@ def main():
     log("[bench] index in HBM (%.1f GB, %d items) in %.1fs" % (ix.info.device_bytes / 1e9, ix.info.items,
                                                             time.time() - t1))
 
-    # this rank's shard of the read stream: reads rank*n .. rank*n+n-1
+    # this rank's shard of the read stream: reads (pairs) rank*n .. rank*n+n-1
     t1 = time.time()
-    rb = simulate_reads(genome, n, L, seed=20261015, first=rank * n, sub=0.01, indel=0.001)
-    log("[bench] simulated %d reads in %.1fs" % (n, time.time() - t1))
+    kind = W["kind"]
+    rb2 = None
+    if kind == "pe":
+        rb, rb2 = simulate_pairs(genome, n, L, seed=4004, first=rank * n)
+    elif kind == "sj":
+        rb = simulate_spliced_reads(genome, n, L, seed=5005 + rank)
+    else:
+        rb = simulate_reads(genome, n, L, seed=20261015, first=rank * n, sub=0.01, indel=0.001)
+    ends = 2 if rb2 is not None else 1
+    log("[bench] simulated %d %s in %.1fs" % (n, "pairs" if ends == 2 else "reads", time.time() - t1))
     dev = torch.device("cuda", local)
-    d_seq = torch.from_numpy(rb.seq).to(dev)
-    d_off = torch.from_numpy(rb.offsets.view(np.int64)).to(dev)
-    d_len = torch.from_numpy(rb.lens.view(np.int16)).to(dev)
-    p = default_params(PROGRAM_ALIGN, False)
-    rec_bytes = MAPPING_DTYPE.itemsize * p.multi_best
+
+    def upload(b):
+        return (torch.from_numpy(b.seq).to(dev), torch.from_numpy(b.offsets.view(np.int64)).to(dev),
+                torch.from_numpy(b.lens.view(np.int16)).to(dev))
+    d1 = upload(rb)
+    d2 = upload(rb2) if rb2 is not None else None
+    p = default_params(PROGRAM_SUBJUNC if kind == "sj" else PROGRAM_ALIGN, ends == 2)
+    rec_bytes = MAPPING_DTYPE.itemsize * p.multi_best * ends
     d_out = torch.empty(n * rec_bytes, dtype=torch.uint8, device=dev)
+    d_jout = torch.empty(n * ends * p.multi_best * 16, dtype=torch.uint8, device=dev) if kind == "sj" else None
+    d_bm = torch.empty(n * ends * BIG_MARGIN_WORDS * 2, dtype=torch.uint8, device=dev) if kind == "sj" else None
+    if kind == "sj":
+        rec_bytes += ends * (p.multi_best * 16 + BIG_MARGIN_WORDS * 2)
     ix.set_max_read_length(int(os.environ.get("SVG_BENCH_MAXLEN", L)))
     stream = torch.cuda.Stream(device=dev)
-    r1 = (d_seq.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n)
+    r1 = (d1[0].data_ptr(), d1[1].data_ptr(), d1[2].data_ptr(), n)
+    r2 = (d2[0].data_ptr(), d2[1].data_ptr(), d2[2].data_ptr(), n) if d2 is not None else None
 
     def step():
-        ix.vote_device(p, r1, None, d_out.data_ptr(), stream=stream.cuda_stream)
+        ix.vote_device(p, r1, r2, d_out.data_ptr(), d_jout.data_ptr() if d_jout is not None else None,
+                       d_bm.data_ptr() if d_bm is not None else None, stream=stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
@@ -148,7 +176,7 @@ def main():
     torch.cuda.synchronize()
     st = ix.stats()
     ix.set_stats(False)
-    in_bytes = n * (L + 8 + 2)                       # ASCII read + offset + length
+    in_bytes = n * ends * (L + 8 + 2)                # ASCII read + offset + length
     probe_bytes = 8 * st["probes"] + 2 * st["bucket_items"] + 4 * st["hits"]
     out_bytes = n * rec_bytes
     algo_bytes = in_bytes + probe_bytes + out_bytes
@@ -174,9 +202,17 @@ def main():
     if rank == 0 and not args.no_check:
         # parity spot check against the oracle restatement (outside the timed region)
         m = min(n, 20000)
-        got = d_out[: m * rec_bytes].cpu().numpy().reshape(m, -1)
-        ref, _, _, _ = oi.vote(p, rb.slice(0, m), threads=args.cpu_threads)
-        check = bool((ref.view(np.uint8).reshape(m, -1) == got).all())
+        mb = p.multi_best
+        got = [d_out[: m * ends * mb * 68].cpu().numpy().reshape(m, -1)]
+        if d_jout is not None:
+            got.append(d_jout[: m * ends * mb * 16].cpu().numpy().reshape(m, -1))
+            got.append(d_bm[: m * ends * BIG_MARGIN_WORDS * 2].cpu().numpy().reshape(m, -1))
+        ref, rj, rbm, _ = oi.vote(p, rb.slice(0, m), rb2.slice(0, m) if rb2 is not None else None,
+                                  threads=args.cpu_threads)
+        want = [ref.view(np.uint8).reshape(m, -1)]
+        if d_jout is not None:
+            want += [rj.view(np.uint8).reshape(m, -1), rbm.view(np.uint8).reshape(m, -1)]
+        check = bool(all((a == b).all() for a, b in zip(got, want)))
         log("[bench] parity spot check on %d reads: %s" % (m, "IDENTICAL" if check else "MISMATCH"))
     cpu = None
     if rank == 0 and not args.no_cpu:
@@ -185,14 +221,15 @@ def main():
         while cs < 10.0 and done < min(n, args.cpu_sample):
             b = min(chunk, n - done)
             t1 = time.perf_counter()
-            oi.vote(p, rb.slice(done, done + b), threads=args.cpu_threads)
+            oi.vote(p, rb.slice(done, done + b), rb2.slice(done, done + b) if rb2 is not None else None,
+                    threads=args.cpu_threads)
             cs += time.perf_counter() - t1
             done += b
-        cpu = {"value": round(done / cs / 1e6, 4), "unit": "Mreads/s", "cores": args.cpu_threads, "kind": "port",
+        cpu = {"value": round(done * ends / cs / 1e6, 4), "unit": "Mreads/s", "cores": args.cpu_threads, "kind": "port",
                "sample": "first %d reads of the timed batch, oracle/svoracle.c restatement, %d pthreads, %.1f s" % (
                    done, args.cpu_threads, cs)}
 
-    total_reads = n * world * args.steps
+    total_reads = n * ends * world * args.steps
     value = total_reads / elapsed / 1e6
     if rank == 0:
         line = {
@@ -200,7 +237,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic",
-            "config": {"workload": W["desc"], "reads_per_gpu_per_step": n, "read_len": L,
+            "config": {"workload": W["desc"], "reads_per_gpu_per_step": n * ends, "read_len": L,
+                       "mode": {"se": "subread-align SE", "pe": "subread-align PE", "sj": "subjunc SE"}[kind],
                        "index": "full one-block (gap 1), %d buckets, %d items, %s" % (
                            ix.info.buckets, ix.info.items,
                            "reference-format files via svg_index_open" if prefix else "built in HBM by svg_index_build_mem"),

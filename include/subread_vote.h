@@ -231,6 +231,11 @@ int  svg_sim_reads(const char *genome, const uint64_t *ctg_start, const uint32_t
                    uint32_t n_ctg, uint64_t first, uint64_t n_reads, int len, double sub,
                    double indel_frac, double n_rate, uint64_t seed, char *seq,
                    uint32_t *truth_ctg, uint32_t *truth_pos, uint8_t *truth_strand, int threads);
+/* paired-end fragments (test/bench input generator): R1 forward, R2 reverse
+ * complement of the fragment end; pairs first..first+n_pairs-1 of the stream. */
+int  svg_sim_pairs(const char *genome, const uint64_t *ctg_start, const uint32_t *ctg_len, uint32_t n_ctg,
+                   uint64_t first, uint64_t n_pairs, int len, double ins_mean, double ins_sd, int ins_max,
+                   double sub, uint64_t seed, char *seq1, char *seq2, int threads);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,7 @@ EXPORTS = [
     "svg_vote_batch", "svg_vote_batch_device", "svg_set_stats", "svg_get_stats",
     "svg_last_error", "svg_abi_version", "svg_build_index", "svg_sim_genome",
     "svg_sim_repeats", "svg_sim_reads", "svg_index_build", "svg_index_build_mem", "svg_index_export",
-    "svg_set_max_read_length",
+    "svg_set_max_read_length", "svg_sim_pairs",
 ]
 
 _lib = None
@@ -82,6 +82,9 @@ def lib():
         L.svg_sim_reads.argtypes = [vp, vp, vp, ctypes.c_uint32, u64, u64, i32, ctypes.c_double,
                                     ctypes.c_double, ctypes.c_double, u64, vp, vp, vp, vp, i32]
         L.svg_sim_reads.restype = i32
+        L.svg_sim_pairs.argtypes = [vp, vp, vp, ctypes.c_uint32, u64, u64, i32, ctypes.c_double, ctypes.c_double,
+                                    i32, ctypes.c_double, u64, vp, vp, i32]
+        L.svg_sim_pairs.restype = i32
         _lib = L
     return _lib
 

@@ -157,16 +157,38 @@ def simulate_spliced_reads(genome, n, length=100, seed=5, spliced=0.3, sub=0.005
         out = out[perm]
     # substitutions and strand
     if sub > 0:
-        hit = rng.random((n, L)) < sub
-        alt = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, (n, L))]
-        out = np.where(hit, alt, out)
+        alphabet = np.frombuffer(b"ACGT", dtype=np.uint8)
+        for c0 in range(0, n, 1 << 20):
+            blk = out[c0:c0 + (1 << 20)]
+            hit = rng.random(blk.shape) < sub
+            blk[hit] = alphabet[rng.integers(0, 4, int(hit.sum()))]
     rev = rng.random(n) < 0.5
     comp = np.zeros(256, dtype=np.uint8)
     comp[:] = ord("N")
     for a_, b_ in (("A", "T"), ("C", "G"), ("G", "C"), ("T", "A")):
         comp[ord(a_)] = ord(b_)
-    out[rev] = comp[out[rev][:, ::-1]]
+    for c0 in range(0, n, 1 << 20):
+        blk, rv = out[c0:c0 + (1 << 20)], rev[c0:c0 + (1 << 20)]
+        blk[rv] = comp[blk[rv][:, ::-1]]
     return ReadBatch.fixed(out)
+
+
+def simulate_pairs(genome, n, length=150, seed=4004, first=0, insert_mean=300.0, insert_sd=50.0,
+                   insert_max=600, sub=0.01, threads=None):
+    """Paired-end reads (config C4), svg_sim_pairs: fragment length N(insert_mean,
+    insert_sd) clipped to [length, insert_max], uniform start, fragment strand 50/50;
+    R1 = first `length` bases of the fragment's strand, R2 = reverse complement of
+    its last `length` bases (the reference's default -S fr).  Pairs
+    first..first+n-1 of the stream.  -> (ReadBatch R1, ReadBatch R2)."""
+    s1 = np.empty((n, length), dtype=np.uint8)
+    s2 = np.empty((n, length), dtype=np.uint8)
+    rc = lib().svg_sim_pairs(genome.flat.ctypes.data, genome.starts.ctypes.data, genome.lens.ctypes.data,
+                             len(genome.lens), int(first), int(n), int(length), float(insert_mean),
+                             float(insert_sd), int(insert_max), float(sub), int(seed), s1.ctypes.data,
+                             s2.ctypes.data, threads or min(16, os.cpu_count() or 1))
+    if rc != 0:
+        raise RuntimeError("svg_sim_pairs failed %d" % rc)
+    return ReadBatch.fixed(s1), ReadBatch.fixed(s2)
 
 
 def write_fastq(path, batch, names=None):
