@@ -36,6 +36,9 @@ extern "C" {
 
 /* reference constants (subread.h:73,88,216-217; core-junction.c:3569) */
 #define SVG_MAX_READ_LENGTH       1210   /* MAX_READ_LENGTH == index padding */
+/* the reference's reader keeps at most MAX_READ_LENGTH-1 bases of a read line
+ * (read_line, input-files.c:277); longer reads are truncated the same way here */
+#define SVG_READ_KEEP             (SVG_MAX_READ_LENGTH - 1)
 #define SVG_MAX_INDEL_SECTIONS    7
 #define SVG_VOTE_TABLE_SIZE       30     /* GENE_VOTE_TABLE_SIZE */
 #define SVG_VOTE_SPACE            24     /* GENE_VOTE_SPACE */

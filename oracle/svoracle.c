@@ -882,6 +882,7 @@ static void *worker(void *arg)
 			for (e = 0; e < ends; e++) {
 				const svg_reads *rr = e ? b->r2 : b->r1;
 				int len = rr->lens[r];
+				if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;   /* read_line keeps MAX_READ_LENGTH-1 (input-files.c:277) */
 				int rev = e ? b->p->reverse_r2 : b->p->reverse_r1;
 				memcpy(c->text[e], rr->seq + rr->offsets[r], len);
 				c->text[e][len] = 0;
@@ -923,8 +924,6 @@ int svo_vote_batch(const svo_index *ix, const svg_params *p, const svg_reads *r1
 	if (p->do_breakpoint_detection && !jout) return SVG_E_ARG;
 	if (p->do_big_margin_filtering_for_junctions && !bm) return SVG_E_ARG;
 	for (i = 0; i < r1->n_reads; i++) {
-		if (r1->lens[i] > SVG_MAX_READ_LENGTH) return SVG_E_UNSUPPORTED;
-		if (r2 && r2->lens[i] > SVG_MAX_READ_LENGTH) return SVG_E_UNSUPPORTED;
 		if (p->do_breakpoint_detection && (r1->lens[i] > LONG_READ || (r2 && r2->lens[i] > LONG_READ))) return SVG_E_UNSUPPORTED;
 	}
 	memset(&b, 0, sizeof b);

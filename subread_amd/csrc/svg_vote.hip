@@ -990,6 +990,7 @@ struct Wave {
 			const char *seq = e ? kp->seq2 : kp->seq1;
 			uint64_t o = e ? kp->off2[r] : kp->off1[r];
 			int len = e ? kp->len2[r] : kp->len1[r];
+			if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;   // read_line keeps MAX_READ_LENGTH-1 (input-files.c:277)
 			int rev = e ? p.reverse_r2 : p.reverse_r1;
 			rc.rl[e] = len;
 			if (len > MAXL) {   // host-validated; never index LDS past the text buffer
@@ -997,21 +998,24 @@ struct Wave {
 				len = 0;
 				rc.rl[e] = 0;
 			}
-			// all MAXL/64 chunk loads are issued before the first LDS write, so the
-			// read costs one HBM latency, not one per 64 bases (measured: -11% when
-			// the compiler kept this as a rolled loop)
-			char c[MAXL / 64], c2[MAXL / 64];
+			// chunk loads are issued in batches of TB (all of a <=256 bp read at once) before
+			// the first LDS write, so a read costs one HBM latency, not one per 64 bases
+			// (measured: -11% when the compiler kept this as a rolled loop)
+			constexpr int TB = MAXL / 64 < 4 ? MAXL / 64 : 4;
+			for (int k0 = 0; k0 < len; k0 += 64 * TB) {
+				char c[TB], c2[TB];
 #pragma unroll
-			for (int k = 0; k < MAXL / 64; k++) {
-				int i = lane + 64 * k;
-				if (i < len) { c[k] = seq[o + i]; c2[k] = seq[o + (len - 1 - i)]; }
-			}
+				for (int k = 0; k < TB; k++) {
+					int i = k0 + lane + 64 * k;
+					if (i < len) { c[k] = seq[o + i]; c2[k] = seq[o + (len - 1 - i)]; }
+				}
 #pragma unroll
-			for (int k = 0; k < MAXL / 64; k++) {
-				int i = lane + 64 * k;
-				if (i < len) {
-					L->text[e][0][i] = rev ? comp(c2[k]) : c[k];
-					L->text[e][1][i] = rev ? comp(comp(c[k])) : comp(c2[k]);   // reverse_read of strand 0
+				for (int k = 0; k < TB; k++) {
+					int i = k0 + lane + 64 * k;
+					if (i < len) {
+						L->text[e][0][i] = rev ? comp(c2[k]) : c[k];
+						L->text[e][1][i] = rev ? comp(comp(c[k])) : comp(c2[k]);   // reverse_read of strand 0
+					}
 				}
 			}
 			if (len >= 15 + gap) {   // shorter reads: out of contract, no hits (see oracle)
@@ -1373,9 +1377,14 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	// subjunc (junction minor search, donor scoring, big-margin records) is a separate
 	// variant so the plain-align kernels carry none of its registers
 	const bool sj = p->do_breakpoint_detection || p->do_big_margin_filtering_for_junctions;
+	if (sj && npmax > 64) { svg_set_error("subjunc mode: %d subreads per strand exceed 64", npmax); return SVG_E_UNSUPPORTED; }
 	if (sj) {
 		if (r2) rc = npmax <= 32 ? launch_t<2, 256, 32, 2, 4, true>(h, kp, st) : launch_t<2, 256, 64, 2, 4, true>(h, kp, st);
 		else rc = npmax <= 32 ? launch_t<1, 256, 32, 2, 4, true>(h, kp, st) : launch_t<1, 256, 64, 2, 4, true>(h, kp, st);
+	} else if (h->max_read_len > 256 || npmax > 64) {
+		// long reads (161..1210 bp: 6 bp subread step, <= 63 subreads per gap slot)
+		if (r2) rc = npmax <= 64 ? launch_t<2, 1216, 64, 2, 4, false>(h, kp, st) : launch_t<2, 1216, 192, 2, 4, false>(h, kp, st);
+		else rc = npmax <= 64 ? launch_t<1, 1216, 64, 2, 4, false>(h, kp, st) : launch_t<1, 1216, 192, 2, 4, false>(h, kp, st);
 	} else {
 		if (r2) rc = npmax <= 32 ? launch_t<2, 256, 32, 2, 4, false>(h, kp, st) : launch_t<2, 256, 64, 2, 4, false>(h, kp, st);
 		else rc = npmax <= 32 ? launch_t<1, 256, 32, 2, 4, false>(h, kp, st) : launch_t<1, 256, 64, 2, 4, false>(h, kp, st);
@@ -1423,12 +1432,12 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 		uint64_t mn = ~0ull, mx = 0;
 		for (uint64_t i = 0; i < n; i++) {
 			int len = rr->lens[i];
-			if (len > 256) { svg_set_error("read %llu longer than 256 bases (long-read kernel not built)", (unsigned long long)i); return SVG_E_UNSUPPORTED; }
+			if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;
 			if (len >= 15 + h->dix.gap) {
 				int cr = (len - 15 - h->dix.gap) << 16, step;
 				if (len <= 160) { step = cr / (p->total_subreads - 1); if (step < (h->dix.gap << 16)) step = h->dix.gap << 16; }
 				else { step = 6 << 16; if (cr / step > 62) step = cr / 62; }
-				if ((1 + cr / step) * h->dix.gap > 64) { svg_set_error("read %llu needs %d probes per strand (> 64; long-read kernel not built)", (unsigned long long)i, (1 + cr / step) * h->dix.gap); return SVG_E_UNSUPPORTED; }
+				if ((1 + cr / step) * h->dix.gap > 192) { svg_set_error("read %llu needs %d probes per strand (> 192)", (unsigned long long)i, (1 + cr / step) * h->dix.gap); return SVG_E_UNSUPPORTED; }
 			}
 			if (rr->offsets[i] < mn) mn = rr->offsets[i];
 			if (rr->offsets[i] + rr->lens[i] > mx) mx = rr->offsets[i] + rr->lens[i];
@@ -1438,7 +1447,7 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 	int saved_len = h->max_read_len, batch_max = 16;
 	for (int e = 0; e < ends; e++) {
 		const svg_reads *rr = e ? r2 : r1;
-		for (uint64_t i = 0; i < n; i++) if (rr->lens[i] > batch_max) batch_max = rr->lens[i];
+		for (uint64_t i = 0; i < n; i++) if (rr->lens[i] > batch_max) batch_max = rr->lens[i] < SVG_READ_KEEP ? rr->lens[i] : SVG_READ_KEEP;
 	}
 	size_t in_bytes = 0, o_seq[2], o_off[2], o_len[2];
 	for (int e = 0; e < ends; e++) {

@@ -213,6 +213,32 @@ def main():
                       ReadBatch.from_list(sr2), "synthetic multi-contig repeat genome seed 4242, pairs seed 99"))
         cases.append(("se_gapped_synth", PROGRAM_ALIGN, False, "synth4242_gapped", {}, ReadBatch.from_list(sr1), None,
                       "synthetic multi-contig repeat genome seed 4242, R1 of pairs seed 99"))
+        # long reads (161..1210 bp: 6 bp subread step, up to 63 subreads x gap per strand)
+        cases.append(("se_full_long", PROGRAM_ALIGN, False, "chr901_full", {},
+                      mixed_reads(g901, 600, 13, [161, 255, 256, 257, 300, 500, 800, 1000, 1210], False), None,
+                      "synthetic mixed long reads seed 13 (161-1210 bp)"))
+        cases.append(("se_gapped_long", PROGRAM_ALIGN, False, "chr901_gapped", {},
+                      mixed_reads(g901, 400, 14, [170, 200, 400, 700, 1210], True), None,
+                      "synthetic mixed long reads seed 14 (170-1210 bp, up to 189 subreads per strand)"))
+        lr1, lr2 = [], []
+        rng = np.random.default_rng(15)
+        g = g901.flat
+        for i in range(400):
+            L = int(rng.choice([200, 250, 400]))
+            ins = int(rng.integers(L, 700))
+            st = int(rng.integers(0, len(g) - ins - 1))
+            a = g[st:st + L].tobytes()
+            comp = {65: 84, 67: 71, 71: 67, 84: 65}
+            b = bytes(comp.get(x, 78) for x in reversed(g[st + ins - L:st + ins].tobytes()))
+            if rng.random() < 0.5:
+                a, b = b, a
+            lr1.append(a)
+            lr2.append(b)
+        cases.append(("pe_full_long", PROGRAM_ALIGN, True, "chr901_full", {}, ReadBatch.from_list(lr1),
+                      ReadBatch.from_list(lr2), "chr901 pairs seed 15, 200/250/400 bp, fragments up to 700 bp"))
+        only = set(sys.argv[1:])
+        if only:
+            cases = [c for c in cases if c[0] in only]
 
         for name, prog, paired, ikey, over, r1, r2, note in cases:
             extra = []

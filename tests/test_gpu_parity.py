@@ -76,6 +76,29 @@ def test_gpu_subjunc_matches_oracle_spliced(key, paired, n, gpu_indexes, index_c
     assert (got == want).all(), describe_mismatch(got, want, 2 if paired else 1, 3)
 
 
+@pytest.mark.parametrize("key,paired,length,n", [("chr901_full", False, 400, 20000), ("chr901_gapped", False, 300, 8000),
+                                                 ("chr901_full", True, 250, 10000), ("chr901_full", False, 1500, 2000)])
+def test_gpu_long_reads_match_oracle(key, paired, length, n, gpu_indexes, index_cache):
+    """Long-read kernel variants (MAXL 1216, up to 192 subreads per strand); reads
+    longer than 1209 bases are truncated like the reference's read_line."""
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.abi import default_params, PROGRAM_ALIGN
+    from subread_amd.sim import Genome, simulate_reads, simulate_pairs
+    pre = index_cache.get(key)
+    g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
+    if paired:
+        r1, r2 = simulate_pairs(g, n, length, seed=77, insert_max=900)
+    else:
+        r1, r2 = simulate_reads(g, n, length, seed=78, sub=0.02, indel=0.05), None
+    p = default_params(PROGRAM_ALIGN, paired)
+    out, _, _ = gpu_indexes(key).vote(p, r1, r2)
+    ref, _, _, _ = OracleIndex(pre).vote(p, r1, r2, threads=16)
+    assert (out["selected_votes"][:, :, 0] > 0).mean() > 0.5
+    got = pack_records(out, None, None)
+    want = pack_records(ref, None, None)
+    assert (got == want).all(), describe_mismatch(got, want, 2 if paired else 1, 3)
+
+
 def test_gpu_batch_split_invariance(gpu_indexes, index_cache):
     """Votes are per-read independent: any batch split gives the same bytes."""
     c = Case("se_full_mixed")
