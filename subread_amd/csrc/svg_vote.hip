@@ -1318,6 +1318,9 @@ static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 	int per_cu = (int)(160 * 1024 / lds);
 	if (per_cu < 1) { svg_set_error("kernel LDS too large"); return SVG_E_DEVICE; }
 	if (per_cu > 4 * OCC / WPB) per_cu = 4 * OCC / WPB;   // 4 SIMDs x OCC waves
+	if (getenv("SVG_DEBUG"))
+		fprintf(stderr, "[svg] vote_kernel<%d,%d,%d,%d,%d,%d>: LDS %zu B/wave, %d blocks/CU\n", ENDS, MAXL,
+		        MAXP, WPB, OCC, (int)SJ, sizeof(LT), per_cu);
 	uint64_t blocks = (uint64_t)h->n_cu * per_cu;
 	uint64_t need = (kp.n_reads + WPB - 1) / WPB;
 	if (blocks > need) blocks = need;

@@ -18,16 +18,25 @@ from subread_amd.sim import random_genome, simulate_reads, c3_lengths  # noqa: E
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 5_000_000
-    paired = len(sys.argv) > 3 and sys.argv[3] == "pe"
     if wl == "c3":
         g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))
     else:
         g = random_genome([1_000_000], 901)
     ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True)
-    r1 = simulate_reads(g, n, 100, seed=20261015)
-    r2 = simulate_reads(g, n, 100, seed=7) if paired else None
-    p = default_params(paired=paired)
-    ix.set_max_read_length(100)
+    mode = sys.argv[3] if len(sys.argv) > 3 else "se"
+    paired = mode == "pe"
+    from subread_amd.abi import PROGRAM_ALIGN, PROGRAM_SUBJUNC
+    from subread_amd.sim import simulate_pairs, simulate_spliced_reads
+    if mode == "pe":
+        r1, r2 = simulate_pairs(g, n, 150)
+        ix.set_max_read_length(150)
+    elif mode == "sj":
+        r1, r2 = simulate_spliced_reads(g, n, 100), None
+        ix.set_max_read_length(100)
+    else:
+        r1, r2 = simulate_reads(g, n, 100, seed=20261015), None
+        ix.set_max_read_length(100)
+    p = default_params(PROGRAM_SUBJUNC if mode == "sj" else PROGRAM_ALIGN, paired)
     ix.vote(p, r1, r2)
     ix.set_stats(True)
     t = time.time()
