@@ -980,44 +980,72 @@ struct Wave {
 	}
 
 	// ---------------------------------------------------------------- one read
-	__device__ void run_read(uint64_t r)
+	// ---------------------------------------------------------------- read text
+	// Aligned dwords covering [seq+o, seq+o+len) (never past the page holding the last
+	// byte), WPL per lane; a read <= 256 bp is one load per lane (+1 on lane 0).
+	static constexpr int WPL = (MAXL + 6) / 256 + 1;
+	uint32_t tw[ENDS][WPL];
+	int t_shift[ENDS], t_len[ENDS];
+
+	__device__ void prefetch_text(uint64_t r)
 	{
-		const svg_params &p = kp->p;
 		const int lane = lane_id();
-		const int gap = kp->ix.gap;
-		// load text (fetch_next_read_pair: -S reversal), both strands
 		for (int e = 0; e < ENDS; e++) {
 			const char *seq = e ? kp->seq2 : kp->seq1;
 			uint64_t o = e ? kp->off2[r] : kp->off1[r];
 			int len = e ? kp->len2[r] : kp->len1[r];
 			if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;   // read_line keeps MAX_READ_LENGTH-1 (input-files.c:277)
-			int rev = e ? p.reverse_r2 : p.reverse_r1;
-			rc.rl[e] = len;
 			if (len > MAXL) {   // host-validated; never index LDS past the text buffer
 				if (lane == 0 && kp->stats) atomicOr((unsigned long long *)&kp->stats[7], 1ull);
 				len = 0;
-				rc.rl[e] = 0;
 			}
-			// chunk loads are issued in batches of TB (all of a <=256 bp read at once) before
-			// the first LDS write, so a read costs one HBM latency, not one per 64 bases
-			// (measured: -11% when the compiler kept this as a rolled loop)
-			constexpr int TB = MAXL / 64 < 4 ? MAXL / 64 : 4;
-			for (int k0 = 0; k0 < len; k0 += 64 * TB) {
-				char c[TB], c2[TB];
+			t_len[e] = len;
+			uintptr_t a = (uintptr_t)(seq + o);
+			const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+			t_shift[e] = (int)(a & 3);
+			int nwd = (t_shift[e] + len + 3) >> 2;
 #pragma unroll
-				for (int k = 0; k < TB; k++) {
-					int i = k0 + lane + 64 * k;
-					if (i < len) { c[k] = seq[o + i]; c2[k] = seq[o + (len - 1 - i)]; }
-				}
-#pragma unroll
-				for (int k = 0; k < TB; k++) {
-					int i = k0 + lane + 64 * k;
-					if (i < len) {
-						L->text[e][0][i] = rev ? comp(c2[k]) : c[k];
-						L->text[e][1][i] = rev ? comp(comp(c[k])) : comp(c2[k]);   // reverse_read of strand 0
-					}
-				}
+			for (int k = 0; k < WPL; k++) {
+				int i = lane + 64 * k;
+				tw[e][k] = i < nwd ? w[i] : 0u;
 			}
+		}
+	}
+
+	// prefetched words -> LDS staging (the vote table, free at this point) -> both strands
+	__device__ void stage_text()
+	{
+		const svg_params &p = kp->p;
+		const int lane = lane_id();
+		for (int e = 0; e < ENDS; e++) {
+			rc.rl[e] = t_len[e];
+			uint32_t *stg = L->pos[e];
+#pragma unroll
+			for (int k = 0; k < WPL; k++) stg[lane + 64 * k] = tw[e][k];
+		}
+		wsync();
+		for (int e = 0; e < ENDS; e++) {
+			const uint8_t *b = (const uint8_t *)L->pos[e] + t_shift[e];
+			const int len = rc.rl[e], rev = e ? p.reverse_r2 : p.reverse_r1;
+			for (int i = lane; i < len; i += 64) {
+				char c = (char)b[i], c2 = (char)b[len - 1 - i];
+				L->text[e][0][i] = rev ? comp(c2) : c;
+				L->text[e][1][i] = rev ? comp(comp(c)) : comp(c2);   // reverse_read of strand 0
+			}
+		}
+		wsync();
+	}
+
+	__device__ void run_read(uint64_t r, uint64_t r_next)
+	{
+		const svg_params &p = kp->p;
+		const int lane = lane_id();
+		const int gap = kp->ix.gap;
+		// text (fetch_next_read_pair: -S reversal), both strands, from the words prefetched
+		// at the end of the previous read (or before the first)
+		stage_text();
+		for (int e = 0; e < ENDS; e++) {
+			const int len = rc.rl[e];
 			if (len >= 15 + gap) {   // shorter reads: out of contract, no hits (see oracle)
 				int cr = (len - 15 - gap) << 16, step;
 				if (len <= 160) {
@@ -1064,10 +1092,13 @@ struct Wave {
 			}
 			STAMP(4);
 		}
-		// write the read's records
+		// the next read's text loads go out before this read's stores: vmcnt retires in
+		// issue order, so the next read's first wait does not also wait for the stores
+		if (r_next < kp->n_reads) prefetch_text(r_next);
+		// write the read's records (multi_best <= 3: 17 * 3 dwords, one store per lane)
 		for (int e = 0; e < ENDS; e++) {
 			uint32_t *dst = (uint32_t *)(kp->out + ((r * ENDS + e) * (uint64_t)p.multi_best) * 68);
-			for (int w = lane; w < 17 * p.multi_best; w += 64) dst[w] = L->res[e][w / 17][w % 17];
+			if (lane < 17 * p.multi_best) dst[lane] = L->res[e][lane / 17][lane % 17];
 		}
 		if constexpr (SJ) {
 			for (int e = 0; e < ENDS; e++) {
@@ -1113,8 +1144,9 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	W.t_last = __builtin_amdgcn_s_memtime();
 #endif
 	W.st_probes = W.st_items = W.st_hits = 0;
+	if (gw < kp.n_reads) W.prefetch_text(gw);
 	for (uint64_t r = gw; r < kp.n_reads; r += nw) {
-		W.run_read(r);
+		W.run_read(r, r + nw);
 #ifdef SVG_STAMPS
 		{ unsigned long long _t = __builtin_amdgcn_s_memtime(); W.acc[5] += _t - W.t_last; W.t_last = _t; }
 #endif
