@@ -71,8 +71,8 @@ struct KParams {
 template <int ENDS, int MAXL, int MAXP>
 struct WaveLDS {
 	static constexpr int MAXS = ENDS == 1 ? 16 : 64;   // max_vote_simples capacity
-	uint32_t pos[ENDS][NSLOT];            // slot positions, [row*24+slot]
-	uint32_t meta[ENDS][NSLOT];           // votes | last<<8 | (toli | shift<<7)<<16 | (u8)cursor<<24
+	uint2 pm[ENDS][NSLOT];                // [row*24+slot]: x = position, y = meta:
+	                                      //   votes | last<<8 | (toli | shift<<7)<<16 | (u8)cursor<<24
 	uint32_t pmid[ENDS][2][MAXP];         // probe: binary-search midpoint (absolute item index)
 	uint16_t pfwd[ENDS][2][MAXP];         // equal-key items at mid..last
 	uint16_t pbwd[ENDS][2][MAXP];         // equal-key items at first..mid-1
@@ -194,6 +194,7 @@ struct Wave {
 	int items_v;            // lane 32*e + r: items[r] of table e (gene_vote_t.items)
 	int max_vote[2];        // gene_vote_t.max_vote per table (wave-uniform)
 	int nshift[2];          // shift_indel_NO per table (wave-uniform)
+	int lseg, lslot;        // fixed lane map of the 3-row fetch (vote_one)
 	int cur_strand;
 
 	__device__ __forceinline__ static int rd(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -283,8 +284,8 @@ struct Wave {
 	{
 		const int lane = lane_id();
 		const int tol = kp->tol;
-		uint32_t P = 0u, M = 0u;
-		if (valid) { P = L->pos[E][slot]; M = L->meta[E][slot]; }
+		const uint2 pmv = L->pm[E][valid ? slot : 0];   // unconditional: no exec-mask branch
+		const uint32_t P = valid ? pmv.x : 0u, M = valid ? pmv.y : 0u;
 		int d = (int)(kv - P);
 		int sh = m_shift(M);
 		int t = (round > 0 && sh) ? 0 : tol;
@@ -333,7 +334,7 @@ struct Wave {
 				}
 				nlast = kP1;
 			}
-			L->meta[E][slot] = m_pack(nvotes, nlast, ntl, nsh, ncur);
+			L->pm[E][slot].y = m_pack(nvotes, nlast, ntl, nsh, ncur);
 		}
 		wsync();
 		if (wm) {
@@ -345,25 +346,35 @@ struct Wave {
 	}
 
 	// ---------------------------------------------------------------- phase V: one candidate (gehash_go_X body)
+	// candidate packing: kP1 (6 bits) | off << 6 (11) | r0 << 17 | rp << 22 | rm << 27 (5 each),
+	// rows of iix = 0, +5, -5 (sorted-hashtable.c:995-1001) computed lane-parallel at gather time
+	__device__ static uint32_t cand_pack(uint32_t kv, int kP1, int off)
+	{
+		uint32_t r0 = (kv / 5u) % ROWS, rp = ((kv + 5u) / 5u) % ROWS, rm = ((kv - 5u) / 5u) % ROWS;
+		return (uint32_t)kP1 | ((uint32_t)off << 6) | (r0 << 17) | (rp << 22) | (rm << 27);
+	}
+
 	template <int E>
-	__device__ void vote_one(uint32_t kv, int kP1, int off, int round, uint32_t high_b)
+	__device__ void vote_one(uint32_t kv, uint32_t pk, int round, uint32_t high_b)
 	{
 		const int lane = lane_id();
 		const int tol = kp->tol;
-		const uint32_t r0 = (kv / 5u) % ROWS;
+		const int kP1 = (int)(pk & 63u), off = (int)((pk >> 6) & 2047u);
+		const uint32_t r0 = (pk >> 17) & 31u;
 		const int n0 = rd(items_v, E * 32 + (int)r0);
 		bool found = false;
 		if (kp->ii_end == 5) {
-			// the three rows r0, r0+1, r0-1 (iix = 0, +5, -5) fetched in one LDS round trip
-			const uint32_t rp = ((kv + 5u) / 5u) % ROWS, rm = ((kv - 5u) / 5u) % ROWS;
+			// rows r0, r0+1, r0-1 (iix = 0, +5, -5) in one LDS round trip with a fixed lane map:
+			// lanes 0-23 row r0, 24-47 row r0+1, 48-63 slots 0-15 of row r0-1 (ballot order =
+			// the reference's scan order); slots 16-23 of row r0-1 (rare) in a second group
+			const uint32_t rp = (pk >> 22) & 31u, rm = pk >> 27;
 			const int np_ = rd(items_v, E * 32 + (int)rp), nm = rd(items_v, E * 32 + (int)rm);
-			const int T = n0 + np_ + nm;
-			for (int f0 = 0; f0 < T && !found; f0 += 64) {
-				int f = f0 + lane;
-				int seg = (f >= n0) + (f >= n0 + np_);
-				int s = f - (seg == 0 ? 0 : (seg == 1 ? n0 : n0 + np_));
-				uint32_t r = seg == 0 ? r0 : (seg == 1 ? rp : rm);
-				found = vote_group<E>(f < T, (int)r * SPACE + s, kv, kP1, off, round);
+			if (n0 + np_ + nm) {
+				const uint32_t row = lseg == 0 ? r0 : (lseg == 1 ? rp : rm);
+				const int cnt = lseg == 0 ? n0 : (lseg == 1 ? np_ : nm);
+				found = vote_group<E>(lslot < cnt, (int)row * SPACE + lslot, kv, kP1, off, round);
+				if (!found && nm > 16)
+					found = vote_group<E>(lane < nm - 16, (int)rm * SPACE + 16 + lane, kv, kP1, off, round);
 			}
 		} else {
 			for (int iix = 0; iix <= kp->ii_end && !found; iix = iix > 0 ? -iix : (-iix + 5)) {
@@ -386,10 +397,9 @@ struct Wave {
 			if (lane == 0) {
 				int slot = (int)r0 * SPACE + n0;
 				uint32_t *cs = cold_slot(cold[E], slot);
-				L->pos[E][slot] = kv;
-				L->meta[E][slot] = m_pack(1, kP1, 0, sh, 0);
-				cs[0] = (uint32_t)(uint16_t)off | ((uint32_t)(uint16_t)(off + 16) << 16);
-				cs[1] = (uint32_t)(uint8_t)kP1 | ((uint32_t)(uint8_t)kP1 << 8);   // rec[0..3] = k+1, k+1, 0, 0
+				L->pm[E][slot] = make_uint2(kv, m_pack(1, kP1, 0, sh, 0));
+				*(uint2 *)cs = make_uint2((uint32_t)(uint16_t)off | ((uint32_t)(uint16_t)(off + 16) << 16),
+				                          (uint32_t)(uint8_t)kP1 | ((uint32_t)(uint8_t)kP1 << 8));   // rec[0..3] = k+1, k+1, 0, 0
 			}
 			if (lane == E * 32 + (int)r0) items_v = n0 + 1;
 			if (max_vote[E] == 0) max_vote[E] = 1;
@@ -430,8 +440,9 @@ struct Wave {
 				uint32_t mid = L->pmid[E][s][p];
 				uint32_t item = j < fwd ? mid + j : mid - 1 - (j - fwd);
 				int off = probe_off(E, p);
-				L->cand[c] = kp->ix.vals[item] - (uint32_t)off;
-				L->cand_ko[c] = (uint32_t)(p / gap) | ((uint32_t)off << 8);
+				uint32_t kv = kp->ix.vals[item] - (uint32_t)off;
+				L->cand[c] = kv;
+				L->cand_ko[c] = cand_pack(kv, p / gap + 1, off);
 			}
 			wsync();
 			STAMP(2);
@@ -441,8 +452,8 @@ struct Wave {
 				int m = cn - cb < 64 ? (int)(cn - cb) : 64;
 				for (int j = 0; j < m; j++) {
 					uint32_t kv = (uint32_t)rd(kvv, j);
-					uint32_t ko = (uint32_t)rd(kov, j);
-					vote_one<E>(kv, (int)(ko & 255) + 1, (int)(ko >> 8), round, high_b);
+					uint32_t pk = (uint32_t)rd(kov, j);
+					vote_one<E>(kv, pk, round, high_b);
 				}
 			}
 			wsync();
@@ -470,8 +481,8 @@ struct Wave {
 		int16_t rv_lo = __shfl(rv, (2 * lane) & 63);
 		if (lane < 11) r[MR_REC / 4 + lane] = (uint32_t)(uint16_t)rv_lo | ((uint32_t)(uint16_t)rv_hi << 16);
 		if (lane == 0) {
-			uint32_t M = L->meta[e][slot];
-			r[0] = L->pos[e][slot];
+			uint32_t M = L->pm[e][slot].y;
+			r[0] = L->pm[e][slot].x;
 			r[2] = (uint32_t)(uint16_t)m_votes(M) | ((uint32_t)(uint16_t)rc.applied[e] << 16);
 			r[3] = (uint32_t)(uint8_t)(int8_t)(nrec > 0 ? last_ind : 0) << 8;   // noninf 0, indels
 			r[15] = cs[0];   // confident_coverage_start | confident_coverage_end << 16
@@ -640,8 +651,8 @@ struct Wave {
 	{
 		const svg_params &p = kp->p;
 		const int lane = lane_id();
-		const uint32_t Mpos = L->pos[e][ms];
-		const int Mv = m_votes(L->meta[e][ms]);
+		const uint32_t Mpos = L->pm[e][ms].x;
+		const int Mv = m_votes(L->pm[e][ms].y);
 		const uint32_t mw = cold_slot(cold[e], ms)[0];
 		const int Mcs = (int)(mw & 0xffff), Mce = (int)(mw >> 16);
 		const int rl = rc.rl[e];
@@ -656,8 +667,8 @@ struct Wave {
 			uint32_t P = 0;
 			int V = 0, cs = 0, ce = 0;
 			if (ok) {
-				P = L->pos[e][sl];
-				V = m_votes(L->meta[e][sl]);
+				P = L->pm[e][sl].x;
+				V = m_votes(L->pm[e][sl].y);
 				uint32_t w = cold_slot(cold[e], sl)[0];
 				cs = (int)(w & 0xffff); ce = (int)(w >> 16);
 				long long dist = (long long)Mpos - (long long)P;
@@ -753,7 +764,7 @@ struct Wave {
 					int f = f0 + lane;
 					int sl = f0 == 0 ? (e ? sl0[1] : sl0[0]) : slot_of(e, rs_v, f);   // all lanes active
 					if (f < U[e]) {
-						int v = m_votes(L->meta[e][sl]);
+						int v = m_votes(L->pm[e][sl].y);
 						if (v < bound && v > best) best = v;
 					}
 				}
@@ -776,7 +787,7 @@ struct Wave {
 				for (int f0 = 0; f0 < U[e] && ns < p.max_vote_simples; f0 += 64) {
 					int f = f0 + lane;
 					int slot = f0 == 0 ? (e ? sl0[1] : sl0[0]) : slot_of(e, rs_v, f), v = -1;   // all lanes active
-					if (f < U[e]) v = m_votes(L->meta[e][slot]);
+					if (f < U[e]) v = m_votes(L->pm[e][slot].y);
 					bool sel = f < U[e] && v == N && v >= p.min_votes_second;
 					unsigned long long sm = ballot(sel);
 					int at = ns + lanes_below(sm);
@@ -795,7 +806,7 @@ struct Wave {
 						}
 					}
 					if (sel && at < p.max_vote_simples) {
-						L->simp_pos[e][at] = L->pos[e][slot];
+						L->simp_pos[e][at] = L->pm[e][slot].x;
 						L->simp_slot[e][at] = (uint16_t)slot;
 						L->simp_votes[e][at] = (uint16_t)v;
 					}
@@ -1019,13 +1030,13 @@ struct Wave {
 		const int lane = lane_id();
 		for (int e = 0; e < ENDS; e++) {
 			rc.rl[e] = t_len[e];
-			uint32_t *stg = L->pos[e];
+			uint32_t *stg = (uint32_t *)L->pm[e];
 #pragma unroll
 			for (int k = 0; k < WPL; k++) stg[lane + 64 * k] = tw[e][k];
 		}
 		wsync();
 		for (int e = 0; e < ENDS; e++) {
-			const uint8_t *b = (const uint8_t *)L->pos[e] + t_shift[e];
+			const uint8_t *b = (const uint8_t *)L->pm[e] + t_shift[e];
 			const int len = rc.rl[e], rev = e ? p.reverse_r2 : p.reverse_r1;
 			for (int i = lane; i < len; i += 64) {
 				char c = (char)b[i], c2 = (char)b[len - 1 - i];
@@ -1133,6 +1144,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	Wave<ENDS, MAXL, MAXP, SJ> W;
 	W.L = reinterpret_cast<LT *>(lds_raw + (size_t)wib * ((sizeof(LT) + 15) & ~(size_t)15));
 	W.kp = &kp;
+	W.lseg = lane_id() < 24 ? 0 : (lane_id() < 48 ? 1 : 2);
+	W.lslot = lane_id() - 24 * W.lseg;
 	const size_t per_end = (size_t)NSLOT * COLD_WORDS + NSLOT;   // cold + shift_locs
 	uint32_t *base = kp.scratch + gw * per_end * ENDS;
 	for (int e = 0; e < ENDS; e++) {
