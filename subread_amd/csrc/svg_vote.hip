@@ -62,6 +62,22 @@ struct KParams {
 	unsigned long long *stats; // probes, bucket_items, hits, results (may be NULL)
 	int tol, ii_end;
 	uint32_t low, high;
+	const uint2 *precs;       // probe records from probe_kernel (NULL: probe in this kernel)
+	int nps;                  // probe slots per (end, strand) in precs
+};
+
+// probe kernel parameters: one thread per (read, end, strand, subread x gap slot)
+struct PParams {
+	DevIndex ix;
+	const char *seq1, *seq2;
+	const uint64_t *off1, *off2;
+	const uint16_t *len1, *len2;
+	uint32_t n_reads;
+	int nps;
+	int total_subreads, reverse_r1, reverse_r2;
+	uint64_t nb_magic;        // ceil(2^64 / nb): key / nb == umulhi64(key, nb_magic) for 32-bit keys
+	uint2 *out;               // [read][end][strand][nps]: x = midpoint item, y = fwd | bwd << 16
+	unsigned long long *stats;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -1023,6 +1039,47 @@ struct Wave {
 		}
 	}
 
+	// probe records of probe_kernel: RPL per lane (prefetched with the text when small)
+	static constexpr int RPL = (ENDS * 2 * MAXP + 63) / 64;
+	static constexpr bool PRE_RECS = RPL <= 2;
+	uint2 trec[PRE_RECS ? RPL : 1];
+	uint64_t t_r;
+
+	__device__ void prefetch_recs(uint64_t r)
+	{
+		t_r = r;
+		if constexpr (PRE_RECS) {
+			if (!kp->precs) return;
+			const int per = ENDS * 2 * kp->nps;
+			const uint2 *src = kp->precs + r * (uint64_t)per;
+#pragma unroll
+			for (int k = 0; k < RPL; k++) {
+				int i = lane_id() + 64 * k;
+				trec[k] = i < per ? src[i] : make_uint2(0, 0);
+			}
+		}
+	}
+
+	__device__ void stage_probes()
+	{
+		const int nps = kp->nps, per = ENDS * 2 * nps;
+		const uint2 *src = kp->precs + t_r * (uint64_t)per;
+#pragma unroll
+		for (int k = 0; k < (PRE_RECS ? RPL : (ENDS * 2 * MAXP + 63) / 64); k++) {
+			int i = lane_id() + 64 * k;
+			if (i < per) {
+				uint2 rec;
+				if constexpr (PRE_RECS) rec = trec[k < RPL ? k : 0];
+				else rec = src[i];
+				int e = i / (2 * nps), rem = i - e * 2 * nps, st = rem >= nps ? 1 : 0, q = rem - st * nps;
+				L->pmid[e][st][q] = rec.x;
+				L->pfwd[e][st][q] = (uint16_t)(rec.y & 0xffff);
+				L->pbwd[e][st][q] = (uint16_t)(rec.y >> 16);
+			}
+		}
+		wsync();
+	}
+
 	// prefetched words -> LDS staging (the vote table, free at this point) -> both strands
 	__device__ void stage_text()
 	{
@@ -1084,7 +1141,8 @@ struct Wave {
 		}
 		wsync();
 		STAMP(0);
-		probe_all();
+		if (kp->precs) stage_probes();
+		else probe_all();
 		STAMP(1);
 		for (int strand = 0; strand < 2; strand++) {
 			cur_strand = strand;
@@ -1105,7 +1163,7 @@ struct Wave {
 		}
 		// the next read's text loads go out before this read's stores: vmcnt retires in
 		// issue order, so the next read's first wait does not also wait for the stores
-		if (r_next < kp->n_reads) prefetch_text(r_next);
+		if (r_next < kp->n_reads) { prefetch_text(r_next); prefetch_recs(r_next); }
 		// write the read's records (multi_best <= 3: 17 * 3 dwords, one store per lane)
 		for (int e = 0; e < ENDS; e++) {
 			uint32_t *dst = (uint32_t *)(kp->out + ((r * ENDS + e) * (uint64_t)p.multi_best) * 68);
@@ -1157,7 +1215,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	W.t_last = __builtin_amdgcn_s_memtime();
 #endif
 	W.st_probes = W.st_items = W.st_hits = 0;
-	if (gw < kp.n_reads) W.prefetch_text(gw);
+	if (gw < kp.n_reads) { W.prefetch_text(gw); W.prefetch_recs(gw); }
 	for (uint64_t r = gw; r < kp.n_reads; r += nw) {
 		W.run_read(r, r + nw);
 #ifdef SVG_STAMPS
@@ -1175,6 +1233,107 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 			atomicAdd(&kp.stats[0], W.st_probes);
 			atomicAdd(&kp.stats[1], a);
 			atomicAdd(&kp.stats[2], h);
+		}
+	}
+}
+
+// =============================================================================================
+// probe kernel: phase P for a whole chunk of reads, one thread per subread probe.  Same
+// arithmetic as Wave::probe_all (genekey2int, key % nb, gehash_go_X's binary search and the
+// equal-key run on both sides of the first-hit midpoint); with no per-read state to keep,
+// it runs at high occupancy and hides the dependent bucket -> keys -> run chain.
+// =============================================================================================
+template <int ENDS>
+__global__ void __launch_bounds__(256) probe_kernel(PParams pp)
+{
+	const DevIndex &ix = pp.ix;
+	const uint32_t nps = (uint32_t)pp.nps, per_read = ENDS * 2 * nps;
+	const uint32_t total = pp.n_reads * per_read;
+	const int gap = ix.gap;
+	unsigned long long st_p = 0, st_i = 0, st_h = 0;
+	for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
+		const uint32_t r = t / per_read, rem = t - r * per_read;
+		const int e = ENDS == 2 ? (int)(rem / (2 * nps)) : 0;
+		const uint32_t rem2 = rem - (uint32_t)e * 2 * nps;
+		const int s = rem2 >= nps ? 1 : 0;
+		const int p = (int)(rem2 - (uint32_t)s * nps);
+		uint2 rec = make_uint2(0u, 0u);
+		int len = e ? pp.len2[r] : pp.len1[r];
+		if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;
+		if (len >= 15 + gap) {
+			const int cr = (len - 15 - gap) << 16;
+			int step;
+			if (len <= 160) { step = cr / (pp.total_subreads - 1); if (step < (gap << 16)) step = gap << 16; }
+			else { step = 6 << 16; if (cr / step > 62) step = cr / 62; }
+			const int np = (1 + cr / step) * gap;
+			if (p < np) {
+				const int k = p / gap, x = p - k * gap;
+				int off = (int)(((int64_t)step * k) >> 16);
+				if (gap > 1) off -= off % gap - x;
+				// 16 bases of strand s at off; strand 1 = reverse_read of strand 0, strand 0 =
+				// the input, reverse-complemented for -S (R2 by default)
+				const int rev = e ? pp.reverse_r2 : pp.reverse_r1;
+				const bool direct = s == rev;
+				const int start = direct ? off : len - 16 - off;
+				const char *src = (e ? pp.seq2 : pp.seq1) + (e ? pp.off2[r] : pp.off1[r]) + start;
+				const uintptr_t a = (uintptr_t)src;
+				const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+				const int sh = (int)(a & 3);
+				uint32_t wd[5];
+#pragma unroll
+				for (int q = 0; q < 4; q++) wd[q] = w[q];
+				wd[4] = sh ? w[4] : 0u;   // only when the window reaches into it
+				uint32_t key = 0;
+#pragma unroll
+				for (int i = 0; i < 16; i++) {
+					const int bi = sh + (direct ? i : 15 - i);
+					char c = (char)((wd[bi >> 2] >> (8 * (bi & 3))) & 0xff);
+					if (!direct) c = comp(c);
+					if (s == 1 && rev) c = comp(comp(c));   // strand 1 of a reversed read: comp(comp(input))
+					key |= b2i(c) << (30 - 2 * i);
+				}
+				const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
+				const uint32_t b = key - q * ix.nb;
+				const int16_t k16 = (int16_t)q;
+				const uint32_t first = ix.bstart[b];
+				const int n = (int)(ix.bstart[b + 1] - first);
+				st_p++;
+				st_i += (unsigned)n;
+				if (n > 0) {
+					const int16_t *K = ix.keys + first;
+					int lo = 0, hi = n - 1, m;
+					bool hit = false;
+					for (;;) {
+						m = (lo + hi) >> 1;
+						int16_t kk = K[m];
+						if (kk > k16) hi = m - 1;
+						else if (kk < k16) lo = m + 1;
+						else { hit = true; break; }
+						if (hi < lo) break;
+					}
+					if (hit) {
+						int qq = m + 1;
+						while (qq < n && K[qq] == k16) qq++;
+						const int fwd = qq - m;
+						qq = m - 1;
+						while (qq >= 0 && K[qq] == k16) qq--;
+						const int bwd = m - 1 - qq;
+						rec = make_uint2(first + (uint32_t)m, (uint32_t)fwd | ((uint32_t)bwd << 16));
+						st_h += (unsigned)(fwd + bwd);
+					}
+				}
+			}
+		}
+		pp.out[t] = rec;
+	}
+	if (pp.stats) {
+		for (int o = 32; o; o >>= 1) {
+			st_p += __shfl_xor(st_p, o); st_i += __shfl_xor(st_i, o); st_h += __shfl_xor(st_h, o);
+		}
+		if (lane_id() == 0 && st_p) {
+			atomicAdd(&pp.stats[0], st_p);
+			atomicAdd(&pp.stats[1], st_i);
+			atomicAdd(&pp.stats[2], st_h);
 		}
 	}
 }
@@ -1216,6 +1375,8 @@ int svg_index_finish_device(svg_index *h)
 	const char *se = getenv("SVG_STATS");
 	h->stats_on = se && se[0] == '1';
 	h->max_read_len = 256;
+	const char *fu = getenv("SVG_FUSED");
+	h->fused = fu && fu[0] == '1';
 	return 0;
 }
 
@@ -1271,6 +1432,7 @@ extern "C" void svg_index_close(svg_index *h)
 	if (!h) return;
 	hipSetDevice(h->device);
 	if (h->stream) hipStreamSynchronize(h->stream);
+	hipFree(h->d_prec);
 	hipFree(h->d_bstart); hipFree(h->d_keys); hipFree(h->d_vals); hipFree(h->d_values); hipFree(h->d_chr);
 	hipFree(h->d_scratch); hipFree(h->d_stats); hipFree(h->d_in); hipFree(h->d_out);
 	if (h->stream) hipStreamDestroy(h->stream);
@@ -1385,6 +1547,26 @@ static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 	return 0;
 }
 
+static int ensure(svg_index *h, void **p, size_t *cap, size_t need);
+
+// kernel variant by mode and announced read-length bound
+static int launch_vote(svg_index *h, KParams &kp, hipStream_t st, int npmax, bool sj, int ends)
+{
+	// subjunc (junction minor search, donor scoring, big-margin records) is a separate
+	// variant so the plain-align kernels carry none of its registers
+	if (sj) {
+		if (ends == 2) return npmax <= 32 ? launch_t<2, 256, 32, 2, 4, true>(h, kp, st) : launch_t<2, 256, 64, 2, 4, true>(h, kp, st);
+		return npmax <= 32 ? launch_t<1, 256, 32, 2, 4, true>(h, kp, st) : launch_t<1, 256, 64, 2, 4, true>(h, kp, st);
+	}
+	if (h->max_read_len > 256 || npmax > 64) {
+		// long reads (161..1210 bp: 6 bp subread step, <= 63 subreads per gap slot)
+		if (ends == 2) return npmax <= 64 ? launch_t<2, 1216, 64, 2, 4, false>(h, kp, st) : launch_t<2, 1216, 192, 2, 4, false>(h, kp, st);
+		return npmax <= 64 ? launch_t<1, 1216, 64, 2, 4, false>(h, kp, st) : launch_t<1, 1216, 192, 2, 4, false>(h, kp, st);
+	}
+	if (ends == 2) return npmax <= 32 ? launch_t<2, 256, 32, 1, 4, false>(h, kp, st) : launch_t<2, 256, 64, 1, 4, false>(h, kp, st);
+	return npmax <= 32 ? launch_t<1, 256, 32, 2, 4, false>(h, kp, st) : launch_t<1, 256, 64, 2, 4, false>(h, kp, st);
+}
+
 extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
                                      svg_mapping_result *out, svg_subjunc_result *jout, uint16_t *big_margin, void *stream)
 {
@@ -1422,20 +1604,51 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	}
 	// probes per strand are bounded by the read lengths the caller announced
 	int npmax = svg_probe_bound(h->max_read_len, h->dix.gap, p->total_subreads);
-	// subjunc (junction minor search, donor scoring, big-margin records) is a separate
-	// variant so the plain-align kernels carry none of its registers
 	const bool sj = p->do_breakpoint_detection || p->do_big_margin_filtering_for_junctions;
 	if (sj && npmax > 64) { svg_set_error("subjunc mode: %d subreads per strand exceed 64", npmax); return SVG_E_UNSUPPORTED; }
-	if (sj) {
-		if (r2) rc = npmax <= 32 ? launch_t<2, 256, 32, 2, 4, true>(h, kp, st) : launch_t<2, 256, 64, 2, 4, true>(h, kp, st);
-		else rc = npmax <= 32 ? launch_t<1, 256, 32, 2, 4, true>(h, kp, st) : launch_t<1, 256, 64, 2, 4, true>(h, kp, st);
-	} else if (h->max_read_len > 256 || npmax > 64) {
-		// long reads (161..1210 bp: 6 bp subread step, <= 63 subreads per gap slot)
-		if (r2) rc = npmax <= 64 ? launch_t<2, 1216, 64, 2, 4, false>(h, kp, st) : launch_t<2, 1216, 192, 2, 4, false>(h, kp, st);
-		else rc = npmax <= 64 ? launch_t<1, 1216, 64, 2, 4, false>(h, kp, st) : launch_t<1, 1216, 192, 2, 4, false>(h, kp, st);
+	const int ends = r2 ? 2 : 1;
+	if (h->fused) {
+		rc = launch_vote(h, kp, st, npmax, sj, ends);
 	} else {
-		if (r2) rc = npmax <= 32 ? launch_t<2, 256, 32, 2, 4, false>(h, kp, st) : launch_t<2, 256, 64, 2, 4, false>(h, kp, st);
-		else rc = npmax <= 32 ? launch_t<1, 256, 32, 2, 4, false>(h, kp, st) : launch_t<1, 256, 64, 2, 4, false>(h, kp, st);
+		// phase P as its own kernel per chunk of reads, then the vote kernel on its records
+		const int nps = npmax > 0 ? npmax : 1;
+		const uint64_t per_read = (uint64_t)ends * 2 * nps;
+		uint64_t chunk = ((uint64_t)1 << 30) / (per_read * 8);
+		if (chunk > (uint64_t)0x7fffffff / per_read) chunk = (uint64_t)0x7fffffff / per_read;
+		if (chunk > kp.n_reads) chunk = kp.n_reads;
+		if (chunk < 1) chunk = 1;
+		if ((rc = ensure(h, &h->d_prec, &h->prec_cap, chunk * per_read * 8))) return rc;
+		PParams pp;
+		memset(&pp, 0, sizeof pp);
+		pp.ix = h->dix;
+		pp.seq1 = kp.seq1; pp.seq2 = kp.seq2;
+		pp.nps = nps;
+		pp.total_subreads = p->total_subreads; pp.reverse_r1 = p->reverse_r1; pp.reverse_r2 = p->reverse_r2;
+		pp.nb_magic = ~0ull / h->dix.nb + 1;   // ceil(2^64 / nb), nb is not a power of two
+		pp.out = (uint2 *)h->d_prec;
+		pp.stats = kp.stats;
+		const uint64_t n = kp.n_reads;
+		for (uint64_t c0 = 0; c0 < n && !rc; c0 += chunk) {
+			const uint64_t cn = n - c0 < chunk ? n - c0 : chunk;
+			pp.off1 = kp.off1 + c0; pp.len1 = kp.len1 + c0;
+			if (r2) { pp.off2 = kp.off2 + c0; pp.len2 = kp.len2 + c0; }
+			pp.n_reads = (uint32_t)cn;
+			uint64_t pb = (cn * per_read + 255) / 256, pmax = (uint64_t)h->n_cu * 32;
+			if (pb > pmax) pb = pmax;
+			if (r2) hipLaunchKernelGGL(probe_kernel<2>, dim3((unsigned)pb), dim3(256), 0, st, pp);
+			else hipLaunchKernelGGL(probe_kernel<1>, dim3((unsigned)pb), dim3(256), 0, st, pp);
+			HIPCHK(hipGetLastError());
+			KParams kc = kp;
+			kc.off1 = kp.off1 + c0; kc.len1 = kp.len1 + c0;
+			if (r2) { kc.off2 = kp.off2 + c0; kc.len2 = kp.len2 + c0; }
+			kc.n_reads = cn;
+			kc.out = kp.out + c0 * ends * p->multi_best * 68;
+			if (kp.jout) kc.jout = kp.jout + c0 * ends * p->multi_best * 16;
+			if (kp.bm_out) kc.bm_out = kp.bm_out + c0 * ends * SVG_BIG_MARGIN_WORDS;
+			kc.precs = (const uint2 *)h->d_prec;
+			kc.nps = nps;
+			rc = launch_vote(h, kc, st, npmax, sj, ends);
+		}
 	}
 	if (rc) return rc;
 	if (h->stats_on) {
