@@ -33,7 +33,6 @@ struct svg_index {
 	uint64_t device_bytes;
 	int n_cu;
 	int max_read_len;        // announced read-length bound (svg_set_max_read_length), picks the kernel variant
-	int fused;               // 1: probe inside the vote kernel (SVG_FUSED=1), 0: probe_kernel + vote kernel
 	void *d_prec; size_t prec_cap;   // probe records of one chunk
 	// staging for svg_vote_batch (host buffers)
 	void *d_in; size_t d_in_cap;

@@ -62,7 +62,7 @@ struct KParams {
 	unsigned long long *stats; // probes, bucket_items, hits, results (may be NULL)
 	int tol, ii_end;
 	uint32_t low, high;
-	const uint2 *precs;       // probe records from probe_kernel (NULL: probe in this kernel)
+	const uint2 *precs;       // probe records of this chunk (probe_kernel)
 	int nps;                  // probe slots per (end, strand) in precs
 };
 
@@ -84,7 +84,7 @@ struct PParams {
 // LDS layout of one wave.  Row occupancy (items[30]) and max_vote live in
 // registers (lane 32*end+row holds items[row]); only slot state is in LDS.
 #define CAND_CAP 64
-template <int ENDS, int MAXL, int MAXP>
+template <int ENDS, int MAXL, int MAXP, bool SJ>
 struct WaveLDS {
 	static constexpr int MAXS = ENDS == 1 ? 16 : 64;   // max_vote_simples capacity
 	uint2 pm[ENDS][NSLOT];                // [row*24+slot]: x = position, y = meta:
@@ -97,13 +97,13 @@ struct WaveLDS {
 	uint32_t cand_ko[CAND_CAP];           // subread_no | offset << 8
 	uint32_t res[ENDS][3][17];            // the read's stored mapping_result_t (68 B)
 	uint32_t tmp[ENDS][3][17];            // top-K output under construction
-	uint32_t jres[ENDS][3][4];            // subjunc_result_t
-	uint32_t jtmp[ENDS][3][4];
+	uint32_t jres[SJ ? ENDS : 1][3][4];   // subjunc_result_t (subjunc variants only)
+	uint32_t jtmp[SJ ? ENDS : 1][3][4];
 	uint32_t simp_pos[ENDS][MAXS];        // simple_mapping_t: position
 	uint16_t simp_slot[ENDS][MAXS];       // slot index, or 0x8000|stored index
 	uint16_t simp_votes[ENDS][MAXS];
-	uint16_t bm[ENDS][10];
-	char text[ENDS][2][MAXL];             // strand 0 form / strand 1 (reverse_read) form
+	uint16_t bm[SJ ? ENDS : 1][10];
+	char text[SJ ? ENDS : 1][2][SJ ? MAXL : 4];   // strand 0 / strand 1 (reverse_read) form, donor scoring only
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -201,7 +201,7 @@ struct Wave {
 #ifdef SVG_STAMPS
 	unsigned long long t_last, acc[8];
 #endif
-	WaveLDS<ENDS, MAXL, MAXP> *L;
+	WaveLDS<ENDS, MAXL, MAXP, SJ> *L;
 	uint32_t *cold[2];      // [ENDS] cold slot state
 	uint32_t *shift_locs[2];
 	const KParams *kp;
@@ -223,66 +223,6 @@ struct Wave {
 		int off = (int)(((int64_t)rc.step[e] * k) >> 16);
 		if (gap > 1) off -= off % gap - x;
 		return off;
-	}
-
-	// ---------------------------------------------------------------- phase P: all probes of the read
-	__device__ void probe_all()
-	{
-		const DevIndex &ix = kp->ix;
-		int total = 0;
-		int base[2][2];
-		for (int e = 0; e < ENDS; e++)
-			for (int s = 0; s < 2; s++) { base[e][s] = total; total += rc.np[e]; }
-		for (int p0 = 0; p0 < total; p0 += 64) {
-			int id = p0 + lane_id();
-			if (id < total) {
-				int e = 0, s = 0;
-				for (int ee = 0; ee < ENDS; ee++)
-					for (int ss = 0; ss < 2; ss++)
-						if (rc.np[ee] > 0 && id >= base[ee][ss]) { e = ee; s = ss; }
-				int p = id - base[e][s];
-				int off = probe_off(e, p);
-				const char *t = L->text[e][s] + off;
-				uint32_t key = 0;
-#pragma unroll
-				for (int i = 0; i < 16; i++) key |= b2i(t[i]) << (30 - 2 * i);
-				uint32_t b = key % ix.nb;
-				int16_t k16 = (int16_t)(key / ix.nb);
-				uint32_t first = ix.bstart[b];
-				int n = (int)(ix.bstart[b + 1] - first);
-				uint32_t mid = 0;
-				int fwd = 0, bwd = 0;
-				st_items += n;
-				if (n > 0) {
-					const int16_t *K = ix.keys + first;
-					int lo = 0, hi = n - 1, m;
-					bool hit = false;
-					for (;;) {
-						m = (lo + hi) >> 1;
-						int16_t kk = K[m];
-						if (kk > k16) hi = m - 1;
-						else if (kk < k16) lo = m + 1;
-						else { hit = true; break; }
-						if (hi < lo) break;
-					}
-					if (hit) {
-						mid = first + m;
-						int q = m + 1;
-						while (q < n && K[q] == k16) q++;
-						fwd = q - m;
-						q = m - 1;
-						while (q >= 0 && K[q] == k16) q--;
-						bwd = m - 1 - q;
-					}
-				}
-				L->pmid[e][s][p] = mid;
-				L->pfwd[e][s][p] = (uint16_t)fwd;
-				L->pbwd[e][s][p] = (uint16_t)bwd;
-				st_hits += fwd + bwd;
-			}
-		}
-		st_probes += total;
-		wsync();
 	}
 
 	// ---------------------------------------------------------------- vote-table reset (init_gene_vote)
@@ -1027,6 +967,7 @@ struct Wave {
 				len = 0;
 			}
 			t_len[e] = len;
+			if constexpr (!SJ) continue;   // the vote step itself never reads the text
 			uintptr_t a = (uintptr_t)(seq + o);
 			const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
 			t_shift[e] = (int)(a & 3);
@@ -1049,7 +990,6 @@ struct Wave {
 	{
 		t_r = r;
 		if constexpr (PRE_RECS) {
-			if (!kp->precs) return;
 			const int per = ENDS * 2 * kp->nps;
 			const uint2 *src = kp->precs + r * (uint64_t)per;
 #pragma unroll
@@ -1085,8 +1025,9 @@ struct Wave {
 	{
 		const svg_params &p = kp->p;
 		const int lane = lane_id();
+		for (int e = 0; e < ENDS; e++) rc.rl[e] = t_len[e];
+		if constexpr (!SJ) return;
 		for (int e = 0; e < ENDS; e++) {
-			rc.rl[e] = t_len[e];
 			uint32_t *stg = (uint32_t *)L->pm[e];
 #pragma unroll
 			for (int k = 0; k < WPL; k++) stg[lane + 64 * k] = tw[e][k];
@@ -1141,8 +1082,7 @@ struct Wave {
 		}
 		wsync();
 		STAMP(0);
-		if (kp->precs) stage_probes();
-		else probe_all();
+		stage_probes();
 		STAMP(1);
 		for (int strand = 0; strand < 2; strand++) {
 			cur_strand = strand;
@@ -1195,7 +1135,7 @@ template <int ENDS, int MAXL, int MAXP, int WPB, int OCC, bool SJ>
 __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 {
 	extern __shared__ __align__(16) uint8_t lds_raw[];
-	typedef WaveLDS<ENDS, MAXL, MAXP> LT;
+	typedef WaveLDS<ENDS, MAXL, MAXP, SJ> LT;
 	const int wib = threadIdx.x >> 6;
 	const uint64_t gw = (uint64_t)blockIdx.x * WPB + wib;
 	const uint64_t nw = (uint64_t)gridDim.x * WPB;
@@ -1375,8 +1315,6 @@ int svg_index_finish_device(svg_index *h)
 	const char *se = getenv("SVG_STATS");
 	h->stats_on = se && se[0] == '1';
 	h->max_read_len = 256;
-	const char *fu = getenv("SVG_FUSED");
-	h->fused = fu && fu[0] == '1';
 	return 0;
 }
 
@@ -1520,7 +1458,7 @@ static int check_params(const svg_index *h, const svg_params *p, int paired)
 template <int ENDS, int MAXL, int MAXP, int WPB, int OCC, bool SJ>
 static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 {
-	typedef WaveLDS<ENDS, MAXL, MAXP> LT;
+	typedef WaveLDS<ENDS, MAXL, MAXP, SJ> LT;
 	size_t lds = (size_t)WPB * ((sizeof(LT) + 15) & ~(size_t)15);
 	int per_cu = (int)(160 * 1024 / lds);
 	if (per_cu < 1) { svg_set_error("kernel LDS too large"); return SVG_E_DEVICE; }
@@ -1564,7 +1502,7 @@ static int launch_vote(svg_index *h, KParams &kp, hipStream_t st, int npmax, boo
 		return npmax <= 64 ? launch_t<1, 1216, 64, 2, 4, false>(h, kp, st) : launch_t<1, 1216, 192, 2, 4, false>(h, kp, st);
 	}
 	if (ends == 2) return npmax <= 32 ? launch_t<2, 256, 32, 1, 4, false>(h, kp, st) : launch_t<2, 256, 64, 1, 4, false>(h, kp, st);
-	return npmax <= 32 ? launch_t<1, 256, 32, 2, 4, false>(h, kp, st) : launch_t<1, 256, 64, 2, 4, false>(h, kp, st);
+	return npmax <= 32 ? launch_t<1, 256, 32, 2, 5, false>(h, kp, st) : launch_t<1, 256, 64, 2, 5, false>(h, kp, st);
 }
 
 extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
@@ -1607,9 +1545,7 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	const bool sj = p->do_breakpoint_detection || p->do_big_margin_filtering_for_junctions;
 	if (sj && npmax > 64) { svg_set_error("subjunc mode: %d subreads per strand exceed 64", npmax); return SVG_E_UNSUPPORTED; }
 	const int ends = r2 ? 2 : 1;
-	if (h->fused) {
-		rc = launch_vote(h, kp, st, npmax, sj, ends);
-	} else {
+	{
 		// phase P as its own kernel per chunk of reads, then the vote kernel on its records
 		const int nps = npmax > 0 ? npmax : 1;
 		const uint64_t per_read = (uint64_t)ends * 2 * nps;
