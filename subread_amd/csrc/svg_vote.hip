@@ -87,8 +87,14 @@ struct PParams {
 template <int ENDS, int MAXL, int MAXP, bool SJ>
 struct WaveLDS {
 	static constexpr int MAXS = ENDS == 1 ? 16 : 64;   // max_vote_simples capacity
-	uint2 pm[ENDS][NSLOT];                // [row*24+slot]: x = position, y = meta:
-	                                      //   votes | last<<8 | (toli | shift<<7)<<16 | (u8)cursor<<24
+	// One physical vote table (gene_vote_t, [row*24+slot]): x = position, y = meta =
+	// votes | last<<8 | (toli | shift<<7)<<16 | (u8)cursor<<24.  PE votes end 0 first, then
+	// compacts its used slots (flattened row order, the order every top-K scan uses) into
+	// cl/cls and votes end 1 in the same table.
+	static constexpr int CAPL = ENDS == 2 ? 64 : 1;
+	uint2 pm[NSLOT];
+	uint2 cl[CAPL];                       // end 0 compacted: position, meta (entries >= CAPL: HBM)
+	uint16_t cls[CAPL];                   // end 0 compacted: table slot (cold-state index)
 	uint32_t pmid[ENDS][2][MAXP];         // probe: binary-search midpoint (absolute item index)
 	uint16_t pfwd[ENDS][2][MAXP];         // equal-key items at mid..last
 	uint16_t pbwd[ENDS][2][MAXP];         // equal-key items at first..mid-1
@@ -211,6 +217,7 @@ struct Wave {
 	int max_vote[2];        // gene_vote_t.max_vote per table (wave-uniform)
 	int nshift[2];          // shift_indel_NO per table (wave-uniform)
 	int lseg, lslot;        // fixed lane map of the 3-row fetch (vote_one)
+	uint32_t *ovf;          // PE: compacted end-0 entries beyond the LDS list (HBM scratch)
 	int cur_strand;
 
 	__device__ __forceinline__ static int rd(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -240,7 +247,7 @@ struct Wave {
 	{
 		const int lane = lane_id();
 		const int tol = kp->tol;
-		const uint2 pmv = L->pm[E][valid ? slot : 0];   // unconditional: no exec-mask branch
+		const uint2 pmv = L->pm[valid ? slot : 0];   // unconditional: no exec-mask branch
 		const uint32_t P = valid ? pmv.x : 0u, M = valid ? pmv.y : 0u;
 		int d = (int)(kv - P);
 		int sh = m_shift(M);
@@ -290,7 +297,7 @@ struct Wave {
 				}
 				nlast = kP1;
 			}
-			L->pm[E][slot].y = m_pack(nvotes, nlast, ntl, nsh, ncur);
+			L->pm[slot].y = m_pack(nvotes, nlast, ntl, nsh, ncur);
 		}
 		wsync();
 		if (wm) {
@@ -353,7 +360,7 @@ struct Wave {
 			if (lane == 0) {
 				int slot = (int)r0 * SPACE + n0;
 				uint32_t *cs = cold_slot(cold[E], slot);
-				L->pm[E][slot] = make_uint2(kv, m_pack(1, kP1, 0, sh, 0));
+				L->pm[slot] = make_uint2(kv, m_pack(1, kP1, 0, sh, 0));
 				*(uint2 *)cs = make_uint2((uint32_t)(uint16_t)off | ((uint32_t)(uint16_t)(off + 16) << 16),
 				                          (uint32_t)(uint8_t)kP1 | ((uint32_t)(uint8_t)kP1 << 8));   // rec[0..3] = k+1, k+1, 0, 0
 			}
@@ -420,10 +427,52 @@ struct Wave {
 	// ---------------------------------------------------------------- record helpers
 	__device__ void rec_zero(uint32_t *r) { if (lane_id() < 17) r[lane_id()] = 0; }
 
-	// copy_vote_to_alignment_res (core-junction.c:1058-1071) for slot -> record r (pre-zeroed)
-	__device__ void copy_vote(int e, int slot, uint32_t *r)
+	// ---------------------------------------------------------------- table entries for top-K
+	// An entry handle h is a table slot, or for PE end 0 an index into the compacted list.
+	__device__ __forceinline__ bool compact(int e) const { return ENDS == 2 && e == 0; }
+	__device__ __forceinline__ void ent_h(int e, int h, uint32_t &P, uint32_t &M, int &slot) const
+	{
+		if (compact(e)) {
+			if (h < L->CAPL) { uint2 v = L->cl[h]; P = v.x; M = v.y; slot = L->cls[h]; }
+			else { const uint32_t *o = ovf + 4 * h; P = o[0]; M = o[1]; slot = (int)o[2]; }
+		} else {
+			uint2 v = L->pm[h]; P = v.x; M = v.y; slot = h;
+		}
+	}
+	// flattened used-slot index f (< U) -> handle; all lanes active (slot_of shuffles)
+	__device__ __forceinline__ int handle_of(int e, int rs_v, int f) const
+	{
+		if (compact(e)) return f;
+		return slot_of(e, rs_v, f);
+	}
+
+	// PE: end 0's used slots, in flattened row order, to the compact list (all lanes active)
+	__device__ void compact_end0()
 	{
 		const int lane = lane_id();
+		int mine = lane < ROWS ? items_v : 0;
+		int v = mine;
+		for (int o = 1; o < 32; o <<= 1) { int t = __shfl_up(v, o); if ((lane & 31) >= o) v += t; }
+		const int U = rd(v, ROWS - 1);
+		for (int f0 = 0; f0 < U; f0 += 64) {
+			int f = f0 + lane;
+			int sl = slot_of(0, v, f);
+			if (f < U) {
+				uint2 pmv = L->pm[sl];
+				if (f < L->CAPL) { L->cl[f] = pmv; L->cls[f] = (uint16_t)sl; }
+				else { uint32_t *o = ovf + 4 * f; o[0] = pmv.x; o[1] = pmv.y; o[2] = (uint32_t)sl; }
+			}
+		}
+		wsync();
+	}
+
+	// copy_vote_to_alignment_res (core-junction.c:1058-1071) for slot -> record r (pre-zeroed)
+	__device__ void copy_vote(int e, int h, uint32_t *r)
+	{
+		const int lane = lane_id();
+		uint32_t P, M;
+		int slot;
+		ent_h(e, h, P, M, slot);
 		const uint32_t *cs = cold_slot(cold[e], slot);
 		// indel_recorder_copy (sorted-hashtable.c:1144): triples while rec[3t] != 0 and 3t < 19
 		int v = 0;
@@ -437,8 +486,7 @@ struct Wave {
 		int16_t rv_lo = __shfl(rv, (2 * lane) & 63);
 		if (lane < 11) r[MR_REC / 4 + lane] = (uint32_t)(uint16_t)rv_lo | ((uint32_t)(uint16_t)rv_hi << 16);
 		if (lane == 0) {
-			uint32_t M = L->pm[e][slot].y;
-			r[0] = L->pm[e][slot].x;
+			r[0] = P;
 			r[2] = (uint32_t)(uint16_t)m_votes(M) | ((uint32_t)(uint16_t)rc.applied[e] << 16);
 			r[3] = (uint32_t)(uint8_t)(int8_t)(nrec > 0 ? last_ind : 0) << 8;   // noninf 0, indels
 			r[15] = cs[0];   // confident_coverage_start | confident_coverage_end << 16
@@ -603,12 +651,14 @@ struct Wave {
 	// junction part of copy_vote_to_alignment_res (core-junction.c:1073-1334, no fusion):
 	// every other used slot of the table is a minor-half candidate.  The J-independent
 	// filters run lane-parallel; the is_better chain and donor scoring run in slot order.
-	__device__ void junction(int e, int ms, uint32_t *r, uint32_t *J, int rs_v, int U)
+	__device__ void junction(int e, int mh, uint32_t *r, uint32_t *J, int rs_v, int U)
 	{
 		const svg_params &p = kp->p;
 		const int lane = lane_id();
-		const uint32_t Mpos = L->pm[e][ms].x;
-		const int Mv = m_votes(L->pm[e][ms].y);
+		uint32_t Mpos, MM;
+		int ms;
+		ent_h(e, mh, Mpos, MM, ms);
+		const int Mv = m_votes(MM);
 		const uint32_t mw = cold_slot(cold[e], ms)[0];
 		const int Mcs = (int)(mw & 0xffff), Mce = (int)(mw >> 16);
 		const int rl = rc.rl[e];
@@ -618,13 +668,15 @@ struct Wave {
 		bool upd = false;
 		for (int f0 = 0; f0 < U; f0 += 64) {
 			int f = f0 + lane;
-			int sl = slot_of(e, rs_v, f);   // all lanes active
-			bool ok = f < U && sl != ms;
+			int hh = handle_of(e, rs_v, f);   // all lanes active
+			bool ok = f < U && hh != mh;
 			uint32_t P = 0;
 			int V = 0, cs = 0, ce = 0;
 			if (ok) {
-				P = L->pm[e][sl].x;
-				V = m_votes(L->pm[e][sl].y);
+				uint32_t MMv;
+				int sl;
+				ent_h(e, hh, P, MMv, sl);
+				V = m_votes(MMv);
 				uint32_t w = cold_slot(cold[e], sl)[0];
 				cs = (int)(w & 0xffff); ce = (int)(w >> 16);
 				long long dist = (long long)Mpos - (long long)P;
@@ -707,10 +759,10 @@ struct Wave {
 		int U[2];
 		U[0] = rd(rs_v, ROWS - 1);
 		U[1] = ENDS == 2 ? rd(rs_v, 32 + ROWS - 1) : 0;
-		// slot of flattened index f = lane (first 64 used slots), computed once per table
+		// handle of flattened index f = lane (first 64 used slots), computed once per table
 		int sl0[2];
-		sl0[0] = slot_of(0, rs_v, lane);
-		sl0[1] = ENDS == 2 ? slot_of(1, rs_v, lane) : 0;
+		sl0[0] = handle_of(0, rs_v, lane);
+		sl0[1] = ENDS == 2 ? handle_of(1, rs_v, lane) : 0;
 		for (int e = 0; e < ENDS; e++) {
 			// top-3 distinct over table votes and stored results (update_top_three)
 			int bound = 0x7fffffff;
@@ -718,9 +770,12 @@ struct Wave {
 				int best = 0;
 				for (int f0 = 0; f0 < U[e]; f0 += 64) {
 					int f = f0 + lane;
-					int sl = f0 == 0 ? (e ? sl0[1] : sl0[0]) : slot_of(e, rs_v, f);   // all lanes active
+					int sl = f0 == 0 ? (e ? sl0[1] : sl0[0]) : handle_of(e, rs_v, f);   // all lanes active
 					if (f < U[e]) {
-						int v = m_votes(L->pm[e][sl].y);
+						uint32_t P, M;
+						int cs_;
+						ent_h(e, sl, P, M, cs_);
+						int v = m_votes(M);
 						if (v < bound && v > best) best = v;
 					}
 				}
@@ -742,8 +797,10 @@ struct Wave {
 				if (N < 1 || (top[e][0] - N > p.max_vote_number_cutoff)) break;
 				for (int f0 = 0; f0 < U[e] && ns < p.max_vote_simples; f0 += 64) {
 					int f = f0 + lane;
-					int slot = f0 == 0 ? (e ? sl0[1] : sl0[0]) : slot_of(e, rs_v, f), v = -1;   // all lanes active
-					if (f < U[e]) v = m_votes(L->pm[e][slot].y);
+					int hd = f0 == 0 ? (e ? sl0[1] : sl0[0]) : handle_of(e, rs_v, f), v = -1;   // all lanes active
+					uint32_t P = 0, M = 0;
+					int slot = 0;
+					if (f < U[e]) { ent_h(e, hd, P, M, slot); v = m_votes(M); }
 					bool sel = f < U[e] && v == N && v >= p.min_votes_second;
 					unsigned long long sm = ballot(sel);
 					int at = ns + lanes_below(sm);
@@ -762,8 +819,8 @@ struct Wave {
 						}
 					}
 					if (sel && at < p.max_vote_simples) {
-						L->simp_pos[e][at] = L->pm[e][slot].x;
-						L->simp_slot[e][at] = (uint16_t)slot;
+						L->simp_pos[e][at] = P;
+						L->simp_slot[e][at] = (uint16_t)hd;
 						L->simp_votes[e][at] = (uint16_t)v;
 					}
 					ns += __popcll(sm);
@@ -1028,13 +1085,13 @@ struct Wave {
 		for (int e = 0; e < ENDS; e++) rc.rl[e] = t_len[e];
 		if constexpr (!SJ) return;
 		for (int e = 0; e < ENDS; e++) {
-			uint32_t *stg = (uint32_t *)L->pm[e];
+			uint32_t *stg = (uint32_t *)(L->pm + e * (NSLOT / 2));
 #pragma unroll
 			for (int k = 0; k < WPL; k++) stg[lane + 64 * k] = tw[e][k];
 		}
 		wsync();
 		for (int e = 0; e < ENDS; e++) {
-			const uint8_t *b = (const uint8_t *)L->pm[e] + t_shift[e];
+			const uint8_t *b = (const uint8_t *)(L->pm + e * (NSLOT / 2)) + t_shift[e];
 			const int len = rc.rl[e], rev = e ? p.reverse_r2 : p.reverse_r1;
 			for (int i = lane; i < len; i += 64) {
 				char c = (char)b[i], c2 = (char)b[len - 1 - i];
@@ -1087,7 +1144,10 @@ struct Wave {
 		for (int strand = 0; strand < 2; strand++) {
 			cur_strand = strand;
 			vote_end<0>(strand);
-			if constexpr (ENDS == 2) vote_end<1>(strand);
+			if constexpr (ENDS == 2) {
+				compact_end0();
+				vote_end<1>(strand);
+			}
 			STAMP(3);
 			if (ENDS == 2) topk(strand);
 			else if (max_vote[0] >= p.min_votes_first) topk(strand);
@@ -1145,11 +1205,13 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	W.lseg = lane_id() < 24 ? 0 : (lane_id() < 48 ? 1 : 2);
 	W.lslot = lane_id() - 24 * W.lseg;
 	const size_t per_end = (size_t)NSLOT * COLD_WORDS + NSLOT;   // cold + shift_locs
-	uint32_t *base = kp.scratch + gw * per_end * ENDS;
+	const size_t per_wave = per_end * ENDS + (ENDS == 2 ? (size_t)NSLOT * 4 : 0);   // + PE overflow list
+	uint32_t *base = kp.scratch + gw * per_wave;
 	for (int e = 0; e < ENDS; e++) {
 		W.cold[e] = base + e * per_end;
 		W.shift_locs[e] = base + e * per_end + (size_t)NSLOT * COLD_WORDS;
 	}
+	W.ovf = base + per_end * ENDS;
 #ifdef SVG_STAMPS
 	for (int k = 0; k < 8; k++) W.acc[k] = 0;
 	W.t_last = __builtin_amdgcn_s_memtime();
@@ -1471,7 +1533,7 @@ static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 	if (blocks > need) blocks = need;
 	if (blocks < 1) blocks = 1;
 	size_t per_end = (size_t)NSLOT * COLD_WORDS + NSLOT;
-	size_t words = blocks * WPB * ENDS * per_end;
+	size_t words = blocks * WPB * (ENDS * per_end + (ENDS == 2 ? (size_t)NSLOT * 4 : 0));
 	if (words > h->scratch_words) {
 		hipFree(h->d_scratch);
 		h->d_scratch = NULL;
