@@ -109,6 +109,7 @@ struct WaveLDS {
 	uint16_t simp_slot[ENDS][MAXS];       // slot index, or 0x8000|stored index
 	uint16_t simp_votes[ENDS][MAXS];
 	uint16_t bm[SJ ? ENDS : 1][10];
+	uint8_t gwin[SJ ? 2 : 1][SJ ? 64 : 4];   // subjunc donor windows of the .array
 	char text[SJ ? ENDS : 1][2][SJ ? MAXL : 4];   // strand 0 / strand 1 (reverse_read) form, donor scoring only
 };
 
@@ -218,6 +219,7 @@ struct Wave {
 	int nshift[2];          // shift_indel_NO per table (wave-uniform)
 	int lseg, lslot;        // fixed lane map of the 3-row fetch (vote_one)
 	uint32_t *ovf;          // PE: compacted end-0 entries beyond the LDS list (HBM scratch)
+	uint32_t wb[2];         // subjunc: first .array byte of the left / right donor window
 	int cur_strand;
 
 	__device__ __forceinline__ static int rd(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -520,17 +522,32 @@ struct Wave {
 
 	// ---------------------------------------------------------------- subjunc helpers (SJ variant)
 	// gvindex_get (gene-value-index.c:1118-1136 via gvindex_get_string): 'N' past the array
-	__device__ __forceinline__ char gv_get(uint32_t pos) const
+	// .array bytes of the current donor search are staged in two 64-byte LDS windows
+	// (left / right half of the junction); a byte outside them is read from HBM
+	__device__ __forceinline__ int vbyte(int w, uint32_t byte) const
+	{
+		const uint32_t d = byte - wb[w];
+		return d < 64 ? (int)L->gwin[w][d] : (int)kp->ix.values[byte];
+	}
+	__device__ __forceinline__ char gv_get(int w, uint32_t pos) const
 	{
 		const DevIndex &ix = kp->ix;
 		uint32_t byte = (pos - ix.start_base_offset) >> 2, bit = pos % 4 * 2;
 		if (byte >= ix.values_bytes - 1) return 'N';
-		return "AGCT"[(ix.values[byte] >> bit) & 3];
+		return "AGCT"[(vbyte(w, byte) >> bit) & 3];
+	}
+	// stage the window of side w starting at array position pos0 (all lanes)
+	__device__ void load_window(int w, uint32_t pos0)
+	{
+		const DevIndex &ix = kp->ix;
+		wb[w] = (pos0 - ix.start_base_offset) >> 2;
+		const uint32_t idx = wb[w] + (uint32_t)lane_id();
+		L->gwin[w][lane_id()] = idx < ix.values_bytes ? ix.values[idx] : 0;
 	}
 
 	// match_chro (gene-value-index.c:856-959, space_type = base): matched bases of
 	// read[0..len) against the array at pos; 0 whenever the walk reaches the array end
-	__device__ int match_chro(const char *read, int read_len, int at, uint32_t pos, int len) const
+	__device__ int match_chro(int w, const char *read, int read_len, int at, uint32_t pos, int len) const
 	{
 		const DevIndex &ix = kp->ix;
 		if ((uint32_t)(pos + len) >= ix.length + ix.start_point) return 0;
@@ -539,14 +556,14 @@ struct Wave {
 		if (byte >= ix.values_bytes) return 0;
 		if (byte + (bit / 2 + len) / 4 >= ix.values_bytes) return 0;   // the walk would hit the end
 		int ret = 0;
-		int iv = (int8_t)ix.values[byte];
+		int iv = vbyte(w, byte);
 		for (int i = 0; i < len; i++) {
 			int tt = (iv >> bit) & 3;
 			int q = at + i;
 			char c = q < read_len ? read[q] : 0;   // the reference's read buffer is NUL-terminated
 			ret += c == 'A' ? tt == 0 : c == 'G' ? tt == 1 : c == 'C' ? tt == 2 : c == 0 ? 0 : tt == 3;
 			bit += 2;
-			if (bit == 8) { byte++; iv = (int8_t)ix.values[byte]; bit = 0; }
+			if (bit == 8) { byte++; iv = vbyte(w, byte); bit = 0; }
 		}
 		return ret;
 	}
@@ -571,6 +588,15 @@ struct Wave {
 		const int allow = p.more_accurate_fusions ? 0 : 1;
 		const int mid = (gs + ge) / 2, n = ge - gs;
 		int best = -111111, bi = 0x7fffffff, bstrand = -1, bsp = -1;
+		{
+			// split points visited lie in [gs-1, ge+1] and pass only inside [17, rl-17]; the
+			// windows cover 20 bases before the lowest to 17 after the highest
+			int lo_sp = gs - 1 > JCW ? gs - 1 : JCW;
+			uint32_t l0 = left + (uint32_t)lo_sp, r0 = right + (uint32_t)lo_sp;
+			load_window(0, l0 >= 20u ? l0 - 20u : 0u);
+			load_window(1, r0 >= 20u ? r0 - 20u : 0u);
+			wsync();
+		}
 		int carry_dr1 = 0;   // dr[1] left by the last earlier split point that fetched it (normal branch)
 		for (int i0 = 0; i0 < n; i0 += 64) {
 			int i = i0 + lane;
@@ -583,17 +609,17 @@ struct Wave {
 					bool ok = false;
 					if (p.prefer_donor_receptor_junctions) {
 						if (normal) {
-							dl0 = gv_get(left + sp); dl1 = gv_get(left + sp + 1);
+							dl0 = gv_get(0, left + sp); dl1 = gv_get(0, left + sp + 1);
 							if (donor_pair(dl0, dl1)) {
-								dr0 = gv_get(right + sp - 2); dr1 = gv_get(right + sp - 1);
+								dr0 = gv_get(1, right + sp - 2); dr1 = gv_get(1, right + sp - 1);
 								dr_set = true;
 								if (donor_pair(dr0, dr1))
 									ok = ((dl0 == 'G' && dl1 == 'T' && dr0 == 'A' && dr1 == 'G') || (dl0 == 'C' && dl1 == 'T' && dr0 == 'A' && dr1 == 'C'))
 									     && ((dl0 == 'C' && dl1 == 'T') || (dl0 == 'G' && dl1 == 'T'));
 							}
 						} else {
-							dl0 = gv_get(right + sp); dl1 = gv_get(right + sp + 1);
-							dr0 = gv_get(left + sp - 2); dr1 = gv_get(left + sp - 1);
+							dl0 = gv_get(1, right + sp); dl1 = gv_get(1, right + sp + 1);
+							dr0 = gv_get(0, left + sp - 2); dr1 = gv_get(0, left + sp - 1);
 							dr_set = true;
 							ok = donor_pair(dl0, dl1) && donor_pair(dr0, dr1)
 							     && ((dl0 == 'G' && dl1 == 'T' && dr0 == 'A' && dr1 == 'G') || (dl0 == 'C' && dl1 == 'T' && dr0 == 'A' && dr1 == 'C'))
@@ -603,20 +629,20 @@ struct Wave {
 					if (ok || !need_donor) {
 						int lm, rm, ln, rn;
 						if (normal) {
-							lm = match_chro(read, rl, sp - JCW, left + sp - JCW, JCW);
+							lm = match_chro(0, read, rl, sp - JCW, left + sp - JCW, JCW);
 							if (lm > JCW - 2) {
-								rm = match_chro(read, rl, sp, right + sp, JCW);
+								rm = match_chro(1, read, rl, sp, right + sp, JCW);
 								if (rm >= 2 * JCW - lm - allow) {
-									ln = match_chro(read, rl, sp, left + sp, JCW);
-									rn = match_chro(read, rl, sp - JCW, right + sp - JCW, JCW);
+									ln = match_chro(0, read, rl, sp, left + sp, JCW);
+									rn = match_chro(1, read, rl, sp - JCW, right + sp - JCW, JCW);
 									if (ln <= JCW - 5 && rn <= JCW - 5) { sc = 100 * ((ok ? 3000 : 0) + lm + rm - ln - rn); cand = true; }
 								}
 							}
 						} else {
-							rm = match_chro(read, rl, sp - JCW, right + sp - JCW, JCW);
-							lm = match_chro(read, rl, sp, left + sp, JCW);
-							rn = match_chro(read, rl, sp, right + sp, JCW);
-							ln = match_chro(read, rl, sp - JCW, left + sp - JCW, JCW);
+							rm = match_chro(1, read, rl, sp - JCW, right + sp - JCW, JCW);
+							lm = match_chro(0, read, rl, sp, left + sp, JCW);
+							rn = match_chro(1, read, rl, sp, right + sp, JCW);
+							ln = match_chro(0, read, rl, sp - JCW, left + sp - JCW, JCW);
 							if (lm + rm >= 2 * JCW - allow && ln <= JCW - 5 && rn <= JCW - 5) { sc = 100 * ((ok ? 3000 : 0) + lm + rm - ln - rn); cand = true; }
 						}
 					}
@@ -672,15 +698,21 @@ struct Wave {
 			bool ok = f < U && hh != mh;
 			uint32_t P = 0;
 			int V = 0, cs = 0, ce = 0;
+			int sl = 0;
+			long long dist = 0;
 			if (ok) {
 				uint32_t MMv;
-				int sl;
 				ent_h(e, hh, P, MMv, sl);
 				V = m_votes(MMv);
+				dist = (long long)Mpos - (long long)P;
+				ok = Mv >= V && (dist < 0 ? -dist : dist) <= (long long)p.maximum_intron_length;
+			}
+			// the coverage (cold state, HBM) only for slots within intron distance -- usually none
+			if (!ballot(ok)) continue;
+			if (ok) {
 				uint32_t w = cold_slot(cold[e], sl)[0];
 				cs = (int)(w & 0xffff); ce = (int)(w >> 16);
-				long long dist = (long long)Mpos - (long long)P;
-				ok = Mv >= V && (dist < 0 ? -dist : dist) <= (long long)p.maximum_intron_length && cs != Mcs && ce != Mce;
+				ok = cs != Mcs && ce != Mce;
 				if (ok) ok = (Mcs > cs) ? (Mpos >= P) : (Mpos <= P);   // test_junction_minor
 				if (ok) {
 					int ov = (Mcs > cs) ? ce - Mcs : Mce - cs;
@@ -808,14 +840,13 @@ struct Wave {
 						// insert_big_margin_record (core-junction.c:2276-2277,789) for every slot the
 						// reference's scan visits before max_vote_simples is reached, first value only
 						if (t == 0 && p.do_big_margin_filtering_for_junctions) {
-							unsigned long long bmm = ballot(f < U[e] && at < p.max_vote_simples && v >= top[e][TS - 1]);
-							while (bmm) {
-								int b = __ffsll((long long)bmm) - 1;
-								bmm &= bmm - 1;
-								int bs = rd(slot, b), bv = rd(v, b);
-								if (lane == 0) big_margin_insert(e, bv, bs);
-								wsync();
+							STAMP(4);
+							const bool elig = f < U[e] && at < p.max_vote_simples && v >= top[e][TS - 1];
+							if (ballot(elig)) {
+								const uint32_t cw = elig ? cold_slot(cold[e], slot)[0] : 0u;
+								big_margin_merge(e, elig, v, cw);
 							}
+							STAMP(7);
 						}
 					}
 					if (sel && at < p.max_vote_simples) {
@@ -965,29 +996,58 @@ struct Wave {
 			if constexpr (SJ) {
 				if (kp->p.do_breakpoint_detection) {
 					wsync();
+					STAMP(4);
 					junction(e, sl, L->tmp[e][c], L->jtmp[e][c], rs_v, U);
+					STAMP(6);
 				}
 			}
 		}
 		wsync();
 	}
 
-	// insert_big_margin_record, core-junction.c:789-811 (lane 0)
-	__device__ void big_margin_insert(int e, int votes, int slot)
+	// insert_big_margin_record (core-junction.c:789-811) for every eligible lane of a chunk,
+	// in lane order.  Each insertion puts the new record before the first one with votes
+	// <= its own, so the record list is always the top size/3 of all insertions so far under
+	// (votes desc, newer first) -- the chunk's top-3 by that key are merged with the list.
+	__device__ void big_margin_merge(int e, bool elig, int votes, uint32_t cw)
 	{
-		const int size = kp->p.big_margin_record_size;
+		const int size = kp->p.big_margin_record_size;   // 0..2 (no records) or 3, 6, 9
 		if (size < 3) return;
-		const uint32_t w = cold_slot(cold[e], slot)[0];
-		const int rs = (int)(w & 0xffff), re = (int)(w >> 16), rl = rc.rl[e];
-		uint16_t *bm = L->bm[e];
-		uint16_t s2 = cur_strand ? (uint16_t)(rl - re) : (uint16_t)rs, e2 = cur_strand ? (uint16_t)(rl - rs) : (uint16_t)re;
-		unsigned char vv = (unsigned char)votes;
-		int x1;
-		for (x1 = 0; x1 < size / 3; x1++) if (vv >= bm[x1 * 3]) break;
-		if (x1 < size / 3) {
-			for (int x2 = size - 4; x2 >= x1 * 3; x2--) bm[x2 + 3] = bm[x2];
-			bm[x1 * 3] = vv; bm[x1 * 3 + 1] = s2; bm[x1 * 3 + 2] = e2;
+		const int lane = lane_id(), ns = size / 3, rl = rc.rl[e];
+		const int rs = (int)(cw & 0xffff), re = (int)(cw >> 16);
+		const uint32_t pay = cur_strand ? (uint32_t)(uint16_t)(rl - re) | ((uint32_t)(uint16_t)(rl - rs) << 16)
+		                                : (uint32_t)(uint16_t)rs | ((uint32_t)(uint16_t)re << 16);
+		int key = elig ? (((votes & 255) << 8) | (64 + lane)) : -1;
+		int nk[3] = {-1, -1, -1};
+		uint32_t np_[3] = {0, 0, 0};
+		for (int t = 0; t < ns; t++) {
+			const int m = wave_max(key);
+			if (m < 0) break;
+			const int l = (m & 255) - 64;
+			nk[t] = m;
+			np_[t] = (uint32_t)rd((int)pay, l);
+			if (lane == l) key = -1;
 		}
+		if (lane == 0) {
+			uint16_t *bm = L->bm[e];
+			int ok[3];
+			uint32_t op[3];
+			for (int i = 0; i < ns; i++) { ok[i] = ((int)bm[3 * i] << 8) | (3 - i); op[i] = bm[3 * i + 1] | ((uint32_t)bm[3 * i + 2] << 16); }
+			int rk[3];
+			uint32_t rp[3];
+			int a = 0, b = 0;
+			for (int k = 0; k < ns; k++) {
+				const bool takeN = a < ns && nk[a] >= 0 && (b >= ns || nk[a] > ok[b]);
+				if (takeN) { rk[k] = nk[a] >> 8; rp[k] = np_[a]; a++; }
+				else { rk[k] = ok[b] >> 8; rp[k] = op[b]; b++; }
+			}
+			for (int k = 0; k < ns; k++) {
+				bm[3 * k] = (uint16_t)rk[k];
+				bm[3 * k + 1] = (uint16_t)(rp[k] & 0xffff);
+				bm[3 * k + 2] = (uint16_t)(rp[k] >> 16);
+			}
+		}
+		wsync();
 	}
 
 	// voting of one end for one strand: init_gene_vote + subread loop + shift-indel round
@@ -1507,8 +1567,9 @@ static int check_params(const svg_index *h, const svg_params *p, int paired)
 	if (p->max_vote_simples > 16 && !paired) { svg_set_error("single-end max_vote_simples must be <= 16"); return SVG_E_UNSUPPORTED; }
 	if (p->total_subreads < 2 || p->total_subreads > 64) { svg_set_error("total_subreads must be 2..64"); return SVG_E_UNSUPPORTED; }
 	if (p->max_indel_length < 0) { svg_set_error("max_indel_length < 0"); return SVG_E_ARG; }
-	if (p->do_big_margin_filtering_for_junctions && (p->big_margin_record_size < 0 || p->big_margin_record_size > SVG_BIG_MARGIN_WORDS)) {
-		svg_set_error("big_margin_record_size must be 0..%d", SVG_BIG_MARGIN_WORDS); return SVG_E_UNSUPPORTED;
+	if (p->do_big_margin_filtering_for_junctions && (p->big_margin_record_size < 0 || p->big_margin_record_size > SVG_BIG_MARGIN_WORDS ||
+	                                                 (p->big_margin_record_size >= 3 && p->big_margin_record_size % 3))) {
+		svg_set_error("big_margin_record_size must be 0, 1, 2, 3, 6 or 9"); return SVG_E_UNSUPPORTED;
 	}
 	if (p->do_breakpoint_detection && p->max_insertion_at_junctions != 0) {
 		svg_set_error("max_insertion_at_junctions > 0 reads past the read end in the reference; not supported"); return SVG_E_UNSUPPORTED;

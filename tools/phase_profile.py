@@ -44,11 +44,11 @@ def main():
     dt = time.time() - t
     c = (ctypes.c_ulonglong * 16)()
     sa.lib().svg_debug_counters(ix.h, c)
-    names = ["text+init", "probe", "gather", "vote", "topk", "output", "-", "-"]
-    tot = sum(c[8 + k] for k in range(6))
+    names = ["text+init", "probe", "gather", "vote", "topk", "output", "junction", "bigmargin"]
+    tot = sum(c[8 + k] for k in range(8))
     print("workload %s reads %d paired %s wall %.3fs probes %d items %d hits %d results %d" % (
         wl, n, paired, dt, c[0], c[1], c[2], c[3]))
-    for k in range(6):
+    for k in range(8):
         print("  %-10s %6.2f%%  %8.0f cycles/read" % (names[k], 100.0 * c[8 + k] / max(1, tot), c[8 + k] / n))
 
 
