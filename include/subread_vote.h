@@ -213,6 +213,13 @@ int svg_set_stats(svg_index *idx, int enable);
 int svg_set_max_read_length(svg_index *idx, int max_len);
 int svg_get_stats(const svg_index *idx, svg_batch_stats *out);
 
+/* Per-kernel device time (diagnostics / roofline): while enabled, every probe_kernel
+ * and vote_kernel launch is bracketed by HIP events on its stream.  svg_get_timing
+ * waits for the last recorded event and returns the summed milliseconds and launch
+ * counts since svg_set_timing(idx, 1). */
+int svg_set_timing(svg_index *idx, int enable);
+int svg_get_timing(svg_index *idx, double *probe_ms, double *vote_ms, int *probe_launches, int *vote_launches);
+
 const char *svg_last_error(void);
 int svg_abi_version(void);
 

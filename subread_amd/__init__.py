@@ -28,7 +28,7 @@ EXPORTS = [
     "svg_vote_batch", "svg_vote_batch_device", "svg_set_stats", "svg_get_stats",
     "svg_last_error", "svg_abi_version", "svg_build_index", "svg_sim_genome",
     "svg_sim_repeats", "svg_sim_reads", "svg_index_build", "svg_index_build_mem", "svg_index_export",
-    "svg_set_max_read_length", "svg_sim_pairs",
+    "svg_set_max_read_length", "svg_sim_pairs", "svg_set_timing", "svg_get_timing",
 ]
 
 _lib = None
@@ -65,6 +65,10 @@ def lib():
         L.svg_vote_batch_device.restype = i32
         L.svg_set_stats.argtypes = [vp, i32]
         L.svg_get_stats.argtypes = [vp, vp]
+        L.svg_set_timing.argtypes = [vp, i32]
+        L.svg_set_timing.restype = i32
+        L.svg_get_timing.argtypes = [vp, vp, vp, vp, vp]
+        L.svg_get_timing.restype = i32
         L.svg_set_max_read_length.argtypes = [vp, i32]
         L.svg_set_max_read_length.restype = i32
         L.svg_last_error.restype = ctypes.c_char_p
@@ -171,6 +175,17 @@ class VoteIndex:
 
     def set_max_read_length(self, n):
         _check(lib().svg_set_max_read_length(self.h, int(n)), "svg_set_max_read_length")
+
+    def set_timing(self, on=True):
+        _check(lib().svg_set_timing(self.h, 1 if on else 0), "svg_set_timing")
+
+    def timing(self):
+        """{probe_ms, vote_ms, probe_launches, vote_launches} summed since set_timing(True)."""
+        pm, vm = ctypes.c_double(), ctypes.c_double()
+        pl, vl = ctypes.c_int(), ctypes.c_int()
+        _check(lib().svg_get_timing(self.h, ctypes.byref(pm), ctypes.byref(vm), ctypes.byref(pl), ctypes.byref(vl)),
+               "svg_get_timing")
+        return {"probe_ms": pm.value, "vote_ms": vm.value, "probe_launches": pl.value, "vote_launches": vl.value}
 
     def set_stats(self, on=True):
         lib().svg_set_stats(self.h, 1 if on else 0)

@@ -34,6 +34,11 @@ struct svg_index {
 	int n_cu;
 	int max_read_len;        // announced read-length bound (svg_set_max_read_length), picks the kernel variant
 	void *d_prec; size_t prec_cap;   // probe records of one chunk
+	// svg_set_timing: event pairs per launch, folded into the sums when the ring fills
+	int timing;
+	hipEvent_t tev[2][64][2];
+	int tn[2], tcount[2];
+	double tms[2];
 	// staging for svg_vote_batch (host buffers)
 	void *d_in; size_t d_in_cap;
 	void *d_out; size_t d_out_cap;

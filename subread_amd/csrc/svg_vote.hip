@@ -213,7 +213,7 @@ struct Wave {
 	uint32_t *shift_locs[2];
 	const KParams *kp;
 	ReadCtx rc;
-	unsigned long long st_probes, st_items, st_hits;
+	unsigned long long st_probes, st_items, st_hits, st_results;
 	int items_v;            // lane 32*e + r: items[r] of table e (gene_vote_t.items)
 	int max_vote[2];        // gene_vote_t.max_vote per table (wave-uniform)
 	int nshift[2];          // shift_indel_NO per table (wave-uniform)
@@ -1242,10 +1242,8 @@ struct Wave {
 			}
 		}
 		if (kp->stats) {
-			int nres = 0;
 			for (int e = 0; e < ENDS; e++)
-				for (int i = 0; i < p.multi_best; i++) nres += rec_votes(L->res[e][i]) > 0;
-			if (lane == 0) atomicAdd(&kp->stats[3], (unsigned long long)nres);
+				for (int i = 0; i < p.multi_best; i++) st_results += rec_votes(L->res[e][i]) > 0;
 		}
 		wsync();
 	}
@@ -1276,7 +1274,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	for (int k = 0; k < 8; k++) W.acc[k] = 0;
 	W.t_last = __builtin_amdgcn_s_memtime();
 #endif
-	W.st_probes = W.st_items = W.st_hits = 0;
+	W.st_probes = W.st_items = W.st_hits = W.st_results = 0;
 	if (gw < kp.n_reads) { W.prefetch_text(gw); W.prefetch_recs(gw); }
 	for (uint64_t r = gw; r < kp.n_reads; r += nw) {
 		W.run_read(r, r + nw);
@@ -1292,6 +1290,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 		unsigned long long a = W.st_items, h = W.st_hits;
 		for (int o = 32; o; o >>= 1) { a += __shfl_xor(a, o); h += __shfl_xor(h, o); }
 		if (lane_id() == 0) {
+			atomicAdd(&kp.stats[3], W.st_results);
 			atomicAdd(&kp.stats[0], W.st_probes);
 			atomicAdd(&kp.stats[1], a);
 			atomicAdd(&kp.stats[2], h);
@@ -1493,6 +1492,10 @@ extern "C" void svg_index_close(svg_index *h)
 	hipSetDevice(h->device);
 	if (h->stream) hipStreamSynchronize(h->stream);
 	hipFree(h->d_prec);
+	for (int k = 0; k < 2; k++)
+		for (int i = 0; i < 64; i++)
+			for (int j = 0; j < 2; j++)
+				if (h->tev[k][i][j]) hipEventDestroy(h->tev[k][i][j]);
 	hipFree(h->d_bstart); hipFree(h->d_keys); hipFree(h->d_vals); hipFree(h->d_values); hipFree(h->d_chr);
 	hipFree(h->d_scratch); hipFree(h->d_stats); hipFree(h->d_in); hipFree(h->d_out);
 	if (h->stream) hipStreamDestroy(h->stream);
@@ -1512,6 +1515,56 @@ extern "C" int svg_index_get_info(const svg_index *h, svg_index_info *o)
 	o->device_bytes = h->device_bytes;
 	o->device = h->device;
 	o->array_values_bytes = h->host.values_bytes;
+	return 0;
+}
+
+// ------------------------------------------------------------------ per-kernel timing
+static int timing_fold(svg_index *h, int k)
+{
+	for (int i = 0; i < h->tn[k]; i++) {
+		float ms = 0.f;
+		HIPCHK(hipEventSynchronize(h->tev[k][i][1]));
+		HIPCHK(hipEventElapsedTime(&ms, h->tev[k][i][0], h->tev[k][i][1]));
+		h->tms[k] += ms;
+	}
+	h->tn[k] = 0;
+	return 0;
+}
+
+// bracket one launch of kind k (0 probe, 1 vote): phase 0 before, 1 after
+static int timing_mark(svg_index *h, int k, int phase, hipStream_t st)
+{
+	if (!h->timing) return 0;
+	if (phase == 0 && h->tn[k] == 64) { int rc = timing_fold(h, k); if (rc) return rc; }
+	HIPCHK(hipEventRecord(h->tev[k][h->tn[k]][phase], st));
+	if (phase == 1) { h->tn[k]++; h->tcount[k]++; }
+	return 0;
+}
+
+extern "C" int svg_set_timing(svg_index *h, int enable)
+{
+	if (!h) { svg_set_error("svg_set_timing: NULL handle"); return SVG_E_ARG; }
+	HIPCHK(hipSetDevice(h->device));
+	if (enable && !h->timing) {
+		for (int k = 0; k < 2; k++)
+			for (int i = 0; i < 64; i++)
+				for (int j = 0; j < 2; j++)
+					if (!h->tev[k][i][j]) HIPCHK(hipEventCreate(&h->tev[k][i][j]));
+	}
+	h->timing = enable ? 1 : 0;
+	for (int k = 0; k < 2; k++) { h->tn[k] = 0; h->tcount[k] = 0; h->tms[k] = 0.0; }
+	return 0;
+}
+
+extern "C" int svg_get_timing(svg_index *h, double *probe_ms, double *vote_ms, int *probe_launches, int *vote_launches)
+{
+	if (!h) { svg_set_error("svg_get_timing: NULL handle"); return SVG_E_ARG; }
+	HIPCHK(hipSetDevice(h->device));
+	for (int k = 0; k < 2; k++) { int rc = timing_fold(h, k); if (rc) return rc; }
+	if (probe_ms) *probe_ms = h->tms[0];
+	if (vote_ms) *vote_ms = h->tms[1];
+	if (probe_launches) *probe_launches = h->tcount[0];
+	if (vote_launches) *vote_launches = h->tcount[1];
 	return 0;
 }
 
@@ -1694,9 +1747,11 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 			pp.n_reads = (uint32_t)cn;
 			uint64_t pb = (cn * per_read + 255) / 256, pmax = (uint64_t)h->n_cu * 32;
 			if (pb > pmax) pb = pmax;
+			if ((rc = timing_mark(h, 0, 0, st))) return rc;
 			if (r2) hipLaunchKernelGGL(probe_kernel<2>, dim3((unsigned)pb), dim3(256), 0, st, pp);
 			else hipLaunchKernelGGL(probe_kernel<1>, dim3((unsigned)pb), dim3(256), 0, st, pp);
 			HIPCHK(hipGetLastError());
+			if ((rc = timing_mark(h, 0, 1, st))) return rc;
 			KParams kc = kp;
 			kc.off1 = kp.off1 + c0; kc.len1 = kp.len1 + c0;
 			if (r2) { kc.off2 = kp.off2 + c0; kc.len2 = kp.len2 + c0; }
@@ -1706,7 +1761,9 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 			if (kp.bm_out) kc.bm_out = kp.bm_out + c0 * ends * SVG_BIG_MARGIN_WORDS;
 			kc.precs = (const uint2 *)h->d_prec;
 			kc.nps = nps;
+			if ((rc = timing_mark(h, 1, 0, st))) return rc;
 			rc = launch_vote(h, kc, st, npmax, sj, ends);
+			if (!rc) rc = timing_mark(h, 1, 1, st);
 		}
 	}
 	if (rc) return rc;

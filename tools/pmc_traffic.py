@@ -54,7 +54,8 @@ def kernel_stats(d):
             res.append((name, int(calls), float(avg) / 1e3, float(pct)))   # top_kernels is in us
         # per-dispatch durations of the vote kernel
         durs = [(int(e) - int(s)) / 1e6 for (s, e) in c.execute(
-            "select start, end from kernels where name like 'void vote_kernel%' order by start")]
+            "select start, end from kernels where name like 'void vote_kernel%' or name like 'void probe_kernel%' "
+            "order by start")]
         return res, durs
     for f in glob.glob(os.path.join(d, "*kernel_stats.csv")):
         for r in csv.DictReader(open(f)):
@@ -65,6 +66,16 @@ def kernel_stats(d):
 def per_dispatch(rs, prefix, counter):
     v = sorted((di, val, dur) for k, n, val, di, dur in rs if k.startswith(prefix) and n == counter)
     return v
+
+
+def step_total(rs, counter, n_steps_dispatches):
+    """Sum of a counter over the probe_kernel + vote_kernel dispatches of the first (timed)
+    bench step: the step's dispatches are the first n_steps_dispatches of each kernel."""
+    tot = 0.0
+    for kern in ("void probe_kernel", "void vote_kernel"):
+        d = per_dispatch(rs, kern, counter)
+        tot += sum(x[1] for x in d[:n_steps_dispatches])
+    return tot
 
 
 def main():
@@ -84,9 +95,12 @@ def main():
     f = per_dispatch(rows(a.fetch), kern, "FETCH_SIZE")
     w = per_dispatch(rows(a.write), kern, "WRITE_SIZE")
     assert f and w, "no vote_kernel dispatches in the PMC passes"
-    kname = [k for k, n, *_ in rows(a.fetch) if k.startswith(kern)][0]
-    fetch_b = f[0][1] * 1024.0
-    write_b = w[0][1] * 1024.0
+    kname = "probe_kernel + " + [k for k, n, *_ in rows(a.fetch) if k.startswith(kern)][0]
+    # bench.py --steps 1 --warmup 0 runs the timed step, then the stats pass: half the
+    # dispatches of each kernel belong to the timed step
+    nd = max(1, len(f) // 2)
+    fetch_b = step_total(rows(a.fetch), "FETCH_SIZE", nd) * 1024.0
+    write_b = step_total(rows(a.write), "WRITE_SIZE", nd) * 1024.0
     res = {"workload": a.workload, "kernel": kname, "reads_per_launch": a.reads,
            "fetch_bytes": fetch_b, "write_bytes": write_b, "traffic_bytes": fetch_b + write_b,
            "traffic_bytes_per_read": (fetch_b + write_b) / a.reads,
@@ -124,7 +138,8 @@ def main():
                   "| kernel | calls | avg ms | % |", "|---|---|---|---|"]
             for k, c, m, p in ks[:8]:
                 L.append("| %s | %d | %.3f | %.1f |" % (k[:70], c, m, p))
-            L += ["", "vote_kernel per-dispatch ms (warmup, 3 timed, stats pass): " +
+            L += ["", "probe_kernel / vote_kernel per-dispatch ms in launch order (warmup step, 3 timed steps, "
+                  "stats pass; each step = one probe_kernel + vote_kernel pair per chunk of reads): " +
                   ", ".join("%.1f" % x for x in durs), ""]
         L += ["## PMC (separate passes, `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE`, bench.py --steps 1 --warmup 0)", "",
               "| | bytes per launch | bytes per read |", "|---|---|---|",
