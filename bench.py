@@ -167,17 +167,20 @@ def main():
     elapsed = time.perf_counter() - t_start
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     tk = ix.timing()
+    kt = ix.kernel_timing()
     ix.set_timing(False)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # algorithmic bytes from the kernel's own counters, outside the timed region
+    # algorithmic bytes from the kernels' own counters, outside the timed region
     ix.set_stats(True)
     step()
     torch.cuda.synchronize()
     st = ix.stats()
+    dcs = ix.debug_counters()
+    lane_hits = dcs[19] + dcs[24]       # candidates voted by the light and heavy lane passes
     ix.set_stats(False)
     in_bytes = n * ends * (L + 8 + 2)                # ASCII read + offset + length
     probe_bytes = 8 * st["probes"] + 2 * st["bucket_items"] + 4 * st["hits"]
@@ -185,16 +188,35 @@ def main():
     algo_bytes = in_bytes + probe_bytes + out_bytes  # SURVEY §8(d) B_read summed over the step
     avg_kern_s = float(np.mean(kern_ms)) / 1e3
     achieved = algo_bytes / avg_kern_s / 1e9
-    # dominant kernel = vote_kernel: its algorithmic bytes are the probe records it consumes
-    # (mid/fwd/bwd, 8 B per probe), the hit values it gathers (4 B each), the read lengths
-    # and the records it writes; probe_kernel: read text + bucket bounds + keys + records out
-    vote_bytes = 8 * st["probes"] + 4 * st["hits"] + 2 * n * ends + out_bytes
-    probe_bytes_k = in_bytes + 8 * st["probes"] + 2 * st["bucket_items"] + 8 * st["probes"]
-    vote_launch_s = tk["vote_ms"] / max(1, tk["vote_launches"]) / 1e3
-    probe_launch_s = tk["probe_ms"] / max(1, tk["probe_launches"]) / 1e3
-    launches_per_step = max(1, tk["vote_launches"] // args.steps)
-    vote_achieved = vote_bytes / launches_per_step / vote_launch_s / 1e9
-    probe_achieved = probe_bytes_k / launches_per_step / probe_launch_s / 1e9
+    # per-kernel algorithmic bytes of one step:
+    #   probe_kernel  read text + bucket bounds (8 B) + bucket keys (2 B/item) + probe records out (8 B/probe)
+    #   gather_kernel probe records in (8 B/probe) + hit values (4 B/hit) + candidates out (6 B/hit) + counts
+    #   lane_kernel   candidates in (6 B/hit of lane reads) + lengths + records out
+    #   vote_kernel   (deferred reads only when the lane path runs) records in + hit values + records out
+    lane_on = kt["lane_kernel"][1] > 0
+    nd = st.get("deferred", 0) if lane_on else n                 # reads voted by vote_kernel
+    dh = st["hits"] - lane_hits if lane_on else st["hits"]       # their hits
+    dp = st["probes"] * nd / float(n)                           # their probes (same length)
+    kbytes = {
+        "probe_kernel": in_bytes + 8 * st["probes"] + 2 * st["bucket_items"] + 8 * st["probes"],
+        "gather_kernel": 8 * st["probes"] + 10 * st["hits"] + 4 * n,
+        "lane_kernel": 6 * lane_hits + 6 * n + out_bytes * (n - nd) / float(n),
+        "vote_kernel": 8 * dp + 4 * dh + 2 * nd * ends + out_bytes * nd / float(n),
+    }
+    kernels = {}
+    for k, (ms, nl) in kt.items():
+        if not nl:
+            continue
+        per_step = max(1, nl // args.steps)
+        launch_s = ms / nl / 1e3
+        kernels[k] = {"launch_ms": round(launch_s * 1e3, 3), "launches_per_step": per_step,
+                      "algorithmic_bytes_per_read": round(kbytes[k] / n, 1),
+                      "achieved": round(kbytes[k] / per_step / launch_s / 1e9, 2)}
+    dom = max(kernels, key=lambda k: kernels[k]["launch_ms"] * kernels[k]["launches_per_step"])
+    vote_achieved = kernels[dom]["achieved"]
+    vote_launch_s = kernels[dom]["launch_ms"] / 1e3
+    launches_per_step = kernels[dom]["launches_per_step"]
+    vote_bytes = kbytes[dom]
 
     # HBM traffic from the committed PMC passes of this workload (tools/pmc_traffic.py;
     # rocprofv3 cannot run inside this process), scaled to this launch's read count
@@ -256,14 +278,14 @@ def main():
                            ix.info.buckets, ix.info.items,
                            "reference-format files via svg_index_open" if prefix else "built in HBM by svg_index_build_mem"),
                        "parallelism": "reads sharded across %d GPU(s), index replicated, no collective" % world},
-            "roofline": {"bound": "hbm", "kernel": "vote_kernel", "achieved": round(vote_achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(vote_achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(vote_achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic, "traffic_unit": "GB per step (probe_kernel + vote_kernel)",
+                         "traffic": traffic, "traffic_unit": "GB per step (all kernels of the step)",
                          "traffic_source": traffic_src,
                          "launch_ms": round(vote_launch_s * 1e3, 3), "launches_per_step": launches_per_step,
                          "algorithmic_bytes_per_read": round(vote_bytes / n, 1),
-                         "probe_kernel": {"achieved": round(probe_achieved, 2), "launch_ms": round(probe_launch_s * 1e3, 3),
-                                          "algorithmic_bytes_per_read": round(probe_bytes_k / n, 1)},
+                         "kernels": kernels,
+                         "deferred_reads": st.get("deferred", 0),
                          "path": {"achieved": round(achieved, 2), "algorithmic_bytes_per_read": round(algo_bytes / n, 1),
                                   "step_ms": round(avg_kern_s * 1e3, 3), "frac": round(achieved / HBM_PEAK_GBS, 5)}},
             "cpu_baseline": cpu,

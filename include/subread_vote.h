@@ -203,6 +203,8 @@ typedef struct svg_batch_stats {
 	uint64_t bucket_items;       /* sum of items in the probed buckets        */
 	uint64_t hits;               /* sum of equal-key run lengths              */
 	uint64_t results;            /* mapping records with selected_votes > 0   */
+	uint64_t deferred;           /* single-end align: reads that left the lane-per-read
+	                                path and were voted by the wave-per-read kernel */
 } svg_batch_stats;
 int svg_set_stats(svg_index *idx, int enable);
 
@@ -219,6 +221,10 @@ int svg_get_stats(const svg_index *idx, svg_batch_stats *out);
  * counts since svg_set_timing(idx, 1). */
 int svg_set_timing(svg_index *idx, int enable);
 int svg_get_timing(svg_index *idx, double *probe_ms, double *vote_ms, int *probe_launches, int *vote_launches);
+/* The same per kernel: ms[k] / launches[k] for k = 0 probe_kernel, 1 vote_kernel (wave per
+ * read), 2 gather_kernel, 3 lane_kernel (lane per read; single-end align).  vote_ms of
+ * svg_get_timing is the sum of kinds 1-3. */
+int svg_get_kernel_timing(svg_index *idx, double ms[4], int launches[4]);
 
 const char *svg_last_error(void);
 int svg_abi_version(void);

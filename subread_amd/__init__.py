@@ -29,6 +29,7 @@ EXPORTS = [
     "svg_last_error", "svg_abi_version", "svg_build_index", "svg_sim_genome",
     "svg_sim_repeats", "svg_sim_reads", "svg_index_build", "svg_index_build_mem", "svg_index_export",
     "svg_set_max_read_length", "svg_sim_pairs", "svg_set_timing", "svg_get_timing",
+    "svg_get_kernel_timing",
 ]
 
 _lib = None
@@ -69,6 +70,8 @@ def lib():
         L.svg_set_timing.restype = i32
         L.svg_get_timing.argtypes = [vp, vp, vp, vp, vp]
         L.svg_get_timing.restype = i32
+        L.svg_get_kernel_timing.argtypes = [vp, vp, vp]
+        L.svg_get_kernel_timing.restype = i32
         L.svg_set_max_read_length.argtypes = [vp, i32]
         L.svg_set_max_read_length.restype = i32
         L.svg_last_error.restype = ctypes.c_char_p
@@ -187,13 +190,29 @@ class VoteIndex:
                "svg_get_timing")
         return {"probe_ms": pm.value, "vote_ms": vm.value, "probe_launches": pl.value, "vote_launches": vl.value}
 
+    KERNELS = ("probe_kernel", "vote_kernel", "gather_kernel", "lane_kernel")
+
+    def kernel_timing(self):
+        """{kernel: (ms, launches)} per kernel kind since set_timing(True)."""
+        ms = (ctypes.c_double * 4)()
+        n = (ctypes.c_int * 4)()
+        _check(lib().svg_get_kernel_timing(self.h, ms, n), "svg_get_kernel_timing")
+        return {k: (ms[i], n[i]) for i, k in enumerate(self.KERNELS)}
+
+    def debug_counters(self):
+        """Raw device counters of the last batch with stats on (see svg_debug_counters)."""
+        c = (ctypes.c_ulonglong * 32)()
+        _check(lib().svg_debug_counters(self.h, c), "svg_debug_counters")
+        return list(c)
+
     def set_stats(self, on=True):
         lib().svg_set_stats(self.h, 1 if on else 0)
 
     def stats(self):
         s = SvgBatchStats()
         lib().svg_get_stats(self.h, ctypes.byref(s))
-        return {"probes": s.probes, "bucket_items": s.bucket_items, "hits": s.hits, "results": s.results}
+        return {"probes": s.probes, "bucket_items": s.bucket_items, "hits": s.hits, "results": s.results,
+                "deferred": s.deferred}
 
     def vote(self, params, r1, r2=None):
         """Host buffers in, host records out: (mapping[n,ends,mb], subjunc|None, big_margin|None)."""

@@ -97,6 +97,7 @@ class SvgBatchStats(ctypes.Structure):
         ("bucket_items", ctypes.c_uint64),
         ("hits", ctypes.c_uint64),
         ("results", ctypes.c_uint64),
+        ("deferred", ctypes.c_uint64),
     ]
 
 

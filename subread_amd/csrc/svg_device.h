@@ -34,11 +34,16 @@ struct svg_index {
 	int n_cu;
 	int max_read_len;        // announced read-length bound (svg_set_max_read_length), picks the kernel variant
 	void *d_prec; size_t prec_cap;   // probe records of one chunk
-	// svg_set_timing: event pairs per launch, folded into the sums when the ring fills
+	// lane-per-read SE path (svg_lane.hip): candidate lists + deferral list, per-wave cold scratch
+	void *d_lane; size_t lane_cap;
+	uint32_t *d_lscratch; size_t lscratch_words;     // light pass
+	uint32_t *d_lscratch2; size_t lscratch2_words;   // heavy pass
+	// svg_set_timing: event pairs per launch (kinds: 0 probe_kernel, 1 vote_kernel, 2 gather_kernel,
+	// 3 lane_kernel), folded into the sums when the ring fills
 	int timing;
-	hipEvent_t tev[2][64][2];
-	int tn[2], tcount[2];
-	double tms[2];
+	hipEvent_t tev[4][64][2];
+	int tn[4], tcount[4];
+	double tms[4];
 	// staging for svg_vote_batch (host buffers)
 	void *d_in; size_t d_in_cap;
 	void *d_out; size_t d_out_cap;
@@ -55,5 +60,11 @@ static inline int dmalloc(svg_index *h, void **p, size_t n)
 }
 
 int svg_index_finish_device(svg_index *h);
+
+// svg_lane.hip
+int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int sj);
+int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint32_t n, const uint2 *precs, int nps,
+                   uint8_t *out, unsigned long long *stats, uint32_t **defer_list, uint32_t **defer_count, hipStream_t st);
+int svg_timing_mark(svg_index *h, int k, int phase, hipStream_t st);
 
 #endif

@@ -1,0 +1,615 @@
+// svg_lane.hip -- lane-per-read fast path of the single-end subread-align voting step.
+//
+// The wave-per-read vote_kernel (svg_vote.hip) replays each read's ~30 candidates one
+// at a time through the whole wavefront; at 3 Gbp that leaves it instruction-bound with
+// most lanes idle.  Here every LANE owns one read, so a wave votes 64 reads at once:
+//
+//   gather_kernel  (thread = read x strand)  walks probe_kernel's records of its read in
+//                  the reference's visiting order (subread_no, xk1, mid..last, mid-1..first;
+//                  gehash_go_X, sorted-hashtable.c:984-1120), fetches the hit values and
+//                  writes the read's candidate list (kv = value - offset, kP1 | offset) in a
+//                  [strand][j][read] layout, so the lane kernel's j-th loads are coalesced.
+//   lane_kernel    (lane = read)  per strand: init_gene_vote (gene-algorithms.h:42), the
+//                  gehash_go_X tally state machine (sorted-hashtable.c:995-1107) on a per-lane
+//                  vote table, then the single-end part of process_voting_junction_PE_topK
+//                  (core-junction.c:2199-2530) and the SE gate of do_voting (core.c:3215-3233);
+//                  finally the multi_best mapping_result_t records (core.h:350-370).
+//
+// Per-lane vote table.  The reference's gene_vote_t is 30 rows x 24 slots, first match
+// wins in (row iix = 0,+5,-5; slot ascending) order, new slots appended to row kv/5 %30.
+// Each lane keeps a pool of K <= 24 slots in LDS ([slot][lane] uint2: position, meta) with
+// one singly linked list per row (heads: 30 x 5-bit fields in 5 registers, next pointer in
+// the slot's meta), which visits a row's slots in exactly the reference's slot order.  The
+// cold part of a slot (coverage start/end, 21-entry indel recorder) lives in a per-wave
+// HBM scratch, one region per strand so that the first strand's results stay readable.
+//
+// A read leaves the fast path (it is appended to a deferral list and voted afterwards by
+// vote_kernel, bit-identical by construction) when it needs anything this table does not
+// model: more than CAP candidates on a strand, more than K slots, a shift-indel mark
+// (which would trigger the reference's second voting round, sorted-hashtable.c:1016-1019),
+// a read shorter than 15+gap or longer than 160 bp, or more than 31 applied subreads.
+// Integer work only: no MFMA.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include "subread_vote.h"
+#include "svg_internal.h"
+#include "svg_device.h"
+
+#define LROWS 30
+#define CW 7                 // cold words per slot: cs | ce << 8, then rec[0..23] as bytes
+
+// ---------------------------------------------------------------------------------------------
+// gather: one thread per (strand, read) of a chunk
+// ---------------------------------------------------------------------------------------------
+struct GParams {
+	const uint2 *precs;      // probe records, SoA: record q of read r at precs[q * n + r]
+	const uint16_t *len;
+	const uint32_t *vals;
+	uint32_t n;
+	int nps, gap, total_subreads, cap;
+	uint32_t *cand;          // [2][cap][cs] kv
+	uint16_t *cpk;           // [2][cap][cs] kP1 | off << 6
+	uint16_t *ccnt;          // [2][cs] candidates, 0xffff = leave the fast path
+	uint32_t cs;             // column stride of cand/cpk/ccnt
+	const uint32_t *idx;     // NULL: column r = read r; else column k = read idx[k], k < min(*idx_count, cs)
+	const uint32_t *idx_count;
+};
+
+__global__ void __launch_bounds__(256) gather_kernel(GParams g)
+{
+	const uint32_t n = g.n;
+	uint32_t m = n;
+	if (g.idx) { m = *g.idx_count; if (m > g.cs) m = g.cs; }
+	for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < 2u * m; t += gridDim.x * 256u) {
+		const uint32_t s = t >= m ? 1u : 0u, k = t - s * m;
+		const uint32_t r = g.idx ? g.idx[k] : k;
+		int len = g.len[r];
+		if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;
+		const int gap = g.gap;
+		uint32_t c = 0xffffu;
+		if (len >= 15 + gap && len <= 160) {
+			// subread offsets, core.c:3117-3171 (reads <= 160 bp)
+			const int cr = (len - 15 - gap) << 16;
+			int step = cr / (g.total_subreads - 1);
+			if (step < (gap << 16)) step = gap << 16;
+			const int applied = 1 + cr / step, np = applied * gap;
+			if (applied <= 31 && np <= g.nps) {
+				c = 0;
+				for (int p = 0; p < np; p++) {
+					const uint2 rec = g.precs[(size_t)(s * (uint32_t)g.nps + (uint32_t)p) * n + r];
+					const uint32_t fwd = rec.y & 0xffffu, hits = fwd + (rec.y >> 16);
+					if (!hits) continue;
+					if (c + hits > (uint32_t)g.cap) { c = 0xffffu; break; }
+					const int sk = p / gap, x = p - sk * gap;   // subread number, gap slot
+					int off = (int)(((int64_t)step * sk) >> 16);
+					if (gap > 1) off -= off % gap - x;
+					const uint16_t pk = (uint16_t)((sk + 1) | (off << 6));
+					for (uint32_t j = 0; j < hits; j++) {
+						const uint32_t item = j < fwd ? rec.x + j : rec.x - 1u - (j - fwd);
+						const size_t o = (size_t)(s * (uint32_t)g.cap + c + j) * g.cs + k;
+						g.cand[o] = g.vals[item] - (uint32_t)off;
+						g.cpk[o] = pk;
+					}
+					c += hits;
+				}
+			}
+		}
+		g.ccnt[(size_t)s * g.cs + k] = (uint16_t)c;
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// lane kernel
+// ---------------------------------------------------------------------------------------------
+struct LParams {
+	const uint32_t *cand;
+	const uint16_t *cpk;
+	const uint16_t *ccnt;
+	const uint16_t *len;
+	uint32_t n;
+	int cap, gap, total_subreads, tol;
+	uint32_t low, high;
+	int multi_best, max_vote_simples, cutoff, min_votes_first, min_votes_second;
+	uint8_t *out;                 // this chunk's mapping records
+	uint32_t *cold;               // per-wave scratch
+	uint32_t *defer_list, *defer_count;
+	int defer_all;                // testing: every read takes the deferred path
+	uint32_t cs;                  // column stride of cand/cpk/ccnt
+	const uint32_t *idx;          // NULL: lane column r = read r; else column k = read idx[k], k < *idx_count
+	const uint32_t *idx_count;    //   (columns >= cs have no candidate list and are deferred)
+	unsigned long long *stats;    // [3] += results; [4] += deferred reads (final pass only);
+	int stat_base, final_pass;    // diagnostics at stats[stat_base..+4]: deferrals by reason (3), candidates, deferrals
+};
+
+// meta: votes [0,6) | last [6,12) | toli [12,17) | cursor [17,23) (6-bit signed) | next [23,29)
+__device__ __forceinline__ int lm_votes(uint32_t m) { return (int)(m & 63u); }
+__device__ __forceinline__ int lm_last(uint32_t m) { return (int)((m >> 6) & 63u); }
+__device__ __forceinline__ int lm_toli(uint32_t m) { return (int)((m >> 12) & 31u); }
+__device__ __forceinline__ int lm_cursor(uint32_t m) { return ((int)(m << 9)) >> 26; }
+__device__ __forceinline__ uint32_t lm_next(uint32_t m) { return (m >> 23) & 63u; }
+__device__ __forceinline__ uint32_t lm_pack(int votes, int last, int toli, int cursor, uint32_t next)
+{
+	return (uint32_t)votes | ((uint32_t)last << 6) | ((uint32_t)toli << 12) | (((uint32_t)cursor & 63u) << 17) | (next << 23);
+}
+__device__ __forceinline__ uint32_t lm_set_next(uint32_t m, uint32_t next) { return (m & ~(63u << 23)) | (next << 23); }
+
+__device__ __forceinline__ uint32_t lrow(uint32_t x) { return (x / 5u) % LROWS; }
+
+// value selects (by-value parameters: a conditional over lvalues would select addresses and
+// pin the variables to scratch)
+__device__ __forceinline__ uint32_t pick(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
+template <typename T>
+__device__ __forceinline__ T sel3(int k, T a, T b, T c) { return k == 0 ? a : (k == 1 ? b : c); }
+
+// update_top_three (core-junction.c:908-922) with top_scores = 3, as value selects
+__device__ __forceinline__ void ltop3(int &t0, int &t1, int &t2, int v)
+{
+	const bool g0 = v > t0, e0 = v == t0, g1 = v > t1, e1 = v == t1, g2 = v > t2;
+	const bool at1 = !g0 && !e0 && g1, at2 = !g0 && !e0 && !g1 && !e1 && g2;
+	const int n0 = g0 ? v : t0;
+	const int n1 = g0 ? t0 : (at1 ? v : t1);
+	const int n2 = (g0 || at1) ? t1 : (at2 ? v : t2);
+	t0 = n0; t1 = n1; t2 = n2;
+}
+
+// 3 smallest keys, ascending (row-major slot order of one vote value)
+__device__ __forceinline__ void lins3(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t k)
+{
+	const uint32_t nc = k < b ? b : (k < c ? k : c);
+	const uint32_t nb = k < a ? a : (k < b ? k : b);
+	const uint32_t na = k < a ? k : a;
+	a = na; b = nb; c = nc;
+}
+
+// element idx of a 3-element register "array" := val, with one select per element
+#define PUT3(idx, a0, a1, a2, val) do { const int _i = (idx); const auto _v = (val); \
+	a0 = _i == 0 ? _v : a0; a1 = _i == 1 ? _v : a1; a2 = _i == 2 ? _v : a2; } while (0)
+
+template <int K>
+struct Lane {
+	// row heads: 30 fields of HB bits (NIL = all ones), HPW per register
+	static constexpr int HB = K > 31 ? 6 : 5;
+	static constexpr uint32_t NIL = (1u << HB) - 1u;
+	static constexpr int HPW = 32 / HB, NHW = (LROWS + HPW - 1) / HPW;
+	int tol;               // min(16, -I) (<= 5 on this path)
+	uint32_t low;          // first valid array position
+	uint2 *pm;             // LDS: pm[slot * 64 + lane]
+	uint32_t *cold;        // this lane's scratch: word w of slot s of strand st at cold[((st*K+s)*CW+w)*64]
+	int lane;
+	uint32_t h[NHW];
+	int nslots, max_vote;
+	bool dfr;
+	int why;               // deferral reason (stats): 1 candidates > CAP or length, 2 slots > K, 3 shift-indel
+
+	__device__ __forceinline__ uint32_t head(uint32_t r) const
+	{
+		const uint32_t q = r / HPW, sh = (r - q * HPW) * HB;
+		uint32_t w = h[0];
+#pragma unroll
+		for (int k = 1; k < NHW; k++) w = pick(q == (uint32_t)k, h[k], w);
+		return (w >> sh) & NIL;
+	}
+	__device__ __forceinline__ void set_head(uint32_t r, uint32_t s)
+	{
+		const uint32_t q = r / HPW, sh = (r - q * HPW) * HB;
+		const uint32_t clr = ~(NIL << sh), v = s << sh;
+#pragma unroll
+		for (int k = 0; k < NHW; k++) h[k] = pick(q == (uint32_t)k, (h[k] & clr) | v, h[k]);
+	}
+	__device__ __forceinline__ uint32_t *cw(int st, int s, int w) const { return cold + ((st * K + s) * CW + w) * 64; }
+	__device__ __forceinline__ int8_t *recb(int st, int s, int i) const
+	{
+		return (int8_t *)cw(st, s, 1 + (i >> 2)) + (i & 3);
+	}
+
+	__device__ __forceinline__ void reset()
+	{
+		uint32_t all = 0;
+#pragma unroll
+		for (int i = 0; i < HPW; i++) all |= NIL << (i * HB);
+#pragma unroll
+		for (int k = 0; k < NHW; k++) h[k] = all;
+		nslots = 0;
+		max_vote = 0;
+	}
+
+	// gehash_go_X body for one candidate (round 0; sorted-hashtable.c:995-1107)
+	__device__ __forceinline__ void vote(int st, uint32_t kv, int kP1, int off, uint32_t high_b)
+	{
+		const uint32_t r0 = lrow(kv), rp = lrow(kv + 5u), rm = lrow(kv - 5u);
+		uint32_t tail = NIL, tailM = 0;
+		int ri = 0, n0 = 0;
+		uint32_t s = head(r0);
+		bool found = false;
+		for (;;) {
+			while (s == NIL && ri < 2) { ri++; s = head(ri == 1 ? rp : rm); }
+			if (s == NIL) break;
+			const uint2 e = pm[s * 64 + lane];
+			uint32_t M = e.y;
+			const int d = (int)(kv - e.x);
+			if (d >= -tol && d <= tol) {
+				int tl = lm_toli(M), last = lm_last(M), votes = lm_votes(M);
+				if (tl > 0 && d == 0) { dfr = true; why = 3; return; }   // shift-indel mark -> second round
+				bool chg = false;
+				if (kP1 == last && tl > 0) {   // roll-back (sorted-hashtable.c:1027-1039)
+					int md = tl >= 3 ? (int)*recb(st, s, tl - 1) : 0;
+					int nd = md - d;
+					md -= (int)*recb(st, s, tl + 2);
+					if (abs(md) > abs(nd)) { tl -= 3; last -= 1; votes -= 1; chg = true; }
+				}
+				if (kP1 > last) {
+					votes += 1;
+					int cur = lm_cursor(M);
+					*((uint8_t *)cw(st, s, 0) + 1) = (uint8_t)(off + 16);   // coverage_end
+					if (d == cur) *recb(st, s, tl + 1) = (int8_t)kP1;
+					else {
+						const int t2 = tl + 3;
+						if (t2 < 21) {
+							tl = t2;
+							*recb(st, s, t2) = (int8_t)kP1;
+							*recb(st, s, t2 + 1) = (int8_t)kP1;
+							*recb(st, s, t2 + 2) = (int8_t)d;
+							if (t2 < 18) *recb(st, s, t2 + 3) = 0;
+						}
+						cur = d;
+					}
+					M = lm_pack(votes, kP1, tl, cur, lm_next(M));
+					pm[s * 64 + lane].y = M;
+					if (max_vote < votes) max_vote = votes;
+					found = true;
+					break;
+				}
+				if (chg) { M = lm_pack(votes, last, tl, lm_cursor(M), lm_next(M)); pm[s * 64 + lane].y = M; }
+			}
+			if (ri == 0) { tail = s; tailM = M; n0++; }
+			s = lm_next(M);
+		}
+		// new slot in row r0 unless it already holds GENE_VOTE_SPACE (24) slots
+		if (!found && kv >= low && kv <= high_b && (K <= 24 || n0 < 24)) {
+			if (nslots == K) { dfr = true; why = 2; return; }
+			const uint32_t ns = (uint32_t)nslots++;
+			pm[ns * 64 + lane] = make_uint2(kv, lm_pack(1, kP1, 0, 0, NIL));
+			*cw(st, (int)ns, 0) = (uint32_t)off | ((uint32_t)(off + 16) << 8);
+			*cw(st, (int)ns, 1) = (uint32_t)kP1 | ((uint32_t)kP1 << 8);   // rec[0..3] = k+1, k+1, 0, 0
+			if (tail == NIL) set_head(r0, ns);
+			else pm[tail * 64 + lane].y = lm_set_next(tailM, ns);
+			if (max_vote < 1) max_vote = 1;
+		}
+	}
+};
+
+template <int K>
+__global__ void __launch_bounds__(64) lane_kernel(LParams lp)
+{
+	extern __shared__ __align__(16) uint8_t lds_raw[];
+	const uint32_t gw = blockIdx.x, nw = gridDim.x;
+	Lane<K> L;
+	L.tol = lp.tol;
+	L.low = lp.low;
+	L.lane = (int)__lane_id();
+	L.pm = reinterpret_cast<uint2 *>(lds_raw);
+	L.cold = lp.cold + (size_t)gw * (2 * K * CW * 64) + L.lane;
+	const int mb = lp.multi_best, mvs = lp.max_vote_simples, mvf = lp.min_votes_first, mvsec = lp.min_votes_second;
+	const int cutoff = lp.cutoff;
+	unsigned long long nres = 0, ndef = 0, nwhy1 = 0, nwhy2 = 0, nwhy3 = 0, ncand = 0;
+	const uint32_t m = lp.idx ? *lp.idx_count : lp.n;
+	for (uint32_t g0 = gw * 64u; g0 < m; g0 += nw * 64u) {
+		const uint32_t k = g0 + (uint32_t)L.lane;
+		const bool live = k < m;
+		const uint32_t r = !live ? 0u : lp.idx ? lp.idx[k] : k;
+		L.dfr = !live || lp.defer_all || k >= lp.cs;
+		L.why = live && k >= lp.cs ? 1 : 0;
+		int len = live ? lp.len[r] : 0;
+		if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;
+		int applied = 0;
+		if (!L.dfr && len >= 15 + lp.gap) {
+			const int cr = (len - 15 - lp.gap) << 16;
+			int step = cr / (lp.total_subreads - 1);
+			if (step < (lp.gap << 16)) step = lp.gap << 16;
+			applied = 1 + cr / step;
+		}
+		const uint32_t high_b = lp.high - (uint32_t)len;
+		// the read's bigtable records: source (-1 none, else strand << 5 | slot), position, votes, used
+		int rsrc0 = -1, rsrc1 = -1, rsrc2 = -1;
+		uint32_t rpos0 = 0, rpos1 = 0, rpos2 = 0;
+		int rv0 = 0, rv1 = 0, rv2 = 0, ru0 = 0, ru1 = 0, ru2 = 0;
+		int nc_read = 0;
+		for (int st = 0; st < 2; st++) {
+			const int cnt = L.dfr ? 0 : (int)lp.ccnt[(size_t)st * lp.cs + k];
+			if (cnt == 0xffff) { L.dfr = true; L.why = 1; }
+			const int mycnt = L.dfr ? 0 : cnt;
+			nc_read += mycnt;
+			L.reset();
+			// ---- voting: the j-th candidates of all lanes are one coalesced load
+			int mc = mycnt;
+			for (int o = 32; o; o >>= 1) { int t = __shfl_xor(mc, o); mc = t > mc ? t : mc; }
+			const uint32_t *cb = lp.cand + (size_t)st * lp.cap * lp.cs + k;
+			const uint16_t *pb = lp.cpk + (size_t)st * lp.cap * lp.cs + k;
+			uint32_t kv_a = 0, kv_b = 0;
+			uint32_t pk_a = 0, pk_b = 0;
+			if (0 < mycnt) { kv_a = cb[0]; pk_a = pb[0]; }
+			if (1 < mycnt) { kv_b = cb[lp.cs]; pk_b = pb[lp.cs]; }
+			for (int j = 0; j < mc; j++) {
+				const uint32_t kv = kv_a, pk = pk_a;
+				kv_a = kv_b; pk_a = pk_b;
+				if (j + 2 < mycnt) { kv_b = cb[(size_t)(j + 2) * lp.cs]; pk_b = pb[(size_t)(j + 2) * lp.cs]; }
+				if (j < mycnt && !L.dfr) L.vote(st, kv, (int)(pk & 63u), (int)(pk >> 6), high_b);
+			}
+			if (L.dfr) continue;
+			// ---- SE gate (core.c:3215-3233) and top-K (core-junction.c:2199-2530, ends = 1)
+			if (L.max_vote >= mvf) {
+				int t0 = 0, t1 = 0, t2 = 0;
+				for (int s = 0; s < L.nslots; s++) ltop3(t0, t1, t2, lm_votes(L.pm[s * 64 + L.lane].y));
+				if (rv0 > 0) ltop3(t0, t1, t2, rv0);
+				if (mb > 1 && rv1 > 0) ltop3(t0, t1, t2, rv1);
+				if (mb > 2 && rv2 > 0) ltop3(t0, t1, t2, rv2);
+				const bool ok0 = t0 >= 1, ok1 = ok0 && t1 >= 1 && t0 - t1 <= cutoff, ok2 = ok1 && t2 >= 1 && t0 - t2 <= cutoff;
+				// table slots of each value in row-major order (row, then slot order = pool order)
+				uint32_t a0 = ~0u, b0 = ~0u, c0 = ~0u, a1 = ~0u, b1 = ~0u, c1 = ~0u, a2 = ~0u, b2 = ~0u, c2 = ~0u;
+				for (int s = 0; s < L.nslots; s++) {
+					const uint2 e = L.pm[s * 64 + L.lane];
+					const int v = lm_votes(e.y);
+					if (v < mvsec) continue;
+					const uint32_t key = (lrow(e.x) << 6) | (uint32_t)s;
+					if (ok0 && v == t0) lins3(a0, b0, c0, key);
+					else if (ok1 && v == t1) lins3(a1, b1, c1, key);
+					else if (ok2 && v == t2) lins3(a2, b2, c2, key);
+				}
+				// simples (simple_mapping_t), in the reference's order; src: slot | 64, or stored index
+				int ns = 0;
+				int sv0 = 0, sv1 = 0, sv2 = 0, sk0 = 0, sk1 = 0, sk2 = 0;
+				uint32_t sp0 = 0, sp1 = 0, sp2 = 0;
+				auto add = [&](int kind, uint32_t pos, int v) __attribute__((always_inline)) {
+					PUT3(ns, sk0, sk1, sk2, kind);
+					PUT3(ns, sp0, sp1, sp2, pos);
+					PUT3(ns, sv0, sv1, sv2, v);
+					ns++;
+				};
+				auto add_val = [&](int N, uint32_t ka, uint32_t kb, uint32_t kc) __attribute__((always_inline)) {
+					if (ka != ~0u && ns < mvs) add(128 | (int)(ka & 63u), L.pm[(ka & 63u) * 64 + L.lane].x, N);
+					if (kb != ~0u && ns < mvs) add(128 | (int)(kb & 63u), L.pm[(kb & 63u) * 64 + L.lane].x, N);
+					if (kc != ~0u && ns < mvs) add(128 | (int)(kc & 63u), L.pm[(kc & 63u) * 64 + L.lane].x, N);
+					if (ns < mvs && rv0 == N) add(0, rpos0, N);
+					if (mb > 1 && ns < mvs && rv1 == N) add(1, rpos1, N);
+					if (mb > 2 && ns < mvs && rv2 == N) add(2, rpos2, N);
+				};
+				if (ok0) add_val(t0, a0, b0, c0);
+				if (ok1 && ns < mvs) add_val(t1, a1, b1, c1);
+				if (ok2 && ns < mvs) add_val(t2, a2, b2, c2);
+				// single-end results: simples with >= min_votes_first votes, distinct positions
+				int cur = 0;
+				int ts0 = -1, ts1 = -1, ts2 = -1, tu0 = 0, tu1 = 0, tu2 = 0, tv0 = 0, tv1 = 0, tv2 = 0;
+				uint32_t tp0 = 0, tp1 = 0, tp2 = 0;
+				auto emit = [&](int kind, uint32_t pos, int v) __attribute__((always_inline)) {
+					if (cur >= mb || v < mvf) return;
+					if ((cur > 0 && tp0 == pos) || (cur > 1 && tp1 == pos)) return;
+					int src, u, vv = v;
+					if (kind & 128) { src = (st << 6) | (kind & 63); u = applied; }
+					else {
+						src = sel3(kind, rsrc0, rsrc1, rsrc2);
+						u = sel3(kind, ru0, ru1, ru2);
+						pos = sel3(kind, rpos0, rpos1, rpos2);
+						vv = sel3(kind, rv0, rv1, rv2);
+					}
+					PUT3(cur, ts0, ts1, ts2, src);
+					PUT3(cur, tp0, tp1, tp2, pos);
+					PUT3(cur, tv0, tv1, tv2, vv);
+					PUT3(cur, tu0, tu1, tu2, u);
+					cur++;
+				};
+				if (ns > 0) emit(sk0, sp0, sv0);
+				if (ns > 1) emit(sk1, sp1, sv1);
+				if (ns > 2) emit(sk2, sp2, sv2);
+				if (cur > 0) { rsrc0 = ts0; rpos0 = tp0; rv0 = tv0; ru0 = tu0; } else rv0 = 0;
+				if (cur > 1) { rsrc1 = ts1; rpos1 = tp1; rv1 = tv1; ru1 = tu1; } else rv1 = 0;
+				if (cur > 2) { rsrc2 = ts2; rpos2 = tp2; rv2 = tv2; ru2 = tu2; } else rv2 = 0;
+			} else if (rv0 < 1) {
+				if (applied > ru0) ru0 = applied;   // used_subreads_in_vote (noninformative stays 0)
+			}
+		}
+		if (!L.dfr) ncand += (unsigned long long)nc_read;
+		// ---- the read's multi_best records (copy_vote_to_alignment_res, core-junction.c:1058-1071;
+		// indel_recorder_copy, sorted-hashtable.c:1144)
+		if (!L.dfr) {
+			uint32_t *dst = (uint32_t *)(lp.out + (size_t)r * mb * 68);
+			for (int i = 0; i < mb; i++) {
+				const int src = sel3(i, rsrc0, rsrc1, rsrc2);
+				const uint32_t pos = sel3(i, rpos0, rpos1, rpos2);
+				const int v = sel3(i, rv0, rv1, rv2);
+				const int u = sel3(i, ru0, ru1, ru2);
+				uint32_t w[17];
+#pragma unroll
+				for (int k = 0; k < 17; k++) w[k] = 0;
+				w[2] = (uint32_t)(uint16_t)v | ((uint32_t)(uint16_t)u << 16);
+				if (src >= 0) {
+					const int st = src >> 6, s = src & 63;
+					uint32_t rw[6];
+#pragma unroll
+					for (int k = 0; k < 6; k++) rw[k] = *L.cw(st, s, 1 + k);
+					const uint32_t c0w = *L.cw(st, s, 0);
+					int nrec = 0, last = 0;
+#pragma unroll
+					for (int t = 0; t < 7; t++) {
+						const int b0 = 3 * t;
+						const int k0 = (int)(int8_t)(rw[b0 >> 2] >> (8 * (b0 & 3)));
+						if (nrec == 3 * t && k0 != 0) {
+							nrec = 3 * t + 3;
+							last = (int)(int8_t)(rw[(b0 + 2) >> 2] >> (8 * ((b0 + 2) & 3)));
+						}
+					}
+#pragma unroll
+					for (int k = 0; k < 11; k++) {
+						const int i0 = 2 * k, i1 = 2 * k + 1;
+						const int v0 = i0 < nrec ? (int)(int8_t)(rw[i0 >> 2] >> (8 * (i0 & 3))) : 0;
+						const int v1 = i1 < nrec ? (int)(int8_t)(rw[i1 >> 2] >> (8 * (i1 & 3))) : 0;
+						w[4 + k] = (uint32_t)(uint16_t)(int16_t)v0 | ((uint32_t)(uint16_t)(int16_t)v1 << 16);
+					}
+					w[0] = pos;
+					w[1] = st ? (uint32_t)SVG_NEGATIVE_STRAND_FLAG : 0u;
+					w[3] = (uint32_t)(uint8_t)(int8_t)last << 8;
+					w[15] = (c0w & 0xffu) | (((c0w >> 8) & 0xffu) << 16);
+				}
+#pragma unroll
+				for (int k = 0; k < 17; k++) dst[i * 17 + k] = w[k];
+				nres += v > 0;
+			}
+		}
+		// ---- deferred reads: one atomic per wave
+		const unsigned long long dm = __ballot(L.dfr && live);
+		if (dm) {
+			uint32_t base = 0;
+			const int leader = __ffsll((long long)dm) - 1;
+			if (L.lane == leader) base = atomicAdd(lp.defer_count, (uint32_t)__popcll(dm));
+			base = __shfl(base, leader);
+			if (L.dfr && live) lp.defer_list[base + __popcll(dm & ((1ull << L.lane) - 1ull))] = r;
+			ndef += (unsigned long long)__popcll(dm);
+		}
+		if (lp.stats) {
+			nwhy1 += (unsigned long long)__popcll(__ballot(L.dfr && live && L.why == 1));
+			nwhy2 += (unsigned long long)__popcll(__ballot(L.dfr && live && L.why == 2));
+			nwhy3 += (unsigned long long)__popcll(__ballot(L.dfr && live && L.why == 3));
+		}
+	}
+	if (lp.stats) {
+		for (int o = 32; o; o >>= 1) { nres += __shfl_xor(nres, o); ncand += __shfl_xor(ncand, o); }
+		if (L.lane == 0) {
+			atomicAdd(&lp.stats[3], nres);
+			if (lp.final_pass) atomicAdd(&lp.stats[4], ndef);
+			// diagnostics (svg_debug_counters): deferrals by reason, candidates voted, deferrals
+			unsigned long long *d = lp.stats + lp.stat_base;
+			atomicAdd(&d[0], nwhy1);
+			atomicAdd(&d[1], nwhy2);
+			atomicAdd(&d[2], nwhy3);
+			atomicAdd(&d[3], ncand);
+			atomicAdd(&d[4], ndef);
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// host: two lane passes for one chunk (SE align), then the wave kernel for what is left
+//   pass 1 (light): every read, <= 40 candidates and <= 16 vote-table slots per strand
+//   pass 2 (heavy, SVG_LANE=3 only): the reads pass 1 deferred (up to n/4 of them), <= 192
+//                   candidates and <= 64 slots per strand.  Measured at C3 it costs more than
+//                   it saves (64-slot tables: 5 waves/CU, long row walks, and most repeat-family
+//                   reads still overflow), so the wave kernel takes pass 1's deferrals directly.
+// ---------------------------------------------------------------------------------------------
+#define LANE_K1 16
+#define LANE_CAP1 40
+#define LANE_K2 64
+#define LANE_CAP2 192
+
+template <int K>
+static int lane_launch(svg_index *h, LParams &lp, uint32_t **cold, size_t *cold_words, hipStream_t st)
+{
+	const size_t lds = (size_t)K * 64 * sizeof(uint2);
+	int per_cu = (int)(160 * 1024 / lds);
+	if (per_cu > 32) per_cu = 32;
+	uint64_t blocks = (uint64_t)h->n_cu * per_cu, need_b = (lp.n + 63) / 64;
+	if (blocks > need_b) blocks = need_b;
+	if (blocks < 1) blocks = 1;
+	const size_t words = blocks * (size_t)(2 * K * CW * 64);
+	if (words > *cold_words) {
+		hipFree(*cold);
+		*cold = NULL;
+		*cold_words = 0;
+		if (dmalloc(h, (void **)cold, words * 4 + 256)) return SVG_E_NOMEM;
+		*cold_words = words;
+	}
+	lp.cold = *cold;
+	int rc = svg_timing_mark(h, 3, 0, st);
+	if (rc) return rc;
+	hipLaunchKernelGGL(lane_kernel<K>, dim3((unsigned)blocks), dim3(64), lds, st, lp);
+	HIPCHK(hipGetLastError());
+	return svg_timing_mark(h, 3, 1, st);
+}
+
+static int gather_launch(svg_index *h, const GParams &g, hipStream_t st)
+{
+	uint64_t blocks = ((uint64_t)2 * g.cs + 255) / 256, bmax = (uint64_t)h->n_cu * 32;
+	if (blocks > bmax) blocks = bmax;
+	if (blocks < 1) blocks = 1;
+	int rc = svg_timing_mark(h, 2, 0, st);
+	if (rc) return rc;
+	hipLaunchKernelGGL(gather_kernel, dim3((unsigned)blocks), dim3(256), 0, st, g);
+	HIPCHK(hipGetLastError());
+	return svg_timing_mark(h, 2, 1, st);
+}
+
+int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int sj)
+{
+	const char *e = getenv("SVG_LANE");
+	if (e && e[0] == '0') return 0;
+	if (paired || sj || h->max_read_len > 160) return 0;
+	int tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
+	if (tol > 5 || p->total_subreads > 31 || p->max_vote_simples > 3 || p->multi_best > 3 || p->top_scores != 3) return 0;
+	return 1;
+}
+
+int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint32_t n, const uint2 *precs, int nps,
+                   uint8_t *out, unsigned long long *stats, uint32_t **defer_list, uint32_t **defer_count, hipStream_t st)
+{
+	const uint32_t n2 = n / 4 + 64;   // heavy-pass columns
+	const char *e = getenv("SVG_LANE");
+	const bool two = e && e[0] == '3';   // heavy pass on request
+	// buffers: light cand/cpk/cnt over n columns, heavy over n2 columns, deferral lists 1 and 2
+	const size_t o_c1 = 0, o_p1 = o_c1 + (size_t)8 * LANE_CAP1 * n, o_n1 = o_p1 + (size_t)4 * LANE_CAP1 * n;
+	const size_t o_c2 = (o_n1 + (size_t)4 * n + 255) & ~(size_t)255;
+	const size_t o_p2 = o_c2 + (size_t)8 * LANE_CAP2 * n2, o_n2 = o_p2 + (size_t)4 * LANE_CAP2 * n2;
+	const size_t o_l1 = (o_n2 + (size_t)4 * n2 + 255) & ~(size_t)255, o_l2 = o_l1 + (size_t)4 * n + 256;
+	const size_t o_cnt = o_l2 + (size_t)4 * n + 256, need = o_cnt + 256;
+	if (need > h->lane_cap) {
+		hipFree(h->d_lane);
+		h->d_lane = NULL;
+		h->lane_cap = 0;
+		if (dmalloc(h, &h->d_lane, need)) return SVG_E_NOMEM;
+		h->lane_cap = need;
+	}
+	uint8_t *b = (uint8_t *)h->d_lane;
+	// [0] pass-1 deferrals, [1] pass-2 deferrals, [2] / [3] wave-kernel work counters after pass 1 / 2
+	uint32_t *cnt = (uint32_t *)(b + o_cnt);
+	HIPCHK(hipMemsetAsync(cnt, 0, 16, st));
+	GParams g;
+	g.precs = precs; g.len = len; g.vals = h->dix.vals; g.n = n; g.nps = nps; g.gap = h->dix.gap;
+	g.total_subreads = p->total_subreads; g.cap = LANE_CAP1;
+	g.cand = (uint32_t *)(b + o_c1); g.cpk = (uint16_t *)(b + o_p1); g.ccnt = (uint16_t *)(b + o_n1);
+	g.cs = n; g.idx = NULL; g.idx_count = NULL;
+	int rc = gather_launch(h, g, st);
+	if (rc) return rc;
+	LParams lp;
+	lp.cand = g.cand; lp.cpk = g.cpk; lp.ccnt = g.ccnt; lp.len = len; lp.n = n; lp.cap = LANE_CAP1;
+	lp.gap = h->dix.gap; lp.total_subreads = p->total_subreads;
+	lp.tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
+	lp.low = h->dix.start_base_offset;
+	lp.high = h->dix.start_base_offset + h->dix.length;
+	lp.multi_best = p->multi_best; lp.max_vote_simples = p->max_vote_simples; lp.cutoff = p->max_vote_number_cutoff;
+	lp.min_votes_first = p->min_votes_first; lp.min_votes_second = p->min_votes_second;
+	lp.out = out;
+	lp.defer_list = (uint32_t *)(b + o_l1);
+	lp.defer_count = cnt;
+	lp.defer_all = e && e[0] == '2';
+	lp.stats = stats;
+	lp.stat_base = 16;
+	lp.final_pass = !two;
+	lp.cs = n; lp.idx = NULL; lp.idx_count = NULL;
+	if ((rc = lane_launch<LANE_K1>(h, lp, &h->d_lscratch, &h->lscratch_words, st))) return rc;
+	*defer_list = lp.defer_list;
+	*defer_count = cnt;
+	if (!two) return 0;
+	// heavy pass over pass 1's deferral list
+	g.cap = LANE_CAP2;
+	g.cand = (uint32_t *)(b + o_c2); g.cpk = (uint16_t *)(b + o_p2); g.ccnt = (uint16_t *)(b + o_n2);
+	g.cs = n2; g.idx = lp.defer_list; g.idx_count = cnt;
+	if ((rc = gather_launch(h, g, st))) return rc;
+	lp.cand = g.cand; lp.cpk = g.cpk; lp.ccnt = g.ccnt; lp.cap = LANE_CAP2;
+	lp.cs = n2; lp.idx = g.idx; lp.idx_count = cnt;
+	lp.defer_list = (uint32_t *)(b + o_l2);
+	lp.defer_count = cnt + 1;
+	lp.stat_base = 21;
+	lp.final_pass = 1;
+	if ((rc = lane_launch<LANE_K2>(h, lp, &h->d_lscratch2, &h->lscratch2_words, st))) return rc;
+	*defer_list = lp.defer_list;
+	*defer_count = cnt + 1;
+	return 0;
+}

@@ -64,6 +64,10 @@ struct KParams {
 	uint32_t low, high;
 	const uint2 *precs;       // probe records of this chunk (probe_kernel)
 	int nps;                  // probe slots per (end, strand) in precs
+	uint32_t prec_stride;     // 0: records of read r at precs[r*per + i]; else SoA precs[i*stride + r]
+	const uint32_t *idx;      // NULL: reads 0..n_reads-1; else the reads idx[0..*idx_count) (deferred by lane_kernel)
+	const uint32_t *idx_count;
+	uint32_t *work;           // indirect mode: zeroed work counter (waves grab deferred reads dynamically)
 };
 
 // probe kernel parameters: one thread per (read, end, strand, subread x gap slot)
@@ -76,7 +80,9 @@ struct PParams {
 	int nps;
 	int total_subreads, reverse_r1, reverse_r2;
 	uint64_t nb_magic;        // ceil(2^64 / nb): key / nb == umulhi64(key, nb_magic) for 32-bit keys
-	uint2 *out;               // [read][end][strand][nps]: x = midpoint item, y = fwd | bwd << 16
+	uint2 *out;               // [read][end][strand][nps] (soa = 0) or [end][strand][nps][read] (soa = 1):
+	                          // x = midpoint item, y = fwd | bwd << 16
+	int soa;
 	unsigned long long *stats;
 };
 
@@ -1108,26 +1114,30 @@ struct Wave {
 		t_r = r;
 		if constexpr (PRE_RECS) {
 			const int per = ENDS * 2 * kp->nps;
-			const uint2 *src = kp->precs + r * (uint64_t)per;
 #pragma unroll
 			for (int k = 0; k < RPL; k++) {
 				int i = lane_id() + 64 * k;
-				trec[k] = i < per ? src[i] : make_uint2(0, 0);
+				trec[k] = i < per ? rec_at(r, i) : make_uint2(0, 0);
 			}
 		}
+	}
+
+	__device__ __forceinline__ uint2 rec_at(uint64_t r, int i) const
+	{
+		const uint32_t sd = kp->prec_stride;
+		return sd ? kp->precs[(uint64_t)i * sd + r] : kp->precs[r * (uint64_t)(ENDS * 2 * kp->nps) + i];
 	}
 
 	__device__ void stage_probes()
 	{
 		const int nps = kp->nps, per = ENDS * 2 * nps;
-		const uint2 *src = kp->precs + t_r * (uint64_t)per;
 #pragma unroll
 		for (int k = 0; k < (PRE_RECS ? RPL : (ENDS * 2 * MAXP + 63) / 64); k++) {
 			int i = lane_id() + 64 * k;
 			if (i < per) {
 				uint2 rec;
 				if constexpr (PRE_RECS) rec = trec[k < RPL ? k : 0];
-				else rec = src[i];
+				else rec = rec_at(t_r, i);
 				int e = i / (2 * nps), rem = i - e * 2 * nps, st = rem >= nps ? 1 : 0, q = rem - st * nps;
 				L->pmid[e][st][q] = rec.x;
 				L->pfwd[e][st][q] = (uint16_t)(rec.y & 0xffff);
@@ -1275,9 +1285,23 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	W.t_last = __builtin_amdgcn_s_memtime();
 #endif
 	W.st_probes = W.st_items = W.st_hits = W.st_results = 0;
-	if (gw < kp.n_reads) { W.prefetch_text(gw); W.prefetch_recs(gw); }
-	for (uint64_t r = gw; r < kp.n_reads; r += nw) {
-		W.run_read(r, r + nw);
+	// direct: reads gw, gw+nw, ...; indirect: the deferred reads idx[gw], idx[gw+nw], ...
+	// deferred reads differ widely in cost (repeat families): taken from a work counter
+	const uint64_t n = kp.idx ? (uint64_t)*kp.idx_count : kp.n_reads;
+	auto grab = [&]() -> uint64_t {
+		if (!kp.idx) return 0;
+		uint32_t v = 0;
+		if (lane_id() == 0) v = atomicAdd(kp.work, 1u);
+		return (uint64_t)__shfl((int)v, 0);
+	};
+	uint64_t i = kp.idx ? grab() : gw;
+	if (i < n) { const uint64_t r0 = kp.idx ? kp.idx[i] : i; W.prefetch_text(r0); W.prefetch_recs(r0); }
+	while (i < n) {
+		const uint64_t in = kp.idx ? grab() : i + nw;
+		const uint64_t r = kp.idx ? kp.idx[i] : i;
+		const uint64_t rn = in < n ? (kp.idx ? kp.idx[in] : in) : kp.n_reads;
+		W.run_read(r, rn);
+		i = in;
 #ifdef SVG_STAMPS
 		{ unsigned long long _t = __builtin_amdgcn_s_memtime(); W.acc[5] += _t - W.t_last; W.t_last = _t; }
 #endif
@@ -1313,7 +1337,9 @@ __global__ void __launch_bounds__(256) probe_kernel(PParams pp)
 	const int gap = ix.gap;
 	unsigned long long st_p = 0, st_i = 0, st_h = 0;
 	for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
-		const uint32_t r = t / per_read, rem = t - r * per_read;
+		uint32_t r, rem;
+		if (pp.soa) { rem = t / pp.n_reads; r = t - rem * pp.n_reads; }
+		else { r = t / per_read; rem = t - r * per_read; }
 		const int e = ENDS == 2 ? (int)(rem / (2 * nps)) : 0;
 		const uint32_t rem2 = rem - (uint32_t)e * 2 * nps;
 		const int s = rem2 >= nps ? 1 : 0;
@@ -1431,8 +1457,8 @@ int svg_index_finish_device(svg_index *h)
 	hipDeviceProp_t prop;
 	HIPCHK(hipGetDeviceProperties(&prop, h->device));
 	h->n_cu = prop.multiProcessorCount;
-	if ((rc = dmalloc(h, (void **)&h->d_stats, 16 * sizeof(unsigned long long)))) return rc;
-	HIPCHK(hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
+	if ((rc = dmalloc(h, (void **)&h->d_stats, 32 * sizeof(unsigned long long)))) return rc;
+	HIPCHK(hipMemset(h->d_stats, 0, 32 * sizeof(unsigned long long)));
 	const char *se = getenv("SVG_STATS");
 	h->stats_on = se && se[0] == '1';
 	h->max_read_len = 256;
@@ -1492,7 +1518,9 @@ extern "C" void svg_index_close(svg_index *h)
 	hipSetDevice(h->device);
 	if (h->stream) hipStreamSynchronize(h->stream);
 	hipFree(h->d_prec);
-	for (int k = 0; k < 2; k++)
+	hipFree(h->d_lane);
+	hipFree(h->d_lscratch);
+	for (int k = 0; k < 4; k++)
 		for (int i = 0; i < 64; i++)
 			for (int j = 0; j < 2; j++)
 				if (h->tev[k][i][j]) hipEventDestroy(h->tev[k][i][j]);
@@ -1531,7 +1559,7 @@ static int timing_fold(svg_index *h, int k)
 	return 0;
 }
 
-// bracket one launch of kind k (0 probe, 1 vote): phase 0 before, 1 after
+// bracket one launch of kind k (0 probe, 1 vote, 2 gather, 3 lane): phase 0 before, 1 after
 static int timing_mark(svg_index *h, int k, int phase, hipStream_t st)
 {
 	if (!h->timing) return 0;
@@ -1546,25 +1574,41 @@ extern "C" int svg_set_timing(svg_index *h, int enable)
 	if (!h) { svg_set_error("svg_set_timing: NULL handle"); return SVG_E_ARG; }
 	HIPCHK(hipSetDevice(h->device));
 	if (enable && !h->timing) {
-		for (int k = 0; k < 2; k++)
+		for (int k = 0; k < 4; k++)
 			for (int i = 0; i < 64; i++)
 				for (int j = 0; j < 2; j++)
 					if (!h->tev[k][i][j]) HIPCHK(hipEventCreate(&h->tev[k][i][j]));
 	}
 	h->timing = enable ? 1 : 0;
-	for (int k = 0; k < 2; k++) { h->tn[k] = 0; h->tcount[k] = 0; h->tms[k] = 0.0; }
+	for (int k = 0; k < 4; k++) { h->tn[k] = 0; h->tcount[k] = 0; h->tms[k] = 0.0; }
 	return 0;
 }
+
+int svg_timing_mark(svg_index *h, int k, int phase, hipStream_t st) { return timing_mark(h, k, phase, st); }
 
 extern "C" int svg_get_timing(svg_index *h, double *probe_ms, double *vote_ms, int *probe_launches, int *vote_launches)
 {
 	if (!h) { svg_set_error("svg_get_timing: NULL handle"); return SVG_E_ARG; }
 	HIPCHK(hipSetDevice(h->device));
-	for (int k = 0; k < 2; k++) { int rc = timing_fold(h, k); if (rc) return rc; }
+	for (int k = 0; k < 4; k++) { int rc = timing_fold(h, k); if (rc) return rc; }
+	// vote = everything after the probe kernel (gather, lane and the wave kernel)
 	if (probe_ms) *probe_ms = h->tms[0];
-	if (vote_ms) *vote_ms = h->tms[1];
+	if (vote_ms) *vote_ms = h->tms[1] + h->tms[2] + h->tms[3];
 	if (probe_launches) *probe_launches = h->tcount[0];
 	if (vote_launches) *vote_launches = h->tcount[1];
+	return 0;
+}
+
+extern "C" int svg_get_kernel_timing(svg_index *h, double ms[4], int launches[4])
+{
+	if (!h || !ms || !launches) { svg_set_error("svg_get_kernel_timing: NULL argument"); return SVG_E_ARG; }
+	HIPCHK(hipSetDevice(h->device));
+	for (int k = 0; k < 4; k++) {
+		int rc = timing_fold(h, k);
+		if (rc) return rc;
+		ms[k] = h->tms[k];
+		launches[k] = h->tcount[k];
+	}
 	return 0;
 }
 
@@ -1575,11 +1619,13 @@ extern "C" int svg_set_stats(svg_index *h, int enable)
 	return 0;
 }
 
-// debug: raw device counters (16 words; 8..15 = per-phase wave cycles in SVG_STAMPS builds)
-extern "C" int svg_debug_counters(svg_index *h, unsigned long long *out16)
+// debug: raw device counters (32 words; 8..15 = per-phase wave cycles in SVG_STAMPS builds,
+// 16..20 = light lane pass: deferrals by reason (candidates > CAP or length, slots > K,
+// shift-indel), candidates voted, deferrals; 21..25 = the same for the heavy lane pass)
+extern "C" int svg_debug_counters(svg_index *h, unsigned long long *out32)
 {
-	if (!h || !out16) return SVG_E_ARG;
-	HIPCHK(hipMemcpy(out16, h->d_stats, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+	if (!h || !out32) return SVG_E_ARG;
+	HIPCHK(hipMemcpy(out32, h->d_stats, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
 	return 0;
 }
 
@@ -1713,7 +1759,7 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	kp.low = h->dix.start_base_offset;
 	kp.high = h->dix.start_base_offset + h->dix.length;
 	if (h->stats_on) {
-		HIPCHK(hipMemsetAsync(h->d_stats, 0, 16 * sizeof(unsigned long long), st));
+		HIPCHK(hipMemsetAsync(h->d_stats, 0, 32 * sizeof(unsigned long long), st));
 		kp.stats = h->d_stats;
 	}
 	// probes per strand are bounded by the read lengths the caller announced
@@ -1739,6 +1785,9 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 		pp.nb_magic = ~0ull / h->dix.nb + 1;   // ceil(2^64 / nb), nb is not a power of two
 		pp.out = (uint2 *)h->d_prec;
 		pp.stats = kp.stats;
+		// single-end align: lane-per-read fast path (svg_lane.hip), probe records in SoA layout
+		const bool lane = svg_lane_eligible(h, p, r2 != NULL, sj) != 0;
+		pp.soa = lane ? 1 : 0;
 		const uint64_t n = kp.n_reads;
 		for (uint64_t c0 = 0; c0 < n && !rc; c0 += chunk) {
 			const uint64_t cn = n - c0 < chunk ? n - c0 : chunk;
@@ -1761,6 +1810,17 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 			if (kp.bm_out) kc.bm_out = kp.bm_out + c0 * ends * SVG_BIG_MARGIN_WORDS;
 			kc.precs = (const uint2 *)h->d_prec;
 			kc.nps = nps;
+			if (lane) {
+				// gather + lane kernels vote every read they can; the rest (deferral list) go to
+				// vote_kernel below, which reads the SoA probe records of the deferred reads
+				uint32_t *dl = NULL, *dc = NULL;
+				rc = svg_lane_chunk(h, p, kc.len1, (uint32_t)cn, kc.precs, nps, kc.out, kp.stats, &dl, &dc, st);
+				if (rc) return rc;
+				kc.prec_stride = (uint32_t)cn;
+				kc.idx = dl;
+				kc.idx_count = dc;
+				kc.work = dc + 2;
+			}
 			if ((rc = timing_mark(h, 1, 0, st))) return rc;
 			rc = launch_vote(h, kc, st, npmax, sj, ends);
 			if (!rc) rc = timing_mark(h, 1, 1, st);
@@ -1768,13 +1828,14 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	}
 	if (rc) return rc;
 	if (h->stats_on) {
-		unsigned long long s[4];
+		unsigned long long s[5];
 		HIPCHK(hipMemcpyAsync(s, h->d_stats, sizeof s, hipMemcpyDeviceToHost, st));
 		HIPCHK(hipStreamSynchronize(st));
 		h->last_stats.probes = s[0];
 		h->last_stats.bucket_items = s[1];
 		h->last_stats.hits = s[2];
 		h->last_stats.results = s[3];
+		h->last_stats.deferred = s[4];
 	}
 	return 0;
 }

@@ -1,0 +1,102 @@
+"""GPU parity of the single-end lane-per-read path (svg_lane.hip) and of its hand-off
+to the wave-per-read kernel: every SE align case is voted four ways -- lane path with
+deferral (default), wave kernel only (SVG_LANE=0), every read deferred through the
+indirect wave-kernel launch (SVG_LANE=2), and lane path plus the 64-slot heavy pass
+(SVG_LANE=3) -- and each must be byte-identical to the reference's records / the oracle."""
+import numpy as np
+import pytest
+
+from tests.common import Case, golden_names, ensure_built, pack_records, describe_mismatch
+
+ensure_built()
+pytestmark = pytest.mark.gpu
+
+MODES = ["1", "0", "2", "3"]   # lane (default), wave kernel only, defer every read, lane + heavy pass
+SE_ALIGN = [n for n in golden_names() if n.startswith("se_")]
+
+
+@pytest.fixture(scope="module")
+def gpu_indexes(index_cache):
+    import subread_amd as sa
+    cache = {}
+
+    def get(key):
+        if key not in cache:
+            cache[key] = sa.VoteIndex(index_cache.get(key), device=0)
+        return cache[key]
+    yield get
+    for v in cache.values():
+        v.close()
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("name", SE_ALIGN)
+def test_lane_modes_match_reference_golden(name, mode, gpu_indexes, monkeypatch):
+    monkeypatch.setenv("SVG_LANE", mode)
+    c = Case(name)
+    ix = gpu_indexes(c.index_key)
+    out, jout, bm = ix.vote(c.params, c.r1, c.r2)
+    got = pack_records(out, jout, bm)
+    assert (got == c.expected).all(), describe_mismatch(got, c.expected, c.ends, c.params.multi_best)
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("key,n,sub,indel", [("chr901_full", 150000, 0.02, 0.02), ("chr901_gapped", 60000, 0.03, 0.05),
+                                             ("synth4242_full", 60000, 0.01, 0.01)])
+def test_lane_modes_match_oracle(key, n, sub, indel, mode, gpu_indexes, index_cache, monkeypatch):
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.abi import default_params, PROGRAM_ALIGN
+    from subread_amd.sim import Genome, simulate_reads
+    monkeypatch.setenv("SVG_LANE", mode)
+    pre = index_cache.get(key)
+    g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
+    r1 = simulate_reads(g, n, 100, seed=321, sub=sub, indel=indel, nrate=0.002)
+    p = default_params(PROGRAM_ALIGN, False)
+    ix = gpu_indexes(key)
+    ix.set_stats(True)
+    out, _, _ = ix.vote(p, r1)
+    st = ix.stats()
+    dc = ix.debug_counters()
+    st["why"] = {"pass1": dc[16:21], "pass2": dc[21:26]}
+    ix.set_stats(False)
+    ref, _, _, _ = OracleIndex(pre).vote(p, r1, threads=16)
+    got, want = pack_records(out, None, None), pack_records(ref, None, None)
+    assert (got == want).all(), describe_mismatch(got, want, 1, 3)
+    if mode == "2":
+        assert st["deferred"] == n
+    elif mode in "13" and key.startswith("chr901"):
+        assert st["deferred"] < n // 4, str(st["why"])    # most reads stay on the lane path (synth4242 is repeat-heavy)
+    assert st["results"] == int((out["selected_votes"] > 0).sum())
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("lengths", [(0, 1, 15, 16, 17, 18, 19, 40, 150, 159, 160),
+                                     (16, 18, 100, 159, 160, 161, 170)])
+def test_lane_edge_lengths(mode, lengths, gpu_indexes, index_cache, monkeypatch):
+    """Reads shorter than 15+gap, at the 160 bp limit of the lane path and (second
+    batch, which makes the whole batch ineligible) above it, on both index kinds;
+    reads with N bases and lowercase letters included."""
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.abi import ReadBatch, default_params, PROGRAM_ALIGN
+    from subread_amd.sim import Genome
+    monkeypatch.setenv("SVG_LANE", mode)
+    rng = np.random.default_rng(5)
+    g = Genome.read_fasta(index_cache.genome_fasta("chr901"))
+    seqs = []
+    for i in range(4000):
+        L = int(rng.choice(lengths))
+        s = int(rng.integers(0, len(g.flat) - 200))
+        t = bytearray(g.flat[s:s + L].tobytes())
+        if L and i % 7 == 0:
+            t[int(rng.integers(0, L))] = ord("N")
+        if L and i % 11 == 0:
+            t[int(rng.integers(0, L))] = ord("a")
+        seqs.append(bytes(t))
+    rb = ReadBatch.from_list(seqs)
+    p = default_params(PROGRAM_ALIGN, False)
+    for key in ("chr901_full", "chr901_gapped"):
+        pre = index_cache.get(key)
+        out, _, _ = gpu_indexes(key).vote(p, rb)
+        ref, _, _, _ = OracleIndex(pre).vote(p, rb, threads=8)
+        got, want = pack_records(out, None, None), pack_records(ref, None, None)
+        assert (got == want).all(), describe_mismatch(got, want, 1, 3)

@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Diagnostic: share of single-end reads that leave the lane-per-read path, by reason
+(candidates > CAP or read length, vote-table slots > K, shift-indel second round).
+Usage: lane_defer.py [c3|chr901] [n_reads]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import subread_amd as sa  # noqa: E402
+from subread_amd.abi import default_params  # noqa: E402
+from subread_amd.sim import random_genome, simulate_reads, c3_lengths  # noqa: E402
+
+
+def main():
+    wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 2_000_000
+    if wl == "c3":
+        g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))
+    else:
+        g = random_genome([1_000_000], 901)
+    ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True)
+    r = simulate_reads(g, n, 100, seed=20261015, sub=0.01, indel=0.001)
+    ix.set_max_read_length(100)
+    ix.set_stats(True)
+    ix.vote(default_params(), r)
+    st, dc = ix.stats(), ix.debug_counters()
+    print("%s: %d reads, %.2f hits/read, to the wave kernel %d (%.2f%%)" % (
+        wl, n, st["hits"] / n, st["deferred"], 100.0 * st["deferred"] / n))
+    for name, b in (("light", 16), ("heavy", 21)):
+        print("  %s pass: deferred %d (cap/length %d, slots %d, shift-indel %d), candidates voted %d" % (
+            name, dc[b + 4], dc[b], dc[b + 1], dc[b + 2], dc[b + 3]))
+    ix.close()
+
+
+if __name__ == "__main__":
+    main()

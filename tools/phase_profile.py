@@ -42,7 +42,7 @@ def main():
     t = time.time()
     ix.vote(p, r1, r2)
     dt = time.time() - t
-    c = (ctypes.c_ulonglong * 16)()
+    c = (ctypes.c_ulonglong * 32)()
     sa.lib().svg_debug_counters(ix.h, c)
     names = ["text+init", "probe", "gather", "vote", "topk", "output", "junction", "bigmargin"]
     tot = sum(c[8 + k] for k in range(8))
