@@ -115,6 +115,7 @@ struct WaveLDS {
 	uint16_t simp_slot[ENDS][MAXS];       // slot index, or 0x8000|stored index
 	uint16_t simp_votes[ENDS][MAXS];
 	uint16_t bm[SJ ? ENDS : 1][10];
+	uint8_t rnew[32];                     // batch mode: new row occupancy (0xff = unchanged)
 	uint8_t gwin[SJ ? 2 : 1][SJ ? 64 : 4];   // subjunc donor windows of the .array
 	char text[SJ ? ENDS : 1][2][SJ ? MAXL : 4];   // strand 0 / strand 1 (reverse_read) form, donor scoring only
 };
@@ -378,6 +379,72 @@ struct Wave {
 		}
 	}
 
+	// ---------------------------------------------------------------- batch mode (SE, round 0)
+	// Lane c holds candidate c of a chunk of m <= 64, in the reference's order.  A candidate
+	// whose outcome cannot depend on the other candidates of the chunk -- no slot of the
+	// table within the tolerance in its three rows (so it finds nothing), no other chunk
+	// candidate within 2*tol (so no slot opened in the chunk can match it, nor its slot
+	// theirs), and no earlier dependent candidate opening slots in its row (so its slot
+	// index is its rank in candidate order) -- only opens a slot in row kv/5 %30
+	// (sorted-hashtable.c:1071-1106); those slots are opened together.  Returns the lanes
+	// left for the serial replay (vote_one, in order).  Exact: every table mutation of the
+	// serial order happens, in an order no candidate can observe.
+	template <int E>
+	__device__ unsigned long long batch_create(int kvv, int kov, int m, uint32_t high_b)
+	{
+		const int lane = lane_id();
+		const bool act = lane < m;
+		const uint32_t kv = (uint32_t)kvv, pk = (uint32_t)kov;
+		const int tol = kp->tol, kP1 = (int)(pk & 63u), off = (int)((pk >> 6) & 2047u);
+		const uint32_t r0 = (pk >> 17) & 31u, rp = (pk >> 22) & 31u, rm = pk >> 27;
+		// row occupancy of the candidate's three rows (every lane active for the shuffles)
+		const int n0 = __shfl(items_v, E * 32 + (int)r0), np_ = __shfl(items_v, E * 32 + (int)rp),
+		          nm = __shfl(items_v, E * 32 + (int)rm);
+		bool dep = false;
+		if (act) {
+			const int tot = n0 + np_ + nm;
+			for (int q = 0; q < tot && !dep; q++) {
+				const uint32_t row = q < n0 ? r0 : (q < n0 + np_ ? rp : rm);
+				const int idx = q < n0 ? q : (q < n0 + np_ ? q - n0 : q - n0 - np_);
+				const int d = (int)(kv - L->pm[row * SPACE + idx].x);
+				dep = d >= -tol && d <= tol;
+			}
+		}
+		unsigned long long same = 0;
+		for (int j = 0; j < m; j++) {
+			const uint32_t kj = (uint32_t)rd(kvv, j), rj = ((uint32_t)rd(kov, j) >> 17) & 31u;
+			const int dd = (int)(kv - kj);
+			if (j != lane && dd >= -2 * tol && dd <= 2 * tol) dep = true;
+			if (rj == r0) same |= 1ull << j;
+		}
+		dep = dep && act;
+		const unsigned long long bd = ballot(dep);
+		const unsigned long long le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1ull);
+		dep = act && (same & bd & le) != 0ull;
+		const bool inr = act && !dep && kv >= kp->low && kv <= high_b;
+		const unsigned long long cm = ballot(inr);
+		const int rank = __popcll(same & cm & (le >> 1));
+		const bool mk = inr && n0 + rank < SPACE;
+		if (lane < 32) L->rnew[lane] = 0xff;
+		wsync();
+		if (mk) {
+			const int slot = (int)r0 * SPACE + n0 + rank;
+			uint32_t *cs = cold_slot(cold[E], slot);
+			L->pm[slot] = make_uint2(kv, m_pack(1, kP1, 0, 0, 0));
+			*(uint2 *)cs = make_uint2((uint32_t)(uint16_t)off | ((uint32_t)(uint16_t)(off + 16) << 16),
+			                          (uint32_t)(uint8_t)kP1 | ((uint32_t)(uint8_t)kP1 << 8));   // rec[0..3] = k+1, k+1, 0, 0
+		}
+		if (inr && (same & cm & ~le) == 0ull) L->rnew[r0] = (uint8_t)(n0 + rank + 1 < SPACE ? n0 + rank + 1 : SPACE);
+		wsync();
+		if ((lane >> 5) == E && (lane & 31) < ROWS) {
+			const int v = L->rnew[lane & 31];
+			if (v != 0xff) items_v = v;
+		}
+		if (ballot(mk) && max_vote[E] == 0) max_vote[E] = 1;
+		wsync();
+		return ballot(dep);
+	}
+
 	// ---------------------------------------------------------------- phases G+V for one (strand, end, round)
 	template <int E>
 	__device__ void replay(int s, int round)
@@ -421,7 +488,13 @@ struct Wave {
 				int kvv = (int)L->cand[cb + (lane & (CAND_CAP - 1))];
 				int kov = (int)L->cand_ko[cb + (lane & (CAND_CAP - 1))];
 				int m = cn - cb < 64 ? (int)(cn - cb) : 64;
-				for (int j = 0; j < m; j++) {
+				unsigned long long serial = m == 64 ? ~0ull : ((1ull << m) - 1ull);
+				if constexpr (ENDS == 1 && !SJ) {
+					if (round == 0 && kp->ii_end == 5 && m >= 8) serial = batch_create<E>(kvv, kov, m, high_b);
+				}
+				while (serial) {
+					const int j = __ffsll((long long)serial) - 1;
+					serial &= serial - 1ull;
 					uint32_t kv = (uint32_t)rd(kvv, j);
 					uint32_t pk = (uint32_t)rd(kov, j);
 					vote_one<E>(kv, pk, round, high_b);
