@@ -83,6 +83,8 @@ struct PParams {
 	uint2 *out;               // [read][end][strand][nps] (soa = 0) or [end][strand][nps][read] (soa = 1):
 	                          // x = midpoint item, y = fwd | bwd << 16
 	int soa;
+	int window;               // one-shot bucket loads (keys of a bucket sorted as int16: nb >= 131073)
+	int readmajor;            // soa output with read-major threads (consecutive threads = one read's probes)
 	unsigned long long *stats;
 };
 
@@ -105,8 +107,6 @@ struct WaveLDS {
 	uint16_t pfwd[ENDS][2][MAXP];         // equal-key items at mid..last
 	uint16_t pbwd[ENDS][2][MAXP];         // equal-key items at first..mid-1
 	uint32_t pcum[MAXP + 1];              // candidate prefix of the (strand,end) being replayed
-	uint32_t cand[CAND_CAP];              // kv of queued candidates
-	uint32_t cand_ko[CAND_CAP];           // subread_no | offset << 8
 	uint32_t res[ENDS][3][17];            // the read's stored mapping_result_t (68 B)
 	uint32_t tmp[ENDS][3][17];            // top-K output under construction
 	uint32_t jres[SJ ? ENDS : 1][3][4];   // subjunc_result_t (subjunc variants only)
@@ -220,7 +220,7 @@ struct Wave {
 	uint32_t *shift_locs[2];
 	const KParams *kp;
 	ReadCtx rc;
-	unsigned long long st_probes, st_items, st_hits, st_results;
+	unsigned long long st_probes, st_items, st_hits, st_results, st_batch, st_serial;
 	int items_v;            // lane 32*e + r: items[r] of table e (gene_vote_t.items)
 	int max_vote[2];        // gene_vote_t.max_vote per table (wave-uniform)
 	int nshift[2];          // shift_indel_NO per table (wave-uniform)
@@ -465,33 +465,38 @@ struct Wave {
 		if (lane == 0) L->pcum[0] = 0;
 		wsync();
 		STAMP(2);
+		// gather in visiting order (probe p, then mid..last, then mid-1..first), lane c = candidate
+		// c0 + c of the chunk; the next chunk's hit values are loaded while this one is voted
+		auto locate_cand = [&](uint32_t cc, uint32_t &item, int &off, int &kP1) __attribute__((always_inline)) {
+			int lo = 0, hi = np - 1;   // probe p with pcum[p] <= cc < pcum[p+1]
+			while (lo < hi) { int m = (lo + hi + 1) >> 1; if (L->pcum[m] <= cc) lo = m; else hi = m - 1; }
+			const int p = lo;
+			const uint32_t j = cc - L->pcum[p];
+			const uint32_t fwd = L->pfwd[E][s][p];
+			const uint32_t mid = L->pmid[E][s][p];
+			item = j < fwd ? mid + j : mid - 1 - (j - fwd);
+			off = probe_off(E, p);
+			kP1 = p / gap + 1;
+		};
+		uint32_t nitem = 0, nval = 0;
+		int noff = 0, nkp1 = 0;
+		if ((uint32_t)lane < total) { locate_cand((uint32_t)lane, nitem, noff, nkp1); nval = kp->ix.vals[nitem]; }
 		for (uint32_t c0 = 0; c0 < total; c0 += CAND_CAP) {
-			uint32_t cn = total - c0 < CAND_CAP ? total - c0 : CAND_CAP;
-			// gather in visiting order: probe p, then mid..last, then mid-1..first
-			for (uint32_t c = lane; c < cn; c += 64) {
-				uint32_t cc = c0 + c;
-				int lo = 0, hi = np - 1;   // probe p with pcum[p] <= cc < pcum[p+1]
-				while (lo < hi) { int m = (lo + hi + 1) >> 1; if (L->pcum[m] <= cc) lo = m; else hi = m - 1; }
-				int p = lo;
-				uint32_t j = cc - L->pcum[p];
-				uint32_t fwd = L->pfwd[E][s][p];
-				uint32_t mid = L->pmid[E][s][p];
-				uint32_t item = j < fwd ? mid + j : mid - 1 - (j - fwd);
-				int off = probe_off(E, p);
-				uint32_t kv = kp->ix.vals[item] - (uint32_t)off;
-				L->cand[c] = kv;
-				L->cand_ko[c] = cand_pack(kv, p / gap + 1, off);
+			const uint32_t cn = total - c0 < CAND_CAP ? total - c0 : CAND_CAP;
+			const uint32_t kv = nval - (uint32_t)noff;
+			const int kvv = (int)kv, kov = (int)cand_pack(kv, nkp1, noff);
+			if (c0 + CAND_CAP + (uint32_t)lane < total) {
+				locate_cand(c0 + CAND_CAP + (uint32_t)lane, nitem, noff, nkp1);
+				nval = kp->ix.vals[nitem];
 			}
-			wsync();
 			STAMP(2);
-			for (uint32_t cb = 0; cb < cn; cb += 64) {
-				int kvv = (int)L->cand[cb + (lane & (CAND_CAP - 1))];
-				int kov = (int)L->cand_ko[cb + (lane & (CAND_CAP - 1))];
-				int m = cn - cb < 64 ? (int)(cn - cb) : 64;
+			{
+				const int m = (int)cn;
 				unsigned long long serial = m == 64 ? ~0ull : ((1ull << m) - 1ull);
 				if constexpr (ENDS == 1 && !SJ) {
 					if (round == 0 && kp->ii_end == 5 && m >= 8) serial = batch_create<E>(kvv, kov, m, high_b);
 				}
+				if (kp->stats) { st_batch += (unsigned long long)(m - __popcll(serial)); st_serial += (unsigned long long)__popcll(serial); }
 				while (serial) {
 					const int j = __ffsll((long long)serial) - 1;
 					serial &= serial - 1ull;
@@ -1357,24 +1362,31 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	for (int k = 0; k < 8; k++) W.acc[k] = 0;
 	W.t_last = __builtin_amdgcn_s_memtime();
 #endif
-	W.st_probes = W.st_items = W.st_hits = W.st_results = 0;
+	W.st_probes = W.st_items = W.st_hits = W.st_results = W.st_batch = W.st_serial = 0;
 	// direct: reads gw, gw+nw, ...; indirect: the deferred reads idx[gw], idx[gw+nw], ...
 	// deferred reads differ widely in cost (repeat families): taken from a work counter
 	const uint64_t n = kp.idx ? (uint64_t)*kp.idx_count : kp.n_reads;
-	auto grab = [&]() -> uint64_t {
-		if (!kp.idx) return 0;
-		uint32_t v = 0;
-		if (lane_id() == 0) v = atomicAdd(kp.work, 1u);
-		return (uint64_t)__shfl((int)v, 0);
-	};
-	uint64_t i = kp.idx ? grab() : gw;
-	if (i < n) { const uint64_t r0 = kp.idx ? kp.idx[i] : i; W.prefetch_text(r0); W.prefetch_recs(r0); }
+	// (the next index is grabbed one read ahead, so the atomic's latency hides behind a read)
+	uint64_t i, in;
+	if (kp.idx) {
+		uint32_t a = 0;
+		if (lane_id() == 0) a = atomicAdd(kp.work, 2u);
+		i = (uint64_t)(uint32_t)__shfl((int)a, 0);
+		in = i + 1;
+	} else {
+		i = gw;
+		in = gw + nw;
+	}
+	uint64_t r = i < n ? (kp.idx ? kp.idx[i] : i) : 0;
+	if (i < n) { W.prefetch_text(r); W.prefetch_recs(r); }
 	while (i < n) {
-		const uint64_t in = kp.idx ? grab() : i + nw;
-		const uint64_t r = kp.idx ? kp.idx[i] : i;
+		uint32_t nxt = 0;
+		if (kp.idx && lane_id() == 0) nxt = atomicAdd(kp.work, 1u);   // consumed after this read
 		const uint64_t rn = in < n ? (kp.idx ? kp.idx[in] : in) : kp.n_reads;
 		W.run_read(r, rn);
 		i = in;
+		r = rn;
+		in = kp.idx ? (uint64_t)(uint32_t)__shfl((int)nxt, 0) : in + nw;
 #ifdef SVG_STAMPS
 		{ unsigned long long _t = __builtin_amdgcn_s_memtime(); W.acc[5] += _t - W.t_last; W.t_last = _t; }
 #endif
@@ -1388,6 +1400,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 		for (int o = 32; o; o >>= 1) { a += __shfl_xor(a, o); h += __shfl_xor(h, o); }
 		if (lane_id() == 0) {
 			atomicAdd(&kp.stats[3], W.st_results);
+			atomicAdd(&kp.stats[26], W.st_batch);    // diagnostics: candidates settled by batch mode
+			atomicAdd(&kp.stats[27], W.st_serial);   //              candidates replayed serially
 			atomicAdd(&kp.stats[0], W.st_probes);
 			atomicAdd(&kp.stats[1], a);
 			atomicAdd(&kp.stats[2], h);
@@ -1411,7 +1425,7 @@ __global__ void __launch_bounds__(256) probe_kernel(PParams pp)
 	unsigned long long st_p = 0, st_i = 0, st_h = 0;
 	for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
 		uint32_t r, rem;
-		if (pp.soa) { rem = t / pp.n_reads; r = t - rem * pp.n_reads; }
+		if (pp.soa && !pp.readmajor) { rem = t / pp.n_reads; r = t - rem * pp.n_reads; }
 		else { r = t / per_read; rem = t - r * per_read; }
 		const int e = ENDS == 2 ? (int)(rem / (2 * nps)) : 0;
 		const uint32_t rem2 = rem - (uint32_t)e * 2 * nps;
@@ -1461,30 +1475,78 @@ __global__ void __launch_bounds__(256) probe_kernel(PParams pp)
 				st_i += (unsigned)n;
 				if (n > 0) {
 					const int16_t *K = ix.keys + first;
-					int lo = 0, hi = n - 1, m;
-					bool hit = false;
-					for (;;) {
-						m = (lo + hi) >> 1;
-						int16_t kk = K[m];
-						if (kk > k16) hi = m - 1;
-						else if (kk < k16) lo = m + 1;
-						else { hit = true; break; }
-						if (hi < lo) break;
+					int m = 0, fwd = 0, bwd = 0;
+					bool hit = false, done = false;
+					if (pp.window && n <= 56) {
+						// the whole bucket in one round trip: <= 8 independent 16-byte loads of the
+						// aligned window holding its keys, equal keys found by a zero-halfword test
+						const uintptr_t base = (uintptr_t)K;
+						const uint4 *w = (const uint4 *)(base & ~(uintptr_t)15);
+						const int sh = (int)((base & 15) >> 1);   // halfword of item 0 in the window
+						const int nq = (sh + n + 7) >> 3;         // 16-byte words holding the bucket
+						uint32_t d[32];
+#pragma unroll
+						for (int k = 0; k < 8; k++) {
+							const uint4 v = k < nq ? w[k] : make_uint4(0u, 0u, 0u, 0u);
+							d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
+						}
+						const uint32_t kk = (uint32_t)(uint16_t)k16 * 0x00010001u;
+						uint64_t eq = 0;
+#pragma unroll
+						for (int j = 0; j < 32; j++) {
+							const uint32_t x = d[j] ^ kk;
+							const uint32_t z = ~(((x & 0x7fff7fffu) + 0x7fff7fffu) | x | 0x7fff7fffu);
+							eq |= ((uint64_t)((z >> 15) & 1u) << (2 * j)) | ((uint64_t)(z >> 31) << (2 * j + 1));
+						}
+						eq = (eq >> sh) & ((1ull << n) - 1ull);
+						const int fe = eq ? __builtin_ctzll(eq) : 0, ne = __popcll(eq);
+						// the equal run must be contiguous (sorted bucket); otherwise the loop below
+						if (!eq || eq == (((ne == 64 ? 0ull : (1ull << ne)) - 1ull) << fe)) {
+							done = true;
+							if (eq) {
+								// gehash_go_X's binary search (sorted-hashtable.c:947-981) on the
+								// positions alone: it stops at the first midpoint inside the run
+								const int le = fe + ne - 1;
+								int lo = 0, hi = n - 1;
+								for (;;) {
+									m = (lo + hi) >> 1;
+									if (m < fe) lo = m + 1;
+									else if (m > le) hi = m - 1;
+									else break;
+								}
+								hit = true;
+								fwd = le - m + 1;
+								bwd = m - fe;
+							}
+						}
+					}
+					if (!done) {
+						int lo = 0, hi = n - 1;
+						for (;;) {
+							m = (lo + hi) >> 1;
+							int16_t kk = K[m];
+							if (kk > k16) hi = m - 1;
+							else if (kk < k16) lo = m + 1;
+							else { hit = true; break; }
+							if (hi < lo) break;
+						}
+						if (hit) {
+							int qq = m + 1;
+							while (qq < n && K[qq] == k16) qq++;
+							fwd = qq - m;
+							qq = m - 1;
+							while (qq >= 0 && K[qq] == k16) qq--;
+							bwd = m - 1 - qq;
+						}
 					}
 					if (hit) {
-						int qq = m + 1;
-						while (qq < n && K[qq] == k16) qq++;
-						const int fwd = qq - m;
-						qq = m - 1;
-						while (qq >= 0 && K[qq] == k16) qq--;
-						const int bwd = m - 1 - qq;
 						rec = make_uint2(first + (uint32_t)m, (uint32_t)fwd | ((uint32_t)bwd << 16));
 						st_h += (unsigned)(fwd + bwd);
 					}
 				}
 			}
 		}
-		pp.out[t] = rec;
+		pp.out[pp.soa ? (size_t)rem * pp.n_reads + r : (size_t)t] = rec;
 	}
 	if (pp.stats) {
 		for (int o = 32; o; o >>= 1) {
@@ -1694,7 +1756,8 @@ extern "C" int svg_set_stats(svg_index *h, int enable)
 
 // debug: raw device counters (32 words; 8..15 = per-phase wave cycles in SVG_STAMPS builds,
 // 16..20 = light lane pass: deferrals by reason (candidates > CAP or length, slots > K,
-// shift-indel), candidates voted, deferrals; 21..25 = the same for the heavy lane pass)
+// shift-indel), candidates voted, deferrals; 21..25 = the same for the heavy lane pass;
+// 26 / 27 = wave-kernel candidates settled by batch mode / replayed serially)
 extern "C" int svg_debug_counters(svg_index *h, unsigned long long *out32)
 {
 	if (!h || !out32) return SVG_E_ARG;
@@ -1861,6 +1924,8 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 		// single-end align: lane-per-read fast path (svg_lane.hip), probe records in SoA layout
 		const bool lane = svg_lane_eligible(h, p, r2 != NULL, sj) != 0;
 		pp.soa = lane ? 1 : 0;
+		pp.window = h->dix.nb >= 131073u && !getenv("SVG_NO_WINDOW");   // key_hi <= 32767: int16 order == key order
+		{ const char *e = getenv("SVG_PROBE_MAP"); pp.readmajor = !(e && e[0] == '0'); }
 		const uint64_t n = kp.n_reads;
 		for (uint64_t c0 = 0; c0 < n && !rc; c0 += chunk) {
 			const uint64_t cn = n - c0 < chunk ? n - c0 : chunk;

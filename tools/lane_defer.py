@@ -27,6 +27,7 @@ def main():
     st, dc = ix.stats(), ix.debug_counters()
     print("%s: %d reads, %.2f hits/read, to the wave kernel %d (%.2f%%)" % (
         wl, n, st["hits"] / n, st["deferred"], 100.0 * st["deferred"] / n))
+    print("  wave kernel: %d candidates settled in batch mode, %d replayed serially" % (dc[26], dc[27]))
     for name, b in (("light", 16), ("heavy", 21)):
         print("  %s pass: deferred %d (cap/length %d, slots %d, shift-indel %d), candidates voted %d" % (
             name, dc[b + 4], dc[b], dc[b + 1], dc[b + 2], dc[b + 3]))

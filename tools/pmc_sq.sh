@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ instruction/stall counters of the vote kernel (three separate --pmc passes, no traces),
+# SQ instruction/stall counters per kernel (three separate --pmc passes, no traces),
 # bench.py on a reduced C3 read count.  Usage: tools/pmc_sq.sh OUTDIR [extra bench args]
 set -e
 out=$1; shift
@@ -16,12 +16,18 @@ python3 - "$out" <<'PY'
 import sqlite3, glob, sys, collections
 out = sys.argv[1]
 tot = collections.defaultdict(float)
+names = ("probe_kernel", "gather_kernel", "lane_kernel", "vote_kernel")
 for d in sorted(glob.glob(out + "/p*/")):
     for db in glob.glob(d + "*results.db"):
         c = sqlite3.connect(db)
         for k, n, v in c.execute("select kernel_name, counter_name, value from counters_collection"):
-            if "vote_kernel" in k:
-                tot[n] += float(v)
-for k in sorted(tot):
-    print("%-26s %.4e" % (k, tot[k]))
+            for kn in names:
+                if kn in k:
+                    tot[(kn, n)] += float(v)
+for kn in names:
+    rows = sorted((n, v) for (k, n), v in tot.items() if k == kn)
+    if rows:
+        print(kn)
+        for n, v in rows:
+            print("  %-26s %.4e" % (n, v))
 PY
