@@ -191,7 +191,8 @@ def main():
     # per-kernel algorithmic bytes of one step:
     #   probe_kernel  read text + bucket bounds (8 B) + bucket keys (2 B/item) + probe records out (8 B/probe)
     #   gather_kernel probe records in (8 B/probe) + hit values (4 B/hit) + candidates out (6 B/hit) + counts
-    #   lane_kernel   candidates in (6 B/hit of lane reads) + lengths + records out
+    #   lane_kernel   candidates in (6 B/hit of lane reads; fused: records 8 B/probe + hit values 4 B/hit)
+    #                 + lengths + records out
     #   vote_kernel   (deferred reads only when the lane path runs) records in + hit values + records out
     lane_on = kt["lane_kernel"][1] > 0
     nd = st.get("deferred", 0) if lane_on else n                 # reads voted by vote_kernel
@@ -200,7 +201,9 @@ def main():
     kbytes = {
         "probe_kernel": in_bytes + 8 * st["probes"] + 2 * st["bucket_items"] + 8 * st["probes"],
         "gather_kernel": 8 * st["probes"] + 10 * st["hits"] + 4 * n,
-        "lane_kernel": 6 * lane_hits + 6 * n + out_bytes * (n - nd) / float(n),
+        # fused gather (no gather_kernel launches): records in + hit values instead of candidate lists
+        "lane_kernel": ((6 * lane_hits) if kt["gather_kernel"][1] else (8 * st["probes"] * (n - nd) / float(n) + 4 * lane_hits))
+                       + 6 * n + out_bytes * (n - nd) / float(n),
         "vote_kernel": 8 * dp + 4 * dh + 2 * nd * ends + out_bytes * nd / float(n),
     }
     kernels = {}

@@ -118,6 +118,9 @@ struct LParams {
 	uint32_t cs;                  // column stride of cand/cpk/ccnt
 	const uint32_t *idx;          // NULL: lane column r = read r; else column k = read idx[k], k < *idx_count
 	const uint32_t *idx_count;    //   (columns >= cs have no candidate list and are deferred)
+	const uint2 *precs;           // fused gather (NPF > 0): probe records, SoA [strand * nps + p][n]
+	const uint32_t *vals;
+	int nps;
 	unsigned long long *stats;    // [3] += results; [4] += deferred reads (final pass only);
 	int stat_base, final_pass;    // diagnostics at stats[stat_base..+4]: deferrals by reason (3), candidates, deferrals
 };
@@ -279,7 +282,7 @@ struct Lane {
 	}
 };
 
-template <int K>
+template <int K, int NPF>
 __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 {
 	extern __shared__ __align__(16) uint8_t lds_raw[];
@@ -302,12 +305,16 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 		L.why = live && k >= lp.cs ? 1 : 0;
 		int len = live ? lp.len[r] : 0;
 		if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;
-		int applied = 0;
+		int applied = 0, step = 0;
 		if (!L.dfr && len >= 15 + lp.gap) {
 			const int cr = (len - 15 - lp.gap) << 16;
-			int step = cr / (lp.total_subreads - 1);
+			step = cr / (lp.total_subreads - 1);
 			if (step < (lp.gap << 16)) step = lp.gap << 16;
 			applied = 1 + cr / step;
+		}
+		if constexpr (NPF > 0) {
+			// fused gather: the lane path's limits (the gather kernel's, for the unfused path)
+			if (!L.dfr && (len < 15 + lp.gap || len > 160 || applied > 31 || applied * lp.gap > NPF)) { L.dfr = true; L.why = 1; }
 		}
 		const uint32_t high_b = lp.high - (uint32_t)len;
 		// the read's bigtable records: source (-1 none, else strand << 5 | slot), position, votes, used
@@ -316,6 +323,7 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 		int rv0 = 0, rv1 = 0, rv2 = 0, ru0 = 0, ru1 = 0, ru2 = 0;
 		int nc_read = 0;
 		for (int st = 0; st < 2; st++) {
+			if constexpr (NPF == 0) {
 			const int cnt = L.dfr ? 0 : (int)lp.ccnt[(size_t)st * lp.cs + k];
 			if (cnt == 0xffff) { L.dfr = true; L.why = 1; }
 			const int mycnt = L.dfr ? 0 : cnt;
@@ -335,6 +343,60 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				kv_a = kv_b; pk_a = pk_b;
 				if (j + 2 < mycnt) { kv_b = cb[(size_t)(j + 2) * lp.cs]; pk_b = pb[(size_t)(j + 2) * lp.cs]; }
 				if (j < mycnt && !L.dfr) L.vote(st, kv, (int)(pk & 63u), (int)(pk >> 6), high_b);
+			}
+			} else {
+			// ---- fused gather: the read's probe records of this strand in a register window
+			// (probe pb is rx[0]/ry[0]; advancing shifts the window), candidates generated in
+			// the reference's visiting order (subread_no, xk1, mid..last, mid-1..first) and their
+			// hit values prefetched four candidates ahead
+			const int np = applied * lp.gap;
+			uint32_t rx[NPF], ry[NPF];
+			int cnt = 0;
+#pragma unroll
+			for (int p = 0; p < NPF; p++) {
+				const bool ok = !L.dfr && p < np;
+				const uint2 v = ok ? lp.precs[(size_t)(st * lp.nps + p) * lp.n + r] : make_uint2(0u, 0u);
+				rx[p] = v.x;
+				ry[p] = v.y;
+				cnt += (int)((v.y & 0xffffu) + (v.y >> 16));
+			}
+			if (!L.dfr && cnt > lp.cap) { L.dfr = true; L.why = 1; }
+			const int mycnt = L.dfr ? 0 : cnt;
+			nc_read += mycnt;
+			L.reset();
+			int mc = mycnt;
+			for (int o = 32; o; o >>= 1) { int t = __shfl_xor(mc, o); mc = t > mc ? t : mc; }
+			int pb = 0;
+			uint32_t jb = 0;
+			auto next = [&](uint32_t &item, uint32_t &pk) __attribute__((always_inline)) {
+				while (jb >= (ry[0] & 0xffffu) + (ry[0] >> 16)) {
+#pragma unroll
+					for (int p = 0; p + 1 < NPF; p++) { rx[p] = rx[p + 1]; ry[p] = ry[p + 1]; }
+					rx[NPF - 1] = 0u;
+					ry[NPF - 1] = 0u;
+					pb++;
+					jb = 0;
+				}
+				const uint32_t fwd = ry[0] & 0xffffu;
+				item = jb < fwd ? rx[0] + jb : rx[0] - 1u - (jb - fwd);
+				jb++;
+				const int sk = lp.gap == 1 ? pb : pb / lp.gap, x = pb - sk * lp.gap;
+				int off = (int)(((int64_t)step * sk) >> 16);
+				if (lp.gap > 1) off -= off % lp.gap - x;
+				pk = (uint32_t)(sk + 1) | ((uint32_t)off << 6);
+			};
+			uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0, it = 0, pkn = 0;
+			if (0 < mycnt) { next(it, pkn); q0 = lp.vals[it]; k0 = pkn; }
+			if (1 < mycnt) { next(it, pkn); q1 = lp.vals[it]; k1 = pkn; }
+			if (2 < mycnt) { next(it, pkn); q2 = lp.vals[it]; k2 = pkn; }
+			if (3 < mycnt) { next(it, pkn); q3 = lp.vals[it]; k3 = pkn; }
+			for (int j = 0; j < mc; j++) {
+				const uint32_t val = q0, pk = k0;
+				q0 = q1; q1 = q2; q2 = q3;
+				k0 = k1; k1 = k2; k2 = k3;
+				if (j + 4 < mycnt) { next(it, pkn); q3 = lp.vals[it]; k3 = pkn; }
+				if (j < mycnt && !L.dfr) L.vote(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b);
+			}
 			}
 			if (L.dfr) continue;
 			// ---- SE gate (core.c:3215-3233) and top-K (core-junction.c:2199-2530, ends = 1)
@@ -496,11 +558,12 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 //                   reads still overflow), so the wave kernel takes pass 1's deferrals directly.
 // ---------------------------------------------------------------------------------------------
 #define LANE_K1 16
+#define LANE_NPF 10   // probe records per strand held in registers by the fused light pass
 #define LANE_CAP1 40
 #define LANE_K2 64
 #define LANE_CAP2 192
 
-template <int K>
+template <int K, int NPF>
 static int lane_launch(svg_index *h, LParams &lp, uint32_t **cold, size_t *cold_words, hipStream_t st)
 {
 	const size_t lds = (size_t)K * 64 * sizeof(uint2);
@@ -520,7 +583,7 @@ static int lane_launch(svg_index *h, LParams &lp, uint32_t **cold, size_t *cold_
 	lp.cold = *cold;
 	int rc = svg_timing_mark(h, 3, 0, st);
 	if (rc) return rc;
-	hipLaunchKernelGGL(lane_kernel<K>, dim3((unsigned)blocks), dim3(64), lds, st, lp);
+	hipLaunchKernelGGL((lane_kernel<K, NPF>), dim3((unsigned)blocks), dim3(64), lds, st, lp);
 	HIPCHK(hipGetLastError());
 	return svg_timing_mark(h, 3, 1, st);
 }
@@ -575,10 +638,14 @@ int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint3
 	g.total_subreads = p->total_subreads; g.cap = LANE_CAP1;
 	g.cand = (uint32_t *)(b + o_c1); g.cpk = (uint16_t *)(b + o_p1); g.ccnt = (uint16_t *)(b + o_n1);
 	g.cs = n; g.idx = NULL; g.idx_count = NULL;
-	int rc = gather_launch(h, g, st);
-	if (rc) return rc;
+	// reads of <= LANE_NPF probes per strand (the full index at the default -n): the gather is
+	// fused into the lane kernel; otherwise the gather kernel writes candidate lists first
+	const bool fused = nps <= LANE_NPF && !(e && e[0] == '1' && e[1] == 'g');   // "1g": unfused (testing)
+	int rc = 0;
+	if (!fused && (rc = gather_launch(h, g, st))) return rc;
 	LParams lp;
 	lp.cand = g.cand; lp.cpk = g.cpk; lp.ccnt = g.ccnt; lp.len = len; lp.n = n; lp.cap = LANE_CAP1;
+	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps;
 	lp.gap = h->dix.gap; lp.total_subreads = p->total_subreads;
 	lp.tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
 	lp.low = h->dix.start_base_offset;
@@ -593,7 +660,9 @@ int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint3
 	lp.stat_base = 16;
 	lp.final_pass = !two;
 	lp.cs = n; lp.idx = NULL; lp.idx_count = NULL;
-	if ((rc = lane_launch<LANE_K1>(h, lp, &h->d_lscratch, &h->lscratch_words, st))) return rc;
+	rc = fused ? lane_launch<LANE_K1, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st)
+	           : lane_launch<LANE_K1, 0>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
+	if (rc) return rc;
 	*defer_list = lp.defer_list;
 	*defer_count = cnt;
 	if (!two) return 0;
@@ -608,7 +677,7 @@ int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint3
 	lp.defer_count = cnt + 1;
 	lp.stat_base = 21;
 	lp.final_pass = 1;
-	if ((rc = lane_launch<LANE_K2>(h, lp, &h->d_lscratch2, &h->lscratch2_words, st))) return rc;
+	if ((rc = lane_launch<LANE_K2, 0>(h, lp, &h->d_lscratch2, &h->lscratch2_words, st))) return rc;
 	*defer_list = lp.defer_list;
 	*defer_count = cnt + 1;
 	return 0;

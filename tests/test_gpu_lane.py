@@ -11,7 +11,9 @@ from tests.common import Case, golden_names, ensure_built, pack_records, describ
 ensure_built()
 pytestmark = pytest.mark.gpu
 
-MODES = ["1", "0", "2", "3"]   # lane (default), wave kernel only, defer every read, lane + heavy pass
+# lane path (default: gather fused into the lane kernel), lane path with the separate gather
+# kernel, wave kernel only, every read deferred, lane + heavy pass
+MODES = ["1", "1g", "0", "2", "3"]
 SE_ALIGN = [n for n in golden_names() if n.startswith("se_")]
 
 
@@ -64,7 +66,7 @@ def test_lane_modes_match_oracle(key, n, sub, indel, mode, gpu_indexes, index_ca
     assert (got == want).all(), describe_mismatch(got, want, 1, 3)
     if mode == "2":
         assert st["deferred"] == n
-    elif mode in "13" and key.startswith("chr901"):
+    elif mode in ("1", "1g", "3") and key.startswith("chr901"):
         assert st["deferred"] < n // 4, str(st["why"])    # most reads stay on the lane path (synth4242 is repeat-heavy)
     assert st["results"] == int((out["selected_votes"] > 0).sum())
 
