@@ -17,6 +17,13 @@ struct DevIndex {
 	uint32_t nb, n_chr;
 	uint32_t start_point, length, start_base_offset, values_bytes;
 	int32_t gap, padding;
+	// compact probe images (device only; NULL when absent, i.e. nb < 16843009):
+	//   bgrp[g]: 8 words per 16 buckets: first item of bucket 16g, then 16 u8 item counts
+	//            (255 = 255 or more: use bstart/keys for that bucket); small enough to stay
+	//            in the Infinity Cache
+	//   keys8[i] = keys[i] as u8 (key_hi = key / nb <= 255 when nb >= 16843009)
+	const uint32_t *bgrp;
+	const uint8_t *keys8;
 };
 
 struct svg_index {
@@ -24,7 +31,7 @@ struct svg_index {
 	hipStream_t stream;
 	svg_host_index host;
 	DevIndex dix;
-	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr;
+	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr, *d_bgrp, *d_keys8;
 	uint32_t *d_scratch;
 	size_t scratch_words;
 	unsigned long long *d_stats;

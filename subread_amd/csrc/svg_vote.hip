@@ -1409,14 +1409,38 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	}
 }
 
+// equal-key run of a bucket given as a bit mask over its items: gehash_go_X's binary search
+// (sorted-hashtable.c:947-981) replayed on the positions alone -- it stops at the first
+// midpoint inside the run.  False (caller falls back to the key loop) if the run is not
+// contiguous, i.e. the bucket is not sorted.
+__device__ __forceinline__ bool try_run(uint64_t eq, int n, int &m, int &fwd, int &bwd, bool &hit)
+{
+	const int fe = eq ? __builtin_ctzll(eq) : 0, ne = __popcll(eq);
+	if (eq && eq != (((ne == 64 ? 0ull : (1ull << ne)) - 1ull) << fe)) return false;
+	if (eq) {
+		const int le = fe + ne - 1;
+		int lo = 0, hi = n - 1;
+		for (;;) {
+			m = (lo + hi) >> 1;
+			if (m < fe) lo = m + 1;
+			else if (m > le) hi = m - 1;
+			else break;
+		}
+		hit = true;
+		fwd = le - m + 1;
+		bwd = m - fe;
+	}
+	return true;
+}
+
 // =============================================================================================
 // probe kernel: phase P for a whole chunk of reads, one thread per subread probe.  Same
 // arithmetic as Wave::probe_all (genekey2int, key % nb, gehash_go_X's binary search and the
 // equal-key run on both sides of the first-hit midpoint); with no per-read state to keep,
 // it runs at high occupancy and hides the dependent bucket -> keys -> run chain.
 // =============================================================================================
-template <int ENDS>
-__global__ void __launch_bounds__(256) probe_kernel(PParams pp)
+template <int ENDS, int BPC>
+__global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 {
 	const DevIndex &ix = pp.ix;
 	const uint32_t nps = (uint32_t)pp.nps, per_read = ENDS * 2 * nps;
@@ -1469,56 +1493,86 @@ __global__ void __launch_bounds__(256) probe_kernel(PParams pp)
 				const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
 				const uint32_t b = key - q * ix.nb;
 				const int16_t k16 = (int16_t)q;
-				const uint32_t first = ix.bstart[b];
-				const int n = (int)(ix.bstart[b + 1] - first);
+				uint32_t first;
+				int n;
+				bool compact = false;
+				if (ix.bgrp) {
+					// bucket bounds from the 32-byte group: first item of the group + the counts
+					// of the buckets before b in it
+					const uint4 *g4 = (const uint4 *)(ix.bgrp + 8 * (size_t)(b >> 4));
+					const uint4 ga = g4[0], gb = g4[1];
+					const uint32_t i = b & 15u;
+					const uint32_t cw[4] = {ga.y, ga.z, ga.w, gb.x};
+					uint32_t pre = 0;
+#pragma unroll
+					for (int q = 0; q < 4; q++) {
+						// bytes of word q below i
+						const int nb_ = (int)i - 4 * q;
+						const uint32_t msk = nb_ >= 4 ? 0xffffffffu : nb_ <= 0 ? 0u : (1u << (8 * nb_)) - 1u;
+						pre = __builtin_amdgcn_sad_u8(cw[q] & msk, 0u, pre);
+					}
+					const uint32_t wsel = i < 4 ? ga.y : i < 8 ? ga.z : i < 12 ? ga.w : gb.x;
+					const uint32_t c = (wsel >> (8 * (i & 3u))) & 255u;
+					first = ga.x + pre;
+					n = (int)c;
+					compact = c != 255u;
+				}
+				if (!compact) {
+					first = ix.bstart[b];
+					n = (int)(ix.bstart[b + 1] - first);
+				}
 				st_p++;
 				st_i += (unsigned)n;
 				if (n > 0) {
 					const int16_t *K = ix.keys + first;
 					int m = 0, fwd = 0, bwd = 0;
 					bool hit = false, done = false;
-					if (pp.window && n <= 56) {
-						// the whole bucket in one round trip: <= 8 independent 16-byte loads of the
-						// aligned window holding its keys, equal keys found by a zero-halfword test
+					if (compact && n <= 48) {
+						// u8 keys: the bucket in <= 4 independent 16-byte loads, equal keys by a
+						// zero-byte test
+						const uintptr_t base = (uintptr_t)(ix.keys8 + first);
+						const uint4 *w = (const uint4 *)(base & ~(uintptr_t)15);
+						const int sh = (int)(base & 15);
+						const int nq = (sh + n + 15) >> 4;
+						const uint32_t kk = (uint32_t)(uint8_t)k16 * 0x01010101u;
+						uint64_t eq = 0;
+#pragma unroll
+						for (int k = 0; k < 4; k++) {
+							const uint4 v = k < nq ? w[k] : make_uint4(0u, 0u, 0u, 0u);
+							const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+							for (int q = 0; q < 4; q++) {
+								const uint32_t x = dw[q] ^ kk;
+								const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+								const uint32_t bits = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+								eq |= (uint64_t)bits << (16 * k + 4 * q);
+							}
+						}
+						eq = (eq >> sh) & ((1ull << n) - 1ull);
+						done = try_run(eq, n, m, fwd, bwd, hit);
+					} else if (pp.window && n <= 56) {
+						// i16 keys: <= 8 independent 16-byte loads of the aligned window holding the
+						// bucket, equal keys by a zero-halfword test
 						const uintptr_t base = (uintptr_t)K;
 						const uint4 *w = (const uint4 *)(base & ~(uintptr_t)15);
 						const int sh = (int)((base & 15) >> 1);   // halfword of item 0 in the window
 						const int nq = (sh + n + 7) >> 3;         // 16-byte words holding the bucket
-						uint32_t d[32];
-#pragma unroll
-						for (int k = 0; k < 8; k++) {
-							const uint4 v = k < nq ? w[k] : make_uint4(0u, 0u, 0u, 0u);
-							d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
-						}
 						const uint32_t kk = (uint32_t)(uint16_t)k16 * 0x00010001u;
 						uint64_t eq = 0;
 #pragma unroll
-						for (int j = 0; j < 32; j++) {
-							const uint32_t x = d[j] ^ kk;
-							const uint32_t z = ~(((x & 0x7fff7fffu) + 0x7fff7fffu) | x | 0x7fff7fffu);
-							eq |= ((uint64_t)((z >> 15) & 1u) << (2 * j)) | ((uint64_t)(z >> 31) << (2 * j + 1));
-						}
-						eq = (eq >> sh) & ((1ull << n) - 1ull);
-						const int fe = eq ? __builtin_ctzll(eq) : 0, ne = __popcll(eq);
-						// the equal run must be contiguous (sorted bucket); otherwise the loop below
-						if (!eq || eq == (((ne == 64 ? 0ull : (1ull << ne)) - 1ull) << fe)) {
-							done = true;
-							if (eq) {
-								// gehash_go_X's binary search (sorted-hashtable.c:947-981) on the
-								// positions alone: it stops at the first midpoint inside the run
-								const int le = fe + ne - 1;
-								int lo = 0, hi = n - 1;
-								for (;;) {
-									m = (lo + hi) >> 1;
-									if (m < fe) lo = m + 1;
-									else if (m > le) hi = m - 1;
-									else break;
-								}
-								hit = true;
-								fwd = le - m + 1;
-								bwd = m - fe;
+						for (int k = 0; k < 8; k++) {
+							const uint4 v = k < nq ? w[k] : make_uint4(0u, 0u, 0u, 0u);
+							const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+							for (int q = 0; q < 4; q++) {
+								const uint32_t x = dw[q] ^ kk;
+								const uint32_t z = ~(((x & 0x7fff7fffu) + 0x7fff7fffu) | x | 0x7fff7fffu);
+								const int j = 4 * k + q;
+								eq |= ((uint64_t)((z >> 15) & 1u) << (2 * j)) | ((uint64_t)(z >> 31) << (2 * j + 1));
 							}
 						}
+						eq = (eq >> sh) & ((1ull << n) - 1ull);
+						done = try_run(eq, n, m, fwd, bwd, hit);
 					}
 					if (!done) {
 						int lo = 0, hi = n - 1;
@@ -1564,6 +1618,32 @@ __global__ void __launch_bounds__(256) probe_kernel(PParams pp)
 // host side: handle, upload, launch
 // =============================================================================================
 
+// compact probe images (DevIndex::bgrp, keys8)
+__global__ void __launch_bounds__(256) build_bgrp(const uint32_t *bstart, uint32_t nb, uint32_t *bgrp)
+{
+	const uint32_t ng = (nb + 15) / 16;
+	for (uint32_t g = blockIdx.x * 256u + threadIdx.x; g < ng; g += gridDim.x * 256u) {
+		uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+		w[0] = bstart[16 * g];
+#pragma unroll
+		for (int i = 0; i < 16; i++) {
+			const uint32_t b = 16 * g + (uint32_t)i;
+			uint32_t c = 0;
+			if (b < nb) { c = bstart[b + 1] - bstart[b]; if (c > 255) c = 255; }
+			w[1 + (i >> 2)] |= c << (8 * (i & 3));
+		}
+		uint4 *d = (uint4 *)(bgrp + 8 * (size_t)g);
+		d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+		d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+	}
+}
+
+__global__ void __launch_bounds__(256) build_keys8(const int16_t *keys, uint64_t items, uint8_t *keys8)
+{
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < items; i += (uint64_t)gridDim.x * 256u)
+		keys8[i] = (uint8_t)keys[i];
+}
+
 // common tail of svg_index_open / svg_index_build*: d_bstart/d_keys/d_vals already in HBM,
 // host part holds .array and the chromosome table
 int svg_index_finish_device(svg_index *h)
@@ -1592,6 +1672,27 @@ int svg_index_finish_device(svg_index *h)
 	hipDeviceProp_t prop;
 	HIPCHK(hipGetDeviceProperties(&prop, h->device));
 	h->n_cu = prop.multiProcessorCount;
+	h->dix.bgrp = NULL;
+	h->dix.keys8 = NULL;
+	if (x->nb >= 16843009u && !getenv("SVG_NO_COMPACT")) {
+		// (2^32-1)/nb <= 255: every key_hi fits a byte
+		const size_t ng = ((size_t)x->nb + 15) / 16;
+		if ((rc = dmalloc(h, &h->d_bgrp, ng * 32 + 64)) || (rc = dmalloc(h, &h->d_keys8, x->items + 128))) return rc;
+		uint64_t blocks = (ng + 255) / 256, bmax = (uint64_t)h->n_cu * 64;
+		if (blocks > bmax) blocks = bmax;
+		hipLaunchKernelGGL(build_bgrp, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart, x->nb,
+		                   (uint32_t *)h->d_bgrp);
+		HIPCHK(hipGetLastError());
+		blocks = (x->items + 255) / 256;
+		if (blocks > bmax) blocks = bmax;
+		hipLaunchKernelGGL(build_keys8, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const int16_t *)h->d_keys, x->items,
+		                   (uint8_t *)h->d_keys8);
+		HIPCHK(hipGetLastError());
+		HIPCHK(hipMemsetAsync((uint8_t *)h->d_keys8 + x->items, 0, 128, h->stream));
+		HIPCHK(hipStreamSynchronize(h->stream));
+		h->dix.bgrp = (const uint32_t *)h->d_bgrp;
+		h->dix.keys8 = (const uint8_t *)h->d_keys8;
+	}
 	if ((rc = dmalloc(h, (void **)&h->d_stats, 32 * sizeof(unsigned long long)))) return rc;
 	HIPCHK(hipMemset(h->d_stats, 0, 32 * sizeof(unsigned long long)));
 	const char *se = getenv("SVG_STATS");
@@ -1660,6 +1761,7 @@ extern "C" void svg_index_close(svg_index *h)
 			for (int j = 0; j < 2; j++)
 				if (h->tev[k][i][j]) hipEventDestroy(h->tev[k][i][j]);
 	hipFree(h->d_bstart); hipFree(h->d_keys); hipFree(h->d_vals); hipFree(h->d_values); hipFree(h->d_chr);
+	hipFree(h->d_bgrp); hipFree(h->d_keys8);
 	hipFree(h->d_scratch); hipFree(h->d_stats); hipFree(h->d_in); hipFree(h->d_out);
 	if (h->stream) hipStreamDestroy(h->stream);
 	svg_host_index_free(&h->host);
@@ -1935,8 +2037,10 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 			uint64_t pb = (cn * per_read + 255) / 256, pmax = (uint64_t)h->n_cu * 32;
 			if (pb > pmax) pb = pmax;
 			if ((rc = timing_mark(h, 0, 0, st))) return rc;
-			if (r2) hipLaunchKernelGGL(probe_kernel<2>, dim3((unsigned)pb), dim3(256), 0, st, pp);
-			else hipLaunchKernelGGL(probe_kernel<1>, dim3((unsigned)pb), dim3(256), 0, st, pp);
+			// 8 blocks of 256 per CU (<= 64 VGPRs): the probe chain is latency-bound, occupancy
+			// is what hides it (C3: 11.3 ms at 4 waves/SIMD, 8.7 ms at 8)
+			if (r2) hipLaunchKernelGGL((probe_kernel<2, 8>), dim3((unsigned)pb), dim3(256), 0, st, pp);
+			else hipLaunchKernelGGL((probe_kernel<1, 8>), dim3((unsigned)pb), dim3(256), 0, st, pp);
 			HIPCHK(hipGetLastError());
 			if ((rc = timing_mark(h, 0, 1, st))) return rc;
 			KParams kc = kp;
