@@ -32,6 +32,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <type_traits>
+#include <string.h>
 #include "subread_vote.h"
 #include "svg_internal.h"
 #include "svg_device.h"
@@ -118,9 +120,13 @@ struct LParams {
 	uint32_t cs;                  // column stride of cand/cpk/ccnt
 	const uint32_t *idx;          // NULL: lane column r = read r; else column k = read idx[k], k < *idx_count
 	const uint32_t *idx_count;    //   (columns >= cs have no candidate list and are deferred)
-	const uint2 *precs;           // fused gather (NPF > 0): probe records, SoA [strand * nps + p][n]
+	const uint2 *precs;           // fused gather (NPF > 0): probe records, SoA [(end * 2 + strand) * nps + p][n]
 	const uint32_t *vals;
 	int nps;
+	// paired-end (lane_pe_kernel)
+	const uint16_t *len2;
+	const uint32_t *chr_end;
+	int n_chr, padding, min_pair, max_pair, mvc;
 	unsigned long long *stats;    // [3] += results; [4] += deferred reads (final pass only);
 	int stat_base, final_pass;    // diagnostics at stats[stat_base..+4]: deferrals by reason (3), candidates, deferrals
 };
@@ -136,6 +142,8 @@ __device__ __forceinline__ uint32_t lm_pack(int votes, int last, int toli, int c
 	return (uint32_t)votes | ((uint32_t)last << 6) | ((uint32_t)toli << 12) | (((uint32_t)cursor & 63u) << 17) | (next << 23);
 }
 __device__ __forceinline__ uint32_t lm_set_next(uint32_t m, uint32_t next) { return (m & ~(63u << 23)) | (next << 23); }
+// bit 29: the slot's read end (paired-end lanes share one slot pool between the two tables)
+__device__ __forceinline__ uint32_t lm_endbit(uint32_t m) { return m & (1u << 29); }
 
 __device__ __forceinline__ uint32_t lrow(uint32_t x) { return (x / 5u) % LROWS; }
 
@@ -169,9 +177,9 @@ __device__ __forceinline__ void lins3(uint32_t &a, uint32_t &b, uint32_t &c, uin
 #define PUT3(idx, a0, a1, a2, val) do { const int _i = (idx); const auto _v = (val); \
 	a0 = _i == 0 ? _v : a0; a1 = _i == 1 ? _v : a1; a2 = _i == 2 ? _v : a2; } while (0)
 
-template <int K>
+template <int K, int ENDS = 1>
 struct Lane {
-	// row heads: 30 fields of HB bits (NIL = all ones), HPW per register
+	// row heads: 30 fields of HB bits (NIL = all ones), HPW per register, one set per end
 	static constexpr int HB = K > 31 ? 6 : 5;
 	static constexpr uint32_t NIL = (1u << HB) - 1u;
 	static constexpr int HPW = 32 / HB, NHW = (LROWS + HPW - 1) / HPW;
@@ -180,25 +188,27 @@ struct Lane {
 	uint2 *pm;             // LDS: pm[slot * 64 + lane]
 	uint32_t *cold;        // this lane's scratch: word w of slot s of strand st at cold[((st*K+s)*CW+w)*64]
 	int lane;
-	uint32_t h[NHW];
-	int nslots, max_vote;
+	uint32_t h[ENDS][NHW];
+	int nslots, max_vote[ENDS];
 	bool dfr;
 	int why;               // deferral reason (stats): 1 candidates > CAP or length, 2 slots > K, 3 shift-indel
 
+	template <int E>
 	__device__ __forceinline__ uint32_t head(uint32_t r) const
 	{
 		const uint32_t q = r / HPW, sh = (r - q * HPW) * HB;
-		uint32_t w = h[0];
+		uint32_t w = h[E][0];
 #pragma unroll
-		for (int k = 1; k < NHW; k++) w = pick(q == (uint32_t)k, h[k], w);
+		for (int k = 1; k < NHW; k++) w = pick(q == (uint32_t)k, h[E][k], w);
 		return (w >> sh) & NIL;
 	}
+	template <int E>
 	__device__ __forceinline__ void set_head(uint32_t r, uint32_t s)
 	{
 		const uint32_t q = r / HPW, sh = (r - q * HPW) * HB;
 		const uint32_t clr = ~(NIL << sh), v = s << sh;
 #pragma unroll
-		for (int k = 0; k < NHW; k++) h[k] = pick(q == (uint32_t)k, (h[k] & clr) | v, h[k]);
+		for (int k = 0; k < NHW; k++) h[E][k] = pick(q == (uint32_t)k, (h[E][k] & clr) | v, h[E][k]);
 	}
 	__device__ __forceinline__ uint32_t *cw(int st, int s, int w) const { return cold + ((st * K + s) * CW + w) * 64; }
 	__device__ __forceinline__ int8_t *recb(int st, int s, int i) const
@@ -206,27 +216,32 @@ struct Lane {
 		return (int8_t *)cw(st, s, 1 + (i >> 2)) + (i & 3);
 	}
 
+	// init_gene_vote for every table of the lane (the slot pool is emptied)
 	__device__ __forceinline__ void reset()
 	{
 		uint32_t all = 0;
 #pragma unroll
 		for (int i = 0; i < HPW; i++) all |= NIL << (i * HB);
 #pragma unroll
-		for (int k = 0; k < NHW; k++) h[k] = all;
+		for (int e = 0; e < ENDS; e++) {
+#pragma unroll
+			for (int k = 0; k < NHW; k++) h[e][k] = all;
+			max_vote[e] = 0;
+		}
 		nslots = 0;
-		max_vote = 0;
 	}
 
-	// gehash_go_X body for one candidate (round 0; sorted-hashtable.c:995-1107)
+	// gehash_go_X body for one candidate of end E (round 0; sorted-hashtable.c:995-1107)
+	template <int E>
 	__device__ __forceinline__ void vote(int st, uint32_t kv, int kP1, int off, uint32_t high_b)
 	{
 		const uint32_t r0 = lrow(kv), rp = lrow(kv + 5u), rm = lrow(kv - 5u);
 		uint32_t tail = NIL, tailM = 0;
 		int ri = 0, n0 = 0;
-		uint32_t s = head(r0);
+		uint32_t s = head<E>(r0);
 		bool found = false;
 		for (;;) {
-			while (s == NIL && ri < 2) { ri++; s = head(ri == 1 ? rp : rm); }
+			while (s == NIL && ri < 2) { ri++; s = head<E>(ri == 1 ? rp : rm); }
 			if (s == NIL) break;
 			const uint2 e = pm[s * 64 + lane];
 			uint32_t M = e.y;
@@ -257,13 +272,13 @@ struct Lane {
 						}
 						cur = d;
 					}
-					M = lm_pack(votes, kP1, tl, cur, lm_next(M));
+					M = lm_pack(votes, kP1, tl, cur, lm_next(M)) | lm_endbit(M);
 					pm[s * 64 + lane].y = M;
-					if (max_vote < votes) max_vote = votes;
+					if (max_vote[E] < votes) max_vote[E] = votes;
 					found = true;
 					break;
 				}
-				if (chg) { M = lm_pack(votes, last, tl, lm_cursor(M), lm_next(M)); pm[s * 64 + lane].y = M; }
+				if (chg) { M = lm_pack(votes, last, tl, lm_cursor(M), lm_next(M)) | lm_endbit(M); pm[s * 64 + lane].y = M; }
 			}
 			if (ri == 0) { tail = s; tailM = M; n0++; }
 			s = lm_next(M);
@@ -272,15 +287,54 @@ struct Lane {
 		if (!found && kv >= low && kv <= high_b && (K <= 24 || n0 < 24)) {
 			if (nslots == K) { dfr = true; why = 2; return; }
 			const uint32_t ns = (uint32_t)nslots++;
-			pm[ns * 64 + lane] = make_uint2(kv, lm_pack(1, kP1, 0, 0, NIL));
+			pm[ns * 64 + lane] = make_uint2(kv, lm_pack(1, kP1, 0, 0, NIL) | ((uint32_t)E << 29));
 			*cw(st, (int)ns, 0) = (uint32_t)off | ((uint32_t)(off + 16) << 8);
 			*cw(st, (int)ns, 1) = (uint32_t)kP1 | ((uint32_t)kP1 << 8);   // rec[0..3] = k+1, k+1, 0, 0
-			if (tail == NIL) set_head(r0, ns);
+			if (tail == NIL) set_head<E>(r0, ns);
 			else pm[tail * 64 + lane].y = lm_set_next(tailM, ns);
-			if (max_vote < 1) max_vote = 1;
+			if (max_vote[E] < 1) max_vote[E] = 1;
 		}
 	}
 };
+
+
+// mapping_result_t of a bigtable record (copy_vote_to_alignment_res, core-junction.c:1058-1071;
+// indel_recorder_copy, sorted-hashtable.c:1144) from its source slot's cold state
+template <class LT>
+__device__ __forceinline__ void write_record(const LT &L, int src, uint32_t pos, int v, int u, uint32_t (&w)[17])
+{
+#pragma unroll
+	for (int k = 0; k < 17; k++) w[k] = 0;
+	w[2] = (uint32_t)(uint16_t)v | ((uint32_t)(uint16_t)u << 16);
+	if (src >= 0) {
+		const int st = src >> 6, s = src & 63;
+		uint32_t rw[6];
+#pragma unroll
+		for (int k = 0; k < 6; k++) rw[k] = *L.cw(st, s, 1 + k);
+		const uint32_t c0w = *L.cw(st, s, 0);
+		int nrec = 0, last = 0;
+#pragma unroll
+		for (int t = 0; t < 7; t++) {
+			const int b0 = 3 * t;
+			const int k0 = (int)(int8_t)(rw[b0 >> 2] >> (8 * (b0 & 3)));
+			if (nrec == 3 * t && k0 != 0) {
+				nrec = 3 * t + 3;
+				last = (int)(int8_t)(rw[(b0 + 2) >> 2] >> (8 * ((b0 + 2) & 3)));
+			}
+		}
+#pragma unroll
+		for (int k = 0; k < 11; k++) {
+			const int i0 = 2 * k, i1 = 2 * k + 1;
+			const int v0 = i0 < nrec ? (int)(int8_t)(rw[i0 >> 2] >> (8 * (i0 & 3))) : 0;
+			const int v1 = i1 < nrec ? (int)(int8_t)(rw[i1 >> 2] >> (8 * (i1 & 3))) : 0;
+			w[4 + k] = (uint32_t)(uint16_t)(int16_t)v0 | ((uint32_t)(uint16_t)(int16_t)v1 << 16);
+		}
+		w[0] = pos;
+		w[1] = st ? (uint32_t)SVG_NEGATIVE_STRAND_FLAG : 0u;
+		w[3] = (uint32_t)(uint8_t)(int8_t)last << 8;
+		w[15] = (c0w & 0xffu) | (((c0w >> 8) & 0xffu) << 16);
+	}
+}
 
 template <int K, int NPF>
 __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
@@ -342,7 +396,7 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				const uint32_t kv = kv_a, pk = pk_a;
 				kv_a = kv_b; pk_a = pk_b;
 				if (j + 2 < mycnt) { kv_b = cb[(size_t)(j + 2) * lp.cs]; pk_b = pb[(size_t)(j + 2) * lp.cs]; }
-				if (j < mycnt && !L.dfr) L.vote(st, kv, (int)(pk & 63u), (int)(pk >> 6), high_b);
+				if (j < mycnt && !L.dfr) L.template vote<0>(st, kv, (int)(pk & 63u), (int)(pk >> 6), high_b);
 			}
 			} else {
 			// ---- fused gather: the read's probe records of this strand in a register window
@@ -395,12 +449,12 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				q0 = q1; q1 = q2; q2 = q3;
 				k0 = k1; k1 = k2; k2 = k3;
 				if (j + 4 < mycnt) { next(it, pkn); q3 = lp.vals[it]; k3 = pkn; }
-				if (j < mycnt && !L.dfr) L.vote(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b);
+				if (j < mycnt && !L.dfr) L.template vote<0>(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b);
 			}
 			}
 			if (L.dfr) continue;
 			// ---- SE gate (core.c:3215-3233) and top-K (core-junction.c:2199-2530, ends = 1)
-			if (L.max_vote >= mvf) {
+			if (L.max_vote[0] >= mvf) {
 				int t0 = 0, t1 = 0, t2 = 0;
 				for (int s = 0; s < L.nslots; s++) ltop3(t0, t1, t2, lm_votes(L.pm[s * 64 + L.lane].y));
 				if (rv0 > 0) ltop3(t0, t1, t2, rv0);
@@ -481,37 +535,7 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				const int v = sel3(i, rv0, rv1, rv2);
 				const int u = sel3(i, ru0, ru1, ru2);
 				uint32_t w[17];
-#pragma unroll
-				for (int k = 0; k < 17; k++) w[k] = 0;
-				w[2] = (uint32_t)(uint16_t)v | ((uint32_t)(uint16_t)u << 16);
-				if (src >= 0) {
-					const int st = src >> 6, s = src & 63;
-					uint32_t rw[6];
-#pragma unroll
-					for (int k = 0; k < 6; k++) rw[k] = *L.cw(st, s, 1 + k);
-					const uint32_t c0w = *L.cw(st, s, 0);
-					int nrec = 0, last = 0;
-#pragma unroll
-					for (int t = 0; t < 7; t++) {
-						const int b0 = 3 * t;
-						const int k0 = (int)(int8_t)(rw[b0 >> 2] >> (8 * (b0 & 3)));
-						if (nrec == 3 * t && k0 != 0) {
-							nrec = 3 * t + 3;
-							last = (int)(int8_t)(rw[(b0 + 2) >> 2] >> (8 * ((b0 + 2) & 3)));
-						}
-					}
-#pragma unroll
-					for (int k = 0; k < 11; k++) {
-						const int i0 = 2 * k, i1 = 2 * k + 1;
-						const int v0 = i0 < nrec ? (int)(int8_t)(rw[i0 >> 2] >> (8 * (i0 & 3))) : 0;
-						const int v1 = i1 < nrec ? (int)(int8_t)(rw[i1 >> 2] >> (8 * (i1 & 3))) : 0;
-						w[4 + k] = (uint32_t)(uint16_t)(int16_t)v0 | ((uint32_t)(uint16_t)(int16_t)v1 << 16);
-					}
-					w[0] = pos;
-					w[1] = st ? (uint32_t)SVG_NEGATIVE_STRAND_FLAG : 0u;
-					w[3] = (uint32_t)(uint8_t)(int8_t)last << 8;
-					w[15] = (c0w & 0xffu) | (((c0w >> 8) & 0xffu) << 16);
-				}
+				write_record(L, src, pos, v, u, w);
 #pragma unroll
 				for (int k = 0; k < 17; k++) dst[i * 17 + k] = w[k];
 				nres += v > 0;
@@ -539,6 +563,353 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 			atomicAdd(&lp.stats[3], nres);
 			if (lp.final_pass) atomicAdd(&lp.stats[4], ndef);
 			// diagnostics (svg_debug_counters): deferrals by reason, candidates voted, deferrals
+			unsigned long long *d = lp.stats + lp.stat_base;
+			atomicAdd(&d[0], nwhy1);
+			atomicAdd(&d[1], nwhy2);
+			atomicAdd(&d[2], nwhy3);
+			atomicAdd(&d[3], ncand);
+			atomicAdd(&d[4], ndef);
+		}
+	}
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// paired-end lane kernel: one lane per read pair
+// ---------------------------------------------------------------------------------------------
+// locate_gene_position_max(..., NULL, NULL, rl = 0), gene-algorithms.c:441-511
+__device__ __forceinline__ int llocate(const uint32_t *ce, int ntot, int padding, uint32_t linear, int &chr, int &pos)
+{
+	int lo = 0, hi = ntot, n;
+	chr = -1;
+	pos = -1;
+	for (;;) {
+		if (hi <= lo + 1) { n = lo - 2 > 0 ? lo - 2 : 0; break; }
+		const int mid = (lo + hi) / 2;
+		if (ce[mid] > linear) hi = mid; else lo = mid + 1;
+	}
+	for (; n < ntot; n++) {
+		const uint32_t c = ce[n];
+		if (c > linear) {
+			pos = n == 0 ? (int)linear : (int)(linear - ce[n - 1]);
+			if (linear > c + 15u - (uint32_t)padding) return 1;
+			if (pos < padding) return 1;
+			pos -= padding;
+			chr = n;
+			return 0;
+		}
+	}
+	return -1;
+}
+
+// simples (simple_mapping_t) of one end as a packed list of 6-bit ids: slot (< 32) or 32 + stored
+// index; PLW words hold 5 * PLW >= 31 slots + 3 stored records
+#define PLW 7
+__device__ __forceinline__ uint32_t pl_get(const uint32_t (&w)[PLW], int i)
+{
+	const int q = i / 5, sh = (i - q * 5) * 6;
+	uint32_t x = w[0];
+#pragma unroll
+	for (int k = 1; k < PLW; k++) x = pick(q == k, w[k], x);
+	return (x >> sh) & 63u;
+}
+__device__ __forceinline__ void pl_put(uint32_t (&w)[PLW], int i, uint32_t id)
+{
+	const int q = i / 5, sh = (i - q * 5) * 6;
+#pragma unroll
+	for (int k = 0; k < PLW; k++) w[k] = pick(q == k, w[k] | (id << sh), w[k]);
+}
+
+// a record of the read's bigtable: rm = (src + 1) | votes << 8 | used << 16 (src = strand << 6 | slot,
+// 0 = none), rp = selected_position
+#define RM(src, v, u) ((uint32_t)((src) + 1) | ((uint32_t)(v) << 8) | ((uint32_t)(u) << 16))
+#define RM_SRC(m) ((int)((m) & 255u) - 1)
+#define RM_V(m) ((int)(((m) >> 8) & 255u))
+#define RM_U(m) ((int)((m) >> 16))
+#define RM_SETV(m, v) (((m) & ~(255u << 8)) | ((uint32_t)(v) << 8))
+
+template <int K, int NPF>
+__global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
+{
+	extern __shared__ __align__(16) uint8_t lds_raw[];
+	const uint32_t gw = blockIdx.x, nw = gridDim.x;
+	Lane<K, 2> L;
+	L.tol = lp.tol;
+	L.low = lp.low;
+	L.lane = (int)__lane_id();
+	L.pm = reinterpret_cast<uint2 *>(lds_raw);
+	L.cold = lp.cold + (size_t)gw * (2 * K * CW * 64) + L.lane;
+	const int mb = lp.multi_best, mvs = lp.max_vote_simples, mvf = lp.min_votes_first, mvsec = lp.min_votes_second;
+	const int cutoff = lp.cutoff, mvc = lp.mvc;
+	unsigned long long nres = 0, ndef = 0, nwhy1 = 0, nwhy2 = 0, nwhy3 = 0, ncand = 0;
+	for (uint32_t g0 = gw * 64u; g0 < lp.n; g0 += nw * 64u) {
+		const uint32_t r = g0 + (uint32_t)L.lane;
+		const bool live = r < lp.n;
+		L.dfr = !live || lp.defer_all;
+		L.why = 0;
+		int len[2], applied[2], step[2];
+		uint32_t high_b[2];
+#pragma unroll
+		for (int e = 0; e < 2; e++) {
+			int l = live ? (e ? lp.len2[r] : lp.len[r]) : 0;
+			if (l > SVG_READ_KEEP) l = SVG_READ_KEEP;
+			len[e] = l;
+			applied[e] = 0;
+			step[e] = 0;
+			if (l >= 15 + lp.gap) {
+				const int cr = (l - 15 - lp.gap) << 16;
+				step[e] = cr / (lp.total_subreads - 1);
+				if (step[e] < (lp.gap << 16)) step[e] = lp.gap << 16;
+				applied[e] = 1 + cr / step[e];
+			}
+			if (!L.dfr && (l < 15 + lp.gap || l > 160 || applied[e] > 31 || applied[e] * lp.gap > NPF)) { L.dfr = true; L.why = 1; }
+			high_b[e] = lp.high - (uint32_t)l;
+		}
+		// bigtable records of both ends
+		uint32_t rm0[3] = {0, 0, 0}, rm1[3] = {0, 0, 0}, rp0[3] = {0, 0, 0}, rp1[3] = {0, 0, 0};
+		int nc_read = 0;
+		for (int st = 0; st < 2; st++) {
+			L.reset();
+			// ---- both ends' tables: fused gather as in lane_kernel, records of (end, strand)
+			auto vote_end = [&](auto E_) __attribute__((always_inline)) {
+				constexpr int E = decltype(E_)::value;
+				const int np = applied[E] * lp.gap;
+				uint32_t rx[NPF], ry[NPF];
+				int cnt = 0;
+#pragma unroll
+				for (int p = 0; p < NPF; p++) {
+					const bool ok = !L.dfr && p < np;
+					const uint2 v = ok ? lp.precs[(size_t)((E * 2 + st) * lp.nps + p) * lp.n + r] : make_uint2(0u, 0u);
+					rx[p] = v.x;
+					ry[p] = v.y;
+					cnt += (int)((v.y & 0xffffu) + (v.y >> 16));
+				}
+				if (!L.dfr && cnt > lp.cap) { L.dfr = true; L.why = 1; }
+				const int mycnt = L.dfr ? 0 : cnt;
+				nc_read += mycnt;
+				int mc = mycnt;
+				for (int o = 32; o; o >>= 1) { int t = __shfl_xor(mc, o); mc = t > mc ? t : mc; }
+				int pb = 0;
+				uint32_t jb = 0;
+				auto next = [&](uint32_t &item, uint32_t &pk) __attribute__((always_inline)) {
+					while (jb >= (ry[0] & 0xffffu) + (ry[0] >> 16)) {
+#pragma unroll
+						for (int p = 0; p + 1 < NPF; p++) { rx[p] = rx[p + 1]; ry[p] = ry[p + 1]; }
+						rx[NPF - 1] = 0u;
+						ry[NPF - 1] = 0u;
+						pb++;
+						jb = 0;
+					}
+					const uint32_t fwd = ry[0] & 0xffffu;
+					item = jb < fwd ? rx[0] + jb : rx[0] - 1u - (jb - fwd);
+					jb++;
+					const int sk = lp.gap == 1 ? pb : pb / lp.gap, x = pb - sk * lp.gap;
+					int off = (int)(((int64_t)step[E] * sk) >> 16);
+					if (lp.gap > 1) off -= off % lp.gap - x;
+					pk = (uint32_t)(sk + 1) | ((uint32_t)off << 6);
+				};
+				uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0, it = 0, pkn = 0;
+				if (0 < mycnt) { next(it, pkn); q0 = lp.vals[it]; k0 = pkn; }
+				if (1 < mycnt) { next(it, pkn); q1 = lp.vals[it]; k1 = pkn; }
+				if (2 < mycnt) { next(it, pkn); q2 = lp.vals[it]; k2 = pkn; }
+				if (3 < mycnt) { next(it, pkn); q3 = lp.vals[it]; k3 = pkn; }
+				for (int j = 0; j < mc; j++) {
+					const uint32_t val = q0, pk = k0;
+					q0 = q1; q1 = q2; q2 = q3;
+					k0 = k1; k1 = k2; k2 = k3;
+					if (j + 4 < mycnt) { next(it, pkn); q3 = lp.vals[it]; k3 = pkn; }
+					if (j < mycnt && !L.dfr) L.template vote<E>(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b[E]);
+				}
+			};
+			vote_end(std::integral_constant<int, 0>());
+			vote_end(std::integral_constant<int, 1>());
+			if (L.dfr) continue;
+			// ---- process_voting_junction_PE_topK (core-junction.c:2199-2530), ends = 2
+			// (1) top-3 distinct vote values per end over its table and stored records
+			int ta[2][3];
+#pragma unroll
+			for (int e = 0; e < 2; e++) { ta[e][0] = 0; ta[e][1] = 0; ta[e][2] = 0; }
+			for (int s = 0; s < L.nslots; s++) {
+				const uint32_t M = L.pm[s * 64 + L.lane].y;
+				const int v = lm_votes(M);
+				if (lm_endbit(M)) ltop3(ta[1][0], ta[1][1], ta[1][2], v);
+				else ltop3(ta[0][0], ta[0][1], ta[0][2], v);
+			}
+#pragma unroll
+			for (int i = 0; i < 3; i++) {
+				if (i < mb && RM_V(rm0[i]) > 0) ltop3(ta[0][0], ta[0][1], ta[0][2], RM_V(rm0[i]));
+				if (i < mb && RM_V(rm1[i]) > 0) ltop3(ta[1][0], ta[1][1], ta[1][2], RM_V(rm1[i]));
+			}
+			// (2) simples per end, in the reference's order: per vote value, the table's slots in
+			// row-major order, then the stored records of that value
+			uint32_t pl[2][PLW];
+			static_assert(5 * PLW >= K + 3, "simples list too short for the slot pool");
+			int ns[2] = {0, 0};
+			auto simples = [&](auto E_) __attribute__((always_inline)) {
+				constexpr int E = decltype(E_)::value;
+#pragma unroll
+				for (int k = 0; k < PLW; k++) pl[E][k] = 0;
+#pragma unroll
+				for (int tk = 0; tk < 3; tk++) {
+					const int N = ta[E][tk];
+					if (ns[E] >= mvs || N < 1 || ta[E][0] - N > cutoff) break;
+					if (N >= mvsec) {
+						for (uint32_t row = 0; row < LROWS; row++) {
+							uint32_t s = L.template head<E>(row);
+							while (s != Lane<K, 2>::NIL) {
+								const uint32_t M = L.pm[s * 64 + L.lane].y;
+								if (lm_votes(M) == N && ns[E] < mvs) { pl_put(pl[E], ns[E], s); ns[E]++; }
+								s = lm_next(M);
+							}
+						}
+					}
+#pragma unroll
+					for (int i = 0; i < 3; i++) {
+						const uint32_t m = E ? rm1[i] : rm0[i];
+						if (i < mb && ns[E] < mvs && RM_V(m) == N) { pl_put(pl[E], ns[E], 32u + (uint32_t)i); ns[E]++; }
+					}
+				}
+			};
+			simples(std::integral_constant<int, 0>());
+			simples(std::integral_constant<int, 1>());
+			if (ns[0] * ns[1] > 96) { L.dfr = true; L.why = 2; continue; }   // bounded per-lane pair loop
+			// value / position / record of a simple
+			auto sv = [&](int E, uint32_t id, uint32_t &pos) __attribute__((always_inline)) -> int {
+				if (id < 32u) { const uint2 x = L.pm[id * 64 + L.lane]; pos = x.x; return lm_votes(x.y); }
+				const int i = (int)id - 32;
+				const uint32_t m = E ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]);
+				pos = E ? sel3(i, rp1[0], rp1[1], rp1[2]) : sel3(i, rp0[0], rp0[1], rp0[2]);
+				return RM_V(m);
+			};
+			// (3) pair scores into the comb buffer (<= max_vote_combinations, first come first kept on ties)
+			int ncomb = 0;
+			uint32_t ca0 = 0, ca1 = 0, ca2 = 0, cb0 = 0, cb1 = 0, cb2 = 0;
+			int cs0 = 0, cs1 = 0, cs2 = 0;
+			for (int i = 0; i < ns[0]; i++) {
+				const uint32_t ida = pl_get(pl[0], i);
+				uint32_t pa;
+				const int va = sv(0, ida, pa);
+				int c1 = -1, q1 = -1;
+				const int e1 = llocate(lp.chr_end, lp.n_chr, lp.padding, pa, c1, q1);
+				for (int j = 0; j < ns[1]; j++) {
+					const uint32_t idb = pl_get(pl[1], j);
+					uint32_t pb2;
+					const int vb = sv(1, idb, pb2);
+					if ((va > vb ? va : vb) < mvf) continue;
+					int c2 = -1, q2 = -1;
+					const int e2 = llocate(lp.chr_end, lp.n_chr, lp.padding, pb2, c2, q2);
+					bool pe = false, same = false;
+					if (e1 == 0 && e2 == 0) {   // test_PE_and_same_chro, core.c:4819-4845
+						long long tl = (long long)q1 - q2;
+						tl = abs((int)tl);
+						tl += (q1 > q2) ? len[0] : len[1];
+						const uint32_t tli = (uint32_t)tl;
+						if (c1 == c2) {
+							same = true;
+							if (tli >= (uint32_t)lp.min_pair && tli <= (uint32_t)lp.max_pair) pe = true;
+						}
+					}
+					if (!pe && (va < vb ? va : vb) < mvf) continue;
+					const int sc = (va + vb) * (pe ? 1300 : (same ? 1000 : 800));
+					const int t = (ncomb > 0 && cs0 >= sc) + (ncomb > 1 && cs1 >= sc) + (ncomb > 2 && cs2 >= sc);
+					if (t < mvc) {
+						// shift entries t.. down by one (the last falls off), insert at t
+						if (t <= 1 && mvc > 2) { ca2 = ca1; cb2 = cb1; cs2 = cs1; }
+						if (t == 0 && mvc > 1) { ca1 = ca0; cb1 = cb0; cs1 = cs0; }
+						PUT3(t, ca0, ca1, ca2, ida);
+						PUT3(t, cb0, cb1, cb2, idb);
+						PUT3(t, cs0, cs1, cs2, sc);
+						if (ncomb < mvc) ncomb++;
+					}
+				}
+			}
+			// (4) results of each end
+			uint32_t tm0[3] = {0, 0, 0}, tm1[3] = {0, 0, 0}, tp0[3] = {0, 0, 0}, tp1[3] = {0, 0, 0};
+			int cur[2] = {0, 0};
+			auto emit = [&](int E, uint32_t id) __attribute__((always_inline)) {
+				uint32_t pos;
+				const int v = sv(E, id, pos);
+				uint32_t m;
+				if (id < 32u) m = RM((st << 6) | (int)id, v, applied[E]);
+				else { const int i = (int)id - 32; m = E ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]); }
+				const int c = cur[E];
+				const uint32_t q0 = E ? tp1[0] : tp0[0], q1 = E ? tp1[1] : tp0[1];
+				if ((c > 0 && q0 == pos) || (c > 1 && q1 == pos)) return;
+				if (E) { PUT3(c, tm1[0], tm1[1], tm1[2], m); PUT3(c, tp1[0], tp1[1], tp1[2], pos); }
+				else { PUT3(c, tm0[0], tm0[1], tm0[2], m); PUT3(c, tp0[0], tp0[1], tp0[2], pos); }
+				cur[E] = c + 1;
+			};
+			if (ncomb > 0) {
+				// merge_sort -> unstable selection sort ascending for <= 11 items (core.c:4716-4729)
+				if (ncomb > 1) {
+					int mj = 0;
+					if (cs0 - cs1 > 0) mj = 1;
+					if (ncomb > 2 && (mj ? cs1 : cs0) - cs2 > 0) mj = 2;
+					if (mj == 1) { uint32_t a = ca0, b = cb0; int c = cs0; ca0 = ca1; cb0 = cb1; cs0 = cs1; ca1 = a; cb1 = b; cs1 = c; }
+					else if (mj == 2) { uint32_t a = ca0, b = cb0; int c = cs0; ca0 = ca2; cb0 = cb2; cs0 = cs2; ca2 = a; cb2 = b; cs2 = c; }
+					if (ncomb > 2 && cs1 - cs2 > 0) { uint32_t a = ca1, b = cb1; int c = cs1; ca1 = ca2; cb1 = cb2; cs1 = cs2; ca2 = a; cb2 = b; cs2 = c; }
+				}
+				// taken from the highest score down
+#pragma unroll
+				for (int e = 0; e < 2; e++)
+#pragma unroll
+					for (int i = 2; i >= 0; i--)
+						if (i < ncomb && cur[e] < mb) emit(e, e ? sel3(i, cb0, cb1, cb2) : sel3(i, ca0, ca1, ca2));
+			} else {
+				// no pair: each end's simples with >= min_votes_first votes
+#pragma unroll
+				for (int e = 0; e < 2; e++)
+					for (int i = 0; i < ns[e]; i++) {
+						if (cur[e] >= mb) break;
+						const uint32_t id = pl_get(pl[e], i);
+						uint32_t pos;
+						if (sv(e, id, pos) < mvf) continue;
+						emit(e, id);
+					}
+			}
+#pragma unroll
+			for (int i = 0; i < 3; i++) {
+				if (i < cur[0]) { rm0[i] = tm0[i]; rp0[i] = tp0[i]; } else rm0[i] = RM_SETV(rm0[i], 0);
+				if (i < cur[1]) { rm1[i] = tm1[i]; rp1[i] = tp1[i]; } else rm1[i] = RM_SETV(rm1[i], 0);
+			}
+		}
+		if (!L.dfr) ncand += (unsigned long long)nc_read;
+		// ---- the pair's 2 x multi_best records
+		if (!L.dfr) {
+#pragma unroll
+			for (int e = 0; e < 2; e++) {
+				uint32_t *dst = (uint32_t *)(lp.out + ((size_t)r * 2 + e) * mb * 68);
+				for (int i = 0; i < mb; i++) {
+					const uint32_t m = e ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]);
+					const uint32_t pos = e ? sel3(i, rp1[0], rp1[1], rp1[2]) : sel3(i, rp0[0], rp0[1], rp0[2]);
+					uint32_t w[17];
+					write_record(L, RM_SRC(m), pos, RM_V(m), RM_U(m), w);
+#pragma unroll
+					for (int k = 0; k < 17; k++) dst[i * 17 + k] = w[k];
+					nres += RM_V(m) > 0;
+				}
+			}
+		}
+		const unsigned long long dm = __ballot(L.dfr && live);
+		if (dm) {
+			uint32_t base = 0;
+			const int leader = __ffsll((long long)dm) - 1;
+			if (L.lane == leader) base = atomicAdd(lp.defer_count, (uint32_t)__popcll(dm));
+			base = __shfl(base, leader);
+			if (L.dfr && live) lp.defer_list[base + __popcll(dm & ((1ull << L.lane) - 1ull))] = r;
+			ndef += (unsigned long long)__popcll(dm);
+		}
+		if (lp.stats) {
+			nwhy1 += (unsigned long long)__popcll(__ballot(L.dfr && live && L.why == 1));
+			nwhy2 += (unsigned long long)__popcll(__ballot(L.dfr && live && L.why == 2));
+			nwhy3 += (unsigned long long)__popcll(__ballot(L.dfr && live && L.why == 3));
+		}
+	}
+	if (lp.stats) {
+		for (int o = 32; o; o >>= 1) { nres += __shfl_xor(nres, o); ncand += __shfl_xor(ncand, o); }
+		if (L.lane == 0) {
+			atomicAdd(&lp.stats[3], nres);
+			if (lp.final_pass) atomicAdd(&lp.stats[4], ndef);
 			unsigned long long *d = lp.stats + lp.stat_base;
 			atomicAdd(&d[0], nwhy1);
 			atomicAdd(&d[1], nwhy2);
@@ -604,10 +975,79 @@ int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int s
 {
 	const char *e = getenv("SVG_LANE");
 	if (e && e[0] == '0') return 0;
-	if (paired || sj || h->max_read_len > 160) return 0;
+	if (sj || h->max_read_len > 160) return 0;
 	int tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
-	if (tol > 5 || p->total_subreads > 31 || p->max_vote_simples > 3 || p->multi_best > 3 || p->top_scores != 3) return 0;
+	if (tol > 5 || p->total_subreads > 31 || p->multi_best > 3 || p->top_scores != 3) return 0;
+	if (!paired && p->max_vote_simples > 3) return 0;
+	if (paired && p->max_vote_combinations > 3) return 0;
 	return 1;
+}
+
+#define LANE_PE_K 31   // shared by both ends' tables; 5-bit slot ids (NIL = 31)
+#define LANE_PE_CAP 40
+
+// paired-end: lane_pe_kernel over every pair of the chunk; deferred pairs listed for vote_kernel
+int svg_lane_pe_chunk(svg_index *h, const svg_params *p, const uint16_t *len1, const uint16_t *len2, uint32_t n,
+                      const uint2 *precs, int nps, uint8_t *out, unsigned long long *stats, uint32_t **defer_list,
+                      uint32_t **defer_count, hipStream_t st)
+{
+	const char *e = getenv("SVG_LANE");
+	const size_t o_l1 = 0, o_cnt = (o_l1 + (size_t)4 * n + 255) & ~(size_t)255, need = o_cnt + 256;
+	if (need > h->lane_cap) {
+		hipFree(h->d_lane);
+		h->d_lane = NULL;
+		h->lane_cap = 0;
+		if (dmalloc(h, &h->d_lane, need)) return SVG_E_NOMEM;
+		h->lane_cap = need;
+	}
+	uint8_t *b = (uint8_t *)h->d_lane;
+	uint32_t *cnt = (uint32_t *)(b + o_cnt);   // [0] deferrals, [2] wave-kernel work counter
+	HIPCHK(hipMemsetAsync(cnt, 0, 16, st));
+	if (nps > LANE_NPF) { svg_set_error("lane_pe: %d probes per strand", nps); return SVG_E_UNSUPPORTED; }
+	LParams lp;
+	memset(&lp, 0, sizeof lp);
+	lp.len = len1; lp.len2 = len2; lp.n = n; lp.cap = LANE_PE_CAP;
+	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps;
+	lp.gap = h->dix.gap; lp.total_subreads = p->total_subreads;
+	lp.tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
+	lp.low = h->dix.start_base_offset;
+	lp.high = h->dix.start_base_offset + h->dix.length;
+	lp.multi_best = p->multi_best; lp.max_vote_simples = p->max_vote_simples; lp.cutoff = p->max_vote_number_cutoff;
+	lp.min_votes_first = p->min_votes_first; lp.min_votes_second = p->min_votes_second;
+	lp.chr_end = h->dix.chr_end; lp.n_chr = (int)h->dix.n_chr; lp.padding = h->dix.padding;
+	lp.min_pair = p->min_pair_distance; lp.max_pair = p->max_pair_distance; lp.mvc = p->max_vote_combinations;
+	lp.out = out;
+	lp.defer_list = (uint32_t *)(b + o_l1);
+	lp.defer_count = cnt;
+	lp.defer_all = e && e[0] == '2';
+	lp.stats = stats;
+	lp.stat_base = 16;
+	lp.final_pass = 1;
+	lp.cs = n;
+	constexpr int K = LANE_PE_K;
+	const size_t lds = (size_t)K * 64 * sizeof(uint2);
+	int per_cu = (int)(160 * 1024 / lds);
+	if (per_cu > 32) per_cu = 32;
+	uint64_t blocks = (uint64_t)h->n_cu * per_cu, need_b = (n + 63) / 64;
+	if (blocks > need_b) blocks = need_b;
+	if (blocks < 1) blocks = 1;
+	const size_t words = blocks * (size_t)(2 * K * CW * 64);
+	if (words > h->lscratch_words) {
+		hipFree(h->d_lscratch);
+		h->d_lscratch = NULL;
+		h->lscratch_words = 0;
+		if (dmalloc(h, (void **)&h->d_lscratch, words * 4 + 256)) return SVG_E_NOMEM;
+		h->lscratch_words = words;
+	}
+	lp.cold = h->d_lscratch;
+	int rc = svg_timing_mark(h, 3, 0, st);
+	if (rc) return rc;
+	hipLaunchKernelGGL((lane_pe_kernel<K, LANE_NPF>), dim3((unsigned)blocks), dim3(64), lds, st, lp);
+	HIPCHK(hipGetLastError());
+	if ((rc = svg_timing_mark(h, 3, 1, st))) return rc;
+	*defer_list = lp.defer_list;
+	*defer_count = cnt;
+	return 0;
 }
 
 int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint32_t n, const uint2 *precs, int nps,

@@ -379,7 +379,7 @@ struct Wave {
 		}
 	}
 
-	// ---------------------------------------------------------------- batch mode (SE, round 0)
+	// ---------------------------------------------------------------- batch mode (align, round 0)
 	// Lane c holds candidate c of a chunk of m <= 64, in the reference's order.  A candidate
 	// whose outcome cannot depend on the other candidates of the chunk -- no slot of the
 	// table within the tolerance in its three rows (so it finds nothing), no other chunk
@@ -493,7 +493,7 @@ struct Wave {
 			{
 				const int m = (int)cn;
 				unsigned long long serial = m == 64 ? ~0ull : ((1ull << m) - 1ull);
-				if constexpr (ENDS == 1 && !SJ) {
+				if constexpr (!SJ) {
 					if (round == 0 && kp->ii_end == 5 && m >= 8) serial = batch_create<E>(kvv, kov, m, high_b);
 				}
 				if (kp->stats) { st_batch += (unsigned long long)(m - __popcll(serial)); st_serial += (unsigned long long)__popcll(serial); }
@@ -1288,6 +1288,9 @@ struct Wave {
 		wsync();
 		STAMP(0);
 		stage_probes();
+		// this read's text and probe records are staged: the next read's loads go out now and
+		// have the whole vote of this read to arrive (deferred reads are scattered over the chunk)
+		if (r_next < kp->n_reads) { prefetch_text(r_next); prefetch_recs(r_next); }
 		STAMP(1);
 		for (int strand = 0; strand < 2; strand++) {
 			cur_strand = strand;
@@ -1309,9 +1312,6 @@ struct Wave {
 			}
 			STAMP(4);
 		}
-		// the next read's text loads go out before this read's stores: vmcnt retires in
-		// issue order, so the next read's first wait does not also wait for the stores
-		if (r_next < kp->n_reads) { prefetch_text(r_next); prefetch_recs(r_next); }
 		// write the read's records (multi_best <= 3: 17 * 3 dwords, one store per lane)
 		for (int e = 0; e < ENDS; e++) {
 			uint32_t *dst = (uint32_t *)(kp->out + ((r * ENDS + e) * (uint64_t)p.multi_best) * 68);
@@ -2023,8 +2023,9 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 		pp.nb_magic = ~0ull / h->dix.nb + 1;   // ceil(2^64 / nb), nb is not a power of two
 		pp.out = (uint2 *)h->d_prec;
 		pp.stats = kp.stats;
-		// single-end align: lane-per-read fast path (svg_lane.hip), probe records in SoA layout
-		const bool lane = svg_lane_eligible(h, p, r2 != NULL, sj) != 0;
+		// align mode, reads <= 160 bp: lane-per-read (SE) / lane-per-pair (PE) fast path
+		// (svg_lane.hip), probe records in SoA layout
+		const bool lane = svg_lane_eligible(h, p, r2 != NULL, sj) != 0 && (!r2 || nps <= 10);
 		pp.soa = lane ? 1 : 0;
 		pp.window = h->dix.nb >= 131073u && !getenv("SVG_NO_WINDOW");   // key_hi <= 32767: int16 order == key order
 		{ const char *e = getenv("SVG_PROBE_MAP"); pp.readmajor = !(e && e[0] == '0'); }
@@ -2056,7 +2057,8 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 				// gather + lane kernels vote every read they can; the rest (deferral list) go to
 				// vote_kernel below, which reads the SoA probe records of the deferred reads
 				uint32_t *dl = NULL, *dc = NULL;
-				rc = svg_lane_chunk(h, p, kc.len1, (uint32_t)cn, kc.precs, nps, kc.out, kp.stats, &dl, &dc, st);
+				rc = r2 ? svg_lane_pe_chunk(h, p, kc.len1, kc.len2, (uint32_t)cn, kc.precs, nps, kc.out, kp.stats, &dl, &dc, st)
+				        : svg_lane_chunk(h, p, kc.len1, (uint32_t)cn, kc.precs, nps, kc.out, kp.stats, &dl, &dc, st);
 				if (rc) return rc;
 				kc.prec_stride = (uint32_t)cn;
 				kc.idx = dl;

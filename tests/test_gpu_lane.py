@@ -15,6 +15,8 @@ pytestmark = pytest.mark.gpu
 # kernel, wave kernel only, every read deferred, lane + heavy pass
 MODES = ["1", "1g", "0", "2", "3"]
 SE_ALIGN = [n for n in golden_names() if n.startswith("se_")]
+PE_ALIGN = [n for n in golden_names() if n.startswith("pe_")]
+PE_MODES = ["1", "0", "2"]
 
 
 @pytest.fixture(scope="module")
@@ -102,3 +104,53 @@ def test_lane_edge_lengths(mode, lengths, gpu_indexes, index_cache, monkeypatch)
         ref, _, _, _ = OracleIndex(pre).vote(p, rb, threads=8)
         got, want = pack_records(out, None, None), pack_records(ref, None, None)
         assert (got == want).all(), describe_mismatch(got, want, 1, 3)
+
+
+@pytest.mark.parametrize("mode", PE_MODES)
+@pytest.mark.parametrize("name", PE_ALIGN)
+def test_lane_pe_modes_match_reference_golden(name, mode, gpu_indexes, monkeypatch):
+    """Paired-end lane path (lane_pe_kernel, one lane per pair) on the reference's PE records."""
+    monkeypatch.setenv("SVG_LANE", mode)
+    c = Case(name)
+    ix = gpu_indexes(c.index_key)
+    out, jout, bm = ix.vote(c.params, c.r1, c.r2)
+    got = pack_records(out, jout, bm)
+    assert (got == c.expected).all(), describe_mismatch(got, c.expected, c.ends, c.params.multi_best)
+
+
+@pytest.mark.parametrize("mode", PE_MODES)
+@pytest.mark.parametrize("key,n,length,params", [("chr901_full", 60000, 150, {}), ("chr901_full", 40000, 100, {}),
+                                                 ("synth4242_full", 30000, 150, {}),
+                                                 ("chr901_full", 30000, 125, {"min_votes_first": 1, "max_vote_simples": 16,
+                                                                               "max_vote_combinations": 2, "multi_best": 2,
+                                                                               "min_pair_distance": 100,
+                                                                               "max_pair_distance": 400})])
+def test_lane_pe_modes_match_oracle(key, n, length, params, mode, gpu_indexes, index_cache, monkeypatch):
+    """Simulated pairs (fragments N(300,50) clipped, R2 reverse complement) and pairs of
+    unrelated reads; the last case changes -m, -B-like limits, multi_best and -d/-D."""
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.abi import default_params, PROGRAM_ALIGN
+    from subread_amd.sim import Genome, simulate_pairs, simulate_reads
+    monkeypatch.setenv("SVG_LANE", mode)
+    pre = index_cache.get(key)
+    g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
+    r1, r2 = simulate_pairs(g, n, length, seed=91, insert_max=700)
+    # a quarter of the pairs: R2 from elsewhere (discordant / different chromosome)
+    u = simulate_reads(g, n, length, seed=92, sub=0.02, indel=0.02)
+    from subread_amd.abi import ReadBatch
+    seqs2 = [bytes(u.seq[u.offsets[i]:u.offsets[i] + u.lens[i]]) if i % 4 == 0 else
+             bytes(r2.seq[r2.offsets[i]:r2.offsets[i] + r2.lens[i]]) for i in range(n)]
+    r2 = ReadBatch.from_list(seqs2)
+    p = default_params(PROGRAM_ALIGN, True, **params)
+    ix = gpu_indexes(key)
+    ix.set_stats(True)
+    out, _, _ = ix.vote(p, r1, r2)
+    st = ix.stats()
+    ix.set_stats(False)
+    ref, _, _, _ = OracleIndex(pre).vote(p, r1, r2, threads=16)
+    got, want = pack_records(out, None, None), pack_records(ref, None, None)
+    assert (got == want).all(), describe_mismatch(got, want, 2, p.multi_best)
+    if mode == "2":
+        assert st["deferred"] == n
+    elif mode == "1" and key.startswith("chr901"):
+        assert st["deferred"] < n // 2, st      # repeat-rich chr901 + discordant pairs defer more

@@ -9,21 +9,25 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import subread_amd as sa  # noqa: E402
 from subread_amd.abi import default_params  # noqa: E402
-from subread_amd.sim import random_genome, simulate_reads, c3_lengths  # noqa: E402
+from subread_amd.sim import random_genome, simulate_reads, simulate_pairs, c3_lengths  # noqa: E402
 
 
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 2_000_000
-    if wl == "c3":
+    if wl in ("c3", "c4"):
         g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))
     else:
         g = random_genome([1_000_000], 901)
     ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True)
-    r = simulate_reads(g, n, 100, seed=20261015, sub=0.01, indel=0.001)
-    ix.set_max_read_length(100)
+    if wl == "c4":
+        r, r2 = simulate_pairs(g, n, 150, seed=4004)
+        ix.set_max_read_length(150)
+    else:
+        r, r2 = simulate_reads(g, n, 100, seed=20261015, sub=0.01, indel=0.001), None
+        ix.set_max_read_length(100)
     ix.set_stats(True)
-    ix.vote(default_params(), r)
+    ix.vote(default_params(paired=r2 is not None), r, r2)
     st, dc = ix.stats(), ix.debug_counters()
     print("%s: %d reads, %.2f hits/read, to the wave kernel %d (%.2f%%)" % (
         wl, n, st["hits"] / n, st["deferred"], 100.0 * st["deferred"] / n))
