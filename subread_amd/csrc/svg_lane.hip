@@ -922,13 +922,13 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 
 // ---------------------------------------------------------------------------------------------
 // host: two lane passes for one chunk (SE align), then the wave kernel for what is left
-//   pass 1 (light): every read, <= 40 candidates and <= 16 vote-table slots per strand
+//   pass 1 (light): every read, <= 40 candidates and <= 20 vote-table slots per strand
 //   pass 2 (heavy, SVG_LANE=3 only): the reads pass 1 deferred (up to n/4 of them), <= 192
 //                   candidates and <= 64 slots per strand.  Measured at C3 it costs more than
 //                   it saves (64-slot tables: 5 waves/CU, long row walks, and most repeat-family
 //                   reads still overflow), so the wave kernel takes pass 1's deferrals directly.
 // ---------------------------------------------------------------------------------------------
-#define LANE_K1 16
+#define LANE_K1 20   // slots per lane: 10 KB LDS per wave = the 4 waves/SIMD the VGPRs allow
 #define LANE_NPF 10   // probe records per strand held in registers by the fused light pass
 #define LANE_CAP1 40
 #define LANE_K2 64
@@ -1100,8 +1100,17 @@ int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint3
 	lp.stat_base = 16;
 	lp.final_pass = !two;
 	lp.cs = n; lp.idx = NULL; lp.idx_count = NULL;
-	rc = fused ? lane_launch<LANE_K1, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st)
-	           : lane_launch<LANE_K1, 0>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
+	{
+		// tuning knobs (diagnostics): SVG_LANE_K=16|20|24, SVG_LANE_CAP
+		const char *ek = getenv("SVG_LANE_K"), *ec = getenv("SVG_LANE_CAP");
+		const int kk = ek ? atoi(ek) : LANE_K1;
+		if (ec && atoi(ec) > 0 && atoi(ec) <= LANE_CAP1) lp.cap = atoi(ec);
+		if (ec && atoi(ec) > LANE_CAP1 && fused) lp.cap = atoi(ec) < 64 ? atoi(ec) : 64;
+		if (!fused) rc = lane_launch<LANE_K1, 0>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
+		else if (kk == 16) rc = lane_launch<16, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
+		else if (kk == 24) rc = lane_launch<24, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
+		else rc = lane_launch<LANE_K1, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
+	}
 	if (rc) return rc;
 	*defer_list = lp.defer_list;
 	*defer_count = cnt;
