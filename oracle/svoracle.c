@@ -916,16 +916,12 @@ int svo_vote_batch(const svo_index *ix, const svg_params *p, const svg_reads *r1
 	batch_t b;
 	pthread_t th[256];
 	int t;
-	uint64_t i;
 	if (!ix || !p || !r1 || !out) return SVG_E_ARG;
 	if (r2 && r2->n_reads != r1->n_reads) return SVG_E_ARG;
 	if (p->multi_best < 1 || p->multi_best > 3 || p->top_scores < 1 || p->top_scores > 9) return SVG_E_UNSUPPORTED;
 	if (p->max_vote_combinations > 11 || p->max_vote_simples < 1) return SVG_E_UNSUPPORTED;
 	if (p->do_breakpoint_detection && !jout) return SVG_E_ARG;
 	if (p->do_big_margin_filtering_for_junctions && !bm) return SVG_E_ARG;
-	for (i = 0; i < r1->n_reads; i++) {
-		if (p->do_breakpoint_detection && (r1->lens[i] > LONG_READ || (r2 && r2->lens[i] > LONG_READ))) return SVG_E_UNSUPPORTED;
-	}
 	memset(&b, 0, sizeof b);
 	b.ix = ix; b.p = p; b.r1 = r1; b.r2 = r2; b.out = out; b.jout = jout; b.bm = bm;
 	pthread_mutex_init(&b.lock, NULL);

@@ -662,7 +662,7 @@ struct Wave {
 	// mid-outward visiting order) with the strictly best score, so the wave takes the
 	// maximum score and, among equal scores, the lowest visiting index.  Returns
 	// (1+best)/100 or 0 and the split point / GT-AG strand / found flag.
-	__device__ int donor(int e, uint32_t left, uint32_t right, int normal, int gs, int ge, int *split, int *gtag, int *found)
+	__device__ int donor(int e, uint32_t left, uint32_t right, int lio, int normal, int gs, int ge, int *split, int *gtag, int *found)
 	{
 		const svg_params &p = kp->p;
 		const int lane = lane_id();
@@ -676,7 +676,7 @@ struct Wave {
 			// split points visited lie in [gs-1, ge+1] and pass only inside [17, rl-17]; the
 			// windows cover 20 bases before the lowest to 17 after the highest
 			int lo_sp = gs - 1 > JCW ? gs - 1 : JCW;
-			uint32_t l0 = left + (uint32_t)lo_sp, r0 = right + (uint32_t)lo_sp;
+			uint32_t l0 = left + (uint32_t)(lo_sp + lio), r0 = right + (uint32_t)lo_sp;
 			load_window(0, l0 >= 20u ? l0 - 20u : 0u);
 			load_window(1, r0 >= 20u ? r0 - 20u : 0u);
 			wsync();
@@ -693,7 +693,7 @@ struct Wave {
 					bool ok = false;
 					if (p.prefer_donor_receptor_junctions) {
 						if (normal) {
-							dl0 = gv_get(0, left + sp); dl1 = gv_get(0, left + sp + 1);
+							dl0 = gv_get(0, left + sp + lio); dl1 = gv_get(0, left + sp + lio + 1);
 							if (donor_pair(dl0, dl1)) {
 								dr0 = gv_get(1, right + sp - 2); dr1 = gv_get(1, right + sp - 1);
 								dr_set = true;
@@ -702,7 +702,7 @@ struct Wave {
 									     && ((dl0 == 'C' && dl1 == 'T') || (dl0 == 'G' && dl1 == 'T'));
 							}
 						} else {
-							dl0 = gv_get(1, right + sp); dl1 = gv_get(1, right + sp + 1);
+							dl0 = gv_get(1, right + sp + lio); dl1 = gv_get(1, right + sp + lio + 1);
 							dr0 = gv_get(0, left + sp - 2); dr1 = gv_get(0, left + sp - 1);
 							dr_set = true;
 							ok = donor_pair(dl0, dl1) && donor_pair(dr0, dr1)
@@ -713,20 +713,20 @@ struct Wave {
 					if (ok || !need_donor) {
 						int lm, rm, ln, rn;
 						if (normal) {
-							lm = match_chro(0, read, rl, sp - JCW, left + sp - JCW, JCW);
+							lm = match_chro(0, read, rl, sp - JCW, left + sp - JCW + lio, JCW);
 							if (lm > JCW - 2) {
 								rm = match_chro(1, read, rl, sp, right + sp, JCW);
 								if (rm >= 2 * JCW - lm - allow) {
-									ln = match_chro(0, read, rl, sp, left + sp, JCW);
+									ln = match_chro(0, read, rl, sp, left + sp + lio, JCW);
 									rn = match_chro(1, read, rl, sp - JCW, right + sp - JCW, JCW);
 									if (ln <= JCW - 5 && rn <= JCW - 5) { sc = 100 * ((ok ? 3000 : 0) + lm + rm - ln - rn); cand = true; }
 								}
 							}
 						} else {
 							rm = match_chro(1, read, rl, sp - JCW, right + sp - JCW, JCW);
-							lm = match_chro(0, read, rl, sp, left + sp, JCW);
+							lm = match_chro(0, read, rl, sp, left + sp + lio, JCW);
 							rn = match_chro(1, read, rl, sp, right + sp, JCW);
-							ln = match_chro(0, read, rl, sp - JCW, left + sp - JCW, JCW);
+							ln = match_chro(0, read, rl, sp - JCW, left + lio + sp - JCW, JCW);
 							if (lm + rm >= 2 * JCW - allow && ln <= JCW - 5 && rn <= JCW - 5) { sc = 100 * ((ok ? 3000 : 0) + lm + rm - ln - rn); cand = true; }
 						}
 					}
@@ -772,7 +772,17 @@ struct Wave {
 		const uint32_t mw = cold_slot(cold[e], ms)[0];
 		const int Mcs = (int)(mw & 0xffff), Mce = (int)(mw >> 16);
 		const int rl = rc.rl[e];
-		int Jv = 0, Jcs = 0, Jce = 0, Jsplit = 0, Jnormal = 0;
+		int Jv = 0, Jcs = 0, Jce = 0, Jsplit = 0, Jnormal = 0, Jdio = 0;
+		// long reads (core-junction.c, curr_read_len > EXON_LONG_READ_LENGTH): the indel offsets
+		// accumulated over each half's indel recorder shift the smaller half's donor tests
+		int major_ind = 0;
+		if (rl > 160) {
+			const uint32_t *mcs = cold_slot(cold[e], ms);
+			for (int kx = 0; kx < SVG_MAX_INDEL_SECTIONS; kx++) {
+				if (!cold_rec(mcs, kx * 3)) break;
+				major_ind += cold_rec(mcs, kx * 3 + 2);
+			}
+		}
 		uint32_t Jpos = 0;
 		int flags = (int)(r[1] & 0xffff);
 		bool upd = false;
@@ -818,10 +828,20 @@ struct Wave {
 				int ge = (Mcs < csb) ? csb + 8 : Mcs + 8;
 				int normal = 1 != (int)(Mcs > csb) + (int)(Mpos > Pb);
 				int split = 0, gtag = 0, found = 0;
-				int sc = donor(e, Mpos < Pb ? Mpos : Pb, Mpos > Pb ? Mpos : Pb, normal, gs > 0 ? gs : 0, ge < rl ? ge : rl,
+				int minor_ind = 0, lio = 0;
+				if (rl > 160) {
+					const uint32_t *ncs = cold_slot(cold[e], rd(sl, b));
+					for (int kx = 0; kx < SVG_MAX_INDEL_SECTIONS; kx++) {
+						if (!cold_rec(ncs, kx * 3)) break;
+						minor_ind += cold_rec(ncs, kx * 3 + 2);
+					}
+					lio = Mpos < Pb ? major_ind : minor_ind;   // the larger half's offset is 0
+				}
+				int sc = donor(e, Mpos < Pb ? Mpos : Pb, Mpos > Pb ? Mpos : Pb, lio, normal, gs > 0 ? gs : 0, ge < rl ? ge : rl,
 				               &split, &gtag, &found);
 				if (sc > 0) {
 					Jpos = Pb; Jv = Vb; Jcs = csb; Jce = ceb; Jsplit = split; Jnormal = normal;
+					Jdio = (minor_ind & 0xf) | ((major_ind & 0xf) << 4);   // double_indel_offset
 					flags &= ~0x3;
 					if (!found || gtag > 2) flags |= 3;
 					else flags = gtag ? (flags | 1) : (flags & ~1);
@@ -834,7 +854,7 @@ struct Wave {
 			// subjunc_result_t: split_point, minor_votes | double_indel_offset 0, indel_at_junction 0,
 			// small/large_side_increasing_coordinate = !normal / normal of the last update
 			J[0] = (uint32_t)(uint16_t)Jsplit | ((uint32_t)(uint16_t)Jv << 16);
-			J[1] = ((uint32_t)(Jnormal ? 0 : 1) << 16) | ((uint32_t)(Jnormal ? 1 : 0) << 24);
+			J[1] = (uint32_t)(uint8_t)Jdio | ((uint32_t)(Jnormal ? 0 : 1) << 16) | ((uint32_t)(Jnormal ? 1 : 0) << 24);
 			J[2] = Jpos;
 			J[3] = (uint32_t)(uint16_t)Jcs | ((uint32_t)(uint16_t)Jce << 16);
 			r[1] = (r[1] & 0xffff0000u) | (uint32_t)(uint16_t)flags;
@@ -1953,6 +1973,11 @@ static int launch_vote(svg_index *h, KParams &kp, hipStream_t st, int npmax, boo
 	// subjunc (junction minor search, donor scoring, big-margin records) is a separate
 	// variant so the plain-align kernels carry none of its registers
 	if (sj) {
+		if (h->max_read_len > 256 || npmax > 64) {
+			// long reads (161..1209 bp): text of both strands in LDS for donor scoring
+			if (ends == 2) return npmax <= 64 ? launch_t<2, 1216, 64, 2, 4, true>(h, kp, st) : launch_t<2, 1216, 192, 2, 4, true>(h, kp, st);
+			return npmax <= 64 ? launch_t<1, 1216, 64, 2, 4, true>(h, kp, st) : launch_t<1, 1216, 192, 2, 4, true>(h, kp, st);
+		}
 		if (ends == 2) return npmax <= 32 ? launch_t<2, 256, 32, 2, 4, true>(h, kp, st) : launch_t<2, 256, 64, 2, 4, true>(h, kp, st);
 		return npmax <= 32 ? launch_t<1, 256, 32, 2, 4, true>(h, kp, st) : launch_t<1, 256, 64, 2, 4, true>(h, kp, st);
 	}
@@ -1974,10 +1999,10 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	if (rc) return rc;
 	if (p->do_breakpoint_detection && !jout) { svg_set_error("do_breakpoint_detection needs jout"); return SVG_E_ARG; }
 	if (p->do_big_margin_filtering_for_junctions && !big_margin) { svg_set_error("big-margin filtering needs big_margin"); return SVG_E_ARG; }
-	// reads > 160 bp use fragile junction voting (gehash_go_q, core-junction.c:5205) in subjunc mode
-	if ((p->do_breakpoint_detection || p->do_big_margin_filtering_for_junctions) && h->max_read_len > 160) {
-		svg_set_error("subjunc mode supports reads up to 160 bp (announce with svg_set_max_read_length)"); return SVG_E_UNSUPPORTED;
-	}
+	// subjunc reads > 160 bp: the reference also runs fragile junction voting (gehash_go_q,
+	// core_fragile_junction_voting, core-junction.c:5151-5424) on them, which only adds junction
+	// and indel events to the event tables (host post-processing, outside this boundary); the
+	// vote records come from the regular voting below (long-read junction branch included)
 	HIPCHK(hipSetDevice(h->device));
 	hipStream_t st = stream ? (hipStream_t)stream : h->stream;
 	if (r1->n_reads == 0) return 0;
@@ -2003,7 +2028,7 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	// probes per strand are bounded by the read lengths the caller announced
 	int npmax = svg_probe_bound(h->max_read_len, h->dix.gap, p->total_subreads);
 	const bool sj = p->do_breakpoint_detection || p->do_big_margin_filtering_for_junctions;
-	if (sj && npmax > 64) { svg_set_error("subjunc mode: %d subreads per strand exceed 64", npmax); return SVG_E_UNSUPPORTED; }
+	if (npmax > 192) { svg_set_error("%d subreads per strand exceed 192", npmax); return SVG_E_UNSUPPORTED; }
 	const int ends = r2 ? 2 : 1;
 	{
 		// phase P as its own kernel per chunk of reads, then the vote kernel on its records

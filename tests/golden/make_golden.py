@@ -236,6 +236,19 @@ def main():
             lr2.append(b)
         cases.append(("pe_full_long", PROGRAM_ALIGN, True, "chr901_full", {}, ReadBatch.from_list(lr1),
                       ReadBatch.from_list(lr2), "chr901 pairs seed 15, 200/250/400 bp, fragments up to 700 bp"))
+        # subjunc long reads (161-400 bp: 6 bp subread step; the junction search adds the indel
+        # offsets of both halves); ~30% span a GT..AG intron of chr901
+        from subread_amd.sim import simulate_spliced_reads
+        sj_long = [simulate_spliced_reads(g901, 200, L, seed=16 + L) for L in (170, 250, 400)]
+        sj_long = ReadBatch.from_list([b.read(i) for b in sj_long for i in range(len(b))])
+        cases.append(("sj_se_full_long", PROGRAM_SUBJUNC, False, "chr901_full", {}, sj_long, None,
+                      "chr901 spliced reads 170/250/400 bp, seeds 186/266/416"))
+        sj_l1 = [simulate_spliced_reads(g901, 150, L, seed=30 + L) for L in (200, 300)]
+        sj_l2 = [simulate_spliced_reads(g901, 150, L, seed=40 + L) for L in (200, 300)]
+        cases.append(("sj_pe_gapped_long", PROGRAM_SUBJUNC, True, "chr901_gapped", {},
+                      ReadBatch.from_list([b.read(i) for b in sj_l1 for i in range(len(b))]),
+                      ReadBatch.from_list([b.read(i) for b in sj_l2 for i in range(len(b))]),
+                      "chr901 spliced read pairs 200/300 bp, seeds 230/330 and 240/340"))
         only = set(sys.argv[1:])
         if only:
             cases = [c for c in cases if c[0] in only]

@@ -76,6 +76,28 @@ def test_gpu_subjunc_matches_oracle_spliced(key, paired, n, gpu_indexes, index_c
     assert (got == want).all(), describe_mismatch(got, want, 2 if paired else 1, 3)
 
 
+@pytest.mark.parametrize("key,paired,length,n", [("chr901_full", False, 200, 12000), ("chr901_gapped", True, 300, 4000),
+                                                 ("chr901_full", False, 600, 3000)])
+def test_gpu_subjunc_long_reads_match_oracle(key, paired, length, n, gpu_indexes, index_cache):
+    """Subjunc mode on reads > 160 bp (6 bp subread step, long-read junction branch with
+    the halves' indel offsets; the reference's fragile junction voting only feeds event
+    tables and leaves these records unchanged -- pinned by the sj_*_long goldens)."""
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.abi import default_params, PROGRAM_SUBJUNC
+    from subread_amd.sim import Genome, simulate_spliced_reads
+    pre = index_cache.get(key)
+    g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
+    r1 = simulate_spliced_reads(g, n, length, seed=21)
+    r2 = simulate_spliced_reads(g, n, length, seed=22) if paired else None
+    p = default_params(PROGRAM_SUBJUNC, paired)
+    out, jout, bm = gpu_indexes(key).vote(p, r1, r2)
+    ref, rj, rbm, _ = OracleIndex(pre).vote(p, r1, r2, threads=16)
+    assert (rj["minor_votes"] > 0).sum() > n // 20
+    got = pack_records(out, jout, bm)
+    want = pack_records(ref, rj, rbm)
+    assert (got == want).all(), describe_mismatch(got, want, 2 if paired else 1, 3)
+
+
 @pytest.mark.parametrize("key,paired,length,n", [("chr901_full", False, 400, 20000), ("chr901_gapped", False, 300, 8000),
                                                  ("chr901_full", True, 250, 10000), ("chr901_full", False, 1500, 2000)])
 def test_gpu_long_reads_match_oracle(key, paired, length, n, gpu_indexes, index_cache):
