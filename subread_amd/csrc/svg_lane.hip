@@ -123,6 +123,10 @@ struct LParams {
 	const uint2 *precs;           // fused gather (NPF > 0): probe records, SoA [(end * 2 + strand) * nps + p][n]
 	const uint32_t *vals;
 	int nps;
+	// subjunc (lane_kernel<..., SJ = true>)
+	uint8_t *jout;                // subjunc_result_t records of the chunk
+	uint16_t *bm_out;             // big-margin records of the chunk
+	int bm_size, max_intron;
 	// paired-end (lane_pe_kernel)
 	const uint16_t *len2;
 	const uint32_t *chr_end;
@@ -336,7 +340,7 @@ __device__ __forceinline__ void write_record(const LT &L, int src, uint32_t pos,
 	}
 }
 
-template <int K, int NPF>
+template <int K, int NPF, bool SJ>
 __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 {
 	extern __shared__ __align__(16) uint8_t lds_raw[];
@@ -376,6 +380,10 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 		uint32_t rpos0 = 0, rpos1 = 0, rpos2 = 0;
 		int rv0 = 0, rv1 = 0, rv2 = 0, ru0 = 0, ru1 = 0, ru2 = 0;
 		int nc_read = 0;
+		// subjunc: the read's big-margin records (insert_big_margin_record, core-junction.c:789-811):
+		// votes | start << 16 ... as (votes, start | end << 16) per record
+		uint32_t bv0 = 0, bv1 = 0, bv2 = 0, bs0 = 0, bs1 = 0, bs2 = 0;
+		const int nbm = SJ ? (lp.bm_size >= 3 ? lp.bm_size / 3 : 0) : 0;
 		for (int st = 0; st < 2; st++) {
 			if constexpr (NPF == 0) {
 			const int cnt = L.dfr ? 0 : (int)lp.ccnt[(size_t)st * lp.cs + k];
@@ -461,6 +469,36 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				if (mb > 1 && rv1 > 0) ltop3(t0, t1, t2, rv1);
 				if (mb > 2 && rv2 > 0) ltop3(t0, t1, t2, rv2);
 				const bool ok0 = t0 >= 1, ok1 = ok0 && t1 >= 1 && t0 - t1 <= cutoff, ok2 = ok1 && t2 >= 1 && t0 - t2 <= cutoff;
+				if constexpr (SJ) {
+					// big-margin records: every slot the first value's row-major scan visits before
+					// max_vote_simples slots of that value are taken (core-junction.c:2276-2277)
+					if (ok0 && nbm > 0) {
+						int taken = 0;
+						for (uint32_t row = 0; row < LROWS && taken < mvs; row++) {
+							uint32_t q = L.template head<0>(row);
+							while (q != Lane<K>::NIL && taken < mvs) {
+								const uint32_t M = L.pm[q * 64 + L.lane].y;
+								const int v = lm_votes(M);
+								if (v >= t2) {
+									const uint32_t w0 = *L.cw(st, (int)q, 0);
+									const int rs = (int)(w0 & 0xffu), re = (int)((w0 >> 8) & 0xffu);
+									const uint32_t vv = (uint32_t)(v & 255);
+									const uint32_t se = st ? ((uint32_t)(uint16_t)(len - re) | ((uint32_t)(uint16_t)(len - rs) << 16))
+									                       : ((uint32_t)rs | ((uint32_t)re << 16));
+									const int x1 = vv >= bv0 ? 0 : (nbm > 1 && vv >= bv1) ? 1 : (nbm > 2 && vv >= bv2) ? 2 : 3;
+									if (x1 < nbm) {
+										if (x1 <= 1 && nbm > 2) { bv2 = bv1; bs2 = bs1; }
+										if (x1 == 0 && nbm > 1) { bv1 = bv0; bs1 = bs0; }
+										PUT3(x1, bv0, bv1, bv2, vv);
+										PUT3(x1, bs0, bs1, bs2, se);
+									}
+								}
+								if (v == t0 && v >= mvsec) taken++;
+								q = lm_next(M);
+							}
+						}
+					}
+				}
 				// table slots of each value in row-major order (row, then slot order = pool order)
 				uint32_t a0 = ~0u, b0 = ~0u, c0 = ~0u, a1 = ~0u, b1 = ~0u, c1 = ~0u, a2 = ~0u, b2 = ~0u, c2 = ~0u;
 				for (int s = 0; s < L.nslots; s++) {
@@ -517,6 +555,38 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				if (ns > 0) emit(sk0, sp0, sv0);
 				if (ns > 1) emit(sk1, sp1, sv1);
 				if (ns > 2) emit(sk2, sp2, sv2);
+				if constexpr (SJ) {
+					// junction part of copy_vote_to_alignment_res (core-junction.c:1073-1334) for each
+					// result taken from this table: a minor half that passes test_junction_minor and
+					// the overlap / distance tests would go to donor_score -- such reads are voted by
+					// the wave kernel; for every other read the junction records stay empty
+					for (int c = 0; c < cur && !L.dfr; c++) {
+						const int src = sel3(c, ts0, ts1, ts2);
+						if (src < 0 || (src >> 6) != st) continue;
+						const int sM = src & 63;
+						const uint2 eM = L.pm[sM * 64 + L.lane];
+						const int vM = lm_votes(eM.y);
+						const uint32_t wM = *L.cw(st, sM, 0);
+						const int csM = (int)(wM & 0xffu), ceM = (int)((wM >> 8) & 0xffu);
+						for (int q = 0; q < L.nslots; q++) {
+							if (q == sM) continue;
+							const uint2 e2 = L.pm[q * 64 + L.lane];
+							if (vM < lm_votes(e2.y)) continue;
+							const long long dist = (long long)eM.x - (long long)e2.x;
+							if ((dist < 0 ? -dist : dist) > (long long)lp.max_intron) continue;
+							const uint32_t w2 = *L.cw(st, q, 0);
+							const int cs2 = (int)(w2 & 0xffu), ce2 = (int)((w2 >> 8) & 0xffu);
+							if (csM == cs2 || ceM == ce2) continue;
+							if (csM > cs2 ? eM.x < e2.x : eM.x > e2.x) continue;
+							const int ov = csM > cs2 ? ce2 - csM : ceM - cs2;
+							if (ov > 14 || abs((int)dist) < 6) continue;
+							L.dfr = true;
+							L.why = 2;
+							break;
+						}
+					}
+					if (L.dfr) continue;
+				}
 				if (cur > 0) { rsrc0 = ts0; rpos0 = tp0; rv0 = tv0; ru0 = tu0; } else rv0 = 0;
 				if (cur > 1) { rsrc1 = ts1; rpos1 = tp1; rv1 = tv1; ru1 = tu1; } else rv1 = 0;
 				if (cur > 2) { rsrc2 = ts2; rpos2 = tp2; rv2 = tv2; ru2 = tu2; } else rv2 = 0;
@@ -525,6 +595,18 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 			}
 		}
 		if (!L.dfr) ncand += (unsigned long long)nc_read;
+		if constexpr (SJ) {
+			if (!L.dfr && lp.bm_out) {
+				uint16_t *bd = lp.bm_out + (size_t)r * SVG_BIG_MARGIN_WORDS;
+				const uint32_t bvv[3] = {bv0, bv1, bv2}, bss[3] = {bs0, bs1, bs2};
+#pragma unroll
+				for (int k = 0; k < 3; k++) {
+					bd[3 * k] = (uint16_t)bvv[k];
+					bd[3 * k + 1] = (uint16_t)(bss[k] & 0xffffu);
+					bd[3 * k + 2] = (uint16_t)(bss[k] >> 16);
+				}
+			}
+		}
 		// ---- the read's multi_best records (copy_vote_to_alignment_res, core-junction.c:1058-1071;
 		// indel_recorder_copy, sorted-hashtable.c:1144)
 		if (!L.dfr) {
@@ -536,6 +618,11 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				const int u = sel3(i, ru0, ru1, ru2);
 				uint32_t w[17];
 				write_record(L, src, pos, v, u, w);
+				if constexpr (SJ) {
+					// no minor half on the lane path: empty subjunc_result_t
+					uint4 *jd = (uint4 *)(lp.jout + ((size_t)r * mb + i) * 16);
+					*jd = make_uint4(0u, 0u, 0u, 0u);
+				}
 #pragma unroll
 				for (int k = 0; k < 17; k++) dst[i * 17 + k] = w[k];
 				nres += v > 0;
@@ -930,6 +1017,7 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 // ---------------------------------------------------------------------------------------------
 #define LANE_K1 20   // slots per lane: 10 KB LDS per wave = the 4 waves/SIMD the VGPRs allow
 #define LANE_NPF 10   // probe records per strand held in registers by the fused light pass
+#define LANE_NPF_SJ 14   // subjunc: -n 14
 #define LANE_CAP1 40
 #define LANE_K2 64
 #define LANE_CAP2 192
@@ -954,7 +1042,8 @@ static int lane_launch(svg_index *h, LParams &lp, uint32_t **cold, size_t *cold_
 	lp.cold = *cold;
 	int rc = svg_timing_mark(h, 3, 0, st);
 	if (rc) return rc;
-	hipLaunchKernelGGL((lane_kernel<K, NPF>), dim3((unsigned)blocks), dim3(64), lds, st, lp);
+	if (lp.jout) hipLaunchKernelGGL((lane_kernel<K, NPF == 0 ? 0 : LANE_NPF_SJ, true>), dim3((unsigned)blocks), dim3(64), lds, st, lp);
+	else hipLaunchKernelGGL((lane_kernel<K, NPF, false>), dim3((unsigned)blocks), dim3(64), lds, st, lp);
 	HIPCHK(hipGetLastError());
 	return svg_timing_mark(h, 3, 1, st);
 }
@@ -975,7 +1064,10 @@ int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int s
 {
 	const char *e = getenv("SVG_LANE");
 	if (e && e[0] == '0') return 0;
-	if (sj || h->max_read_len > 160) return 0;
+	if (h->max_read_len > 160) return 0;
+	// subjunc: single end, junction search on (the lane path carries big-margin records and
+	// defers every read that needs donor scoring)
+	if (sj && (paired || !p->do_breakpoint_detection || p->max_insertion_at_junctions)) return 0;
 	int tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
 	if (tol > 5 || p->total_subreads > 31 || p->multi_best > 3 || p->top_scores != 3) return 0;
 	if (!paired && p->max_vote_simples > 3) return 0;
@@ -1051,7 +1143,8 @@ int svg_lane_pe_chunk(svg_index *h, const svg_params *p, const uint16_t *len1, c
 }
 
 int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint32_t n, const uint2 *precs, int nps,
-                   uint8_t *out, unsigned long long *stats, uint32_t **defer_list, uint32_t **defer_count, hipStream_t st)
+                   uint8_t *out, uint8_t *jout, uint16_t *bm, unsigned long long *stats, uint32_t **defer_list,
+                   uint32_t **defer_count, hipStream_t st)
 {
 	const uint32_t n2 = n / 4 + 64;   // heavy-pass columns
 	const char *e = getenv("SVG_LANE");
@@ -1080,7 +1173,8 @@ int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint3
 	g.cs = n; g.idx = NULL; g.idx_count = NULL;
 	// reads of <= LANE_NPF probes per strand (the full index at the default -n): the gather is
 	// fused into the lane kernel; otherwise the gather kernel writes candidate lists first
-	const bool fused = nps <= LANE_NPF && !(e && e[0] == '1' && e[1] == 'g');   // "1g": unfused (testing)
+	const bool sjm = jout != NULL;   // subjunc (lane_kernel<..., true>)
+	const bool fused = nps <= (sjm ? LANE_NPF_SJ : LANE_NPF) && !(e && e[0] == '1' && e[1] == 'g');   // "1g": unfused (testing)
 	int rc = 0;
 	if (!fused && (rc = gather_launch(h, g, st))) return rc;
 	LParams lp;
@@ -1093,12 +1187,16 @@ int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint3
 	lp.multi_best = p->multi_best; lp.max_vote_simples = p->max_vote_simples; lp.cutoff = p->max_vote_number_cutoff;
 	lp.min_votes_first = p->min_votes_first; lp.min_votes_second = p->min_votes_second;
 	lp.out = out;
+	lp.jout = jout;
+	lp.bm_out = p->do_big_margin_filtering_for_junctions ? bm : NULL;
+	lp.bm_size = p->do_big_margin_filtering_for_junctions ? p->big_margin_record_size : 0;
+	lp.max_intron = p->maximum_intron_length;
 	lp.defer_list = (uint32_t *)(b + o_l1);
 	lp.defer_count = cnt;
 	lp.defer_all = e && e[0] == '2';
 	lp.stats = stats;
 	lp.stat_base = 16;
-	lp.final_pass = !two;
+	lp.final_pass = !two || sjm;
 	lp.cs = n; lp.idx = NULL; lp.idx_count = NULL;
 	{
 		// tuning knobs (diagnostics): SVG_LANE_K=16|20|24, SVG_LANE_CAP
@@ -1107,6 +1205,7 @@ int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint3
 		if (ec && atoi(ec) > 0 && atoi(ec) <= LANE_CAP1) lp.cap = atoi(ec);
 		if (ec && atoi(ec) > LANE_CAP1 && fused) lp.cap = atoi(ec) < 64 ? atoi(ec) : 64;
 		if (!fused) rc = lane_launch<LANE_K1, 0>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
+		else if (sjm) rc = lane_launch<LANE_K1, LANE_NPF_SJ>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
 		else if (kk == 16) rc = lane_launch<16, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
 		else if (kk == 24) rc = lane_launch<24, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
 		else rc = lane_launch<LANE_K1, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
@@ -1114,7 +1213,7 @@ int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint3
 	if (rc) return rc;
 	*defer_list = lp.defer_list;
 	*defer_count = cnt;
-	if (!two) return 0;
+	if (!two || sjm) return 0;
 	// heavy pass over pass 1's deferral list
 	g.cap = LANE_CAP2;
 	g.cand = (uint32_t *)(b + o_c2); g.cpk = (uint16_t *)(b + o_p2); g.ccnt = (uint16_t *)(b + o_n2);

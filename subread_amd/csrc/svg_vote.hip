@@ -2050,7 +2050,7 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 		pp.stats = kp.stats;
 		// align mode, reads <= 160 bp: lane-per-read (SE) / lane-per-pair (PE) fast path
 		// (svg_lane.hip), probe records in SoA layout
-		const bool lane = svg_lane_eligible(h, p, r2 != NULL, sj) != 0 && (!r2 || nps <= 10);
+		const bool lane = svg_lane_eligible(h, p, r2 != NULL, sj) != 0 && (!r2 || nps <= 10) && (!sj || nps <= 14);
 		pp.soa = lane ? 1 : 0;
 		pp.window = h->dix.nb >= 131073u && !getenv("SVG_NO_WINDOW");   // key_hi <= 32767: int16 order == key order
 		{ const char *e = getenv("SVG_PROBE_MAP"); pp.readmajor = !(e && e[0] == '0'); }
@@ -2083,7 +2083,8 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 				// vote_kernel below, which reads the SoA probe records of the deferred reads
 				uint32_t *dl = NULL, *dc = NULL;
 				rc = r2 ? svg_lane_pe_chunk(h, p, kc.len1, kc.len2, (uint32_t)cn, kc.precs, nps, kc.out, kp.stats, &dl, &dc, st)
-				        : svg_lane_chunk(h, p, kc.len1, (uint32_t)cn, kc.precs, nps, kc.out, kp.stats, &dl, &dc, st);
+				        : svg_lane_chunk(h, p, kc.len1, (uint32_t)cn, kc.precs, nps, kc.out, sj ? kc.jout : NULL, kc.bm_out,
+				                         kp.stats, &dl, &dc, st);
 				if (rc) return rc;
 				kc.prec_stride = (uint32_t)cn;
 				kc.idx = dl;

@@ -154,3 +154,47 @@ def test_lane_pe_modes_match_oracle(key, n, length, params, mode, gpu_indexes, i
         assert st["deferred"] == n
     elif mode == "1" and key.startswith("chr901"):
         assert st["deferred"] < n // 2, st      # repeat-rich chr901 + discordant pairs defer more
+
+
+SJ_SE = [n for n in golden_names() if n.startswith("sj_se_")]
+
+
+@pytest.mark.parametrize("mode", PE_MODES)
+@pytest.mark.parametrize("name", SJ_SE)
+def test_lane_sj_modes_match_reference_golden(name, mode, gpu_indexes, monkeypatch):
+    """Subjunc SE on the lane path (big-margin records, junction pre-filter deferring
+    every read that needs donor scoring) on the reference's subjunc records."""
+    monkeypatch.setenv("SVG_LANE", mode)
+    c = Case(name)
+    ix = gpu_indexes(c.index_key)
+    out, jout, bm = ix.vote(c.params, c.r1, c.r2)
+    got = pack_records(out, jout, bm)
+    assert (got == c.expected).all(), describe_mismatch(got, c.expected, c.ends, c.params.multi_best)
+
+
+@pytest.mark.parametrize("mode", PE_MODES)
+@pytest.mark.parametrize("key,n,length,params", [("chr901_full", 60000, 100, {}), ("synth4242_full", 30000, 120, {}),
+                                                 ("chr901_full", 20000, 150, {"big_margin_record_size": 6}),
+                                                 ("chr901_full", 20000, 100, {"maximum_intron_length": 2000,
+                                                                              "big_margin_record_size": 3})])
+def test_lane_sj_modes_match_oracle(key, n, length, params, mode, gpu_indexes, index_cache, monkeypatch):
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.abi import default_params, PROGRAM_SUBJUNC
+    from subread_amd.sim import Genome, simulate_spliced_reads
+    monkeypatch.setenv("SVG_LANE", mode)
+    pre = index_cache.get(key)
+    g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
+    r1 = simulate_spliced_reads(g, n, length, seed=61)
+    p = default_params(PROGRAM_SUBJUNC, False, **params)
+    ix = gpu_indexes(key)
+    ix.set_stats(True)
+    out, jout, bm = ix.vote(p, r1)
+    st = ix.stats()
+    ix.set_stats(False)
+    ref, rj, rbm, _ = OracleIndex(pre).vote(p, r1, threads=16)
+    got, want = pack_records(out, jout, bm), pack_records(ref, rj, rbm)
+    assert (got == want).all(), describe_mismatch(got, want, 1, p.multi_best)
+    if mode == "2":
+        assert st["deferred"] == n
+    elif mode == "1" and key.startswith("chr901"):
+        assert st["deferred"] < n * 3 // 4, st
