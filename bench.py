@@ -221,16 +221,20 @@ def main():
     launches_per_step = kernels[dom]["launches_per_step"]
     vote_bytes = kbytes[dom]
 
-    # HBM traffic from the committed PMC passes of this workload (tools/pmc_traffic.py;
-    # rocprofv3 cannot run inside this process), scaled to this launch's read count
+    # HBM traffic of the dominant kernel from the committed PMC passes of this workload
+    # (tools/profile_workload.sh -> profiles/r*_<workload>_kernels*.json; rocprofv3 cannot run
+    # inside this process), per launch, scaled to this run's reads per launch
     traffic, traffic_src = None, None
     import glob
-    tj = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_traffic.json" % args.workload)))
+    tj = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_kernels*.json" % args.workload)))
     if tj:
         t = json.load(open(tj[-1]))
-        traffic = round(t["traffic_bytes_per_read"] * n / 1e9, 3)
-        traffic_src = "%s (FETCH_SIZE+WRITE_SIZE, %.0f B/read, GB per launch)" % (
-            os.path.relpath(tj[-1], ROOT), t["traffic_bytes_per_read"])
+        kd = t.get("kernels", {}).get(dom)
+        if kd:
+            per_read = kd["traffic_bytes_per_read"]
+            traffic = round(per_read * n / launches_per_step / 1e9, 3)
+            traffic_src = "%s (%s FETCH_SIZE+WRITE_SIZE, %.0f B/read, GB per launch)" % (
+                os.path.relpath(tj[-1], ROOT), dom, per_read)
 
     check = None
     oi = None
@@ -283,7 +287,7 @@ def main():
                        "parallelism": "reads sharded across %d GPU(s), index replicated, no collective" % world},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(vote_achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(vote_achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic, "traffic_unit": "GB per step (all kernels of the step)",
+                         "traffic": traffic, "traffic_unit": "GB per launch",
                          "traffic_source": traffic_src,
                          "launch_ms": round(vote_launch_s * 1e3, 3), "launches_per_step": launches_per_step,
                          "algorithmic_bytes_per_read": round(vote_bytes / n, 1),
