@@ -29,6 +29,8 @@ KERNELS = ("probe_kernel", "gather_kernel", "lane_kernel", "vote_kernel")
 
 
 def short(name):
+    if "lane_pe_kernel" in name:      # bench.py times both lane kernels as "lane_kernel"
+        return "lane_kernel"
     for k in KERNELS:
         if k in name:
             return k
