@@ -40,9 +40,13 @@ struct svg_index {
 	uint64_t device_bytes;
 	int n_cu;
 	int max_read_len;        // announced read-length bound (svg_set_max_read_length), picks the kernel variant
-	void *d_prec; size_t prec_cap;   // probe records of one chunk
+	// chunk pipeline: probe + lane kernels of chunk c run on the caller's stream while the wave
+	// kernel of chunk c-1 runs on stream2, so the per-chunk buffers come in two slots (c & 1)
+	hipStream_t stream2;
+	hipEvent_t ev_lane[2], ev_wave[2];   // slot's records + deferral list ready / wave kernel done
+	void *d_prec[2]; size_t prec_cap[2];   // probe records of one chunk
 	// lane-per-read SE path (svg_lane.hip): candidate lists + deferral list, per-wave cold scratch
-	void *d_lane; size_t lane_cap;
+	void *d_lane[2]; size_t lane_cap[2];
 	uint32_t *d_lscratch; size_t lscratch_words;     // light pass
 	uint32_t *d_lscratch2; size_t lscratch2_words;   // heavy pass
 	// svg_set_timing: event pairs per launch (kinds: 0 probe_kernel, 1 vote_kernel, 2 gather_kernel,
@@ -70,10 +74,10 @@ int svg_index_finish_device(svg_index *h);
 
 // svg_lane.hip
 int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int sj);
-int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint32_t n, const uint2 *precs, int nps,
-                   uint8_t *out, uint8_t *jout, uint16_t *bm, unsigned long long *stats, uint32_t **defer_list,
+int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *len, uint32_t n, const uint2 *precs,
+                   int nps, uint8_t *out, uint8_t *jout, uint16_t *bm, unsigned long long *stats, uint32_t **defer_list,
                    uint32_t **defer_count, hipStream_t st);
-int svg_lane_pe_chunk(svg_index *h, const svg_params *p, const uint16_t *len1, const uint16_t *len2, uint32_t n,
+int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *len1, const uint16_t *len2, uint32_t n,
                       const uint2 *precs, int nps, uint8_t *out, unsigned long long *stats, uint32_t **defer_list,
                       uint32_t **defer_count, hipStream_t st);
 int svg_timing_mark(svg_index *h, int k, int phase, hipStream_t st);

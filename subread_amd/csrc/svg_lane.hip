@@ -1079,20 +1079,20 @@ int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int s
 #define LANE_PE_CAP 40
 
 // paired-end: lane_pe_kernel over every pair of the chunk; deferred pairs listed for vote_kernel
-int svg_lane_pe_chunk(svg_index *h, const svg_params *p, const uint16_t *len1, const uint16_t *len2, uint32_t n,
+int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *len1, const uint16_t *len2, uint32_t n,
                       const uint2 *precs, int nps, uint8_t *out, unsigned long long *stats, uint32_t **defer_list,
                       uint32_t **defer_count, hipStream_t st)
 {
 	const char *e = getenv("SVG_LANE");
 	const size_t o_l1 = 0, o_cnt = (o_l1 + (size_t)4 * n + 255) & ~(size_t)255, need = o_cnt + 256;
-	if (need > h->lane_cap) {
-		hipFree(h->d_lane);
-		h->d_lane = NULL;
-		h->lane_cap = 0;
-		if (dmalloc(h, &h->d_lane, need)) return SVG_E_NOMEM;
-		h->lane_cap = need;
+	if (need > h->lane_cap[slot]) {
+		hipFree(h->d_lane[slot]);
+		h->d_lane[slot] = NULL;
+		h->lane_cap[slot] = 0;
+		if (dmalloc(h, &h->d_lane[slot], need)) return SVG_E_NOMEM;
+		h->lane_cap[slot] = need;
 	}
-	uint8_t *b = (uint8_t *)h->d_lane;
+	uint8_t *b = (uint8_t *)h->d_lane[slot];
 	uint32_t *cnt = (uint32_t *)(b + o_cnt);   // [0] deferrals, [2] wave-kernel work counter
 	HIPCHK(hipMemsetAsync(cnt, 0, 16, st));
 	if (nps > LANE_NPF) { svg_set_error("lane_pe: %d probes per strand", nps); return SVG_E_UNSUPPORTED; }
@@ -1142,7 +1142,7 @@ int svg_lane_pe_chunk(svg_index *h, const svg_params *p, const uint16_t *len1, c
 	return 0;
 }
 
-int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint32_t n, const uint2 *precs, int nps,
+int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *len, uint32_t n, const uint2 *precs, int nps,
                    uint8_t *out, uint8_t *jout, uint16_t *bm, unsigned long long *stats, uint32_t **defer_list,
                    uint32_t **defer_count, hipStream_t st)
 {
@@ -1155,14 +1155,14 @@ int svg_lane_chunk(svg_index *h, const svg_params *p, const uint16_t *len, uint3
 	const size_t o_p2 = o_c2 + (size_t)8 * LANE_CAP2 * n2, o_n2 = o_p2 + (size_t)4 * LANE_CAP2 * n2;
 	const size_t o_l1 = (o_n2 + (size_t)4 * n2 + 255) & ~(size_t)255, o_l2 = o_l1 + (size_t)4 * n + 256;
 	const size_t o_cnt = o_l2 + (size_t)4 * n + 256, need = o_cnt + 256;
-	if (need > h->lane_cap) {
-		hipFree(h->d_lane);
-		h->d_lane = NULL;
-		h->lane_cap = 0;
-		if (dmalloc(h, &h->d_lane, need)) return SVG_E_NOMEM;
-		h->lane_cap = need;
+	if (need > h->lane_cap[slot]) {
+		hipFree(h->d_lane[slot]);
+		h->d_lane[slot] = NULL;
+		h->lane_cap[slot] = 0;
+		if (dmalloc(h, &h->d_lane[slot], need)) return SVG_E_NOMEM;
+		h->lane_cap[slot] = need;
 	}
-	uint8_t *b = (uint8_t *)h->d_lane;
+	uint8_t *b = (uint8_t *)h->d_lane[slot];
 	// [0] pass-1 deferrals, [1] pass-2 deferrals, [2] / [3] wave-kernel work counters after pass 1 / 2
 	uint32_t *cnt = (uint32_t *)(b + o_cnt);
 	HIPCHK(hipMemsetAsync(cnt, 0, 16, st));

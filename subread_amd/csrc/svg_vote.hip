@@ -1467,7 +1467,14 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 	const uint32_t total = pp.n_reads * per_read;
 	const int gap = ix.gap;
 	unsigned long long st_p = 0, st_i = 0, st_h = 0;
-	for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
+	// each block walks one contiguous range of 256-probe tiles: blocks are dealt round-robin to
+	// the 8 XCDs, so a grid-stride walk would put neighbouring reads (which share the lines of
+	// the SoA record rows) on different L2s and turn every record store into a partial-line write
+	const uint32_t tiles = (total + 255u) / 256u, per_blk = (tiles + gridDim.x - 1u) / gridDim.x;
+	const uint32_t tile_end = min(tiles, (blockIdx.x + 1u) * per_blk);
+	for (uint32_t tile = blockIdx.x * per_blk; tile < tile_end; tile++) {
+		const uint32_t t = tile * 256u + threadIdx.x;
+		if (t >= total) break;
 		uint32_t r, rem;
 		if (pp.soa && !pp.readmajor) { rem = t / pp.n_reads; r = t - rem * pp.n_reads; }
 		else { r = t / per_read; rem = t - r * per_read; }
@@ -1674,6 +1681,11 @@ int svg_index_finish_device(svg_index *h)
 	if ((rc = dmalloc(h, &h->d_values, (size_t)x->values_bytes + 64)) || (rc = dmalloc(h, &h->d_chr, 4 * (size_t)x->n_chr + 64)))
 		return rc;
 	HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+	HIPCHK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+	for (int s = 0; s < 2; s++) {
+		HIPCHK(hipEventCreateWithFlags(&h->ev_lane[s], hipEventDisableTiming));
+		HIPCHK(hipEventCreateWithFlags(&h->ev_wave[s], hipEventDisableTiming));
+	}
 	HIPCHK(hipMemcpy(h->d_values, x->values, x->values_bytes, hipMemcpyHostToDevice));
 	HIPCHK(hipMemcpy(h->d_chr, x->chr_end, 4 * (size_t)x->n_chr, hipMemcpyHostToDevice));
 	h->dix.bstart = (const uint32_t *)h->d_bstart;
@@ -1773,9 +1785,15 @@ extern "C" void svg_index_close(svg_index *h)
 	if (!h) return;
 	hipSetDevice(h->device);
 	if (h->stream) hipStreamSynchronize(h->stream);
-	hipFree(h->d_prec);
-	hipFree(h->d_lane);
+	if (h->stream2) hipStreamSynchronize(h->stream2);
+	for (int s = 0; s < 2; s++) {
+		hipFree(h->d_prec[s]);
+		hipFree(h->d_lane[s]);
+		if (h->ev_lane[s]) hipEventDestroy(h->ev_lane[s]);
+		if (h->ev_wave[s]) hipEventDestroy(h->ev_wave[s]);
+	}
 	hipFree(h->d_lscratch);
+	hipFree(h->d_lscratch2);
 	for (int k = 0; k < 4; k++)
 		for (int i = 0; i < 64; i++)
 			for (int j = 0; j < 2; j++)
@@ -1784,6 +1802,7 @@ extern "C" void svg_index_close(svg_index *h)
 	hipFree(h->d_bgrp); hipFree(h->d_keys8);
 	hipFree(h->d_scratch); hipFree(h->d_stats); hipFree(h->d_in); hipFree(h->d_out);
 	if (h->stream) hipStreamDestroy(h->stream);
+	if (h->stream2) hipStreamDestroy(h->stream2);
 	svg_host_index_free(&h->host);
 	free(h);
 }
@@ -2038,7 +2057,17 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 		if (chunk > (uint64_t)0x7fffffff / per_read) chunk = (uint64_t)0x7fffffff / per_read;
 		if (chunk > kp.n_reads) chunk = kp.n_reads;
 		if (chunk < 1) chunk = 1;
-		if ((rc = ensure(h, &h->d_prec, &h->prec_cap, chunk * per_read * 8))) return rc;
+		// chunk pipeline: the wave kernel of chunk c runs on stream2 while the probe and lane
+		// kernels of chunk c+1 run on st; slot c & 1 holds a chunk's probe records and lane
+		// buffers until its wave kernel is done.  On by default for single-end align only
+		// (C3: 289 -> 304 Mreads/s; PE and subjunc, whose wave kernels are 2-3x longer, lost
+		// 1-2%: the kernels time-share the CUs there).  SVG_OVERLAP=0/1 forces it off/on.
+		const char *eo = getenv("SVG_OVERLAP");
+		const bool overlap = (eo ? eo[0] == '1' : (!sj && !r2)) && chunk < kp.n_reads;
+		hipStream_t st2 = overlap ? h->stream2 : st;
+		for (int s = 0; s < (overlap ? 2 : 1); s++)
+			if ((rc = ensure(h, &h->d_prec[s], &h->prec_cap[s], chunk * per_read * 8))) return rc;
+		bool slot_busy[2] = {false, false};
 		PParams pp;
 		memset(&pp, 0, sizeof pp);
 		pp.ix = h->dix;
@@ -2046,7 +2075,6 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 		pp.nps = nps;
 		pp.total_subreads = p->total_subreads; pp.reverse_r1 = p->reverse_r1; pp.reverse_r2 = p->reverse_r2;
 		pp.nb_magic = ~0ull / h->dix.nb + 1;   // ceil(2^64 / nb), nb is not a power of two
-		pp.out = (uint2 *)h->d_prec;
 		pp.stats = kp.stats;
 		// align mode, reads <= 160 bp: lane-per-read (SE) / lane-per-pair (PE) fast path
 		// (svg_lane.hip), probe records in SoA layout
@@ -2057,6 +2085,9 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 		const uint64_t n = kp.n_reads;
 		for (uint64_t c0 = 0; c0 < n && !rc; c0 += chunk) {
 			const uint64_t cn = n - c0 < chunk ? n - c0 : chunk;
+			const int slot = overlap ? (int)((c0 / chunk) & 1) : 0;
+			if (slot_busy[slot]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[slot], 0));
+			pp.out = (uint2 *)h->d_prec[slot];
 			pp.off1 = kp.off1 + c0; pp.len1 = kp.len1 + c0;
 			if (r2) { pp.off2 = kp.off2 + c0; pp.len2 = kp.len2 + c0; }
 			pp.n_reads = (uint32_t)cn;
@@ -2076,14 +2107,14 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 			kc.out = kp.out + c0 * ends * p->multi_best * 68;
 			if (kp.jout) kc.jout = kp.jout + c0 * ends * p->multi_best * 16;
 			if (kp.bm_out) kc.bm_out = kp.bm_out + c0 * ends * SVG_BIG_MARGIN_WORDS;
-			kc.precs = (const uint2 *)h->d_prec;
+			kc.precs = (const uint2 *)h->d_prec[slot];
 			kc.nps = nps;
 			if (lane) {
 				// gather + lane kernels vote every read they can; the rest (deferral list) go to
 				// vote_kernel below, which reads the SoA probe records of the deferred reads
 				uint32_t *dl = NULL, *dc = NULL;
-				rc = r2 ? svg_lane_pe_chunk(h, p, kc.len1, kc.len2, (uint32_t)cn, kc.precs, nps, kc.out, kp.stats, &dl, &dc, st)
-				        : svg_lane_chunk(h, p, kc.len1, (uint32_t)cn, kc.precs, nps, kc.out, sj ? kc.jout : NULL, kc.bm_out,
+				rc = r2 ? svg_lane_pe_chunk(h, slot, p, kc.len1, kc.len2, (uint32_t)cn, kc.precs, nps, kc.out, kp.stats, &dl, &dc, st)
+				        : svg_lane_chunk(h, slot, p, kc.len1, (uint32_t)cn, kc.precs, nps, kc.out, sj ? kc.jout : NULL, kc.bm_out,
 				                         kp.stats, &dl, &dc, st);
 				if (rc) return rc;
 				kc.prec_stride = (uint32_t)cn;
@@ -2091,10 +2122,21 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 				kc.idx_count = dc;
 				kc.work = dc + 2;
 			}
-			if ((rc = timing_mark(h, 1, 0, st))) return rc;
-			rc = launch_vote(h, kc, st, npmax, sj, ends);
-			if (!rc) rc = timing_mark(h, 1, 1, st);
+			if (overlap) {
+				HIPCHK(hipEventRecord(h->ev_lane[slot], st));
+				HIPCHK(hipStreamWaitEvent(st2, h->ev_lane[slot], 0));
+			}
+			if ((rc = timing_mark(h, 1, 0, st2))) return rc;
+			rc = launch_vote(h, kc, st2, npmax, sj, ends);
+			if (!rc) rc = timing_mark(h, 1, 1, st2);
+			if (!rc && overlap) {
+				HIPCHK(hipEventRecord(h->ev_wave[slot], st2));
+				slot_busy[slot] = true;
+			}
 		}
+		// join: the caller's stream sees every wave kernel of the batch
+		for (int s = 0; s < 2 && overlap; s++)
+			if (slot_busy[s]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[s], 0));
 	}
 	if (rc) return rc;
 	if (h->stats_on) {
