@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
+    ap.add_argument("--host-reads", type=int, default=16_000_000)
     args = ap.parse_args()
 
     import torch
@@ -256,6 +258,43 @@ def main():
             want += [rj.view(np.uint8).reshape(m, -1), rbm.view(np.uint8).reshape(m, -1)]
         check = bool(all((a == b).all() for a, b in zip(got, want)))
         log("[bench] parity spot check on %d reads: %s" % (m, "IDENTICAL" if check else "MISMATCH"))
+    host = None
+    if rank == 0 and not args.no_host:
+        # the drop-in entry point with host buffers (svg_vote_batch), PCIe both ways included
+        # (sub-batch pipeline): reads and records in pinned host memory (SURVEY.md §8(d)'s
+        # definition), and in pageable numpy memory.  Reported beside `value`, never as it.
+        from subread_amd.abi import ReadBatch
+        m = min(n, args.host_reads)
+        keep = []
+
+        def pinned(a):
+            t = torch.empty(max(1, a.nbytes), dtype=torch.uint8, pin_memory=True)
+            keep.append(t)
+            v = t.numpy()[:a.nbytes].view(a.dtype).reshape(a.shape)
+            v[...] = a
+            return v
+
+        def run(h1, h2, bufs):
+            ix.vote(p, h1, h2, bufs=bufs)      # first call sizes the staging buffers
+            t1 = time.perf_counter()
+            ix.vote(p, h1, h2, bufs=bufs)
+            return time.perf_counter() - t1
+
+        h1, h2 = rb.slice(0, m), (rb2.slice(0, m) if rb2 is not None else None)
+        t_page = run(h1, h2, ix.vote(p, h1, h2))
+        pin_batch = lambda b: ReadBatch(pinned(b.seq[:int(b.offsets[m - 1]) + int(b.lens[m - 1])]),
+                                        pinned(b.offsets[:m]), pinned(b.lens[:m]))
+        p1, p2 = pin_batch(rb), (pin_batch(rb2) if rb2 is not None else None)
+        o, j, bmh = ix.vote(p, h1, h2)
+        bufs = (pinned(o), pinned(j) if j is not None else None, pinned(bmh) if bmh is not None else None)
+        t_pin = run(p1, p2, bufs)
+        host = {"value": round(m * ends / t_pin / 1e6, 3), "unit": "Mreads/s", "reads": m * ends,
+                "seconds": round(t_pin, 4), "pageable_value": round(m * ends / t_page / 1e6, 3),
+                "entry": "svg_vote_batch: ASCII reads in, records out, PCIe both ways included; value = pinned "
+                "host buffers (torch pin_memory), pageable_value = numpy buffers (output reused)"}
+        log("[bench] host-buffer path: %.1f Mreads/s pinned, %.1f pageable, over %d reads" % (
+            host["value"], host["pageable_value"], m * ends))
+        del keep, bufs, p1, p2
     cpu = None
     if rank == 0 and not args.no_cpu:
         # bounded CPU sample: chunks of the same reads until >= 10 s of CPU work
@@ -295,6 +334,7 @@ def main():
                          "deferred_reads": st.get("deferred", 0),
                          "path": {"achieved": round(achieved, 2), "algorithmic_bytes_per_read": round(algo_bytes / n, 1),
                                   "step_ms": round(avg_kern_s * 1e3, 3), "frac": round(achieved / HBM_PEAK_GBS, 5)}},
+            "host_path": host,
             "cpu_baseline": cpu,
             "parity_check": check,
         }

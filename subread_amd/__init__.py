@@ -214,15 +214,29 @@ class VoteIndex:
         return {"probes": s.probes, "bucket_items": s.bucket_items, "hits": s.hits, "results": s.results,
                 "deferred": s.deferred}
 
-    def vote(self, params, r1, r2=None):
-        """Host buffers in, host records out: (mapping[n,ends,mb], subjunc|None, big_margin|None)."""
+    def vote(self, params, r1, r2=None, bufs=None):
+        """Host buffers in, host records out: (mapping[n,ends,mb], subjunc|None, big_margin|None).
+        `bufs` = a previous call's return value of the same shape, reused as the output
+        (the reference's bigtable is likewise allocated once and rewritten per chunk)."""
         n = len(r1)
         ends = 2 if r2 is not None else 1
         mb = params.multi_best
-        out = np.zeros((n, ends, mb), dtype=MAPPING_DTYPE)
-        jout = np.zeros((n, ends, mb), dtype=SUBJUNC_DTYPE) if params.do_breakpoint_detection else None
-        bm = (np.zeros((n, ends, BIG_MARGIN_WORDS), dtype=np.uint16)
-              if params.do_big_margin_filtering_for_junctions else None)
+        if bufs is not None:
+            out, jout, bm = bufs
+            if out.shape != (n, ends, mb) or out.dtype != MAPPING_DTYPE:
+                raise ValueError("bufs: mapping array of shape %s expected" % ((n, ends, mb),))
+            if (jout is None) != (not params.do_breakpoint_detection) or \
+               (bm is None) != (not params.do_big_margin_filtering_for_junctions):
+                raise ValueError("bufs: subjunc / big-margin arrays do not match the parameters")
+            if jout is not None and (jout.shape != (n, ends, mb) or jout.dtype != SUBJUNC_DTYPE):
+                raise ValueError("bufs: subjunc array of shape %s expected" % ((n, ends, mb),))
+            if bm is not None and (bm.shape != (n, ends, BIG_MARGIN_WORDS) or bm.dtype != np.uint16):
+                raise ValueError("bufs: big-margin array of shape %s expected" % ((n, ends, BIG_MARGIN_WORDS),))
+        else:
+            out = np.zeros((n, ends, mb), dtype=MAPPING_DTYPE)
+            jout = np.zeros((n, ends, mb), dtype=SUBJUNC_DTYPE) if params.do_breakpoint_detection else None
+            bm = (np.zeros((n, ends, BIG_MARGIN_WORDS), dtype=np.uint16)
+                  if params.do_big_margin_filtering_for_junctions else None)
         s1 = r1.struct()
         s2 = r2.struct() if r2 is not None else None
         rc = lib().svg_vote_batch(self.h, ctypes.byref(params), ctypes.byref(s1),

@@ -55,9 +55,12 @@ struct svg_index {
 	hipEvent_t tev[4][64][2];
 	int tn[4], tcount[4];
 	double tms[4];
-	// staging for svg_vote_batch (host buffers)
-	void *d_in; size_t d_in_cap;
-	void *d_out; size_t d_out_cap;
+	// staging for svg_vote_batch (host buffers): two sub-batch slots, uploads and downloads on
+	// their own streams so PCIe traffic of sub-batches i+1 / i-1 overlaps the vote of i
+	void *d_in[2]; size_t d_in_cap[2];
+	void *d_out[2]; size_t d_out_cap[2];
+	hipStream_t up_stream, down_stream;
+	hipEvent_t ev_up[2], ev_done[2], ev_down[2];
 };
 
 #define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) { svg_set_error("HIP error %s at %s:%d", hipGetErrorString(_e), __FILE__, __LINE__); return SVG_E_DEVICE; } } while (0)

@@ -1685,6 +1685,9 @@ int svg_index_finish_device(svg_index *h)
 	for (int s = 0; s < 2; s++) {
 		HIPCHK(hipEventCreateWithFlags(&h->ev_lane[s], hipEventDisableTiming));
 		HIPCHK(hipEventCreateWithFlags(&h->ev_wave[s], hipEventDisableTiming));
+		HIPCHK(hipEventCreateWithFlags(&h->ev_up[s], hipEventDisableTiming));
+		HIPCHK(hipEventCreateWithFlags(&h->ev_done[s], hipEventDisableTiming));
+		HIPCHK(hipEventCreateWithFlags(&h->ev_down[s], hipEventDisableTiming));
 	}
 	HIPCHK(hipMemcpy(h->d_values, x->values, x->values_bytes, hipMemcpyHostToDevice));
 	HIPCHK(hipMemcpy(h->d_chr, x->chr_end, 4 * (size_t)x->n_chr, hipMemcpyHostToDevice));
@@ -1786,11 +1789,16 @@ extern "C" void svg_index_close(svg_index *h)
 	hipSetDevice(h->device);
 	if (h->stream) hipStreamSynchronize(h->stream);
 	if (h->stream2) hipStreamSynchronize(h->stream2);
+	if (h->up_stream) hipStreamSynchronize(h->up_stream);
+	if (h->down_stream) hipStreamSynchronize(h->down_stream);
 	for (int s = 0; s < 2; s++) {
 		hipFree(h->d_prec[s]);
 		hipFree(h->d_lane[s]);
-		if (h->ev_lane[s]) hipEventDestroy(h->ev_lane[s]);
-		if (h->ev_wave[s]) hipEventDestroy(h->ev_wave[s]);
+		hipFree(h->d_in[s]);
+		hipFree(h->d_out[s]);
+		hipEvent_t *evs[5] = {h->ev_lane, h->ev_wave, h->ev_up, h->ev_done, h->ev_down};
+		for (int k = 0; k < 5; k++)
+			if (evs[k][s]) hipEventDestroy(evs[k][s]);
 	}
 	hipFree(h->d_lscratch);
 	hipFree(h->d_lscratch2);
@@ -1800,9 +1808,11 @@ extern "C" void svg_index_close(svg_index *h)
 				if (h->tev[k][i][j]) hipEventDestroy(h->tev[k][i][j]);
 	hipFree(h->d_bstart); hipFree(h->d_keys); hipFree(h->d_vals); hipFree(h->d_values); hipFree(h->d_chr);
 	hipFree(h->d_bgrp); hipFree(h->d_keys8);
-	hipFree(h->d_scratch); hipFree(h->d_stats); hipFree(h->d_in); hipFree(h->d_out);
+	hipFree(h->d_scratch); hipFree(h->d_stats);
 	if (h->stream) hipStreamDestroy(h->stream);
 	if (h->stream2) hipStreamDestroy(h->stream2);
+	if (h->up_stream) hipStreamDestroy(h->up_stream);
+	if (h->down_stream) hipStreamDestroy(h->down_stream);
 	svg_host_index_free(&h->host);
 	free(h);
 }
@@ -2055,6 +2065,7 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 		const uint64_t per_read = (uint64_t)ends * 2 * nps;
 		uint64_t chunk = ((uint64_t)1 << 30) / (per_read * 8);
 		if (chunk > (uint64_t)0x7fffffff / per_read) chunk = (uint64_t)0x7fffffff / per_read;
+		{ const char *ec = getenv("SVG_CHUNK"); if (ec && atoll(ec) > 0 && (uint64_t)atoll(ec) < chunk) chunk = (uint64_t)atoll(ec); }   // testing
 		if (chunk > kp.n_reads) chunk = kp.n_reads;
 		if (chunk < 1) chunk = 1;
 		// chunk pipeline: the wave kernel of chunk c runs on stream2 while the probe and lane
@@ -2065,6 +2076,9 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 		const char *eo = getenv("SVG_OVERLAP");
 		const bool overlap = (eo ? eo[0] == '1' : (!sj && !r2)) && chunk < kp.n_reads;
 		hipStream_t st2 = overlap ? h->stream2 : st;
+		if (getenv("SVG_DEBUG"))
+			fprintf(stderr, "[svg] batch of %llu reads: chunks of %llu, chunk pipeline %s\n", (unsigned long long)kp.n_reads,
+			        (unsigned long long)chunk, overlap ? "on" : "off");
 		for (int s = 0; s < (overlap ? 2 : 1); s++)
 			if ((rc = ensure(h, &h->d_prec[s], &h->prec_cap[s], chunk * per_read * 8))) return rc;
 		bool slot_busy[2] = {false, false};
@@ -2163,7 +2177,10 @@ static int ensure(svg_index *h, void **p, size_t *cap, size_t need)
 	return 0;
 }
 
-// host buffers in/out: stage through HBM
+// host buffers in/out: stage through HBM in sub-batches.  Sub-batch i is uploaded (up_stream)
+// into slot i & 1 while sub-batch i-1 is voted (stream) and i-2's records come back
+// (down_stream); with pageable caller memory each copy call blocks the host until it is done,
+// which is still concurrent with the kernels already queued on the vote stream.
 extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
                               svg_mapping_result *out, svg_subjunc_result *jout, uint16_t *big_margin)
 {
@@ -2171,74 +2188,117 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 	if (r2 && r2->n_reads != r1->n_reads) { svg_set_error("R1/R2 read counts differ"); return SVG_E_ARG; }
 	int rc = check_params(h, p, r2 != NULL);
 	if (rc) return rc;
-	uint64_t n = r1->n_reads;
-	if (!n) return 0;
-	int ends = r2 ? 2 : 1;
-	HIPCHK(hipSetDevice(h->device));
-	// total sequence span per end
-	uint64_t span[2] = {0, 0}, lo[2] = {0, 0};
-	for (int e = 0; e < ends; e++) {
-		const svg_reads *rr = e ? r2 : r1;
-		uint64_t mn = ~0ull, mx = 0;
-		for (uint64_t i = 0; i < n; i++) {
-			int len = rr->lens[i];
-			if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;
-			if (len >= 15 + h->dix.gap) {
-				int cr = (len - 15 - h->dix.gap) << 16, step;
-				if (len <= 160) { step = cr / (p->total_subreads - 1); if (step < (h->dix.gap << 16)) step = h->dix.gap << 16; }
-				else { step = 6 << 16; if (cr / step > 62) step = cr / 62; }
-				if ((1 + cr / step) * h->dix.gap > 192) { svg_set_error("read %llu needs %d probes per strand (> 192)", (unsigned long long)i, (1 + cr / step) * h->dix.gap); return SVG_E_UNSUPPORTED; }
-			}
-			if (rr->offsets[i] < mn) mn = rr->offsets[i];
-			if (rr->offsets[i] + rr->lens[i] > mx) mx = rr->offsets[i] + rr->lens[i];
-		}
-		lo[e] = mn; span[e] = mx - mn;
-	}
-	int saved_len = h->max_read_len, batch_max = 16;
-	for (int e = 0; e < ends; e++) {
-		const svg_reads *rr = e ? r2 : r1;
-		for (uint64_t i = 0; i < n; i++) if (rr->lens[i] > batch_max) batch_max = rr->lens[i] < SVG_READ_KEEP ? rr->lens[i] : SVG_READ_KEEP;
-	}
-	size_t in_bytes = 0, o_seq[2], o_off[2], o_len[2];
-	for (int e = 0; e < ends; e++) {
-		o_seq[e] = in_bytes; in_bytes += (span[e] + 15) & ~15ull;
-		o_off[e] = in_bytes; in_bytes += 8 * n;
-		o_len[e] = in_bytes; in_bytes += (2 * n + 15) & ~15ull;
-	}
-	size_t out_bytes = (size_t)n * ends * p->multi_best * 68;
-	size_t j_bytes = p->do_breakpoint_detection ? (size_t)n * ends * p->multi_best * 16 : 0;
-	size_t bm_bytes = p->do_big_margin_filtering_for_junctions ? (size_t)n * ends * SVG_BIG_MARGIN_WORDS * 2 : 0;
-	size_t o_j = (out_bytes + 255) & ~(size_t)255, o_bm = (o_j + j_bytes + 255) & ~(size_t)255;
 	if (p->do_breakpoint_detection && !jout) { svg_set_error("do_breakpoint_detection needs jout"); return SVG_E_ARG; }
 	if (p->do_big_margin_filtering_for_junctions && !big_margin) { svg_set_error("big-margin filtering needs big_margin"); return SVG_E_ARG; }
-	if ((rc = ensure(h, &h->d_in, &h->d_in_cap, in_bytes))) return rc;
-	if ((rc = ensure(h, &h->d_out, &h->d_out_cap, o_bm + bm_bytes))) return rc;
-	uint8_t *din = (uint8_t *)h->d_in;
-	uint64_t *tmpoff = (uint64_t *)malloc(8 * n);
-	svg_reads dr[2];
+	const uint64_t n = r1->n_reads;
+	if (!n) return 0;
+	const int ends = r2 ? 2 : 1;
+	HIPCHK(hipSetDevice(h->device));
+	// copy streams on first use only: HIP deals a process's streams round-robin onto
+	// GPU_MAX_HW_QUEUES (4) hardware queues, and idle extra streams can land the chunk
+	// pipeline's second stream on the caller's queue
+	if (!h->up_stream) HIPCHK(hipStreamCreateWithFlags(&h->up_stream, hipStreamNonBlocking));
+	if (!h->down_stream) HIPCHK(hipStreamCreateWithFlags(&h->down_stream, hipStreamNonBlocking));
+	// the batch's longest read (picks the kernel variant); every kept length must fit the
+	// kernels' 192 probes per strand (checked once per length, not per read)
+	int batch_max = 16;
 	for (int e = 0; e < ends; e++) {
-		const svg_reads *rr = e ? r2 : r1;
-		for (uint64_t i = 0; i < n; i++) tmpoff[i] = rr->offsets[i] - lo[e];
-		HIPCHK(hipMemcpyAsync(din + o_seq[e], rr->seq + lo[e], span[e], hipMemcpyHostToDevice, h->stream));
-		HIPCHK(hipMemcpyAsync(din + o_off[e], tmpoff, 8 * n, hipMemcpyHostToDevice, h->stream));
-		HIPCHK(hipMemcpyAsync(din + o_len[e], rr->lens, 2 * n, hipMemcpyHostToDevice, h->stream));
-		HIPCHK(hipStreamSynchronize(h->stream));
-		dr[e].seq = (const char *)(din + o_seq[e]);
-		dr[e].offsets = (const uint64_t *)(din + o_off[e]);
-		dr[e].lens = (const uint16_t *)(din + o_len[e]);
-		dr[e].n_reads = n;
+		const uint16_t *ln = (e ? r2 : r1)->lens;
+		int mx = 0;
+		for (uint64_t i = 0; i < n; i++) mx = ln[i] > mx ? ln[i] : mx;
+		if (mx > SVG_READ_KEEP) mx = SVG_READ_KEEP;
+		if (mx > batch_max) batch_max = mx;
 	}
-	free(tmpoff);
+	for (int len = 15 + h->dix.gap; len <= batch_max; len++) {
+		int cr = (len - 15 - h->dix.gap) << 16, step;
+		if (len <= 160) { step = cr / (p->total_subreads - 1); if (step < (h->dix.gap << 16)) step = h->dix.gap << 16; }
+		else { step = 6 << 16; if (cr / step > 62) step = cr / 62; }
+		if ((1 + cr / step) * h->dix.gap > 192) { svg_set_error("reads of %d bases need %d probes per strand (> 192)", len, (1 + cr / step) * h->dix.gap); return SVG_E_UNSUPPORTED; }
+	}
+	const size_t rec_b = (size_t)ends * p->multi_best * 68;
+	const size_t j_b = p->do_breakpoint_detection ? (size_t)ends * p->multi_best * 16 : 0;
+	const size_t bm_b = p->do_big_margin_filtering_for_junctions ? (size_t)ends * SVG_BIG_MARGIN_WORDS * 2 : 0;
+	// sub-batches of ~320 MB of PCIe traffic (1M 100 bp SE reads): short enough that the
+	// pipeline's fill and drain are small, long enough to keep the GPU busy (C3 host path:
+	// 162 / 174 / 179 Mreads/s at 4M / 2M / 1M reads).  SVG_HOST_SUB overrides.
+	const size_t per_read = (size_t)ends * (batch_max + 10) + rec_b + j_b + bm_b;
+	uint64_t sub = 320000000ull / per_read;
+	if (sub < 65536) sub = 65536;
+	{ const char *es = getenv("SVG_HOST_SUB"); if (es && atoll(es) > 0) sub = (uint64_t)atoll(es); }
+	if (sub > n) sub = n;
+	const int saved_len = h->max_read_len;
 	h->max_read_len = batch_max;
-	uint8_t *dout = (uint8_t *)h->d_out;
-	rc = svg_vote_batch_device(h, p, &dr[0], r2 ? &dr[1] : NULL, (svg_mapping_result *)dout,
-	                           j_bytes ? (svg_subjunc_result *)(dout + o_j) : NULL,
-	                           bm_bytes ? (uint16_t *)(dout + o_bm) : NULL, h->stream);
+	bool used[2] = {false, false};
+	uint64_t prev_b = 0, prev_n = 0;
+	size_t prev_oj = 0, prev_obm = 0;
+	int prev_s = -1;
+	// D2H of the sub-batch in slot s (reads b .. b+m)
+	auto download = [&](int s, uint64_t b, uint64_t m, size_t o_j, size_t o_bm) -> int {
+		const uint8_t *dout = (const uint8_t *)h->d_out[s];
+		HIPCHK(hipStreamWaitEvent(h->down_stream, h->ev_done[s], 0));
+		HIPCHK(hipMemcpyAsync((uint8_t *)out + b * rec_b, dout, m * rec_b, hipMemcpyDeviceToHost, h->down_stream));
+		if (j_b) HIPCHK(hipMemcpyAsync((uint8_t *)jout + b * j_b, dout + o_j, m * j_b, hipMemcpyDeviceToHost, h->down_stream));
+		if (bm_b) HIPCHK(hipMemcpyAsync((uint8_t *)big_margin + b * bm_b, dout + o_bm, m * bm_b, hipMemcpyDeviceToHost, h->down_stream));
+		HIPCHK(hipEventRecord(h->ev_down[s], h->down_stream));
+		return 0;
+	};
+	for (uint64_t b = 0; b < n && !rc; b += sub) {
+		const uint64_t m = n - b < sub ? n - b : sub;
+		const int s = (int)((b / sub) & 1);
+		// the slot's previous sub-batch must be downloaded before it is overwritten
+		if (used[s]) HIPCHK(hipEventSynchronize(h->ev_down[s]));
+		uint64_t span[2] = {0, 0}, lo[2] = {0, 0};
+		for (int e = 0; e < ends; e++) {
+			const svg_reads *rr = e ? r2 : r1;
+			uint64_t mn = ~0ull, mx = 0;
+			for (uint64_t i = b; i < b + m; i++) {
+				if (rr->offsets[i] < mn) mn = rr->offsets[i];
+				if (rr->offsets[i] + rr->lens[i] > mx) mx = rr->offsets[i] + rr->lens[i];
+			}
+			lo[e] = mn; span[e] = mx - mn;
+		}
+		size_t in_bytes = 0, o_seq[2], o_off[2], o_len[2];
+		for (int e = 0; e < ends; e++) {
+			o_seq[e] = in_bytes; in_bytes += (span[e] + 15) & ~15ull;
+			o_off[e] = in_bytes; in_bytes += 8 * m;
+			o_len[e] = in_bytes; in_bytes += (2 * m + 15) & ~15ull;
+		}
+		const size_t o_j = (m * rec_b + 255) & ~(size_t)255, o_bm = (o_j + m * j_b + 255) & ~(size_t)255;
+		if ((rc = ensure(h, &h->d_in[s], &h->d_in_cap[s], in_bytes))) break;
+		if ((rc = ensure(h, &h->d_out[s], &h->d_out_cap[s], o_bm + m * bm_b))) break;
+		uint8_t *din = (uint8_t *)h->d_in[s], *dout = (uint8_t *)h->d_out[s];
+		svg_reads dr[2];
+		for (int e = 0; e < ends; e++) {
+			const svg_reads *rr = e ? r2 : r1;
+			// the caller's offsets go up unchanged: the device text pointer is rebased by lo
+			// instead (seq + offsets[i] addresses the uploaded span)
+			HIPCHK(hipMemcpyAsync(din + o_seq[e], rr->seq + lo[e], span[e], hipMemcpyHostToDevice, h->up_stream));
+			HIPCHK(hipMemcpyAsync(din + o_off[e], rr->offsets + b, 8 * m, hipMemcpyHostToDevice, h->up_stream));
+			HIPCHK(hipMemcpyAsync(din + o_len[e], rr->lens + b, 2 * m, hipMemcpyHostToDevice, h->up_stream));
+			dr[e].seq = (const char *)(din + o_seq[e]) - lo[e];
+			dr[e].offsets = (const uint64_t *)(din + o_off[e]);
+			dr[e].lens = (const uint16_t *)(din + o_len[e]);
+			dr[e].n_reads = m;
+		}
+		HIPCHK(hipEventRecord(h->ev_up[s], h->up_stream));
+		HIPCHK(hipStreamWaitEvent(h->stream, h->ev_up[s], 0));
+		rc = svg_vote_batch_device(h, p, &dr[0], r2 ? &dr[1] : NULL, (svg_mapping_result *)dout,
+		                           j_b ? (svg_subjunc_result *)(dout + o_j) : NULL, bm_b ? (uint16_t *)(dout + o_bm) : NULL,
+		                           h->stream);
+		if (rc) break;
+		HIPCHK(hipEventRecord(h->ev_done[s], h->stream));
+		used[s] = true;
+		// records of the previous sub-batch come back while this one is voted
+		if (prev_s >= 0 && (rc = download(prev_s, prev_b, prev_n, prev_oj, prev_obm))) break;
+		prev_s = s; prev_b = b; prev_n = m; prev_oj = o_j; prev_obm = o_bm;
+	}
+	if (!rc && prev_s >= 0) rc = download(prev_s, prev_b, prev_n, prev_oj, prev_obm);
 	h->max_read_len = saved_len;
+	hipError_t e1 = hipStreamSynchronize(h->stream), e2 = hipStreamSynchronize(h->down_stream);
 	if (rc) return rc;
-	HIPCHK(hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, h->stream));
-	if (j_bytes) HIPCHK(hipMemcpyAsync(jout, dout + o_j, j_bytes, hipMemcpyDeviceToHost, h->stream));
-	if (bm_bytes) HIPCHK(hipMemcpyAsync(big_margin, dout + o_bm, bm_bytes, hipMemcpyDeviceToHost, h->stream));
-	HIPCHK(hipStreamSynchronize(h->stream));
+	if (e1 != hipSuccess || e2 != hipSuccess) {
+		svg_set_error("HIP error %s in svg_vote_batch", hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+		return SVG_E_DEVICE;
+	}
 	return 0;
 }

@@ -135,3 +135,36 @@ def test_gpu_empty_batch(gpu_indexes):
     ix = gpu_indexes("chr901_gapped")
     out, _, _ = ix.vote(default_params(), ReadBatch.from_list([]))
     assert out.shape[0] == 0
+
+
+@pytest.mark.parametrize("mode", ["se", "pe", "sj"])
+def test_gpu_pipelines_match_oracle(mode, gpu_indexes, index_cache, monkeypatch):
+    """The two pipelines: host sub-batches (SVG_HOST_SUB: upload / vote / download of
+    neighbouring sub-batches overlap) and probe-record chunks (SVG_CHUNK, SVG_OVERLAP=1:
+    the wave kernel of chunk c on a second stream beside chunk c+1's probe and lane
+    kernels, double-buffered records) -- many small sub-batches and chunks, ragged tails."""
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.abi import default_params, PROGRAM_ALIGN, PROGRAM_SUBJUNC
+    from subread_amd.sim import Genome, simulate_reads, simulate_spliced_reads
+    key = "chr901_full"
+    pre = index_cache.get(key)
+    g = Genome.read_fasta(index_cache.genome_fasta("chr901"))
+    n = 30011
+    if mode == "sj":
+        r1, r2 = simulate_spliced_reads(g, n, 100, seed=31), None
+    else:
+        r1 = simulate_reads(g, n, 100, seed=32, sub=0.02, indel=0.02)
+        r2 = simulate_reads(g, n, 100, seed=33, sub=0.02, indel=0.02) if mode == "pe" else None
+    p = default_params(PROGRAM_SUBJUNC if mode == "sj" else PROGRAM_ALIGN, mode == "pe")
+    ref, rj, rbm, _ = OracleIndex(pre).vote(p, r1, r2, threads=16)
+    want = pack_records(ref, rj if mode == "sj" else None, rbm if mode == "sj" else None)
+    ix = gpu_indexes(key)
+    for env in ({"SVG_HOST_SUB": "7001"}, {"SVG_CHUNK": "2999", "SVG_OVERLAP": "1"},
+                {"SVG_HOST_SUB": "10007", "SVG_CHUNK": "3001", "SVG_OVERLAP": "1"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        out, jout, bm = ix.vote(p, r1, r2)
+        for k in env:
+            monkeypatch.delenv(k)
+        got = pack_records(out, jout if mode == "sj" else None, bm if mode == "sj" else None)
+        assert (got == want).all(), "%s: %s" % (env, describe_mismatch(got, want, 2 if mode == "pe" else 1, 3))

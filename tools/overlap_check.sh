@@ -7,7 +7,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 gpurun_out/ov/tests.log
 for wl in ${@:-c3}; do
   for ov in 1 0; do
-    SVG_OVERLAP=$ov timeout -k 10 300 python -u bench.py --workload $wl --no-cpu --steps 3 > gpurun_out/ov/${wl}_$ov.json 2> gpurun_out/ov/${wl}_$ov.log || exit 1
+    SVG_OVERLAP=$ov timeout -k 10 300 python -u bench.py --workload $wl --no-cpu --no-host --steps 3 > gpurun_out/ov/${wl}_$ov.json 2> gpurun_out/ov/${wl}_$ov.log || exit 1
     python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[1],d['value'],d['parity_check'],{k:v['launch_ms'] for k,v in d['roofline']['kernels'].items()})" gpurun_out/ov/${wl}_$ov.json
   done
 done

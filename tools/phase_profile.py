@@ -50,6 +50,8 @@ def main():
         wl, n, paired, dt, c[0], c[1], c[2], c[3]))
     for k in range(8):
         print("  %-10s %6.2f%%  %8.0f cycles/read" % (names[k], 100.0 * c[8 + k] / max(1, tot), c[8 + k] / n))
+    print("  lane pass: defer cap/len %d, slots %d, shift %d, candidates %d, deferrals %d" % tuple(c[16:21]))
+    print("  wave kernel: batch-settled %d, serially replayed %d" % (c[26], c[27]))
 
 
 if __name__ == "__main__":
