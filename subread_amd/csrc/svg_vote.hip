@@ -493,9 +493,7 @@ struct Wave {
 			{
 				const int m = (int)cn;
 				unsigned long long serial = m == 64 ? ~0ull : ((1ull << m) - 1ull);
-				if constexpr (!SJ) {
-					if (round == 0 && kp->ii_end == 5 && m >= 8) serial = batch_create<E>(kvv, kov, m, high_b);
-				}
+				if (round == 0 && kp->ii_end == 5 && m >= 8) serial = batch_create<E>(kvv, kov, m, high_b);
 				if (kp->stats) { st_batch += (unsigned long long)(m - __popcll(serial)); st_serial += (unsigned long long)__popcll(serial); }
 				while (serial) {
 					const int j = __ffsll((long long)serial) - 1;
@@ -2229,6 +2227,8 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 	const int saved_len = h->max_read_len;
 	h->max_read_len = batch_max;
 	bool used[2] = {false, false};
+	svg_batch_stats acc;
+	memset(&acc, 0, sizeof acc);
 	uint64_t prev_b = 0, prev_n = 0;
 	size_t prev_oj = 0, prev_obm = 0;
 	int prev_s = -1;
@@ -2286,6 +2286,11 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 		                           j_b ? (svg_subjunc_result *)(dout + o_j) : NULL, bm_b ? (uint16_t *)(dout + o_bm) : NULL,
 		                           h->stream);
 		if (rc) break;
+		if (h->stats_on) {   // the device call synchronised and left its sub-batch's counts
+			acc.probes += h->last_stats.probes; acc.bucket_items += h->last_stats.bucket_items;
+			acc.hits += h->last_stats.hits; acc.results += h->last_stats.results;
+			acc.deferred += h->last_stats.deferred;
+		}
 		HIPCHK(hipEventRecord(h->ev_done[s], h->stream));
 		used[s] = true;
 		// records of the previous sub-batch come back while this one is voted
@@ -2294,6 +2299,7 @@ extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads
 	}
 	if (!rc && prev_s >= 0) rc = download(prev_s, prev_b, prev_n, prev_oj, prev_obm);
 	h->max_read_len = saved_len;
+	if (h->stats_on) h->last_stats = acc;   // the whole batch
 	hipError_t e1 = hipStreamSynchronize(h->stream), e2 = hipStreamSynchronize(h->down_stream);
 	if (rc) return rc;
 	if (e1 != hipSuccess || e2 != hipSuccess) {
