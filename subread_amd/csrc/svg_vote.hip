@@ -2014,7 +2014,10 @@ static int launch_vote(svg_index *h, KParams &kp, hipStream_t st, int npmax, boo
 		return npmax <= 64 ? launch_t<1, 1216, 64, 2, 4, false>(h, kp, st) : launch_t<1, 1216, 192, 2, 4, false>(h, kp, st);
 	}
 	if (ends == 2) return npmax <= 32 ? launch_t<2, 256, 32, 1, 4, false>(h, kp, st) : launch_t<2, 256, 64, 1, 4, false>(h, kp, st);
-	return npmax <= 32 ? launch_t<1, 256, 32, 2, 5, false>(h, kp, st) : launch_t<1, 256, 64, 2, 5, false>(h, kp, st);
+#ifndef SVG_SE_OCC
+#define SVG_SE_OCC 5
+#endif
+	return npmax <= 32 ? launch_t<1, 256, 32, 2, SVG_SE_OCC, false>(h, kp, st) : launch_t<1, 256, 64, 2, SVG_SE_OCC, false>(h, kp, st);
 }
 
 extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,

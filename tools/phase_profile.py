@@ -7,6 +7,8 @@ import os
 import sys
 import time
 
+os.environ.setdefault("SVG_HOST_SUB", "1000000000")   # one device call: the counters cover the batch
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
