@@ -24,6 +24,10 @@ struct DevIndex {
 	//   keys8[i] = keys[i] as u8 (key_hi = key / nb <= 255 when nb >= 16843009)
 	const uint32_t *bgrp;
 	const uint8_t *keys8;
+	//   bline[b]: one 64-byte line per bucket: u32 first item, u8 item count (255 = 255 or
+	//            more), then the u8 keys of its first <= 59 items -- bounds and keys of a probe
+	//            in ONE random line (replaces bgrp + keys8 when present)
+	const uint4 *bline;
 };
 
 struct svg_index {
@@ -31,7 +35,7 @@ struct svg_index {
 	hipStream_t stream;
 	svg_host_index host;
 	DevIndex dix;
-	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr, *d_bgrp, *d_keys8;
+	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr, *d_bgrp, *d_keys8, *d_bline;
 	uint32_t *d_scratch;
 	size_t scratch_words;
 	unsigned long long *d_stats;

@@ -1457,7 +1457,7 @@ __device__ __forceinline__ bool try_run(uint64_t eq, int n, int &m, int &fwd, in
 // equal-key run on both sides of the first-hit midpoint); with no per-read state to keep,
 // it runs at high occupancy and hides the dependent bucket -> keys -> run chain.
 // =============================================================================================
-template <int ENDS, int BPC>
+template <int ENDS, int BPC, bool LINE>
 __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 {
 	const DevIndex &ix = pp.ix;
@@ -1520,8 +1520,19 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 				const int16_t k16 = (int16_t)q;
 				uint32_t first;
 				int n;
-				bool compact = false;
-				if (ix.bgrp) {
+				bool compact = false, inl = false;
+				uint4 lw[4];
+				if constexpr (LINE) {
+					// the bucket's 64-byte line: bounds and u8 keys in one random access
+					const uint4 *l4 = ix.bline + 4 * (size_t)b;
+#pragma unroll
+					for (int q = 0; q < 4; q++) lw[q] = l4[q];
+					const uint32_t c = lw[0].y & 255u;
+					first = lw[0].x;
+					n = (int)c;
+					compact = c != 255u;
+					inl = c <= 59u;
+				} else if (ix.bgrp) {
 					// bucket bounds from the 32-byte group: first item of the group + the counts
 					// of the buckets before b in it
 					const uint4 *g4 = (const uint4 *)(ix.bgrp + 8 * (size_t)(b >> 4));
@@ -1552,7 +1563,24 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 					const int16_t *K = ix.keys + first;
 					int m = 0, fwd = 0, bwd = 0;
 					bool hit = false, done = false;
-					if (compact && n <= 48) {
+					if (LINE && inl) {
+						// u8 keys at bytes 5..63 of the line, equal keys by a zero-byte test
+						const uint32_t kk = (uint32_t)(uint8_t)k16 * 0x01010101u;
+						uint64_t eq = 0;
+#pragma unroll
+						for (int k = 0; k < 4; k++) {
+							const uint32_t dw[4] = {lw[k].x, lw[k].y, lw[k].z, lw[k].w};
+#pragma unroll
+							for (int q = 0; q < 4; q++) {
+								const uint32_t x = dw[q] ^ kk;
+								const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+								const uint32_t bits = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+								eq |= (uint64_t)bits << (16 * k + 4 * q);
+							}
+						}
+						eq = (eq >> 5) & ((1ull << n) - 1ull);
+						done = try_run(eq, n, m, fwd, bwd, hit);
+					} else if (!LINE && compact && n <= 48) {
 						// u8 keys: the bucket in <= 4 independent 16-byte loads, equal keys by a
 						// zero-byte test
 						const uintptr_t base = (uintptr_t)(ix.keys8 + first);
@@ -1575,7 +1603,7 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 						}
 						eq = (eq >> sh) & ((1ull << n) - 1ull);
 						done = try_run(eq, n, m, fwd, bwd, hit);
-					} else if (pp.window && n <= 56) {
+					} else if (!LINE && pp.window && n <= 56) {
 						// i16 keys: <= 8 independent 16-byte loads of the aligned window holding the
 						// bucket, equal keys by a zero-halfword test
 						const uintptr_t base = (uintptr_t)K;
@@ -1669,6 +1697,27 @@ __global__ void __launch_bounds__(256) build_keys8(const int16_t *keys, uint64_t
 		keys8[i] = (uint8_t)keys[i];
 }
 
+// DevIndex::bline: one 64-byte line per bucket (first item, count, the u8 keys of <= 59 items)
+__global__ void __launch_bounds__(256) build_bline(const uint32_t *bstart, const int16_t *keys, uint32_t nb, uint4 *bline)
+{
+	for (uint32_t b = blockIdx.x * 256u + threadIdx.x; b < nb; b += gridDim.x * 256u) {
+		const uint32_t first = bstart[b], n = bstart[b + 1] - first;
+		uint32_t w[16];
+#pragma unroll
+		for (int q = 0; q < 16; q++) w[q] = 0u;
+		w[0] = first;
+		w[1] = n > 255u ? 255u : n;
+		if (n <= 59u) {
+#pragma unroll
+			for (int i = 0; i < 59; i++)
+				if ((uint32_t)i < n) w[(5 + i) >> 2] |= (uint32_t)(uint8_t)keys[first + i] << (8 * ((5 + i) & 3));
+		}
+		uint4 *d = bline + 4 * (size_t)b;
+#pragma unroll
+		for (int q = 0; q < 4; q++) d[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+	}
+}
+
 // common tail of svg_index_open / svg_index_build*: d_bstart/d_keys/d_vals already in HBM,
 // host part holds .array and the chromosome table
 int svg_index_finish_device(svg_index *h)
@@ -1707,7 +1756,18 @@ int svg_index_finish_device(svg_index *h)
 	h->n_cu = prop.multiProcessorCount;
 	h->dix.bgrp = NULL;
 	h->dix.keys8 = NULL;
-	if (x->nb >= 16843009u && !getenv("SVG_NO_COMPACT")) {
+	h->dix.bline = NULL;
+	if (x->nb >= 16843009u && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_BLINE")) {
+		// (2^32-1)/nb <= 255: every key_hi fits a byte; 64 B per bucket (5.95 GB at nb = 93M)
+		if ((rc = dmalloc(h, &h->d_bline, (size_t)x->nb * 64 + 64))) return rc;
+		uint64_t blocks = ((uint64_t)x->nb + 255) / 256, bmax = (uint64_t)h->n_cu * 64;
+		if (blocks > bmax) blocks = bmax;
+		hipLaunchKernelGGL(build_bline, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
+		                   (const int16_t *)h->d_keys, x->nb, (uint4 *)h->d_bline);
+		HIPCHK(hipGetLastError());
+		HIPCHK(hipStreamSynchronize(h->stream));
+		h->dix.bline = (const uint4 *)h->d_bline;
+	} else if (x->nb >= 16843009u && !getenv("SVG_NO_COMPACT")) {
 		// (2^32-1)/nb <= 255: every key_hi fits a byte
 		const size_t ng = ((size_t)x->nb + 15) / 16;
 		if ((rc = dmalloc(h, &h->d_bgrp, ng * 32 + 64)) || (rc = dmalloc(h, &h->d_keys8, x->items + 128))) return rc;
@@ -1805,7 +1865,7 @@ extern "C" void svg_index_close(svg_index *h)
 			for (int j = 0; j < 2; j++)
 				if (h->tev[k][i][j]) hipEventDestroy(h->tev[k][i][j]);
 	hipFree(h->d_bstart); hipFree(h->d_keys); hipFree(h->d_vals); hipFree(h->d_values); hipFree(h->d_chr);
-	hipFree(h->d_bgrp); hipFree(h->d_keys8);
+	hipFree(h->d_bgrp); hipFree(h->d_keys8); hipFree(h->d_bline);
 	hipFree(h->d_scratch); hipFree(h->d_stats);
 	if (h->stream) hipStreamDestroy(h->stream);
 	if (h->stream2) hipStreamDestroy(h->stream2);
@@ -2111,8 +2171,14 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 			if ((rc = timing_mark(h, 0, 0, st))) return rc;
 			// 8 blocks of 256 per CU (<= 64 VGPRs): the probe chain is latency-bound, occupancy
 			// is what hides it (C3: 11.3 ms at 4 waves/SIMD, 8.7 ms at 8)
-			if (r2) hipLaunchKernelGGL((probe_kernel<2, 8>), dim3((unsigned)pb), dim3(256), 0, st, pp);
-			else hipLaunchKernelGGL((probe_kernel<1, 8>), dim3((unsigned)pb), dim3(256), 0, st, pp);
+			// bucket-line image (one random 64-B line per probe) when the index has one
+			if (h->dix.bline) {
+				if (r2) hipLaunchKernelGGL((probe_kernel<2, 8, true>), dim3((unsigned)pb), dim3(256), 0, st, pp);
+				else hipLaunchKernelGGL((probe_kernel<1, 8, true>), dim3((unsigned)pb), dim3(256), 0, st, pp);
+			} else {
+				if (r2) hipLaunchKernelGGL((probe_kernel<2, 8, false>), dim3((unsigned)pb), dim3(256), 0, st, pp);
+				else hipLaunchKernelGGL((probe_kernel<1, 8, false>), dim3((unsigned)pb), dim3(256), 0, st, pp);
+			}
 			HIPCHK(hipGetLastError());
 			if ((rc = timing_mark(h, 0, 1, st))) return rc;
 			KParams kc = kp;
