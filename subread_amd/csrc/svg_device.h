@@ -43,6 +43,7 @@ struct svg_index {
 	svg_batch_stats last_stats;
 	uint64_t device_bytes;
 	int n_cu;
+	int wave_cap;   // > 0: blocks per CU cap of the wave kernel (set while it overlaps the probe kernel)
 	int max_read_len;        // announced read-length bound (svg_set_max_read_length), picks the kernel variant
 	// chunk pipeline: probe + lane kernels of chunk c run on the caller's stream while the wave
 	// kernel of chunk c-1 runs on stream2, so the per-chunk buffers come in two slots (c & 1)

@@ -2030,6 +2030,7 @@ static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 	int per_cu = (int)(160 * 1024 / lds);
 	if (per_cu < 1) { svg_set_error("kernel LDS too large"); return SVG_E_DEVICE; }
 	if (per_cu > 4 * OCC / WPB) per_cu = 4 * OCC / WPB;   // 4 SIMDs x OCC waves
+	if (h->wave_cap > 0 && per_cu > h->wave_cap) per_cu = h->wave_cap;
 	if (getenv("SVG_DEBUG"))
 		fprintf(stderr, "[svg] vote_kernel<%d,%d,%d,%d,%d,%d>: LDS %zu B/wave, %d blocks/CU\n", ENDS, MAXL,
 		        MAXP, WPB, OCC, (int)SJ, sizeof(LT), per_cu);
@@ -2074,6 +2075,9 @@ static int launch_vote(svg_index *h, KParams &kp, hipStream_t st, int npmax, boo
 		return npmax <= 64 ? launch_t<1, 1216, 64, 2, 4, false>(h, kp, st) : launch_t<1, 1216, 192, 2, 4, false>(h, kp, st);
 	}
 	if (ends == 2) return npmax <= 32 ? launch_t<2, 256, 32, 1, 4, false>(h, kp, st) : launch_t<2, 256, 64, 1, 4, false>(h, kp, st);
+#ifndef SVG_WAVE_CAP
+#define SVG_WAVE_CAP 6   // C3: 317 (uncapped, 10) -> 328 Mreads/s; 4 and 3 starve the wave kernel
+#endif
 #ifndef SVG_SE_OCC
 #define SVG_SE_OCC 5
 #endif
@@ -2137,6 +2141,13 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 		const char *eo = getenv("SVG_OVERLAP");
 		const bool overlap = (eo ? eo[0] == '1' : (!sj && !r2)) && chunk < kp.n_reads;
 		hipStream_t st2 = overlap ? h->stream2 : st;
+		// overlapped, the wave kernel leaves CU slots to the next chunk's probe kernel, whose
+		// latency-bound chain needs the occupancy (the wave kernel has slack on its stream)
+		h->wave_cap = 0;
+		if (overlap) {
+			const char *ew = getenv("SVG_WAVE_CAP");
+			h->wave_cap = ew ? atoi(ew) : SVG_WAVE_CAP;
+		}
 		if (getenv("SVG_DEBUG"))
 			fprintf(stderr, "[svg] batch of %llu reads: chunks of %llu, chunk pipeline %s\n", (unsigned long long)kp.n_reads,
 			        (unsigned long long)chunk, overlap ? "on" : "off");
