@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """bench.py -- throughput of the MI355X vote path (BASELINE.json metric).
 
-A "step" = one svg_vote_batch_device pass over one batch of synthetic reads
-resident in HBM (reads in, mapping_result_t[3] per read out).  Workloads
+A "step" = one pass of the vote path over one batch of synthetic reads, measured as
+SURVEY.md §8(d) defines the metric: from 2-bit packed reads resident in host-pinned
+memory to mapping_result_t[3] per read end in host memory (svg_vote_batch_packed:
+PCIe both ways included; reads are packed once, before timing).  Secondary fields:
+the same kernels with reads and records already in HBM (device_path,
+svg_vote_batch_device) and the ASCII host entry point (svg_vote_batch).  Workloads
 (SURVEY.md §8(d)):
   c2: 10M x 100 bp SE reads per GPU vs a chr901-scale 1,000,000 bp
       i.i.d. genome (seed 901), full one-block index (subread-buildindex -F -B),
@@ -56,6 +60,30 @@ def workload(name):
     raise SystemExit("unknown workload " + name)
 
 
+def cpu_info():
+    """Host CPU model, logical CPUs, and the CPUs this process may use (affinity, cgroup quota)."""
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    ncpu = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else ncpu
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    if quota:
+        usable = min(usable, max(1, int(quota)))
+    return {"model": model, "logical_cpus": ncpu, "usable_cpus": usable, "cgroup_quota_cpus": quota}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -65,11 +93,11 @@ def main():
     ap.add_argument("--reads", type=int, default=0, help="reads per GPU per step (default: workload size)")
     ap.add_argument("--workdir", default=os.environ.get("SVG_BENCH_DIR", ""))
     ap.add_argument("--cpu-sample", type=int, default=20_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="default: the CPUs this process may use")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
-    ap.add_argument("--no-host", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
-    ap.add_argument("--host-reads", type=int, default=16_000_000)
+    ap.add_argument("--device-steps", type=int, default=5, help="timed steps of the HBM-resident secondary figure")
+    ap.add_argument("--ascii-reads", type=int, default=8_000_000, help="reads of the ASCII host-entry figure (0: skip)")
     args = ap.parse_args()
 
     import torch
@@ -83,9 +111,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import subread_amd as sa
-    from subread_amd.abi import default_params, PROGRAM_ALIGN, PROGRAM_SUBJUNC, MAPPING_DTYPE, BIG_MARGIN_WORDS
+    from subread_amd.abi import default_params, PROGRAM_ALIGN, PROGRAM_SUBJUNC, MAPPING_DTYPE, SUBJUNC_DTYPE, \
+        BIG_MARGIN_WORDS
     from subread_amd.sim import random_genome, simulate_reads, simulate_pairs, simulate_spliced_reads
 
+    cpu = cpu_info()
+    threads = args.cpu_threads or cpu["usable_cpus"]
     W = workload(args.workload)
     n = args.reads or W["reads"]
     L = W["read_len"]
@@ -127,83 +158,121 @@ def main():
     ends = 2 if rb2 is not None else 1
     log("[bench] simulated %d %s in %.1fs" % (n, "pairs" if ends == 2 else "reads", time.time() - t1))
     dev = torch.device("cuda", local)
-
-    def upload(b):
-        return (torch.from_numpy(b.seq).to(dev), torch.from_numpy(b.offsets.view(np.int64)).to(dev),
-                torch.from_numpy(b.lens.view(np.int16)).to(dev))
-    d1 = upload(rb)
-    d2 = upload(rb2) if rb2 is not None else None
     p = default_params(PROGRAM_SUBJUNC if kind == "sj" else PROGRAM_ALIGN, ends == 2)
-    rec_bytes = MAPPING_DTYPE.itemsize * p.multi_best * ends
-    d_out = torch.empty(n * rec_bytes, dtype=torch.uint8, device=dev)
-    d_jout = torch.empty(n * ends * p.multi_best * 16, dtype=torch.uint8, device=dev) if kind == "sj" else None
-    d_bm = torch.empty(n * ends * BIG_MARGIN_WORDS * 2, dtype=torch.uint8, device=dev) if kind == "sj" else None
-    if kind == "sj":
-        rec_bytes += ends * (p.multi_best * 16 + BIG_MARGIN_WORDS * 2)
-    ix.set_max_read_length(int(os.environ.get("SVG_BENCH_MAXLEN", L)))
-    stream = torch.cuda.Stream(device=dev)
-    r1 = (d1[0].data_ptr(), d1[1].data_ptr(), d1[2].data_ptr(), n)
-    r2 = (d2[0].data_ptr(), d2[1].data_ptr(), d2[2].data_ptr(), n) if d2 is not None else None
+    mb = p.multi_best
+    sj = kind == "sj"
 
-    def step():
-        ix.vote_device(p, r1, r2, d_out.data_ptr(), d_jout.data_ptr() if d_jout is not None else None,
-                       d_bm.data_ptr() if d_bm is not None else None, stream=stream.cuda_stream)
+    # ---- host-pinned 2-bit packed reads and host-pinned output records
+    keep = []
 
+    def pinned(count, dt):
+        dt = np.dtype(dt)
+        t = torch.empty(max(1, count * dt.itemsize), dtype=torch.uint8, pin_memory=True)
+        keep.append(t)
+        return t.numpy()[:count * dt.itemsize].view(dt)
+    t1 = time.time()
+    pk1 = sa.pack_reads(rb, L, threads=threads, alloc=pinned)
+    pk2 = sa.pack_reads(rb2, L, threads=threads, alloc=pinned) if rb2 is not None else None
+    pk1.lens = pinned(n, np.uint16)
+    pk1.lens[:] = rb.lens
+    if pk2 is not None:
+        pk2.lens = pinned(n, np.uint16)
+        pk2.lens[:] = rb2.lens
+    out = pinned(n * ends * mb, MAPPING_DTYPE).reshape(n, ends, mb)
+    jout = pinned(n * ends * mb, SUBJUNC_DTYPE).reshape(n, ends, mb) if sj else None
+    bmo = pinned(n * ends * BIG_MARGIN_WORDS, np.uint16).reshape(n, ends, BIG_MARGIN_WORDS) if sj else None
+    bufs = (out, jout, bmo)
+    in_bytes_host = pk1.bases.nbytes + pk1.lens.nbytes + (pk2.bases.nbytes + pk2.lens.nbytes if pk2 else 0)
+    log("[bench] packed reads (%.1f B/read) and pinned output in %.1fs" % (in_bytes_host / float(n * ends),
+                                                                         time.time() - t1))
+    rec_bytes = MAPPING_DTYPE.itemsize * mb * ends + (ends * (mb * 16 + BIG_MARGIN_WORDS * 2) if sj else 0)
+
+    def host_step():
+        ix.vote_packed(p, pk1, pk2, bufs=bufs)
+
+    # ---- the metric: packed host reads -> host records, W warmup + K timed steps
     for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+        host_step()
     ix.set_timing(True)          # per-launch HIP events inside the library, read back after the timed region
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t_start = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
+    for _ in range(args.steps):
+        host_step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    tk = ix.timing()
     kt = ix.kernel_timing()
     ix.set_timing(False)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    log("[bench] packed host path: %.1f Mreads/s (%.1f ms/step)" % (n * ends * args.steps / elapsed / 1e6,
+                                                                  elapsed / args.steps * 1e3))
+
+    # ---- secondary: the same kernels with reads and records already in HBM
+    def upload(b):
+        return (torch.from_numpy(b.seq).to(dev), torch.from_numpy(b.offsets.view(np.int64)).to(dev),
+                torch.from_numpy(b.lens.view(np.int16)).to(dev))
+    d1 = upload(rb)
+    d2 = upload(rb2) if rb2 is not None else None
+    d_out = torch.empty(n * MAPPING_DTYPE.itemsize * mb * ends, dtype=torch.uint8, device=dev)
+    d_jout = torch.empty(n * ends * mb * 16, dtype=torch.uint8, device=dev) if sj else None
+    d_bm = torch.empty(n * ends * BIG_MARGIN_WORDS * 2, dtype=torch.uint8, device=dev) if sj else None
+    ix.set_max_read_length(int(os.environ.get("SVG_BENCH_MAXLEN", L)))
+    # the handle's own stream: a stream created now could share a hardware queue with the
+    # library's second stream (HIP deals streams round-robin onto GPU_MAX_HW_QUEUES = 4 queues)
+    r1 = (d1[0].data_ptr(), d1[1].data_ptr(), d1[2].data_ptr(), n)
+    r2 = (d2[0].data_ptr(), d2[1].data_ptr(), d2[2].data_ptr(), n) if d2 is not None else None
+
+    def dev_step():
+        ix.vote_device(p, r1, r2, d_out.data_ptr(), d_jout.data_ptr() if d_jout is not None else None,
+                       d_bm.data_ptr() if d_bm is not None else None, stream=None)
+    dev_step()
+    torch.cuda.synchronize()
+    ds = max(1, args.device_steps)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    td = time.perf_counter()
+    for _ in range(ds):
+        dev_step()
+    torch.cuda.synchronize()
+    td = time.perf_counter() - td
+    ix.device_status()
+    device_path = {"value": round(n * ends * ds / td / 1e6, 3), "unit": "Mreads/s", "steps": ds,
+                   "ms_per_step": round(td / ds * 1e3, 3),
+                   "entry": "svg_vote_batch_device: reads and records resident in HBM (no PCIe)"}
 
     # algorithmic bytes from the kernels' own counters, outside the timed region
     ix.set_stats(True)
-    step()
+    dev_step()
     torch.cuda.synchronize()
     st = ix.stats()
     dcs = ix.debug_counters()
     lane_hits = dcs[19] + dcs[24]       # candidates voted by the light and heavy lane passes
     ix.set_stats(False)
-    in_bytes = n * ends * (L + 8 + 2)                # ASCII read + offset + length
+    in_bytes = in_bytes_host                         # 2-bit packed reads + lengths (the metric's input)
     probe_bytes = 8 * st["probes"] + 2 * st["bucket_items"] + 4 * st["hits"]
     out_bytes = n * rec_bytes
     algo_bytes = in_bytes + probe_bytes + out_bytes  # SURVEY §8(d) B_read summed over the step
-    avg_kern_s = float(np.mean(kern_ms)) / 1e3
-    achieved = algo_bytes / avg_kern_s / 1e9
-    # per-kernel algorithmic bytes of one step:
+    # per-kernel algorithmic bytes of one step (text read by the probe kernel: ASCII in HBM):
     #   probe_kernel  read text + bucket bounds (8 B) + bucket keys (2 B/item) + probe records out (8 B/probe)
     #   gather_kernel probe records in (8 B/probe) + hit values (4 B/hit) + candidates out (6 B/hit) + counts
-    #   lane_kernel   candidates in (6 B/hit of lane reads; fused: records 8 B/probe + hit values 4 B/hit)
-    #                 + lengths + records out
+    #   lane_kernel   fused: records 8 B/probe + hit values 4 B/hit of its reads + lengths + records out
     #   vote_kernel   (deferred reads only when the lane path runs) records in + hit values + records out
     lane_on = kt["lane_kernel"][1] > 0
     nd = st.get("deferred", 0) if lane_on else n                 # reads voted by vote_kernel
     dh = st["hits"] - lane_hits if lane_on else st["hits"]       # their hits
     dp = st["probes"] * nd / float(n)                           # their probes (same length)
+    text_bytes = n * ends * (L + 8 + 2)
     kbytes = {
-        "probe_kernel": in_bytes + 8 * st["probes"] + 2 * st["bucket_items"] + 8 * st["probes"],
+        "probe_kernel": text_bytes + 8 * st["probes"] + 2 * st["bucket_items"] + 8 * st["probes"],
         "gather_kernel": 8 * st["probes"] + 10 * st["hits"] + 4 * n,
-        # fused gather (no gather_kernel launches): records in + hit values instead of candidate lists
         "lane_kernel": ((6 * lane_hits) if kt["gather_kernel"][1] else (8 * st["probes"] * (n - nd) / float(n) + 4 * lane_hits))
                        + 6 * n + out_bytes * (n - nd) / float(n),
         "vote_kernel": 8 * dp + 4 * dh + 2 * nd * ends + out_bytes * nd / float(n),
@@ -222,6 +291,8 @@ def main():
     vote_launch_s = kernels[dom]["launch_ms"] / 1e3
     launches_per_step = kernels[dom]["launches_per_step"]
     vote_bytes = kbytes[dom]
+    step_s = elapsed / args.steps
+    achieved = algo_bytes / step_s / 1e9
 
     # HBM traffic of the dominant kernel from the committed PMC passes of this workload
     # (tools/profile_workload.sh -> profiles/r*_<workload>_kernels*.json; rocprofv3 cannot run
@@ -244,58 +315,38 @@ def main():
         from oracle.pyoracle import OracleIndex
         oi = OracleIndex(prefix) if prefix else OracleIndex(arrays=ix.export())
     if rank == 0 and not args.no_check:
-        # parity spot check against the oracle restatement (outside the timed region)
+        # parity spot check against the oracle restatement (outside the timed region): the first and
+        # the last 20k reads of the timed host-path output (first and last sub-batch / chunk)
         m = min(n, 20000)
-        mb = p.multi_best
-        got = [d_out[: m * ends * mb * 68].cpu().numpy().reshape(m, -1)]
-        if d_jout is not None:
-            got.append(d_jout[: m * ends * mb * 16].cpu().numpy().reshape(m, -1))
-            got.append(d_bm[: m * ends * BIG_MARGIN_WORDS * 2].cpu().numpy().reshape(m, -1))
-        ref, rj, rbm, _ = oi.vote(p, rb.slice(0, m), rb2.slice(0, m) if rb2 is not None else None,
-                                  threads=args.cpu_threads)
-        want = [ref.view(np.uint8).reshape(m, -1)]
-        if d_jout is not None:
-            want += [rj.view(np.uint8).reshape(m, -1), rbm.view(np.uint8).reshape(m, -1)]
-        check = bool(all((a == b).all() for a, b in zip(got, want)))
-        log("[bench] parity spot check on %d reads: %s" % (m, "IDENTICAL" if check else "MISMATCH"))
-    host = None
-    if rank == 0 and not args.no_host:
-        # the drop-in entry point with host buffers (svg_vote_batch), PCIe both ways included
-        # (sub-batch pipeline): reads and records in pinned host memory (SURVEY.md §8(d)'s
-        # definition), and in pageable numpy memory.  Reported beside `value`, never as it.
-        from subread_amd.abi import ReadBatch
-        m = min(n, args.host_reads)
-        keep = []
-
-        def pinned(a):
-            t = torch.empty(max(1, a.nbytes), dtype=torch.uint8, pin_memory=True)
-            keep.append(t)
-            v = t.numpy()[:a.nbytes].view(a.dtype).reshape(a.shape)
-            v[...] = a
-            return v
-
-        def run(h1, h2, bufs):
-            ix.vote(p, h1, h2, bufs=bufs)      # first call sizes the staging buffers
-            t1 = time.perf_counter()
-            ix.vote(p, h1, h2, bufs=bufs)
-            return time.perf_counter() - t1
-
+        windows = [(0, m), (n - m, n)] if n > m else [(0, n)]
+        check = True
+        for a, b in windows:
+            got = [out[a:b].view(np.uint8).reshape(b - a, -1)]
+            if sj:
+                got += [jout[a:b].view(np.uint8).reshape(b - a, -1), bmo[a:b].view(np.uint8).reshape(b - a, -1)]
+            ref, rj, rbm, _ = oi.vote(p, rb.slice(a, b), rb2.slice(a, b) if rb2 is not None else None, threads=threads)
+            want = [ref.view(np.uint8).reshape(b - a, -1)]
+            if sj:
+                want += [rj.view(np.uint8).reshape(b - a, -1), rbm.view(np.uint8).reshape(b - a, -1)]
+            ok = bool(all((x == y).all() for x, y in zip(got, want)))
+            # the HBM-resident run wrote the same records
+            dv = d_out[a * mb * ends * 68:b * mb * ends * 68].cpu().numpy().reshape(b - a, -1)
+            ok = ok and bool((dv == want[0]).all())
+            check = check and ok
+            log("[bench] parity check on reads %d..%d: %s" % (a, b, "IDENTICAL" if ok else "MISMATCH"))
+    ascii_host = None
+    if rank == 0 and args.ascii_reads:
+        # the ASCII host entry point (svg_vote_batch, pageable numpy reads, pinned records)
+        m = min(n, args.ascii_reads)
         h1, h2 = rb.slice(0, m), (rb2.slice(0, m) if rb2 is not None else None)
-        t_page = run(h1, h2, ix.vote(p, h1, h2))
-        pin_batch = lambda b: ReadBatch(pinned(b.seq[:int(b.offsets[m - 1]) + int(b.lens[m - 1])]),
-                                        pinned(b.offsets[:m]), pinned(b.lens[:m]))
-        p1, p2 = pin_batch(rb), (pin_batch(rb2) if rb2 is not None else None)
-        o, j, bmh = ix.vote(p, h1, h2)
-        bufs = (pinned(o), pinned(j) if j is not None else None, pinned(bmh) if bmh is not None else None)
-        t_pin = run(p1, p2, bufs)
-        host = {"value": round(m * ends / t_pin / 1e6, 3), "unit": "Mreads/s", "reads": m * ends,
-                "seconds": round(t_pin, 4), "pageable_value": round(m * ends / t_page / 1e6, 3),
-                "entry": "svg_vote_batch: ASCII reads in, records out, PCIe both ways included; value = pinned "
-                "host buffers (torch pin_memory), pageable_value = numpy buffers (output reused)"}
-        log("[bench] host-buffer path: %.1f Mreads/s pinned, %.1f pageable, over %d reads" % (
-            host["value"], host["pageable_value"], m * ends))
-        del keep, bufs, p1, p2
-    cpu = None
+        sub = (out[:m], jout[:m] if sj else None, bmo[:m] if sj else None)
+        ix.vote(p, h1, h2, bufs=sub)
+        ta = time.perf_counter()
+        ix.vote(p, h1, h2, bufs=sub)
+        ta = time.perf_counter() - ta
+        ascii_host = {"value": round(m * ends / ta / 1e6, 3), "unit": "Mreads/s", "reads": m * ends,
+                      "entry": "svg_vote_batch: ASCII reads (pageable) in, records (pinned) out, PCIe both ways"}
+    cpu_base = None
     if rank == 0 and not args.no_cpu:
         # bounded CPU sample: chunks of the same reads until >= 10 s of CPU work
         done, cs, chunk = 0, 0.0, 200000
@@ -303,12 +354,20 @@ def main():
             b = min(chunk, n - done)
             t1 = time.perf_counter()
             oi.vote(p, rb.slice(done, done + b), rb2.slice(done, done + b) if rb2 is not None else None,
-                    threads=args.cpu_threads)
+                    threads=threads)
             cs += time.perf_counter() - t1
             done += b
-        cpu = {"value": round(done * ends / cs / 1e6, 4), "unit": "Mreads/s", "cores": args.cpu_threads, "kind": "port",
-               "sample": "first %d reads of the timed batch, oracle/svoracle.c restatement, %d pthreads, %.1f s" % (
-                   done, args.cpu_threads, cs)}
+        cpu_base = {"value": round(done * ends / cs / 1e6, 4), "unit": "Mreads/s", "cores": threads, "kind": "port",
+                    "sample": "first %d reads of the timed batch, oracle/svoracle.c restatement, %d pthreads, %.1f s" % (
+                        done, threads, cs),
+                    "cpu_model": cpu["model"], "host_logical_cpus": cpu["logical_cpus"],
+                    "usable_cpus": cpu["usable_cpus"], "cgroup_quota_cpus": cpu["cgroup_quota_cpus"]}
+        cal = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
+        if os.path.exists(cal):
+            c = json.load(open(cal))
+            cpu_base["reference_over_port"] = c.get("reference_over_port")
+            cpu_base["reference_equiv_value"] = round(cpu_base["value"] * c["reference_over_port"], 4)
+            cpu_base["calibration"] = "%s: %s" % (os.path.relpath(cal, ROOT), c.get("summary", ""))
 
     total_reads = n * ends * world * args.steps
     value = total_reads / elapsed / 1e6
@@ -320,6 +379,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": W["desc"], "reads_per_gpu_per_step": n * ends, "read_len": L,
                        "mode": {"se": "subread-align SE", "pe": "subread-align PE", "sj": "subjunc SE"}[kind],
+                       "entry": "svg_vote_batch_packed: 2-bit packed reads in host-pinned memory -> mapping_result_t "
+                                "in host-pinned memory (H2D + vote + compacted D2H + host expansion)",
                        "index": "full one-block (gap 1), %d buckets, %d items, %s" % (
                            ix.info.buckets, ix.info.items,
                            "reference-format files via svg_index_open" if prefix else "built in HBM by svg_index_build_mem"),
@@ -333,12 +394,14 @@ def main():
                          "kernels": kernels,
                          "deferred_reads": st.get("deferred", 0),
                          "path": {"achieved": round(achieved, 2), "algorithmic_bytes_per_read": round(algo_bytes / n, 1),
-                                  "step_ms": round(avg_kern_s * 1e3, 3), "frac": round(achieved / HBM_PEAK_GBS, 5)}},
-            "host_path": host,
-            "cpu_baseline": cpu,
+                                  "step_ms": round(step_s * 1e3, 3), "frac": round(achieved / HBM_PEAK_GBS, 5)}},
+            "device_path": device_path,
+            "ascii_host_path": ascii_host,
+            "cpu_baseline": cpu_base,
             "parity_check": check,
         }
         print(json.dumps(line), flush=True)
+    del keep
     ix.close()
     if dist is not None:
         dist.destroy_process_group()

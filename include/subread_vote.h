@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SVG_ABI_VERSION 1
+#define SVG_ABI_VERSION 2
 
 /* reference constants (subread.h:73,88,216-217; core-junction.c:3569) */
 #define SVG_MAX_READ_LENGTH       1210   /* MAX_READ_LENGTH == index padding */
@@ -134,6 +134,36 @@ typedef struct svg_reads {
 	uint64_t        n_reads;
 } svg_reads;
 
+/*
+ * The same reads 2-bit packed: ~4x fewer bytes to move than ASCII.
+ *   bases : base2int codes (subread.h:238: A=0 G=1 C=2 T=3; any other character 2 if it
+ *           sorts below 'G', else 3), 16 per word; base k of the stream in bits
+ *           31-2(k%16) .. 30-2(k%16) of word k/16, so 16 bases starting at a word boundary
+ *           read as genekey2int's key (input-files.c:1232).
+ *   xmask : NULL when every base is A/C/G/T/U; else 1 bit per base (bit 31-(k%32) of word
+ *           k/32) set for any other character (N, '.', lowercase, IUPAC ...).  Those all
+ *           complement to 'N' in reverse_read (input-files.c:1111) and never match the
+ *           genome there; 'U' behaves as 'T' everywhere and packs as T.  (A read holds no
+ *           NUL byte -- it would end the reference's C string.)
+ *   starts: base index of read i in the stream; NULL = i * stride.
+ * Read i = bases starts[i] .. starts[i]+lens[i]-1.  svg_pack_reads() builds this form.
+ */
+typedef struct svg_packed_reads {
+	const uint32_t *bases;
+	const uint32_t *xmask;
+	const uint64_t *starts;
+	uint64_t        stride;
+	const uint16_t *lens;
+	uint64_t        n_reads;
+} svg_packed_reads;
+
+/* Pack ASCII reads: with starts != NULL the reads go back to back (starts[i] filled in,
+ * bases sized ceil(sum(lens)/16) words, xmask ceil(sum(lens)/32)); with starts == NULL read
+ * i goes to base i*stride (every lens[i] <= stride; n*stride bases).  Returns the number of
+ * exception bases (0: the caller may pass xmask = NULL to the vote) or a negative SVG_E_*. */
+int64_t svg_pack_reads(const svg_reads *in, uint64_t stride, uint32_t *bases, uint32_t *xmask, uint64_t *starts,
+                       int threads);
+
 /* opaque index handle: owns the HBM copy of <prefix>.00.b.tab / .array / .reads */
 typedef struct svg_index svg_index;
 
@@ -184,6 +214,14 @@ int svg_vote_batch(svg_index *idx, const svg_params *p,
                    const svg_reads *r1, const svg_reads *r2,
                    svg_mapping_result *out, svg_subjunc_result *jout,
                    uint16_t *big_margin);
+/* The same from 2-bit packed reads (host buffers).  Both host entry points run a sub-batch
+ * pipeline: upload of sub-batch i+1, vote of i, download of i-1 (only the non-zero records,
+ * compacted on the GPU) and expansion of i-2 into `out` by worker threads overlap
+ * (SVG_HOST_THREADS, default min(8, cores)).  Pinned caller buffers copy fastest. */
+int svg_vote_batch_packed(svg_index *idx, const svg_params *p,
+                          const svg_packed_reads *r1, const svg_packed_reads *r2,
+                          svg_mapping_result *out, svg_subjunc_result *jout,
+                          uint16_t *big_margin);
 
 /*
  * Same computation on device-resident buffers, asynchronous on `hip_stream`
@@ -194,6 +232,12 @@ int svg_vote_batch_device(svg_index *idx, const svg_params *p,
                           const svg_reads *r1, const svg_reads *r2,
                           svg_mapping_result *out, svg_subjunc_result *jout,
                           uint16_t *big_margin, void *hip_stream);
+/* Packed reads in device memory (unpacked on the GPU into a buffer of the handle, sized by
+ * svg_set_max_read_length's bound), asynchronous on `hip_stream`. */
+int svg_vote_batch_packed_device(svg_index *idx, const svg_params *p,
+                                 const svg_packed_reads *r1, const svg_packed_reads *r2,
+                                 svg_mapping_result *out, svg_subjunc_result *jout,
+                                 uint16_t *big_margin, void *hip_stream);
 
 /* Per-batch statistics of the last svg_vote_batch* call on this handle
  * (filled only when the handle was opened with SVG_STATS=1 in the environment
@@ -211,8 +255,15 @@ int svg_set_stats(svg_index *idx, int enable);
 /* Upper bound of read lengths passed to svg_vote_batch_device on this handle
  * (default 256; svg_vote_batch measures its own batch).  A tighter bound lets
  * the library pick a kernel variant with smaller probe tables and higher
- * occupancy; reads beyond the bound are rejected. */
+ * occupancy.  A read that needs more subread probes than the bound provides
+ * gets zeroed records and raises the handle's sticky device error, which
+ * svg_device_status() reports as SVG_E_ARG (svg_vote_batch checks it itself). */
 int svg_set_max_read_length(svg_index *idx, int max_len);
+/* Waits for the work queued on the handle and returns 0, or SVG_E_ARG (message in
+ * svg_last_error) when a read since the previous check violated the read-length
+ * bound; clears the error.  Calls on one handle are ordered on the device even
+ * when they are given different streams. */
+int svg_device_status(svg_index *idx);
 int svg_get_stats(const svg_index *idx, svg_batch_stats *out);
 
 /* Per-kernel device time (diagnostics / roofline): while enabled, every probe_kernel

@@ -1,0 +1,195 @@
+/*
+ * integration/do_voting_gpu.c -- the reference-side binding of include/subread_vote.h.
+ *
+ * What a Subread maintainer adds to subread-align / subjunc (v2.0.6) to run the voting
+ * step on an MI355X: do_voting_gpu() replaces do_voting() (src/core.c:3049) for one-block
+ * indexes.  It is compiled here against the REFERENCE's own headers
+ * (tests/test_boundary_ref.py: gcc -c -I/root/reference/src -Iinclude), so every field
+ * name and type below is checked by a compiler; it is not linked into anything in this
+ * repository.
+ *
+ *   svg_attach           once, after load_global_context (core.c:4013) has the index prefix
+ *   do_voting_gpu        per chunk, from ONE host thread per GPU (run_in_thread, core.c:3366)
+ *
+ * The chunk's reads come from fetch_next_read_pair (core.c:1121) exactly as do_voting
+ * reads them -- that function already applies the -S reversal (core.c:1186-1198), so the
+ * library is told not to reverse again (reverse_r1 = reverse_r2 = 0).  Reads are 2-bit
+ * packed on the host (svg_pack_reads) and voted with svg_vote_batch_packed straight into
+ * the chunk's bigtable (core-bigtable.c:84-131).  The final-voting-run block of do_voting
+ * (core.c:3240-3290: find_new_indels / find_new_junctions per record) then runs on the
+ * host unchanged, from the same records.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "subread.h"
+#include "core.h"
+#include "core-indel.h"
+#include "core-junction.h"
+#include "input-files.h"
+#include "subread_vote.h"
+
+/* defined in core.c (non-static there, not declared in a header) */
+int fetch_next_read_pair(global_context_t *global_context, thread_context_t *thread_context, gene_input_t *ginp1,
+                         gene_input_t *ginp2, int *read_len_1, int *read_len_2, char *read_name_1, char *read_name_2,
+                         char *read_text_1, char *read_text_2, char *qual_text_1, char *qual_text_2,
+                         int remove_color_head, subread_read_number_t *read_no_in_chunk);
+void init_chunk_scanning_parameters(global_context_t *global_context, thread_context_t *thread_context,
+                                    gene_input_t **ginp1, gene_input_t **ginp2);
+int locate_current_value_index(global_context_t *global_context, thread_context_t *thread_context,
+                               mapping_result_t *result, int rlen);
+int has_better_mapping(global_context_t *global_context, thread_context_t *thread_context,
+                       subread_read_number_t current_read_number, int is_second_read, int this_aln_id);
+
+static svg_index *svg_ix;   /* one per process, one process per GPU */
+
+int svg_attach(global_context_t *gc, int device)
+{
+	char prefix[MAX_FILE_NAME_LENGTH + 1];
+	snprintf(prefix, sizeof prefix, "%s", gc->config.index_prefix);
+	int rc = svg_index_open(prefix, device, &svg_ix);
+	if (rc) SUBREADprintf("GPU voting unavailable: %s\n", svg_last_error());
+	return rc;
+}
+
+static void svg_fill_params(global_context_t *gc, svg_params *p)
+{
+	svg_params_default(p, gc->config.do_breakpoint_detection ? SVG_PROGRAM_SUBJUNC : SVG_PROGRAM_ALIGN,
+	                   gc->input_reads.is_paired_end_reads);
+	p->total_subreads = gc->config.total_subreads;
+	p->min_votes_first = gc->config.minimum_subread_for_first_read;
+	p->min_votes_second = gc->config.minimum_subread_for_second_read;
+	p->max_indel_length = gc->config.max_indel_length;
+	p->multi_best = gc->config.multi_best_reads;
+	p->top_scores = gc->config.top_scores;
+	p->max_vote_simples = gc->config.max_vote_simples;
+	p->max_vote_combinations = gc->config.max_vote_combinations;
+	p->max_vote_number_cutoff = gc->config.max_vote_number_cutoff;
+	p->min_pair_distance = gc->config.minimum_pair_distance;
+	p->max_pair_distance = gc->config.maximum_pair_distance;
+	/* fetch_next_read_pair has already reversed the reads that -S asks for */
+	p->reverse_r1 = 0;
+	p->reverse_r2 = 0;
+	p->do_breakpoint_detection = gc->config.do_breakpoint_detection;
+	p->do_big_margin_filtering_for_junctions = gc->config.do_big_margin_filtering_for_junctions;
+	p->big_margin_record_size = gc->config.big_margin_record_size;
+	p->maximum_intron_length = gc->config.maximum_intron_length;
+	p->prefer_donor_receptor_junctions = gc->config.prefer_donor_receptor_junctions;
+	p->check_donor_at_junctions = gc->config.check_donor_at_junctions;
+	p->max_insertion_at_junctions = gc->config.max_insertion_at_junctions;
+	p->more_accurate_fusions = gc->config.more_accurate_fusions;
+}
+
+/* the chunk's reads as the reference reads them: text, names, qualities, lengths */
+typedef struct {
+	char *text[2], *qual[2], *name[2];
+	uint16_t *len[2];
+	uint64_t *off[2];
+	uint64_t n, cap, bytes[2], bcap[2];
+} svg_chunk_reads;
+
+static int chunk_push(svg_chunk_reads *c, int e, const char *text, const char *qual, const char *name, int len)
+{
+	if (c->bytes[e] + len + 1 > c->bcap[e]) {
+		c->bcap[e] = (c->bcap[e] + len + 1) * 2;
+		c->text[e] = realloc(c->text[e], c->bcap[e]);
+		c->qual[e] = realloc(c->qual[e], c->bcap[e]);
+		if (!c->text[e] || !c->qual[e]) return -1;
+	}
+	memcpy(c->text[e] + c->bytes[e], text, len);
+	memcpy(c->qual[e] + c->bytes[e], qual, len);
+	c->off[e][c->n] = c->bytes[e];
+	c->len[e][c->n] = (uint16_t)len;
+	snprintf(c->name[e] + c->n * (MAX_READ_NAME_LEN + 1), MAX_READ_NAME_LEN + 1, "%s", name);
+	c->bytes[e] += len;
+	return 0;
+}
+
+int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
+{
+	gene_input_t *ginp1 = NULL, *ginp2 = NULL;
+	char text[2][MAX_READ_LENGTH + 1], qual[2][MAX_READ_LENGTH + 1], name[2][MAX_READ_NAME_LEN + 1];
+	int len[2] = {0, 0}, ends = 1 + gc->input_reads.is_paired_end_reads, rc = 0, e;
+	subread_read_number_t rno = 0;
+	svg_chunk_reads c;
+	memset(&c, 0, sizeof c);
+	init_chunk_scanning_parameters(gc, tc, &ginp1, &ginp2);
+
+	/* 1. the chunk's reads, in chunk read-number order (one thread: numbers are sequential) */
+	for (;;) {
+		fetch_next_read_pair(gc, tc, ginp1, ginp2, &len[0], &len[1], name[0], name[1], text[0], text[1], qual[0], qual[1], 1, &rno);
+		if (rno < 0) break;
+		if (c.n == c.cap) {
+			c.cap = c.cap ? 2 * c.cap : 1 << 16;
+			for (e = 0; e < ends; e++) {
+				c.len[e] = realloc(c.len[e], c.cap * sizeof(uint16_t));
+				c.off[e] = realloc(c.off[e], c.cap * sizeof(uint64_t));
+				c.name[e] = realloc(c.name[e], c.cap * (MAX_READ_NAME_LEN + 1));
+				if (!c.len[e] || !c.off[e] || !c.name[e]) return 1;
+			}
+		}
+		for (e = 0; e < ends; e++)
+			if (chunk_push(&c, e, text[e], qual[e], name[e], len[e])) return 1;
+		c.n++;
+	}
+
+	/* 2. one packed call for the whole chunk, records into the bigtable */
+	svg_params p;
+	svg_fill_params(gc, &p);
+	svg_packed_reads pk[2];
+	uint32_t *bases[2] = {NULL, NULL}, *xmask[2] = {NULL, NULL};
+	uint64_t *starts[2] = {NULL, NULL};
+	for (e = 0; e < ends && !rc; e++) {
+		svg_reads r = {c.text[e], c.off[e], c.len[e], c.n};
+		bases[e] = malloc(4 * (c.bytes[e] / 16 + 1));
+		xmask[e] = malloc(4 * (c.bytes[e] / 32 + 1));
+		starts[e] = malloc(8 * (c.n + 1));
+		int64_t nx = svg_pack_reads(&r, 0, bases[e], xmask[e], starts[e], gc->config.all_threads);
+		if (nx < 0) { rc = (int)nx; break; }
+		svg_packed_reads q = {bases[e], nx ? xmask[e] : NULL, starts[e], 0, c.len[e], c.n};
+		pk[e] = q;
+	}
+	if (!rc && c.n)
+		rc = svg_vote_batch_packed(svg_ix, &p, &pk[0], ends == 2 ? &pk[1] : NULL,
+		                           (svg_mapping_result *)_global_retrieve_alignment_ptr(gc, 0, 0, 0),
+		                           p.do_breakpoint_detection ? (svg_subjunc_result *)_global_retrieve_subjunc_ptr(gc, 0, 0, 0) : NULL,
+		                           p.do_big_margin_filtering_for_junctions ? _global_retrieve_big_margin_ptr(gc, 0, 0) : NULL);
+	if (rc) SUBREADprintf("svg_vote_batch_packed: %s\n", svg_last_error());
+
+	/* 3. unchanged host step: the final-voting-run block of do_voting (core.c:3240-3290) */
+	int need_junction_step = gc->config.do_breakpoint_detection || gc->config.do_fusion_detection || gc->config.do_long_del_detection;
+	subread_read_number_t r;
+	for (r = 0; !rc && gc->is_final_voting_run && r < (subread_read_number_t)c.n; r++) {
+		for (e = 0; e < ends; e++) {
+			int has_reversed = 0;   /* the text as fetched (do_voting's copy is reversed after its strand loop) */
+			char *rt = text[0], *rq = qual[0];
+			int rl = c.len[e][r];
+			memcpy(rt, c.text[e] + c.off[e][r], rl);
+			memcpy(rq, c.qual[e] + c.off[e][r], rl);
+			rt[rl] = rq[rl] = 0;
+			char *rn = c.name[e] + r * (MAX_READ_NAME_LEN + 1);
+			int b;
+			for (b = 0; b < gc->config.multi_best_reads; b++) {
+				mapping_result_t *cur = _global_retrieve_alignment_ptr(gc, r, e, b);
+				if (cur->selected_votes < 1) continue;
+				int should = (cur->result_flags & CORE_IS_NEGATIVE_STRAND) ? 1 : 0;
+				if (should != has_reversed) {
+					has_reversed = !has_reversed;
+					reverse_read(rt, rl, gc->config.space_type);
+					reverse_quality(rq, rl);
+				}
+				gene_value_index_t *saved = tc ? tc->current_value_index : gc->current_value_index;
+				locate_current_value_index(gc, tc, cur, rl);
+				if (!has_better_mapping(gc, tc, r, e, b)) find_new_indels(gc, tc, r, rn, rt, rq, rl, e, b);
+				if (need_junction_step) find_new_junctions(gc, tc, r, rn, rt, rq, rl, e, b);
+				if (tc) tc->current_value_index = saved;
+				else gc->current_value_index = saved;
+			}
+		}
+	}
+	for (e = 0; e < 2; e++) {
+		free(bases[e]); free(xmask[e]); free(starts[e]);
+		free(c.text[e]); free(c.qual[e]); free(c.name[e]); free(c.len[e]); free(c.off[e]);
+	}
+	return rc ? 1 : 0;
+}

@@ -3,7 +3,7 @@
 The product is the C-ABI shared library ``subread_amd/lib/libsubread_amd.so``
 (include/subread_vote.h): host C (index loader, format-exact index builder,
 read simulator) + hand-written HIP kernels for gfx950.  This module is a thin
-ctypes wrapper used by the CLI front end, the tests and bench.py.
+ctypes wrapper used by the tests and bench.py.
 
 There is no CPU fallback anywhere in this package: if the library is missing,
 or the GPU is missing when a vote is requested, the call raises.
@@ -15,8 +15,8 @@ import subprocess
 import numpy as np
 
 from .abi import (MAPPING_DTYPE, SUBJUNC_DTYPE, BIG_MARGIN_WORDS, ERRORS, PROGRAM_ALIGN,
-                  PROGRAM_SUBJUNC, SvgParams, SvgReads, SvgIndexInfo, SvgBatchStats, ReadBatch,
-                  default_params, read_fastq)
+                  PROGRAM_SUBJUNC, SvgParams, SvgReads, SvgPackedReads, SvgIndexInfo, SvgBatchStats, ReadBatch,
+                  PackedBatch, default_params, read_fastq)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SVG_LIB") or os.path.join(HERE, "lib", "libsubread_amd.so")
@@ -29,7 +29,8 @@ EXPORTS = [
     "svg_last_error", "svg_abi_version", "svg_build_index", "svg_sim_genome",
     "svg_sim_repeats", "svg_sim_reads", "svg_index_build", "svg_index_build_mem", "svg_index_export",
     "svg_set_max_read_length", "svg_sim_pairs", "svg_set_timing", "svg_get_timing",
-    "svg_get_kernel_timing",
+    "svg_get_kernel_timing", "svg_device_status", "svg_pack_reads", "svg_vote_batch_packed",
+    "svg_vote_batch_packed_device",
 ]
 
 _lib = None
@@ -53,6 +54,12 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise SvgError("libsubread_amd.so not built (run __graft_entry__.build() or make -C subread_amd/csrc)")
+        # one HIP runtime per process: when PyTorch is present, let it load its HIP runtime first
+        # so that this library binds to the same one (device buffers are shared with torch)
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         vp, i32, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64
         L.svg_params_default.argtypes = [vp, i32, i32]
@@ -74,6 +81,14 @@ def lib():
         L.svg_get_kernel_timing.restype = i32
         L.svg_set_max_read_length.argtypes = [vp, i32]
         L.svg_set_max_read_length.restype = i32
+        L.svg_device_status.argtypes = [vp]
+        L.svg_device_status.restype = i32
+        L.svg_pack_reads.argtypes = [vp, u64, vp, vp, vp, i32]
+        L.svg_pack_reads.restype = ctypes.c_int64
+        L.svg_vote_batch_packed.argtypes = [vp] * 7
+        L.svg_vote_batch_packed.restype = i32
+        L.svg_vote_batch_packed_device.argtypes = [vp] * 8
+        L.svg_vote_batch_packed_device.restype = i32
         L.svg_last_error.restype = ctypes.c_char_p
         L.svg_index_build.argtypes = [ctypes.c_char_p, i32, i32, i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
         L.svg_index_build.restype = i32
@@ -113,6 +128,30 @@ def build_index(fasta, prefix, gap=3, memory_mb=8000, force_one_block=False, rep
     rc = lib().svg_build_index(str(fasta).encode(), str(prefix).encode(), gap, memory_mb,
                                1 if force_one_block else 0, repeat_threshold)
     _check(rc, "svg_build_index")
+
+
+def pack_reads(batch, stride=None, threads=8, alloc=None):
+    """svg_pack_reads: ASCII ReadBatch -> PackedBatch.  stride=None packs the reads back to
+    back (starts filled in); else read i goes to base i*stride.  `alloc(nbytes, dtype)` may
+    supply the arrays (e.g. pinned memory)."""
+    n = len(batch)
+    if alloc is None:
+        alloc = lambda count, dt: np.empty(count, dt)
+    if stride is None:
+        total = int(batch.lens.astype(np.int64).sum())
+        starts = alloc(max(1, n), np.uint64)
+    else:
+        total = n * int(stride)
+        starts = None
+    bases = alloc(max(1, (total + 15) // 16), np.uint32)
+    xmask = alloc(max(1, (total + 31) // 32), np.uint32)
+    s = batch.struct()
+    ne = lib().svg_pack_reads(ctypes.byref(s), int(stride or 0), bases.ctypes.data, xmask.ctypes.data,
+                              starts.ctypes.data if starts is not None else None, int(threads))
+    if ne < 0:
+        _check(int(ne), "svg_pack_reads")
+    return PackedBatch(bases, xmask if ne > 0 else None, starts[:n] if starts is not None else None,
+                       stride or 0, batch.lens)
 
 
 class VoteIndex:
@@ -178,6 +217,10 @@ class VoteIndex:
 
     def set_max_read_length(self, n):
         _check(lib().svg_set_max_read_length(self.h, int(n)), "svg_set_max_read_length")
+
+    def device_status(self):
+        """Wait for queued work; raise SvgError if a read broke the read-length bound."""
+        _check(lib().svg_device_status(self.h), "svg_device_status")
 
     def set_timing(self, on=True):
         _check(lib().svg_set_timing(self.h, 1 if on else 0), "svg_set_timing")
@@ -245,6 +288,36 @@ class VoteIndex:
                                   bm.ctypes.data if bm is not None else None)
         _check(rc, "svg_vote_batch")
         return out, jout, bm
+
+    def _outputs(self, params, n, ends, bufs):
+        mb = params.multi_best
+        if bufs is not None:
+            return bufs
+        out = np.zeros((n, ends, mb), dtype=MAPPING_DTYPE)
+        jout = np.zeros((n, ends, mb), dtype=SUBJUNC_DTYPE) if params.do_breakpoint_detection else None
+        bm = (np.zeros((n, ends, BIG_MARGIN_WORDS), dtype=np.uint16)
+              if params.do_big_margin_filtering_for_junctions else None)
+        return out, jout, bm
+
+    def vote_packed(self, params, p1, p2=None, bufs=None):
+        """svg_vote_batch_packed: PackedBatch in (host), records out like vote()."""
+        n = len(p1)
+        out, jout, bm = self._outputs(params, n, 2 if p2 is not None else 1, bufs)
+        s1 = p1.struct()
+        s2 = p2.struct() if p2 is not None else None
+        rc = lib().svg_vote_batch_packed(self.h, ctypes.byref(params), ctypes.byref(s1),
+                                         ctypes.byref(s2) if s2 is not None else None,
+                                         out.ctypes.data, jout.ctypes.data if jout is not None else None,
+                                         bm.ctypes.data if bm is not None else None)
+        _check(rc, "svg_vote_batch_packed")
+        return out, jout, bm
+
+    def vote_packed_device(self, params, q1, q2, out_ptr, jout_ptr=None, bm_ptr=None, stream=None):
+        """svg_vote_batch_packed_device: q* = SvgPackedReads holding device pointers."""
+        rc = lib().svg_vote_batch_packed_device(self.h, ctypes.byref(params), ctypes.byref(q1),
+                                                ctypes.byref(q2) if q2 is not None else None,
+                                                out_ptr, jout_ptr, bm_ptr, stream)
+        _check(rc, "svg_vote_batch_packed_device")
 
     def vote_device(self, params, r1_ptrs, r2_ptrs, out_ptr, jout_ptr=None, bm_ptr=None, stream=None):
         """Device pointers in/out, async on `stream` (int handle or None).

@@ -77,6 +77,17 @@ class SvgReads(ctypes.Structure):
     ]
 
 
+class SvgPackedReads(ctypes.Structure):
+    _fields_ = [
+        ("bases", ctypes.c_void_p),
+        ("xmask", ctypes.c_void_p),
+        ("starts", ctypes.c_void_p),
+        ("stride", ctypes.c_uint64),
+        ("lens", ctypes.c_void_p),
+        ("n_reads", ctypes.c_uint64),
+    ]
+
+
 class SvgIndexInfo(ctypes.Structure):
     _fields_ = [
         ("items", ctypes.c_uint64),
@@ -185,6 +196,69 @@ class ReadBatch:
         s.lens = self.lens.ctypes.data
         s.n_reads = len(self)
         return s
+
+
+PACK_CODE = np.full(256, 3, np.uint8)        # base2int, subread.h:238
+PACK_CODE[:ord("G")] = 2
+PACK_CODE[ord("A")] = 0
+PACK_CODE[ord("G")] = 1
+PACK_EXCEPTION = np.ones(256, bool)           # complements to 'N' in reverse_read (input-files.c:1111)
+PACK_EXCEPTION[[ord(c) for c in "ACGTU"]] = False
+
+
+class PackedBatch:
+    """Reads in the 2-bit form of svg_packed_reads (include/subread_vote.h).
+    `xmask` is None when every base is A/C/G/T/U; `starts` None means read i at i*stride."""
+
+    def __init__(self, bases, xmask, starts, stride, lens):
+        self.bases = np.ascontiguousarray(bases, dtype=np.uint32)
+        self.xmask = None if xmask is None else np.ascontiguousarray(xmask, dtype=np.uint32)
+        self.starts = None if starts is None else np.ascontiguousarray(starts, dtype=np.uint64)
+        self.stride = int(stride)
+        self.lens = np.ascontiguousarray(lens, dtype=np.uint16)
+
+    def __len__(self):
+        return int(self.lens.shape[0])
+
+    def struct(self):
+        s = SvgPackedReads()
+        s.bases = self.bases.ctypes.data
+        s.xmask = self.xmask.ctypes.data if self.xmask is not None else None
+        s.starts = self.starts.ctypes.data if self.starts is not None else None
+        s.stride = self.stride
+        s.lens = self.lens.ctypes.data
+        s.n_reads = len(self)
+        return s
+
+    @classmethod
+    def pack_numpy(cls, batch, stride=None):
+        """Pure-numpy packer (test cross-check of svg_pack_reads): back to back when
+        stride is None, else read i at base i*stride."""
+        n = len(batch)
+        lens = batch.lens.astype(np.int64)
+        if stride is None:
+            starts = np.zeros(n, np.uint64)
+            if n > 1:
+                starts[1:] = np.cumsum(lens[:-1]).astype(np.uint64)
+            total = int(lens.sum())
+            pos = starts.astype(np.int64)
+        else:
+            starts = None
+            total = n * stride
+            pos = np.arange(n, dtype=np.int64) * stride
+        codes = np.zeros(total + 32, np.uint8)
+        xm = np.zeros(total + 32, bool)
+        for i in range(n):
+            c = np.frombuffer(batch.read(i), dtype=np.uint8)
+            codes[pos[i]:pos[i] + len(c)] = PACK_CODE[c]
+            xm[pos[i]:pos[i] + len(c)] = PACK_EXCEPTION[c]
+        nw = (total + 15) // 16
+        cw = codes[:nw * 16].reshape(nw, 16).astype(np.uint32)
+        bases = (cw << (30 - 2 * np.arange(16, dtype=np.uint32))).sum(1, dtype=np.uint64).astype(np.uint32)
+        nx = (total + 31) // 32
+        xw = xm[:nx * 32].reshape(nx, 32).astype(np.uint64)
+        xmask = (xw << (31 - np.arange(32, dtype=np.uint64))).sum(1).astype(np.uint32)
+        return cls(bases, xmask if xm.any() else None, starts, stride or 0, batch.lens)
 
 
 def read_fastq(path):

@@ -62,10 +62,17 @@ struct svg_index {
 	double tms[4];
 	// staging for svg_vote_batch (host buffers): two sub-batch slots, uploads and downloads on
 	// their own streams so PCIe traffic of sub-batches i+1 / i-1 overlaps the vote of i
-	void *d_in[2]; size_t d_in_cap[2];
+	void *d_in[3]; size_t d_in_cap[3];     // uploads run one sub-batch ahead: three input slots
 	void *d_out[2]; size_t d_out_cap[2];
 	hipStream_t up_stream, down_stream;
-	hipEvent_t ev_up[2], ev_done[2], ev_down[2];
+	hipEvent_t ev_up[3], ev_done[3], ev_down[3];
+	// sticky device error word (KParams::err) and the handle's last queued work: every call
+	// orders its stream after the previous call's work, since both reuse the buffers above
+	uint32_t *d_err;
+	hipEvent_t ev_last;
+	int last_pending;
+	// host-buffer entry points (svg_io.hip): record compaction slots, pinned staging, worker pool
+	struct svg_hostio *io;
 };
 
 #define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) { svg_set_error("HIP error %s at %s:%d", hipGetErrorString(_e), __FILE__, __LINE__); return SVG_E_DEVICE; } } while (0)
@@ -79,6 +86,87 @@ static inline int dmalloc(svg_index *h, void **p, size_t n)
 }
 
 int svg_index_finish_device(svg_index *h);
+
+// grow-only device buffer
+static inline int svg_ensure(svg_index *h, void **p, size_t *cap, size_t need)
+{
+	if (need <= *cap) return 0;
+	hipFree(*p);
+	*p = NULL;
+	*cap = 0;
+	if (dmalloc(h, p, need)) return SVG_E_NOMEM;
+	*cap = need;
+	return 0;
+}
+
+// svg_io.hip
+void svg_io_free(svg_index *h);
+
+// ---------------------------------------------------------------------------------------------
+// kernel parameters (passed by value)
+struct KParams {
+	svg_params p;
+	DevIndex ix;
+	const char *seq1, *seq2;
+	const uint64_t *off1, *off2;
+	const uint16_t *len1, *len2;
+	uint64_t n_reads;
+	uint8_t *out;             // mapping records
+	uint8_t *jout;            // subjunc records
+	uint16_t *bm_out;
+	uint32_t *scratch;        // per-wave cold state
+	unsigned long long *stats; // probes, bucket_items, hits, results (may be NULL)
+	int tol, ii_end;
+	uint32_t low, high;
+	const uint2 *precs;       // probe records of this chunk (probe_kernel)
+	int nps;                  // probe slots per (end, strand) in precs
+	uint32_t prec_stride;     // 0: records of read r at precs[r*per + i]; else SoA precs[i*stride + r]
+	const uint32_t *idx;      // NULL: reads 0..n_reads-1; else the reads idx[0..*idx_count) (deferred by lane_kernel)
+	const uint32_t *idx_count;
+	uint32_t *work;           // indirect mode: zeroed work counter (waves grab deferred reads dynamically)
+	uint32_t *err;            // sticky device error word (svg_device_status): bit 0 = a read needs more
+	                          // probes than the announced read-length bound provides, bit 1 = a read
+	                          // longer than the kernel variant's text buffer; such reads get zero records
+};
+
+// probe kernel parameters: one thread per (read, end, strand, subread x gap slot)
+struct PParams {
+	DevIndex ix;
+	const char *seq1, *seq2;
+	const uint64_t *off1, *off2;
+	const uint16_t *len1, *len2;
+	uint32_t n_reads;
+	int nps;
+	int total_subreads, reverse_r1, reverse_r2;
+	uint64_t nb_magic;        // ceil(2^64 / nb): key / nb == umulhi64(key, nb_magic) for 32-bit keys
+	uint2 *out;               // [read][end][strand][nps] (soa = 0) or [end][strand][nps][read] (soa = 1):
+	                          // x = midpoint item, y = fwd | bwd << 16
+	int soa;
+	int window;               // one-shot bucket loads (keys of a bucket sorted as int16: nb >= 131073)
+	int readmajor;            // soa output with read-major threads (consecutive threads = one read's probes)
+	unsigned long long *stats;
+	// 2-bit packed input (svg_packed_reads) per end, read r of the chunk at base
+	// pk_starts[e][r] or pk_base0[e] + r * pk_stride[e]; seq/off unused when packed
+	int packed;
+	const uint32_t *pk_bases[2], *pk_xmask[2];
+	const uint64_t *pk_starts[2];
+	uint64_t pk_stride[2], pk_base0[2];
+};
+
+// svg_vote.hip: a prepared batch (kernel parameters) and its per-chunk launch
+struct VoteJob {
+	KParams kp;
+	PParams pp;
+	int npmax, nps, ends;
+	bool sj, lane, overlap_mode;
+	uint64_t per_read, chunk;   // probe records per read; reads per chunk (<= 1 GiB of records)
+};
+int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2, svg_mapping_result *out,
+                     svg_subjunc_result *jout, uint16_t *big_margin, VoteJob *job);
+int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slot, hipStream_t st, hipStream_t st2);
+int svg_vote_batch_device_packed(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                                 const svg_packed_reads *pk, svg_mapping_result *out, svg_subjunc_result *jout,
+                                 uint16_t *big_margin, hipStream_t stream);
 
 // svg_lane.hip
 int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int sj);

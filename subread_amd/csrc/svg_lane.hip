@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 		}
 		if constexpr (NPF > 0) {
 			// fused gather: the lane path's limits (the gather kernel's, for the unfused path)
-			if (!L.dfr && (len < 15 + lp.gap || len > 160 || applied > 31 || applied * lp.gap > NPF)) { L.dfr = true; L.why = 1; }
+			if (!L.dfr && (len < 15 + lp.gap || len > 160 || applied > 31 || applied * lp.gap > NPF || applied * lp.gap > lp.nps)) { L.dfr = true; L.why = 1; }
 		}
 		const uint32_t high_b = lp.high - (uint32_t)len;
 		// the read's bigtable records: source (-1 none, else strand << 5 | slot), position, votes, used
@@ -749,7 +749,7 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 				if (step[e] < (lp.gap << 16)) step[e] = lp.gap << 16;
 				applied[e] = 1 + cr / step[e];
 			}
-			if (!L.dfr && (l < 15 + lp.gap || l > 160 || applied[e] > 31 || applied[e] * lp.gap > NPF)) { L.dfr = true; L.why = 1; }
+			if (!L.dfr && (l < 15 + lp.gap || l > 160 || applied[e] > 31 || applied[e] * lp.gap > NPF || applied[e] * lp.gap > lp.nps)) { L.dfr = true; L.why = 1; }
 			high_b[e] = lp.high - (uint32_t)l;
 		}
 		// bigtable records of both ends

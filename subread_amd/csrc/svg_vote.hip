@@ -47,47 +47,6 @@
 #define COLD_WORDS 8          // per slot: cs|ce<<16, rec[21] as bytes, pad
 #define JCW 17
 
-// kernel parameters (passed by value)
-struct KParams {
-	svg_params p;
-	DevIndex ix;
-	const char *seq1, *seq2;
-	const uint64_t *off1, *off2;
-	const uint16_t *len1, *len2;
-	uint64_t n_reads;
-	uint8_t *out;             // mapping records
-	uint8_t *jout;            // subjunc records
-	uint16_t *bm_out;
-	uint32_t *scratch;        // per-wave cold state
-	unsigned long long *stats; // probes, bucket_items, hits, results (may be NULL)
-	int tol, ii_end;
-	uint32_t low, high;
-	const uint2 *precs;       // probe records of this chunk (probe_kernel)
-	int nps;                  // probe slots per (end, strand) in precs
-	uint32_t prec_stride;     // 0: records of read r at precs[r*per + i]; else SoA precs[i*stride + r]
-	const uint32_t *idx;      // NULL: reads 0..n_reads-1; else the reads idx[0..*idx_count) (deferred by lane_kernel)
-	const uint32_t *idx_count;
-	uint32_t *work;           // indirect mode: zeroed work counter (waves grab deferred reads dynamically)
-};
-
-// probe kernel parameters: one thread per (read, end, strand, subread x gap slot)
-struct PParams {
-	DevIndex ix;
-	const char *seq1, *seq2;
-	const uint64_t *off1, *off2;
-	const uint16_t *len1, *len2;
-	uint32_t n_reads;
-	int nps;
-	int total_subreads, reverse_r1, reverse_r2;
-	uint64_t nb_magic;        // ceil(2^64 / nb): key / nb == umulhi64(key, nb_magic) for 32-bit keys
-	uint2 *out;               // [read][end][strand][nps] (soa = 0) or [end][strand][nps][read] (soa = 1):
-	                          // x = midpoint item, y = fwd | bwd << 16
-	int soa;
-	int window;               // one-shot bucket loads (keys of a bucket sorted as int16: nb >= 131073)
-	int readmajor;            // soa output with read-major threads (consecutive threads = one read's probes)
-	unsigned long long *stats;
-};
-
 // ---------------------------------------------------------------------------------------------
 // LDS layout of one wave.  Row occupancy (items[30]) and max_vote live in
 // registers (lane 32*end+row holds items[row]); only slot state is in LDS.
@@ -1177,16 +1136,16 @@ struct Wave {
 	{
 		const int lane = lane_id();
 		for (int e = 0; e < ENDS; e++) {
-			const char *seq = e ? kp->seq2 : kp->seq1;
-			uint64_t o = e ? kp->off2[r] : kp->off1[r];
 			int len = e ? kp->len2[r] : kp->len1[r];
 			if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;   // read_line keeps MAX_READ_LENGTH-1 (input-files.c:277)
 			if (len > MAXL) {   // host-validated; never index LDS past the text buffer
-				if (lane == 0 && kp->stats) atomicOr((unsigned long long *)&kp->stats[7], 1ull);
+				if (lane == 0) atomicOr(kp->err, 2u);
 				len = 0;
 			}
 			t_len[e] = len;
 			if constexpr (!SJ) continue;   // the vote step itself never reads the text
+			const char *seq = e ? kp->seq2 : kp->seq1;
+			const uint64_t o = e ? kp->off2[r] : kp->off1[r];
 			uintptr_t a = (uintptr_t)(seq + o);
 			const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
 			t_shift[e] = (int)(a & 3);
@@ -1290,8 +1249,10 @@ struct Wave {
 				rc.step[e] = step;
 				rc.applied[e] = 1 + cr / step;
 				rc.np[e] = rc.applied[e] * gap;
-				if (rc.np[e] > MAXP) {   // host-validated; keep LDS probe tables in bounds
-					if (lane == 0 && kp->stats) atomicOr((unsigned long long *)&kp->stats[7], 2ull);
+				if (rc.np[e] > MAXP || rc.np[e] > kp->nps) {
+					// beyond the probe records of this batch (svg_set_max_read_length) or the LDS
+					// probe tables: zero records and a sticky error (svg_device_status)
+					if (lane == 0) atomicOr(kp->err, 1u);
 					rc.np[e] = 0; rc.applied[e] = 0;
 				}
 			} else {
@@ -1457,7 +1418,7 @@ __device__ __forceinline__ bool try_run(uint64_t eq, int n, int &m, int &fwd, in
 // equal-key run on both sides of the first-hit midpoint); with no per-read state to keep,
 // it runs at high occupancy and hides the dependent bucket -> keys -> run chain.
 // =============================================================================================
-template <int ENDS, int BPC, bool LINE>
+template <int ENDS, int BPC, bool LINE, bool PACKED>
 __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 {
 	const DevIndex &ix = pp.ix;
@@ -1498,6 +1459,35 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 				const int rev = e ? pp.reverse_r2 : pp.reverse_r1;
 				const bool direct = s == rev;
 				const int start = direct ? off : len - 16 - off;
+				uint32_t key = 0;
+				if constexpr (PACKED) {
+					// 2-bit input (svg_packed_reads): the 16 codes at base k0 are one 32-bit window,
+					// already genekey2int's key.  Reverse strand: complement (~code; an exception base
+					// complements to 'N' = 3) and reverse the 2-bit groups.  Strand 1 of a reversed
+					// read is comp(comp(input)): the codes, with exception bases turned into 'N'.
+					const uint64_t k0 = (pp.pk_starts[e] ? pp.pk_starts[e][r] : pp.pk_base0[e] + (uint64_t)r * pp.pk_stride[e]) +
+					                    (uint64_t)start;
+					const uint32_t *bw = pp.pk_bases[e] + (k0 >> 4);
+					const uint32_t s2 = 2u * (uint32_t)(k0 & 15u);
+					const uint32_t W = s2 ? (bw[0] << s2) | (bw[1] >> (32u - s2)) : bw[0];
+					uint32_t X2 = 0;
+					if (pp.pk_xmask[e]) {
+						const uint32_t *xw = pp.pk_xmask[e] + (k0 >> 5);
+						const uint32_t s1 = (uint32_t)(k0 & 31u);
+						// bases k0..k0+15 (the next word only when they reach into it)
+						uint32_t t = (s1 > 16u ? (xw[0] << s1) | (xw[1] >> (32u - s1)) : xw[0] << s1) >> 16;
+						t = (t | (t << 8)) & 0x00ff00ffu;
+						t = (t | (t << 4)) & 0x0f0f0f0fu;
+						t = (t | (t << 2)) & 0x33333333u;
+						t = (t | (t << 1)) & 0x55555555u;
+						X2 = t | (t << 1);   // base i -> bits 31-2i .. 30-2i
+					}
+					if (direct) key = (s == 1 && rev) ? (W | X2) : W;
+					else {
+						const uint32_t v = __builtin_bitreverse32(~W | X2);
+						key = ((v >> 1) & 0x55555555u) | ((v & 0x55555555u) << 1);
+					}
+				} else {
 				const char *src = (e ? pp.seq2 : pp.seq1) + (e ? pp.off2[r] : pp.off1[r]) + start;
 				const uintptr_t a = (uintptr_t)src;
 				const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
@@ -1506,7 +1496,6 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 #pragma unroll
 				for (int q = 0; q < 4; q++) wd[q] = w[q];
 				wd[4] = sh ? w[4] : 0u;   // only when the window reaches into it
-				uint32_t key = 0;
 #pragma unroll
 				for (int i = 0; i < 16; i++) {
 					const int bi = sh + (direct ? i : 15 - i);
@@ -1514,6 +1503,7 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 					if (!direct) c = comp(c);
 					if (s == 1 && rev) c = comp(comp(c));   // strand 1 of a reversed read: comp(comp(input))
 					key |= b2i(c) << (30 - 2 * i);
+				}
 				}
 				const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
 				const uint32_t b = key - q * ix.nb;
@@ -1729,6 +1719,9 @@ int svg_index_finish_device(svg_index *h)
 		return rc;
 	HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
 	HIPCHK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+	HIPCHK(hipEventCreateWithFlags(&h->ev_up[2], hipEventDisableTiming));
+	HIPCHK(hipEventCreateWithFlags(&h->ev_done[2], hipEventDisableTiming));
+	HIPCHK(hipEventCreateWithFlags(&h->ev_down[2], hipEventDisableTiming));
 	for (int s = 0; s < 2; s++) {
 		HIPCHK(hipEventCreateWithFlags(&h->ev_lane[s], hipEventDisableTiming));
 		HIPCHK(hipEventCreateWithFlags(&h->ev_wave[s], hipEventDisableTiming));
@@ -1759,15 +1752,21 @@ int svg_index_finish_device(svg_index *h)
 	h->dix.bline = NULL;
 	if (x->nb >= 16843009u && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_BLINE")) {
 		// (2^32-1)/nb <= 255: every key_hi fits a byte; 64 B per bucket (5.95 GB at nb = 93M)
-		if ((rc = dmalloc(h, &h->d_bline, (size_t)x->nb * 64 + 64))) return rc;
-		uint64_t blocks = ((uint64_t)x->nb + 255) / 256, bmax = (uint64_t)h->n_cu * 64;
-		if (blocks > bmax) blocks = bmax;
-		hipLaunchKernelGGL(build_bline, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
-		                   (const int16_t *)h->d_keys, x->nb, (uint4 *)h->d_bline);
-		HIPCHK(hipGetLastError());
-		HIPCHK(hipStreamSynchronize(h->stream));
-		h->dix.bline = (const uint4 *)h->d_bline;
-	} else if (x->nb >= 16843009u && !getenv("SVG_NO_COMPACT")) {
+		// optional image: without the HBM for it the index still opens with the group/key images
+		if (dmalloc(h, &h->d_bline, (size_t)x->nb * 64 + 64) == 0) {
+			uint64_t blocks = ((uint64_t)x->nb + 255) / 256, bmax = (uint64_t)h->n_cu * 64;
+			if (blocks > bmax) blocks = bmax;
+			hipLaunchKernelGGL(build_bline, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
+			                   (const int16_t *)h->d_keys, x->nb, (uint4 *)h->d_bline);
+			HIPCHK(hipGetLastError());
+			HIPCHK(hipStreamSynchronize(h->stream));
+			h->dix.bline = (const uint4 *)h->d_bline;
+		} else {
+			h->d_bline = NULL;
+			(void)hipGetLastError();
+		}
+	}
+	if (!h->dix.bline && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT")) {
 		// (2^32-1)/nb <= 255: every key_hi fits a byte
 		const size_t ng = ((size_t)x->nb + 15) / 16;
 		if ((rc = dmalloc(h, &h->d_bgrp, ng * 32 + 64)) || (rc = dmalloc(h, &h->d_keys8, x->items + 128))) return rc;
@@ -1788,6 +1787,9 @@ int svg_index_finish_device(svg_index *h)
 	}
 	if ((rc = dmalloc(h, (void **)&h->d_stats, 32 * sizeof(unsigned long long)))) return rc;
 	HIPCHK(hipMemset(h->d_stats, 0, 32 * sizeof(unsigned long long)));
+	if ((rc = dmalloc(h, (void **)&h->d_err, 64))) return rc;
+	HIPCHK(hipMemset(h->d_err, 0, 64));
+	HIPCHK(hipEventCreateWithFlags(&h->ev_last, hipEventDisableTiming));
 	const char *se = getenv("SVG_STATS");
 	h->stats_on = se && se[0] == '1';
 	h->max_read_len = 256;
@@ -1849,11 +1851,18 @@ extern "C" void svg_index_close(svg_index *h)
 	if (h->stream2) hipStreamSynchronize(h->stream2);
 	if (h->up_stream) hipStreamSynchronize(h->up_stream);
 	if (h->down_stream) hipStreamSynchronize(h->down_stream);
+	svg_io_free(h);
 	for (int s = 0; s < 2; s++) {
 		hipFree(h->d_prec[s]);
 		hipFree(h->d_lane[s]);
 		hipFree(h->d_in[s]);
+		if (s == 1) hipFree(h->d_in[2]);
 		hipFree(h->d_out[s]);
+		if (s == 1) {
+			hipEvent_t e3[3] = {h->ev_up[2], h->ev_done[2], h->ev_down[2]};
+			for (int k = 0; k < 3; k++)
+				if (e3[k]) hipEventDestroy(e3[k]);
+		}
 		hipEvent_t *evs[5] = {h->ev_lane, h->ev_wave, h->ev_up, h->ev_done, h->ev_down};
 		for (int k = 0; k < 5; k++)
 			if (evs[k][s]) hipEventDestroy(evs[k][s]);
@@ -1866,7 +1875,8 @@ extern "C" void svg_index_close(svg_index *h)
 				if (h->tev[k][i][j]) hipEventDestroy(h->tev[k][i][j]);
 	hipFree(h->d_bstart); hipFree(h->d_keys); hipFree(h->d_vals); hipFree(h->d_values); hipFree(h->d_chr);
 	hipFree(h->d_bgrp); hipFree(h->d_keys8); hipFree(h->d_bline);
-	hipFree(h->d_scratch); hipFree(h->d_stats);
+	hipFree(h->d_scratch); hipFree(h->d_stats); hipFree(h->d_err);
+	if (h->ev_last) hipEventDestroy(h->ev_last);
 	if (h->stream) hipStreamDestroy(h->stream);
 	if (h->stream2) hipStreamDestroy(h->stream2);
 	if (h->up_stream) hipStreamDestroy(h->up_stream);
@@ -1974,6 +1984,22 @@ extern "C" int svg_debug_counters(svg_index *h, unsigned long long *out32)
 	return 0;
 }
 
+// waits for the handle's queued work and reports (and clears) the sticky device error word
+extern "C" int svg_device_status(svg_index *h)
+{
+	if (!h) { svg_set_error("svg_device_status: NULL handle"); return SVG_E_ARG; }
+	HIPCHK(hipSetDevice(h->device));
+	if (h->last_pending) HIPCHK(hipEventSynchronize(h->ev_last));
+	uint32_t e = 0;
+	HIPCHK(hipMemcpy(&e, h->d_err, 4, hipMemcpyDeviceToHost));
+	if (!e) return 0;
+	HIPCHK(hipMemset(h->d_err, 0, 4));
+	if (e & 1u) svg_set_error("a read needs more subread probes than the read-length bound of svg_set_max_read_length "
+	                          "(%d) provides; its records were zeroed", h->max_read_len);
+	else svg_set_error("a read is longer than the kernel variant's text buffer; its records were zeroed");
+	return SVG_E_ARG;
+}
+
 extern "C" int svg_get_stats(const svg_index *h, svg_batch_stats *o)
 {
 	if (!h || !o) return SVG_E_ARG;
@@ -2053,7 +2079,6 @@ static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 	return 0;
 }
 
-static int ensure(svg_index *h, void **p, size_t *cap, size_t need);
 
 // kernel variant by mode and announced read-length bound
 static int launch_vote(svg_index *h, KParams &kp, hipStream_t st, int npmax, bool sj, int ends)
@@ -2084,8 +2109,13 @@ static int launch_vote(svg_index *h, KParams &kp, hipStream_t st, int npmax, boo
 	return npmax <= 32 ? launch_t<1, 256, 32, 2, SVG_SE_OCC, false>(h, kp, st) : launch_t<1, 256, 64, 2, SVG_SE_OCC, false>(h, kp, st);
 }
 
-extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
-                                     svg_mapping_result *out, svg_subjunc_result *jout, uint16_t *big_margin, void *stream)
+// ------------------------------------------------------------------ batch set-up and chunk launch
+// svg_vote_prepare checks a batch and fills the kernel parameters; svg_vote_chunk launches the
+// probe and lane kernels of reads [c0, c0+cn) on st (records in slot `slot`) and the wave
+// kernel on st2 (event handoff when st2 != st).  svg_vote_batch_device drives the chunks of one
+// call; the host-buffer pipeline (svg_io.hip) drives one chunk per sub-batch with its own slots.
+int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2, svg_mapping_result *out,
+                     svg_subjunc_result *jout, uint16_t *big_margin, VoteJob *job)
 {
 	if (!h || !p || !r1 || !out) { svg_set_error("svg_vote_batch_device: NULL argument"); return SVG_E_ARG; }
 	if (r2 && r2->n_reads != r1->n_reads) { svg_set_error("R1/R2 read counts differ"); return SVG_E_ARG; }
@@ -2097,11 +2127,9 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	// core_fragile_junction_voting, core-junction.c:5151-5424) on them, which only adds junction
 	// and indel events to the event tables (host post-processing, outside this boundary); the
 	// vote records come from the regular voting below (long-read junction branch included)
-	HIPCHK(hipSetDevice(h->device));
-	hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-	if (r1->n_reads == 0) return 0;
-	KParams kp;
+	KParams &kp = job->kp;
 	memset(&kp, 0, sizeof kp);
+	kp.err = h->d_err;
 	kp.p = *p;
 	kp.ix = h->dix;
 	kp.seq1 = r1->seq; kp.off1 = r1->offsets; kp.len1 = r1->lens;
@@ -2115,122 +2143,170 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	if (kp.tol > 5) kp.ii_end = (kp.tol % 5) ? (kp.tol - kp.tol % 5 + 5) : kp.tol;
 	kp.low = h->dix.start_base_offset;
 	kp.high = h->dix.start_base_offset + h->dix.length;
-	if (h->stats_on) {
-		HIPCHK(hipMemsetAsync(h->d_stats, 0, 32 * sizeof(unsigned long long), st));
-		kp.stats = h->d_stats;
-	}
+	kp.stats = h->stats_on ? h->d_stats : NULL;
 	// probes per strand are bounded by the read lengths the caller announced
-	int npmax = svg_probe_bound(h->max_read_len, h->dix.gap, p->total_subreads);
-	const bool sj = p->do_breakpoint_detection || p->do_big_margin_filtering_for_junctions;
-	if (npmax > 192) { svg_set_error("%d subreads per strand exceed 192", npmax); return SVG_E_UNSUPPORTED; }
-	const int ends = r2 ? 2 : 1;
-	{
-		// phase P as its own kernel per chunk of reads, then the vote kernel on its records
-		const int nps = npmax > 0 ? npmax : 1;
-		const uint64_t per_read = (uint64_t)ends * 2 * nps;
-		uint64_t chunk = ((uint64_t)1 << 30) / (per_read * 8);
-		if (chunk > (uint64_t)0x7fffffff / per_read) chunk = (uint64_t)0x7fffffff / per_read;
-		{ const char *ec = getenv("SVG_CHUNK"); if (ec && atoll(ec) > 0 && (uint64_t)atoll(ec) < chunk) chunk = (uint64_t)atoll(ec); }   // testing
-		if (chunk > kp.n_reads) chunk = kp.n_reads;
-		if (chunk < 1) chunk = 1;
-		// chunk pipeline: the wave kernel of chunk c runs on stream2 while the probe and lane
-		// kernels of chunk c+1 run on st; slot c & 1 holds a chunk's probe records and lane
-		// buffers until its wave kernel is done.  On by default for single-end align only
-		// (C3: 289 -> 304 Mreads/s; PE and subjunc, whose wave kernels are 2-3x longer, lost
-		// 1-2%: the kernels time-share the CUs there).  SVG_OVERLAP=0/1 forces it off/on.
-		const char *eo = getenv("SVG_OVERLAP");
-		const bool overlap = (eo ? eo[0] == '1' : (!sj && !r2)) && chunk < kp.n_reads;
-		hipStream_t st2 = overlap ? h->stream2 : st;
-		// overlapped, the wave kernel leaves CU slots to the next chunk's probe kernel, whose
-		// latency-bound chain needs the occupancy (the wave kernel has slack on its stream)
-		h->wave_cap = 0;
-		if (overlap) {
-			const char *ew = getenv("SVG_WAVE_CAP");
-			h->wave_cap = ew ? atoi(ew) : SVG_WAVE_CAP;
-		}
-		if (getenv("SVG_DEBUG"))
-			fprintf(stderr, "[svg] batch of %llu reads: chunks of %llu, chunk pipeline %s\n", (unsigned long long)kp.n_reads,
-			        (unsigned long long)chunk, overlap ? "on" : "off");
-		for (int s = 0; s < (overlap ? 2 : 1); s++)
-			if ((rc = ensure(h, &h->d_prec[s], &h->prec_cap[s], chunk * per_read * 8))) return rc;
-		bool slot_busy[2] = {false, false};
-		PParams pp;
-		memset(&pp, 0, sizeof pp);
-		pp.ix = h->dix;
-		pp.seq1 = kp.seq1; pp.seq2 = kp.seq2;
-		pp.nps = nps;
-		pp.total_subreads = p->total_subreads; pp.reverse_r1 = p->reverse_r1; pp.reverse_r2 = p->reverse_r2;
-		pp.nb_magic = ~0ull / h->dix.nb + 1;   // ceil(2^64 / nb), nb is not a power of two
-		pp.stats = kp.stats;
-		// align mode, reads <= 160 bp: lane-per-read (SE) / lane-per-pair (PE) fast path
-		// (svg_lane.hip), probe records in SoA layout
-		const bool lane = svg_lane_eligible(h, p, r2 != NULL, sj) != 0 && (!r2 || nps <= 10) && (!sj || nps <= 14);
-		pp.soa = lane ? 1 : 0;
-		pp.window = h->dix.nb >= 131073u && !getenv("SVG_NO_WINDOW");   // key_hi <= 32767: int16 order == key order
-		{ const char *e = getenv("SVG_PROBE_MAP"); pp.readmajor = !(e && e[0] == '0'); }
-		const uint64_t n = kp.n_reads;
-		for (uint64_t c0 = 0; c0 < n && !rc; c0 += chunk) {
-			const uint64_t cn = n - c0 < chunk ? n - c0 : chunk;
-			const int slot = overlap ? (int)((c0 / chunk) & 1) : 0;
-			if (slot_busy[slot]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[slot], 0));
-			pp.out = (uint2 *)h->d_prec[slot];
-			pp.off1 = kp.off1 + c0; pp.len1 = kp.len1 + c0;
-			if (r2) { pp.off2 = kp.off2 + c0; pp.len2 = kp.len2 + c0; }
-			pp.n_reads = (uint32_t)cn;
-			uint64_t pb = (cn * per_read + 255) / 256, pmax = (uint64_t)h->n_cu * 32;
-			if (pb > pmax) pb = pmax;
-			if ((rc = timing_mark(h, 0, 0, st))) return rc;
-			// 8 blocks of 256 per CU (<= 64 VGPRs): the probe chain is latency-bound, occupancy
-			// is what hides it (C3: 11.3 ms at 4 waves/SIMD, 8.7 ms at 8)
-			// bucket-line image (one random 64-B line per probe) when the index has one
-			if (h->dix.bline) {
-				if (r2) hipLaunchKernelGGL((probe_kernel<2, 8, true>), dim3((unsigned)pb), dim3(256), 0, st, pp);
-				else hipLaunchKernelGGL((probe_kernel<1, 8, true>), dim3((unsigned)pb), dim3(256), 0, st, pp);
-			} else {
-				if (r2) hipLaunchKernelGGL((probe_kernel<2, 8, false>), dim3((unsigned)pb), dim3(256), 0, st, pp);
-				else hipLaunchKernelGGL((probe_kernel<1, 8, false>), dim3((unsigned)pb), dim3(256), 0, st, pp);
-			}
-			HIPCHK(hipGetLastError());
-			if ((rc = timing_mark(h, 0, 1, st))) return rc;
-			KParams kc = kp;
-			kc.off1 = kp.off1 + c0; kc.len1 = kp.len1 + c0;
-			if (r2) { kc.off2 = kp.off2 + c0; kc.len2 = kp.len2 + c0; }
-			kc.n_reads = cn;
-			kc.out = kp.out + c0 * ends * p->multi_best * 68;
-			if (kp.jout) kc.jout = kp.jout + c0 * ends * p->multi_best * 16;
-			if (kp.bm_out) kc.bm_out = kp.bm_out + c0 * ends * SVG_BIG_MARGIN_WORDS;
-			kc.precs = (const uint2 *)h->d_prec[slot];
-			kc.nps = nps;
-			if (lane) {
-				// gather + lane kernels vote every read they can; the rest (deferral list) go to
-				// vote_kernel below, which reads the SoA probe records of the deferred reads
-				uint32_t *dl = NULL, *dc = NULL;
-				rc = r2 ? svg_lane_pe_chunk(h, slot, p, kc.len1, kc.len2, (uint32_t)cn, kc.precs, nps, kc.out, kp.stats, &dl, &dc, st)
-				        : svg_lane_chunk(h, slot, p, kc.len1, (uint32_t)cn, kc.precs, nps, kc.out, sj ? kc.jout : NULL, kc.bm_out,
-				                         kp.stats, &dl, &dc, st);
-				if (rc) return rc;
-				kc.prec_stride = (uint32_t)cn;
-				kc.idx = dl;
-				kc.idx_count = dc;
-				kc.work = dc + 2;
-			}
-			if (overlap) {
-				HIPCHK(hipEventRecord(h->ev_lane[slot], st));
-				HIPCHK(hipStreamWaitEvent(st2, h->ev_lane[slot], 0));
-			}
-			if ((rc = timing_mark(h, 1, 0, st2))) return rc;
-			rc = launch_vote(h, kc, st2, npmax, sj, ends);
-			if (!rc) rc = timing_mark(h, 1, 1, st2);
-			if (!rc && overlap) {
-				HIPCHK(hipEventRecord(h->ev_wave[slot], st2));
-				slot_busy[slot] = true;
-			}
-		}
-		// join: the caller's stream sees every wave kernel of the batch
-		for (int s = 0; s < 2 && overlap; s++)
-			if (slot_busy[s]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[s], 0));
+	job->npmax = svg_probe_bound(h->max_read_len, h->dix.gap, p->total_subreads);
+	job->sj = p->do_breakpoint_detection || p->do_big_margin_filtering_for_junctions;
+	if (job->npmax > 192) { svg_set_error("%d subreads per strand exceed 192", job->npmax); return SVG_E_UNSUPPORTED; }
+	job->ends = r2 ? 2 : 1;
+	// phase P as its own kernel per chunk of reads (<= 1 GiB of probe records), then the vote
+	// kernels on its records
+	const int nps = job->npmax > 0 ? job->npmax : 1;
+	job->nps = nps;
+	job->per_read = (uint64_t)job->ends * 2 * nps;
+	uint64_t chunk = ((uint64_t)1 << 30) / (job->per_read * 8);
+	if (chunk > (uint64_t)0x7fffffff / job->per_read) chunk = (uint64_t)0x7fffffff / job->per_read;
+	{ const char *ec = getenv("SVG_CHUNK"); if (ec && atoll(ec) > 0 && (uint64_t)atoll(ec) < chunk) chunk = (uint64_t)atoll(ec); }   // testing
+	if (chunk < 1) chunk = 1;
+	job->chunk = chunk;
+	// chunk pipeline: the wave kernel of chunk c runs on stream2 while the probe and lane kernels
+	// of chunk c+1 run on st; slot c & 1 holds a chunk's probe records and lane buffers until its
+	// wave kernel is done.  On by default for single-end align only (C3: 289 -> 304 Mreads/s; PE
+	// and subjunc, whose wave kernels are 2-3x longer, lost 1-2%: the kernels time-share the CUs
+	// there).  SVG_OVERLAP=0/1 forces it off/on.
+	const char *eo = getenv("SVG_OVERLAP");
+	job->overlap_mode = eo ? eo[0] == '1' : (!job->sj && !r2);
+	PParams &pp = job->pp;
+	memset(&pp, 0, sizeof pp);
+	pp.ix = h->dix;
+	pp.seq1 = kp.seq1; pp.seq2 = kp.seq2;
+	pp.nps = nps;
+	pp.total_subreads = p->total_subreads; pp.reverse_r1 = p->reverse_r1; pp.reverse_r2 = p->reverse_r2;
+	pp.nb_magic = ~0ull / h->dix.nb + 1;   // ceil(2^64 / nb), nb is not a power of two
+	pp.stats = kp.stats;
+	// align mode, reads <= 160 bp: lane-per-read (SE) / lane-per-pair (PE) fast path
+	// (svg_lane.hip), probe records in SoA layout
+	job->lane = svg_lane_eligible(h, p, r2 != NULL, job->sj) != 0 && (!r2 || nps <= 10) && (!job->sj || nps <= 14);
+	pp.soa = job->lane ? 1 : 0;
+	pp.window = h->dix.nb >= 131073u && !getenv("SVG_NO_WINDOW");   // key_hi <= 32767: int16 order == key order
+	{ const char *e = getenv("SVG_PROBE_MAP"); pp.readmajor = !(e && e[0] == '0'); }
+	return 0;
+}
+
+// reads [c0, c0+cn) of the prepared batch; slot's probe records / lane buffers must be free
+int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slot, hipStream_t st, hipStream_t st2)
+{
+	const KParams &kp = job->kp;
+	const svg_params *p = &kp.p;
+	const int ends = job->ends, nps = job->nps;
+	int rc;
+	if ((rc = svg_ensure(h, &h->d_prec[slot], &h->prec_cap[slot], cn * job->per_read * 8))) return rc;
+	// overlapped, the wave kernel leaves CU slots to the next chunk's probe kernel, whose
+	// latency-bound chain needs the occupancy (the wave kernel has slack on its stream)
+	h->wave_cap = 0;
+	if (st2 != st) {
+		const char *ew = getenv("SVG_WAVE_CAP");
+		h->wave_cap = ew ? atoi(ew) : SVG_WAVE_CAP;
 	}
+	PParams pp = job->pp;
+	pp.out = (uint2 *)h->d_prec[slot];
+	pp.off1 = kp.off1 + c0; pp.len1 = kp.len1 + c0;
+	if (kp.len2) { pp.off2 = kp.off2 + c0; pp.len2 = kp.len2 + c0; }
+	pp.n_reads = (uint32_t)cn;
+	uint64_t pb = (cn * job->per_read + 255) / 256, pmax = (uint64_t)h->n_cu * 32;
+	if (pb > pmax) pb = pmax;
+	if ((rc = timing_mark(h, 0, 0, st))) return rc;
+	// 8 blocks of 256 per CU (<= 64 VGPRs): the probe chain is latency-bound, occupancy is what
+	// hides it (C3: 11.3 ms at 4 waves/SIMD, 8.7 ms at 8); bucket-line image (one random 64-B
+	// line per probe) when the index has one
+	const bool pe = kp.len2 != NULL;
+	if (pp.packed) {
+		// 2-bit input: chunk-relative read starts
+		for (int e = 0; e < (pe ? 2 : 1); e++) {
+			if (pp.pk_starts[e]) pp.pk_starts[e] += c0;
+			else pp.pk_base0[e] += c0 * pp.pk_stride[e];
+		}
+	}
+#define PROBE_LAUNCH(E, L, P) hipLaunchKernelGGL((probe_kernel<E, 8, L, P>), dim3((unsigned)pb), dim3(256), 0, st, pp)
+	if (h->dix.bline) {
+		if (pp.packed) { if (pe) PROBE_LAUNCH(2, true, true); else PROBE_LAUNCH(1, true, true); }
+		else { if (pe) PROBE_LAUNCH(2, true, false); else PROBE_LAUNCH(1, true, false); }
+	} else {
+		if (pp.packed) { if (pe) PROBE_LAUNCH(2, false, true); else PROBE_LAUNCH(1, false, true); }
+		else { if (pe) PROBE_LAUNCH(2, false, false); else PROBE_LAUNCH(1, false, false); }
+	}
+#undef PROBE_LAUNCH
+	HIPCHK(hipGetLastError());
+	if ((rc = timing_mark(h, 0, 1, st))) return rc;
+	KParams kc = kp;
+	kc.off1 = kp.off1 + c0; kc.len1 = kp.len1 + c0;
+	if (pe) { kc.off2 = kp.off2 + c0; kc.len2 = kp.len2 + c0; }
+	kc.n_reads = cn;
+	kc.out = kp.out + c0 * ends * p->multi_best * 68;
+	if (kp.jout) kc.jout = kp.jout + c0 * ends * p->multi_best * 16;
+	if (kp.bm_out) kc.bm_out = kp.bm_out + c0 * ends * SVG_BIG_MARGIN_WORDS;
+	kc.precs = (const uint2 *)h->d_prec[slot];
+	kc.nps = nps;
+	if (job->lane) {
+		// gather + lane kernels vote every read they can; the rest (deferral list) go to
+		// vote_kernel below, which reads the SoA probe records of the deferred reads
+		uint32_t *dl = NULL, *dc = NULL;
+		rc = pe ? svg_lane_pe_chunk(h, slot, p, kc.len1, kc.len2, (uint32_t)cn, kc.precs, nps, kc.out, kp.stats, &dl, &dc, st)
+		        : svg_lane_chunk(h, slot, p, kc.len1, (uint32_t)cn, kc.precs, nps, kc.out, job->sj ? kc.jout : NULL, kc.bm_out,
+		                         kp.stats, &dl, &dc, st);
+		if (rc) return rc;
+		kc.prec_stride = (uint32_t)cn;
+		kc.idx = dl;
+		kc.idx_count = dc;
+		kc.work = dc + 2;
+	}
+	if (st2 != st) {
+		HIPCHK(hipEventRecord(h->ev_lane[slot], st));
+		HIPCHK(hipStreamWaitEvent(st2, h->ev_lane[slot], 0));
+	}
+	if ((rc = timing_mark(h, 1, 0, st2))) return rc;
+	rc = launch_vote(h, kc, st2, job->npmax, job->sj, ends);
+	if (!rc) rc = timing_mark(h, 1, 1, st2);
+	return rc;
+}
+
+static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                             const svg_packed_reads *pk, svg_mapping_result *out, svg_subjunc_result *jout,
+                             uint16_t *big_margin, void *stream)
+{
+	VoteJob job;
+	int rc = svg_vote_prepare(h, p, r1, r2, out, jout, big_margin, &job);
 	if (rc) return rc;
+	if (pk) {
+		job.pp.packed = 1;
+		for (int e = 0; e < (r2 ? 2 : 1); e++) {
+			job.pp.pk_bases[e] = pk[e].bases;
+			job.pp.pk_xmask[e] = pk[e].xmask;
+			job.pp.pk_starts[e] = pk[e].starts;
+			job.pp.pk_stride[e] = pk[e].stride;
+			job.pp.pk_base0[e] = 0;
+		}
+	}
+	HIPCHK(hipSetDevice(h->device));
+	hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+	if (r1->n_reads == 0) return 0;
+	// the handle's buffers (probe records, lane lists, scratch) are shared by every call: this
+	// call's work starts after the previous call's, whatever streams the two were given
+	if (h->last_pending) HIPCHK(hipStreamWaitEvent(st, h->ev_last, 0));
+	if (h->stats_on) HIPCHK(hipMemsetAsync(h->d_stats, 0, 32 * sizeof(unsigned long long), st));
+	const uint64_t n = r1->n_reads, chunk = job.chunk;
+	const bool overlap = job.overlap_mode && chunk < n;
+	hipStream_t st2 = overlap ? h->stream2 : st;
+	if (getenv("SVG_DEBUG"))
+		fprintf(stderr, "[svg] batch of %llu reads: chunks of %llu, chunk pipeline %s\n", (unsigned long long)n,
+		        (unsigned long long)chunk, overlap ? "on" : "off");
+	bool slot_busy[2] = {false, false};
+	for (uint64_t c0 = 0; c0 < n && !rc; c0 += chunk) {
+		const uint64_t cn = n - c0 < chunk ? n - c0 : chunk;
+		const int slot = overlap ? (int)((c0 / chunk) & 1) : 0;
+		if (slot_busy[slot]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[slot], 0));
+		rc = svg_vote_chunk(h, &job, c0, cn, slot, st, st2);
+		if (!rc && overlap) {
+			HIPCHK(hipEventRecord(h->ev_wave[slot], st2));
+			slot_busy[slot] = true;
+		}
+	}
+	// join: the caller's stream sees every wave kernel of the batch
+	for (int s = 0; s < 2 && overlap; s++)
+		if (slot_busy[s]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[s], 0));
+	if (rc) return rc;
+	HIPCHK(hipEventRecord(h->ev_last, st));
+	h->last_pending = 1;
 	if (h->stats_on) {
 		unsigned long long s[5];
 		HIPCHK(hipMemcpyAsync(s, h->d_stats, sizeof s, hipMemcpyDeviceToHost, st));
@@ -2244,147 +2320,16 @@ extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const sv
 	return 0;
 }
 
-static int ensure(svg_index *h, void **p, size_t *cap, size_t need)
+extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                                     svg_mapping_result *out, svg_subjunc_result *jout, uint16_t *big_margin, void *stream)
 {
-	if (need <= *cap) return 0;
-	hipFree(*p);
-	*p = NULL;
-	*cap = 0;
-	if (dmalloc(h, p, need)) return SVG_E_NOMEM;
-	*cap = need;
-	return 0;
+	return vote_batch_device(h, p, r1, r2, NULL, out, jout, big_margin, stream);
 }
 
-// host buffers in/out: stage through HBM in sub-batches.  Sub-batch i is uploaded (up_stream)
-// into slot i & 1 while sub-batch i-1 is voted (stream) and i-2's records come back
-// (down_stream); with pageable caller memory each copy call blocks the host until it is done,
-// which is still concurrent with the kernels already queued on the vote stream.
-extern "C" int svg_vote_batch(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
-                              svg_mapping_result *out, svg_subjunc_result *jout, uint16_t *big_margin)
+// align mode from 2-bit packed device reads: r1/r2 carry the lengths, pk[e] the codes
+int svg_vote_batch_device_packed(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                                 const svg_packed_reads *pk, svg_mapping_result *out, svg_subjunc_result *jout,
+                                 uint16_t *big_margin, hipStream_t stream)
 {
-	if (!h || !p || !r1 || !out) { svg_set_error("svg_vote_batch: NULL argument"); return SVG_E_ARG; }
-	if (r2 && r2->n_reads != r1->n_reads) { svg_set_error("R1/R2 read counts differ"); return SVG_E_ARG; }
-	int rc = check_params(h, p, r2 != NULL);
-	if (rc) return rc;
-	if (p->do_breakpoint_detection && !jout) { svg_set_error("do_breakpoint_detection needs jout"); return SVG_E_ARG; }
-	if (p->do_big_margin_filtering_for_junctions && !big_margin) { svg_set_error("big-margin filtering needs big_margin"); return SVG_E_ARG; }
-	const uint64_t n = r1->n_reads;
-	if (!n) return 0;
-	const int ends = r2 ? 2 : 1;
-	HIPCHK(hipSetDevice(h->device));
-	// copy streams on first use only: HIP deals a process's streams round-robin onto
-	// GPU_MAX_HW_QUEUES (4) hardware queues, and idle extra streams can land the chunk
-	// pipeline's second stream on the caller's queue
-	if (!h->up_stream) HIPCHK(hipStreamCreateWithFlags(&h->up_stream, hipStreamNonBlocking));
-	if (!h->down_stream) HIPCHK(hipStreamCreateWithFlags(&h->down_stream, hipStreamNonBlocking));
-	// the batch's longest read (picks the kernel variant); every kept length must fit the
-	// kernels' 192 probes per strand (checked once per length, not per read)
-	int batch_max = 16;
-	for (int e = 0; e < ends; e++) {
-		const uint16_t *ln = (e ? r2 : r1)->lens;
-		int mx = 0;
-		for (uint64_t i = 0; i < n; i++) mx = ln[i] > mx ? ln[i] : mx;
-		if (mx > SVG_READ_KEEP) mx = SVG_READ_KEEP;
-		if (mx > batch_max) batch_max = mx;
-	}
-	for (int len = 15 + h->dix.gap; len <= batch_max; len++) {
-		int cr = (len - 15 - h->dix.gap) << 16, step;
-		if (len <= 160) { step = cr / (p->total_subreads - 1); if (step < (h->dix.gap << 16)) step = h->dix.gap << 16; }
-		else { step = 6 << 16; if (cr / step > 62) step = cr / 62; }
-		if ((1 + cr / step) * h->dix.gap > 192) { svg_set_error("reads of %d bases need %d probes per strand (> 192)", len, (1 + cr / step) * h->dix.gap); return SVG_E_UNSUPPORTED; }
-	}
-	const size_t rec_b = (size_t)ends * p->multi_best * 68;
-	const size_t j_b = p->do_breakpoint_detection ? (size_t)ends * p->multi_best * 16 : 0;
-	const size_t bm_b = p->do_big_margin_filtering_for_junctions ? (size_t)ends * SVG_BIG_MARGIN_WORDS * 2 : 0;
-	// sub-batches of ~320 MB of PCIe traffic (1M 100 bp SE reads): short enough that the
-	// pipeline's fill and drain are small, long enough to keep the GPU busy (C3 host path:
-	// 162 / 174 / 179 Mreads/s at 4M / 2M / 1M reads).  SVG_HOST_SUB overrides.
-	const size_t per_read = (size_t)ends * (batch_max + 10) + rec_b + j_b + bm_b;
-	uint64_t sub = 320000000ull / per_read;
-	if (sub < 65536) sub = 65536;
-	{ const char *es = getenv("SVG_HOST_SUB"); if (es && atoll(es) > 0) sub = (uint64_t)atoll(es); }
-	if (sub > n) sub = n;
-	const int saved_len = h->max_read_len;
-	h->max_read_len = batch_max;
-	bool used[2] = {false, false};
-	svg_batch_stats acc;
-	memset(&acc, 0, sizeof acc);
-	uint64_t prev_b = 0, prev_n = 0;
-	size_t prev_oj = 0, prev_obm = 0;
-	int prev_s = -1;
-	// D2H of the sub-batch in slot s (reads b .. b+m)
-	auto download = [&](int s, uint64_t b, uint64_t m, size_t o_j, size_t o_bm) -> int {
-		const uint8_t *dout = (const uint8_t *)h->d_out[s];
-		HIPCHK(hipStreamWaitEvent(h->down_stream, h->ev_done[s], 0));
-		HIPCHK(hipMemcpyAsync((uint8_t *)out + b * rec_b, dout, m * rec_b, hipMemcpyDeviceToHost, h->down_stream));
-		if (j_b) HIPCHK(hipMemcpyAsync((uint8_t *)jout + b * j_b, dout + o_j, m * j_b, hipMemcpyDeviceToHost, h->down_stream));
-		if (bm_b) HIPCHK(hipMemcpyAsync((uint8_t *)big_margin + b * bm_b, dout + o_bm, m * bm_b, hipMemcpyDeviceToHost, h->down_stream));
-		HIPCHK(hipEventRecord(h->ev_down[s], h->down_stream));
-		return 0;
-	};
-	for (uint64_t b = 0; b < n && !rc; b += sub) {
-		const uint64_t m = n - b < sub ? n - b : sub;
-		const int s = (int)((b / sub) & 1);
-		// the slot's previous sub-batch must be downloaded before it is overwritten
-		if (used[s]) HIPCHK(hipEventSynchronize(h->ev_down[s]));
-		uint64_t span[2] = {0, 0}, lo[2] = {0, 0};
-		for (int e = 0; e < ends; e++) {
-			const svg_reads *rr = e ? r2 : r1;
-			uint64_t mn = ~0ull, mx = 0;
-			for (uint64_t i = b; i < b + m; i++) {
-				if (rr->offsets[i] < mn) mn = rr->offsets[i];
-				if (rr->offsets[i] + rr->lens[i] > mx) mx = rr->offsets[i] + rr->lens[i];
-			}
-			lo[e] = mn; span[e] = mx - mn;
-		}
-		size_t in_bytes = 0, o_seq[2], o_off[2], o_len[2];
-		for (int e = 0; e < ends; e++) {
-			o_seq[e] = in_bytes; in_bytes += (span[e] + 15) & ~15ull;
-			o_off[e] = in_bytes; in_bytes += 8 * m;
-			o_len[e] = in_bytes; in_bytes += (2 * m + 15) & ~15ull;
-		}
-		const size_t o_j = (m * rec_b + 255) & ~(size_t)255, o_bm = (o_j + m * j_b + 255) & ~(size_t)255;
-		if ((rc = ensure(h, &h->d_in[s], &h->d_in_cap[s], in_bytes))) break;
-		if ((rc = ensure(h, &h->d_out[s], &h->d_out_cap[s], o_bm + m * bm_b))) break;
-		uint8_t *din = (uint8_t *)h->d_in[s], *dout = (uint8_t *)h->d_out[s];
-		svg_reads dr[2];
-		for (int e = 0; e < ends; e++) {
-			const svg_reads *rr = e ? r2 : r1;
-			// the caller's offsets go up unchanged: the device text pointer is rebased by lo
-			// instead (seq + offsets[i] addresses the uploaded span)
-			HIPCHK(hipMemcpyAsync(din + o_seq[e], rr->seq + lo[e], span[e], hipMemcpyHostToDevice, h->up_stream));
-			HIPCHK(hipMemcpyAsync(din + o_off[e], rr->offsets + b, 8 * m, hipMemcpyHostToDevice, h->up_stream));
-			HIPCHK(hipMemcpyAsync(din + o_len[e], rr->lens + b, 2 * m, hipMemcpyHostToDevice, h->up_stream));
-			dr[e].seq = (const char *)(din + o_seq[e]) - lo[e];
-			dr[e].offsets = (const uint64_t *)(din + o_off[e]);
-			dr[e].lens = (const uint16_t *)(din + o_len[e]);
-			dr[e].n_reads = m;
-		}
-		HIPCHK(hipEventRecord(h->ev_up[s], h->up_stream));
-		HIPCHK(hipStreamWaitEvent(h->stream, h->ev_up[s], 0));
-		rc = svg_vote_batch_device(h, p, &dr[0], r2 ? &dr[1] : NULL, (svg_mapping_result *)dout,
-		                           j_b ? (svg_subjunc_result *)(dout + o_j) : NULL, bm_b ? (uint16_t *)(dout + o_bm) : NULL,
-		                           h->stream);
-		if (rc) break;
-		if (h->stats_on) {   // the device call synchronised and left its sub-batch's counts
-			acc.probes += h->last_stats.probes; acc.bucket_items += h->last_stats.bucket_items;
-			acc.hits += h->last_stats.hits; acc.results += h->last_stats.results;
-			acc.deferred += h->last_stats.deferred;
-		}
-		HIPCHK(hipEventRecord(h->ev_done[s], h->stream));
-		used[s] = true;
-		// records of the previous sub-batch come back while this one is voted
-		if (prev_s >= 0 && (rc = download(prev_s, prev_b, prev_n, prev_oj, prev_obm))) break;
-		prev_s = s; prev_b = b; prev_n = m; prev_oj = o_j; prev_obm = o_bm;
-	}
-	if (!rc && prev_s >= 0) rc = download(prev_s, prev_b, prev_n, prev_oj, prev_obm);
-	h->max_read_len = saved_len;
-	if (h->stats_on) h->last_stats = acc;   // the whole batch
-	hipError_t e1 = hipStreamSynchronize(h->stream), e2 = hipStreamSynchronize(h->down_stream);
-	if (rc) return rc;
-	if (e1 != hipSuccess || e2 != hipSuccess) {
-		svg_set_error("HIP error %s in svg_vote_batch", hipGetErrorString(e1 != hipSuccess ? e1 : e2));
-		return SVG_E_DEVICE;
-	}
-	return 0;
+	return vote_batch_device(h, p, r1, r2, pk, out, jout, big_margin, (void *)stream);
 }

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(sa.EXPORTS) == set(syms)
-    assert L.svg_abi_version() == 1
+    assert L.svg_abi_version() == 2
 
 
 def test_struct_sizes_match_reference():
