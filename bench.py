@@ -193,7 +193,6 @@ def main():
     # ---- the metric: packed host reads -> host records, W warmup + K timed steps
     for _ in range(args.warmup):
         host_step()
-    ix.set_timing(True)          # per-launch HIP events inside the library, read back after the timed region
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -205,6 +204,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    # per-kernel times: one more host step with per-launch HIP events (recorded by the library on
+    # each launch's stream), outside the timed region -- folding the event ring synchronises
+    ix.set_timing(True)
+    host_step()
     kt = ix.kernel_timing()
     ix.set_timing(False)
     if dist is not None:
@@ -281,7 +284,7 @@ def main():
     for k, (ms, nl) in kt.items():
         if not nl:
             continue
-        per_step = max(1, nl // args.steps)
+        per_step = nl                     # launches of the one timing step
         launch_s = ms / nl / 1e3
         kernels[k] = {"launch_ms": round(launch_s * 1e3, 3), "launches_per_step": per_step,
                       "algorithmic_bytes_per_read": round(kbytes[k] / n, 1),

@@ -1,0 +1,87 @@
+"""GPU parity at the benchmark's own scale (BASELINE.json configs C3-C5): the 3.0 Gbp
+24-contig genome with injected repeat families, its full one-block index built in HBM
+(nb = 93,018,839 buckets, ~2.94 G items: ~32-item buckets, repeat-capped runs, item
+offsets near the u32 limit), voted through the C ABI and compared byte for byte with the
+oracle restatement on the same index arrays:
+  * C3 shape: 100 bp SE reads -- including the repeat-family reads the lane path defers to
+    the wave kernel -- through the packed and the ASCII host entry points;
+  * C4 shape: 150 bp PE pairs (fragments N(300,50));
+  * C5 shape: subjunc on spliced RNA-seq-like reads.
+Reference semantics: sorted-hashtable.c:937-1123 (probe + tally), core-junction.c:2199-2530
+(top-K), core-junction.c:1073-1334,3675-3834 (junction voting)."""
+import numpy as np
+import pytest
+
+from tests.common import ensure_built, pack_records, describe_mismatch
+
+ensure_built()
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c3():
+    import subread_amd as sa
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.sim import random_genome, c3_lengths
+    g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))   # bench.py's C3 genome
+    ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True, device=0)
+    assert ix.info.buckets == 93018839 and ix.info.items > 2_900_000_000
+    oi = OracleIndex(arrays=ix.export())
+    yield g, ix, oi
+    ix.close()
+    oi.close()
+
+
+def _check(got, want, ends):
+    assert (got == want).all(), describe_mismatch(got, want, ends, 3)
+
+
+def test_c3_se_100bp_with_deferred_repeat_reads(c3):
+    import subread_amd as sa
+    from subread_amd.abi import default_params, ReadBatch
+    from subread_amd.sim import simulate_reads
+    g, ix, oi = c3
+    a = simulate_reads(g, 200_000, 100, seed=20261015, first=7_000_000, sub=0.01, indel=0.001)
+    b = simulate_reads(g, 40_000, 100, seed=99, sub=0.03, indel=0.02, nrate=0.003)   # N bases: exception mask
+    r = ReadBatch(np.concatenate([a.seq, b.seq]), np.arange(240_000, dtype=np.uint64) * 100,
+                  np.full(240_000, 100, np.uint16))
+    p = default_params()
+    ref, _, _, _ = oi.vote(p, r, None, threads=16)
+    want = pack_records(ref, None, None)
+    ix.set_stats(True)
+    pk = sa.pack_reads(r, 100)
+    assert pk.xmask is not None
+    out, _, _ = ix.vote_packed(p, pk)
+    st = ix.stats()
+    ix.set_stats(False)
+    _check(pack_records(out, None, None), want, 1)
+    assert st["deferred"] > 0.05 * len(r), st           # repeat-family reads took the wave-kernel path
+    out2, _, _ = ix.vote(p, r)
+    _check(pack_records(out2, None, None), want, 1)
+    assert (out["selected_votes"][:, 0, 0] > 0).mean() > 0.9
+
+
+def test_c4_pe_150bp(c3):
+    import subread_amd as sa
+    from subread_amd.abi import default_params
+    from subread_amd.sim import simulate_pairs
+    g, ix, oi = c3
+    r1, r2 = simulate_pairs(g, 100_000, 150, seed=4004, first=3_000_000)
+    p = default_params(paired=True)
+    ref, _, _, _ = oi.vote(p, r1, r2, threads=16)
+    out, _, _ = ix.vote_packed(p, sa.pack_reads(r1, 150), sa.pack_reads(r2, 150))
+    _check(pack_records(out, None, None), pack_records(ref, None, None), 2)
+    assert (out["selected_votes"][:, :, 0] > 0).mean() > 0.9
+
+
+def test_c5_subjunc_spliced(c3):
+    import subread_amd as sa
+    from subread_amd.abi import default_params, PROGRAM_SUBJUNC
+    from subread_amd.sim import simulate_spliced_reads
+    g, ix, oi = c3
+    r = simulate_spliced_reads(g, 100_000, 100, seed=5005)
+    p = default_params(PROGRAM_SUBJUNC)
+    ref, rj, rbm, _ = oi.vote(p, r, None, threads=16)
+    assert (rj["minor_votes"] > 0).sum() > 10_000      # the junction branch is exercised
+    out, jout, bm = ix.vote_packed(p, sa.pack_reads(r, 100))
+    _check(pack_records(out, jout, bm), pack_records(ref, rj, rbm), 1)
