@@ -36,6 +36,12 @@ int __real_anti_supporting_read_scan(global_context_t *global_context);
 
 int __wrap_anti_supporting_read_scan(global_context_t *gc)
 {
+	/* SVG_REF_TIMING=1: the reference's own voting-phase clock (read_chunk_circles,
+	 * core.c:3592-3595, cumulative over chunks; the print of core.c:480-485 is commented out
+	 * in the reference) -- the CPU baseline calibration of tools/cpu_calibration.py */
+	if (getenv("SVG_REF_TIMING"))
+		fprintf(stderr, "SVG_REF_TIMECOST_VOTING %.6f %lld\n", gc->timecost_voting,
+		        (long long)gc->processed_reads_in_chunk);
 	const char *fn = getenv("SVG_REF_DUMP");
 	if (fn && fn[0]) {
 		FILE *fp = fopen(fn, "ab");
