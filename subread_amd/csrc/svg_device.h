@@ -50,6 +50,7 @@ struct svg_index {
 	hipStream_t stream2;
 	hipEvent_t ev_lane[2], ev_wave[2];   // slot's records + deferral list ready / wave kernel done
 	void *d_prec[2]; size_t prec_cap[2];   // probe records of one chunk
+	void *d_big[2]; size_t big_cap[2];     // probe_line_kernel's big-bucket list (count, slot indexes)
 	// lane-per-read SE path (svg_lane.hip): candidate lists + deferral list, per-wave cold scratch
 	void *d_lane[2]; size_t lane_cap[2];
 	uint32_t *d_lscratch; size_t lscratch_words;     // light pass
@@ -147,6 +148,10 @@ struct PParams {
 	unsigned long long *stats;
 	// 2-bit packed input (svg_packed_reads) per end, read r of the chunk at base
 	// pk_starts[e][r] or pk_base0[e] + r * pk_stride[e]; seq/off unused when packed
+	// bucket-line kernel: reads per LDS group; list of probes with > 59-item buckets
+	uint32_t group;
+	uint32_t *big_list, *big_count;   // [region][big_stride] slot indexes, [region] counts
+	uint32_t big_stride, big_regions;
 	int packed;
 	const uint32_t *pk_bases[2], *pk_xmask[2];
 	const uint64_t *pk_starts[2];

@@ -1412,6 +1412,79 @@ __device__ __forceinline__ bool try_run(uint64_t eq, int n, int &m, int &fwd, in
 	return true;
 }
 
+// 16-mer key of probe p (subread x gap slot) of strand s of end e of read r (genekey2int,
+// input-files.c:1232, at the subread offset of core.c:3117-3171); false if the read has no
+// such probe (shorter than 15 + gap, or p beyond its applied subreads)
+template <int ENDS, bool PACKED>
+__device__ __forceinline__ bool probe_key(const PParams &pp, uint32_t r, int e, int s, int p, uint32_t &key)
+{
+	int len = e ? pp.len2[r] : pp.len1[r];
+	if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;
+	const int gap = pp.ix.gap;
+	if (len < 15 + gap) return false;
+	const int cr = (len - 15 - gap) << 16;
+	int step;
+	if (len <= 160) { step = cr / (pp.total_subreads - 1); if (step < (gap << 16)) step = gap << 16; }
+	else { step = 6 << 16; if (cr / step > 62) step = cr / 62; }
+	const int np = (1 + cr / step) * gap;
+	if (p >= np) return false;
+	const int k = p / gap, x = p - k * gap;
+	int off = (int)(((int64_t)step * k) >> 16);
+	if (gap > 1) off -= off % gap - x;
+	// 16 bases of strand s at off; strand 1 = reverse_read of strand 0, strand 0 = the input,
+	// reverse-complemented for -S (R2 by default)
+	const int rev = e ? pp.reverse_r2 : pp.reverse_r1;
+	const bool direct = s == rev;
+	const int start = direct ? off : len - 16 - off;
+	key = 0;
+	if constexpr (PACKED) {
+		// 2-bit input (svg_packed_reads): the 16 codes at base k0 are one 32-bit window,
+		// already genekey2int's key.  Reverse strand: complement (~code; an exception base
+		// complements to 'N' = 3) and reverse the 2-bit groups.  Strand 1 of a reversed
+		// read is comp(comp(input)): the codes, with exception bases turned into 'N'.
+		const uint64_t k0 = (pp.pk_starts[e] ? pp.pk_starts[e][r] : pp.pk_base0[e] + (uint64_t)r * pp.pk_stride[e]) +
+		                    (uint64_t)start;
+		const uint32_t *bw = pp.pk_bases[e] + (k0 >> 4);
+		const uint32_t s2 = 2u * (uint32_t)(k0 & 15u);
+		const uint32_t W = s2 ? (bw[0] << s2) | (bw[1] >> (32u - s2)) : bw[0];
+		uint32_t X2 = 0;
+		if (pp.pk_xmask[e]) {
+			const uint32_t *xw = pp.pk_xmask[e] + (k0 >> 5);
+			const uint32_t s1 = (uint32_t)(k0 & 31u);
+			// bases k0..k0+15 (the next word only when they reach into it)
+			uint32_t t = (s1 > 16u ? (xw[0] << s1) | (xw[1] >> (32u - s1)) : xw[0] << s1) >> 16;
+			t = (t | (t << 8)) & 0x00ff00ffu;
+			t = (t | (t << 4)) & 0x0f0f0f0fu;
+			t = (t | (t << 2)) & 0x33333333u;
+			t = (t | (t << 1)) & 0x55555555u;
+			X2 = t | (t << 1);   // base i -> bits 31-2i .. 30-2i
+		}
+		if (direct) key = (s == 1 && rev) ? (W | X2) : W;
+		else {
+			const uint32_t v = __builtin_bitreverse32(~W | X2);
+			key = ((v >> 1) & 0x55555555u) | ((v & 0x55555555u) << 1);
+		}
+	} else {
+		const char *src = (e ? pp.seq2 : pp.seq1) + (e ? pp.off2[r] : pp.off1[r]) + start;
+		const uintptr_t a = (uintptr_t)src;
+		const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+		const int sh = (int)(a & 3);
+		uint32_t wd[5];
+#pragma unroll
+		for (int q = 0; q < 4; q++) wd[q] = w[q];
+		wd[4] = sh ? w[4] : 0u;   // only when the window reaches into it
+#pragma unroll
+		for (int i = 0; i < 16; i++) {
+			const int bi = sh + (direct ? i : 15 - i);
+			char c = (char)((wd[bi >> 2] >> (8 * (bi & 3))) & 0xff);
+			if (!direct) c = comp(c);
+			if (s == 1 && rev) c = comp(comp(c));   // strand 1 of a reversed read: comp(comp(input))
+			key |= b2i(c) << (30 - 2 * i);
+		}
+	}
+	return true;
+}
+
 // =============================================================================================
 // probe kernel: phase P for a whole chunk of reads, one thread per subread probe.  Same
 // arithmetic as Wave::probe_all (genekey2int, key % nb, gehash_go_X's binary search and the
@@ -1442,69 +1515,9 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 		const int s = rem2 >= nps ? 1 : 0;
 		const int p = (int)(rem2 - (uint32_t)s * nps);
 		uint2 rec = make_uint2(0u, 0u);
-		int len = e ? pp.len2[r] : pp.len1[r];
-		if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;
-		if (len >= 15 + gap) {
-			const int cr = (len - 15 - gap) << 16;
-			int step;
-			if (len <= 160) { step = cr / (pp.total_subreads - 1); if (step < (gap << 16)) step = gap << 16; }
-			else { step = 6 << 16; if (cr / step > 62) step = cr / 62; }
-			const int np = (1 + cr / step) * gap;
-			if (p < np) {
-				const int k = p / gap, x = p - k * gap;
-				int off = (int)(((int64_t)step * k) >> 16);
-				if (gap > 1) off -= off % gap - x;
-				// 16 bases of strand s at off; strand 1 = reverse_read of strand 0, strand 0 =
-				// the input, reverse-complemented for -S (R2 by default)
-				const int rev = e ? pp.reverse_r2 : pp.reverse_r1;
-				const bool direct = s == rev;
-				const int start = direct ? off : len - 16 - off;
-				uint32_t key = 0;
-				if constexpr (PACKED) {
-					// 2-bit input (svg_packed_reads): the 16 codes at base k0 are one 32-bit window,
-					// already genekey2int's key.  Reverse strand: complement (~code; an exception base
-					// complements to 'N' = 3) and reverse the 2-bit groups.  Strand 1 of a reversed
-					// read is comp(comp(input)): the codes, with exception bases turned into 'N'.
-					const uint64_t k0 = (pp.pk_starts[e] ? pp.pk_starts[e][r] : pp.pk_base0[e] + (uint64_t)r * pp.pk_stride[e]) +
-					                    (uint64_t)start;
-					const uint32_t *bw = pp.pk_bases[e] + (k0 >> 4);
-					const uint32_t s2 = 2u * (uint32_t)(k0 & 15u);
-					const uint32_t W = s2 ? (bw[0] << s2) | (bw[1] >> (32u - s2)) : bw[0];
-					uint32_t X2 = 0;
-					if (pp.pk_xmask[e]) {
-						const uint32_t *xw = pp.pk_xmask[e] + (k0 >> 5);
-						const uint32_t s1 = (uint32_t)(k0 & 31u);
-						// bases k0..k0+15 (the next word only when they reach into it)
-						uint32_t t = (s1 > 16u ? (xw[0] << s1) | (xw[1] >> (32u - s1)) : xw[0] << s1) >> 16;
-						t = (t | (t << 8)) & 0x00ff00ffu;
-						t = (t | (t << 4)) & 0x0f0f0f0fu;
-						t = (t | (t << 2)) & 0x33333333u;
-						t = (t | (t << 1)) & 0x55555555u;
-						X2 = t | (t << 1);   // base i -> bits 31-2i .. 30-2i
-					}
-					if (direct) key = (s == 1 && rev) ? (W | X2) : W;
-					else {
-						const uint32_t v = __builtin_bitreverse32(~W | X2);
-						key = ((v >> 1) & 0x55555555u) | ((v & 0x55555555u) << 1);
-					}
-				} else {
-				const char *src = (e ? pp.seq2 : pp.seq1) + (e ? pp.off2[r] : pp.off1[r]) + start;
-				const uintptr_t a = (uintptr_t)src;
-				const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
-				const int sh = (int)(a & 3);
-				uint32_t wd[5];
-#pragma unroll
-				for (int q = 0; q < 4; q++) wd[q] = w[q];
-				wd[4] = sh ? w[4] : 0u;   // only when the window reaches into it
-#pragma unroll
-				for (int i = 0; i < 16; i++) {
-					const int bi = sh + (direct ? i : 15 - i);
-					char c = (char)((wd[bi >> 2] >> (8 * (bi & 3))) & 0xff);
-					if (!direct) c = comp(c);
-					if (s == 1 && rev) c = comp(comp(c));   // strand 1 of a reversed read: comp(comp(input))
-					key |= b2i(c) << (30 - 2 * i);
-				}
-				}
+		uint32_t key;
+		if (probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
+			{
 				const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
 				const uint32_t b = key - q * ix.nb;
 				const int16_t k16 = (int16_t)q;
@@ -1653,6 +1666,234 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 			atomicAdd(&pp.stats[0], st_p);
 			atomicAdd(&pp.stats[1], st_i);
 			atomicAdd(&pp.stats[2], st_h);
+		}
+	}
+}
+
+// =============================================================================================
+// bucket-line probe kernel (indexes with the 64-B bucket-line image: every -F -B index):
+//   * reads in groups of pp.group (group * per_read <= PROBE_GROUP_RECS probes): a group's
+//     records are staged in LDS and leave as whole rows ([row][read], SoA) or one contiguous
+//     range (AoS) instead of one scattered 8-byte store per probe;
+//   * a probe whose bucket holds more than 59 items -- no room for its keys in the line; at C3
+//     the repeat-family buckets -- does not search here: it leaves its key in its record slot
+//     (marked fwd = bwd = 0xffff) and its slot index in a list, and probe_big_kernel searches
+//     those 32 lanes per probe.  Before this split one such probe held its whole wave in a
+//     dependent binary search plus a one-load-per-step run scan.
+// =============================================================================================
+#define PROBE_GROUP_RECS 2048
+template <int ENDS, bool PACKED>
+__global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
+{
+	__shared__ uint2 srec[PROBE_GROUP_RECS];
+	__shared__ uint32_t s_big;   // entries of this block's region of the big-bucket list
+	const DevIndex &ix = pp.ix;
+	const uint32_t nps = (uint32_t)pp.nps, per_read = ENDS * 2 * nps, n = pp.n_reads, G = pp.group;
+	const uint32_t ngroups = (n + G - 1) / G, per_blk = (ngroups + gridDim.x - 1) / gridDim.x;
+	const uint32_t g_end = min(ngroups, (blockIdx.x + 1) * per_blk);
+	uint32_t *const big_list = pp.big_list + (size_t)blockIdx.x * pp.big_stride;
+	unsigned long long st_p = 0, st_i = 0, st_h = 0;
+	if (threadIdx.x == 0) s_big = 0;
+	__syncthreads();
+	// contiguous group ranges per block: neighbouring reads stay on one XCD's L2
+	for (uint32_t g = blockIdx.x * per_blk; g < g_end; g++) {
+		const uint32_t r0 = g * G, nr = min(G, n - r0), np = nr * per_read, npr = (np + 255u) & ~255u;
+		for (uint32_t i = threadIdx.x; i < npr; i += 256u) {
+			uint2 rec = make_uint2(0u, 0u);
+			bool big = false;
+			uint32_t outidx = 0;
+			if (i < np) {
+				const uint32_t rl = i / per_read, rem = i - rl * per_read, r = r0 + rl;
+				const int e = ENDS == 2 ? (int)(rem / (2 * nps)) : 0;
+				const uint32_t rem2 = rem - (uint32_t)e * 2 * nps;
+				const int s = rem2 >= nps ? 1 : 0;
+				const int p = (int)(rem2 - (uint32_t)s * nps);
+				outidx = pp.soa ? rem * n + r : r * per_read + rem;
+				uint32_t key;
+				if (probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
+					const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
+					const uint32_t b = key - q * ix.nb;
+					// the bucket's 64-byte line: bounds and u8 keys in one random access
+					const uint4 *l4 = ix.bline + 4 * (size_t)b;
+					uint4 lw[4];
+#pragma unroll
+					for (int k = 0; k < 4; k++) lw[k] = l4[k];
+					const uint32_t c = lw[0].y & 255u, first = lw[0].x;
+					st_p++;
+					big = c > 59u;
+					if (!big && c) {
+						// u8 keys at bytes 5..63 of the line, equal keys by a zero-byte test
+						const uint32_t kk = (uint32_t)(uint8_t)q * 0x01010101u;
+						uint64_t eq = 0;
+#pragma unroll
+						for (int k = 0; k < 4; k++) {
+							const uint32_t dw[4] = {lw[k].x, lw[k].y, lw[k].z, lw[k].w};
+#pragma unroll
+							for (int qq = 0; qq < 4; qq++) {
+								const uint32_t x = dw[qq] ^ kk;
+								const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+								const uint32_t bits = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+								eq |= (uint64_t)bits << (16 * k + 4 * qq);
+							}
+						}
+						eq = (eq >> 5) & ((1ull << c) - 1ull);
+						int m = 0, fwd = 0, bwd = 0;
+						bool hit = false;
+						if (try_run(eq, (int)c, m, fwd, bwd, hit)) {
+							st_i += c;
+							if (hit) {
+								rec = make_uint2(first + (uint32_t)m, (uint32_t)fwd | ((uint32_t)bwd << 16));
+								st_h += (unsigned)(fwd + bwd);
+							}
+						} else big = true;   // unsorted bucket: the literal search, in probe_big_kernel
+					}
+					if (big) rec = make_uint2(key, 0xffffffffu);
+				}
+			}
+			// the block's region of the big-bucket list: one LDS atomic per wave (a single global
+			// counter for the whole grid serialised ~2M atomics per launch)
+			const unsigned long long bm = ballot(big);
+			if (bm) {
+				const int leader = __ffsll((long long)bm) - 1;
+				uint32_t base = 0;
+				if (lane_id() == leader) base = atomicAdd(&s_big, (uint32_t)__popcll(bm));
+				base = __shfl(base, leader);
+				if (big) big_list[base + lanes_below(bm)] = outidx;
+			}
+			if (i < np) srec[i] = rec;
+		}
+		__syncthreads();
+		for (uint32_t i = threadIdx.x; i < np; i += 256u) {
+			if (pp.soa) {
+				const uint32_t row = i / nr, rl = i - row * nr;
+				pp.out[(size_t)row * n + r0 + rl] = srec[rl * per_read + row];
+			} else pp.out[(size_t)r0 * per_read + i] = srec[i];
+		}
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) pp.big_count[blockIdx.x] = s_big;
+	if (pp.stats) {
+		for (int o = 32; o; o >>= 1) {
+			st_p += __shfl_xor(st_p, o); st_i += __shfl_xor(st_i, o); st_h += __shfl_xor(st_h, o);
+		}
+		if (lane_id() == 0 && st_p) {
+			atomicAdd(&pp.stats[0], st_p);
+			atomicAdd(&pp.stats[1], st_i);
+			atomicAdd(&pp.stats[2], st_h);
+		}
+	}
+}
+
+// The big-bucket probes of probe_line_kernel, 8 lanes per probe: in each pass lane j loads the
+// 16-byte word 8*pass+j of the aligned window holding the bucket's i16 keys (8 keys, one 128-B
+// row per 8 lanes; up to four passes = 256 items in flight at once), the 8 lanes reduce first /
+// last / count of the equal keys, and gehash_go_X's binary search (sorted-hashtable.c:947-981)
+// is replayed on the run's positions to get the reference's first-hit midpoint.  A bucket
+// whose equal keys are not one run (not sorted) takes the literal search.
+__global__ void __launch_bounds__(256) probe_big_kernel(PParams pp)
+{
+	const DevIndex &ix = pp.ix;
+	const int sub = (int)(threadIdx.x & 7u);
+	unsigned long long st_i = 0, st_h = 0, st_n = 0;
+	// list regions of the line kernel's blocks (pp.big_regions of them)
+	for (uint32_t reg = blockIdx.x; reg < pp.big_regions; reg += gridDim.x) {
+		const uint32_t cnt = pp.big_count[reg];
+		const uint32_t *list = pp.big_list + (size_t)reg * pp.big_stride;
+		st_n += threadIdx.x == 0 ? cnt : 0u;
+		for (uint32_t j = threadIdx.x >> 3; j < cnt; j += 32u) {
+			const uint32_t outidx = list[j];
+			const uint32_t key = pp.out[outidx].x;
+			const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
+			const uint32_t b = key - q * ix.nb;
+			const uint16_t k16 = (uint16_t)q;
+			const uint2 l0 = *(const uint2 *)(ix.bline + 4 * (size_t)b);
+			const uint32_t first = l0.x;
+			uint32_t nn = l0.y & 255u;
+			if (nn == 255u) nn = ix.bstart[b + 1] - first;   // 255 = 255 or more items
+			const int16_t *K = ix.keys + first;
+			const uint4 *W = (const uint4 *)((uintptr_t)K & ~(uintptr_t)15);
+			const int sh = (int)(((uintptr_t)K & 15) >> 1);   // item 0 is halfword sh of word 0
+			const int nw = (sh + (int)nn + 7) >> 3;           // 16-byte words holding the bucket
+			int fe = 0x7fffffff, le = -1, ne = 0;
+			for (int w0 = 0; w0 < nw; w0 += 32) {
+				uint4 v[4];
+#pragma unroll
+				for (int ps = 0; ps < 4; ps++) {
+					const int w = w0 + 8 * ps + sub;
+					v[ps] = w < nw ? W[w] : make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+				}
+#pragma unroll
+				for (int ps = 0; ps < 4; ps++) {
+					const int w = w0 + 8 * ps + sub;
+					const uint32_t dw[4] = {v[ps].x, v[ps].y, v[ps].z, v[ps].w};
+#pragma unroll
+					for (int h = 0; h < 8; h++) {
+						const int it = 8 * w + h - sh;
+						if (it >= 0 && it < (int)nn && (uint16_t)(dw[h >> 1] >> (16 * (h & 1))) == k16) {
+							fe = min(fe, it); le = max(le, it); ne++;
+						}
+					}
+				}
+			}
+#pragma unroll
+			for (int o = 4; o; o >>= 1) {
+				fe = min(fe, __shfl_xor(fe, o));
+				le = max(le, __shfl_xor(le, o));
+				ne += __shfl_xor(ne, o);
+			}
+			uint2 rec = make_uint2(0u, 0u);
+			if (ne > 0) {
+				int m, fwd, bwd;
+				if (le - fe + 1 == ne) {
+					int lo = 0, hi = (int)nn - 1;
+					for (;;) {
+						m = (lo + hi) >> 1;
+						if (m < fe) lo = m + 1;
+						else if (m > le) hi = m - 1;
+						else break;
+					}
+					fwd = le - m + 1;
+					bwd = m - fe;
+				} else {
+					const int16_t kq = (int16_t)k16;
+					bool hit = false;
+					int lo = 0, hi = (int)nn - 1;
+					m = 0;
+					for (;;) {
+						m = (lo + hi) >> 1;
+						const int16_t kk = K[m];
+						if (kk > kq) hi = m - 1;
+						else if (kk < kq) lo = m + 1;
+						else { hit = true; break; }
+						if (hi < lo) break;
+					}
+					fwd = bwd = 0;
+					if (hit) {
+						int qq = m + 1;
+						while (qq < (int)nn && K[qq] == kq) qq++;
+						fwd = qq - m;
+						qq = m - 1;
+						while (qq >= 0 && K[qq] == kq) qq--;
+						bwd = m - 1 - qq;
+					}
+				}
+				if (fwd + bwd > 0) rec = make_uint2(first + (uint32_t)m, (uint32_t)fwd | ((uint32_t)bwd << 16));
+			}
+			if (sub == 0) {
+				pp.out[outidx] = rec;
+				st_i += nn;
+				st_h += (rec.y & 0xffffu) + (rec.y >> 16);
+			}
+		}
+	}
+	if (pp.stats) {
+		for (int o = 32; o; o >>= 1) {
+			st_i += __shfl_xor(st_i, o); st_h += __shfl_xor(st_h, o); st_n += __shfl_xor(st_n, o);
+		}
+		if (lane_id() == 0 && (st_i || st_h || st_n)) {
+			atomicAdd(&pp.stats[1], st_i);
+			atomicAdd(&pp.stats[2], st_h);
+			atomicAdd(&pp.stats[5], st_n);   // diagnostics: probes searched here
 		}
 	}
 }
@@ -1855,6 +2096,7 @@ extern "C" void svg_index_close(svg_index *h)
 	for (int s = 0; s < 2; s++) {
 		hipFree(h->d_prec[s]);
 		hipFree(h->d_lane[s]);
+		hipFree(h->d_big[s]);
 		hipFree(h->d_in[s]);
 		if (s == 1) hipFree(h->d_in[2]);
 		hipFree(h->d_out[s]);
@@ -2218,7 +2460,32 @@ int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slo
 		}
 	}
 #define PROBE_LAUNCH(E, L, P) hipLaunchKernelGGL((probe_kernel<E, 8, L, P>), dim3((unsigned)pb), dim3(256), 0, st, pp)
-	if (h->dix.bline) {
+	if (h->dix.bline && !getenv("SVG_PROBE_V1")) {
+		// bucket lines: grouped probe kernel + the big-bucket kernel on its list
+		pp.group = (uint32_t)(PROBE_GROUP_RECS / job->per_read);
+		if (pp.group > 64) pp.group = 64;
+		if (pp.group < 1) pp.group = 1;
+		const uint64_t ng = (cn + pp.group - 1) / pp.group;
+		uint64_t gb = ng, gmax = (uint64_t)h->n_cu * 8 * 4;
+		if (gb > gmax) gb = gmax;
+		// one list region per line-kernel block, sized for all of its probes; per-block counts
+		const uint64_t per_blk = (ng + gb - 1) / gb, stride = per_blk * pp.group * job->per_read;
+		const uint64_t cnt_words = (gb + 63) & ~63ull;
+		if ((rc = svg_ensure(h, &h->d_big[slot], &h->big_cap[slot], (cnt_words + gb * stride) * 4 + 256))) return rc;
+		pp.big_count = (uint32_t *)h->d_big[slot];
+		pp.big_list = (uint32_t *)h->d_big[slot] + cnt_words;
+		pp.big_stride = (uint32_t)stride;
+		pp.big_regions = (uint32_t)gb;
+		if (pp.packed) {
+			if (pe) hipLaunchKernelGGL((probe_line_kernel<2, true>), dim3((unsigned)gb), dim3(256), 0, st, pp);
+			else hipLaunchKernelGGL((probe_line_kernel<1, true>), dim3((unsigned)gb), dim3(256), 0, st, pp);
+		} else {
+			if (pe) hipLaunchKernelGGL((probe_line_kernel<2, false>), dim3((unsigned)gb), dim3(256), 0, st, pp);
+			else hipLaunchKernelGGL((probe_line_kernel<1, false>), dim3((unsigned)gb), dim3(256), 0, st, pp);
+		}
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(probe_big_kernel, dim3((unsigned)(h->n_cu * 8)), dim3(256), 0, st, pp);
+	} else if (h->dix.bline) {
 		if (pp.packed) { if (pe) PROBE_LAUNCH(2, true, true); else PROBE_LAUNCH(1, true, true); }
 		else { if (pe) PROBE_LAUNCH(2, true, false); else PROBE_LAUNCH(1, true, false); }
 	} else {
