@@ -28,6 +28,10 @@ struct DevIndex {
 	//            more), then the u8 keys of its first <= 59 items -- bounds and keys of a probe
 	//            in ONE random line (replaces bgrp + keys8 when present)
 	const uint4 *bline;
+	//   bcode[b]: one 32-byte sector per bucket: u32 first item, u8 count (255 = not coded), the
+	//            sorted key_hi multiset as a unary count code (build_bcode); replaces bline when
+	//            the index's key_hi range is small (V = 0xffffffff / nb + 1 <= 80)
+	const uint4 *bcode;
 };
 
 struct svg_index {
@@ -35,7 +39,7 @@ struct svg_index {
 	hipStream_t stream;
 	svg_host_index host;
 	DevIndex dix;
-	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr, *d_bgrp, *d_keys8, *d_bline;
+	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr, *d_bgrp, *d_keys8, *d_bline, *d_bcode;
 	uint32_t *d_scratch;
 	size_t scratch_words;
 	unsigned long long *d_stats;

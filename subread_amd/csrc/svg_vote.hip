@@ -1388,6 +1388,33 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	}
 }
 
+// position (0..63) of the j-th (0-based) set bit of x; x has more than j set bits
+__device__ __forceinline__ int select64(uint64_t x, int j)
+{
+	int pos = 0, c = __popc((uint32_t)x);
+	if (j >= c) { j -= c; x >>= 32; pos = 32; }
+	uint32_t v = (uint32_t)x;
+	c = __popc(v & 0xffffu); if (j >= c) { j -= c; v >>= 16; pos += 16; }
+	c = __popc(v & 0xffu); if (j >= c) { j -= c; v >>= 8; pos += 8; }
+	c = __popc(v & 0xfu); if (j >= c) { j -= c; v >>= 4; pos += 4; }
+	c = __popc(v & 0x3u); if (j >= c) { j -= c; v >>= 2; pos += 2; }
+	return pos + (j >= (int)(v & 1u) ? 1 : 0);
+}
+
+// position of the j-th (0-based) zero bit at or above bit 40 of a 32-byte bucket code (LSB-first)
+__device__ __forceinline__ int code_zero(const uint64_t z[4], int j)
+{
+	int base = 0;
+#pragma unroll
+	for (int q = 0; q < 4; q++) {
+		const int c = __popcll(z[q]);
+		if (j < c) return base + select64(z[q], j);
+		j -= c;
+		base += 64;
+	}
+	return 256;
+}
+
 // equal-key run of a bucket given as a bit mask over its items: gehash_go_X's binary search
 // (sorted-hashtable.c:947-981) replayed on the positions alone -- it stops at the first
 // midpoint inside the run.  False (caller falls back to the key loop) if the run is not
@@ -1543,18 +1570,21 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 					const uint32_t i = b & 15u;
 					const uint32_t cw[4] = {ga.y, ga.z, ga.w, gb.x};
 					uint32_t pre = 0;
+					bool sat = false;   // a bucket before b in the group has 255+ items: its byte is no count
 #pragma unroll
 					for (int q = 0; q < 4; q++) {
 						// bytes of word q below i
 						const int nb_ = (int)i - 4 * q;
 						const uint32_t msk = nb_ >= 4 ? 0xffffffffu : nb_ <= 0 ? 0u : (1u << (8 * nb_)) - 1u;
 						pre = __builtin_amdgcn_sad_u8(cw[q] & msk, 0u, pre);
+						const uint32_t t = ~cw[q] | ~msk;   // zero byte <=> a 0xff count below i
+						sat |= ((t - 0x01010101u) & ~t & 0x80808080u) != 0u;
 					}
 					const uint32_t wsel = i < 4 ? ga.y : i < 8 ? ga.z : i < 12 ? ga.w : gb.x;
 					const uint32_t c = (wsel >> (8 * (i & 3u))) & 255u;
 					first = ga.x + pre;
 					n = (int)c;
-					compact = c != 255u;
+					compact = c != 255u && !sat;
 				}
 				if (!compact) {
 					first = ix.bstart[b];
@@ -1682,7 +1712,7 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 //     dependent binary search plus a one-load-per-step run scan.
 // =============================================================================================
 #define PROBE_GROUP_RECS 2048
-template <int ENDS, bool PACKED>
+template <int ENDS, bool PACKED, bool CODE>
 __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 {
 	__shared__ uint2 srec[PROBE_GROUP_RECS];
@@ -1710,7 +1740,38 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 				const int p = (int)(rem2 - (uint32_t)s * nps);
 				outidx = pp.soa ? rem * n + r : r * per_read + rem;
 				uint32_t key;
-				if (probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
+				if (CODE && probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
+					const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
+					const uint32_t b = key - q * ix.nb;
+					// the bucket's 32-byte code: first item, count, unary key_hi counts
+					const uint4 *c4 = ix.bcode + 2 * (size_t)b;
+					const uint4 u0 = c4[0], u1 = c4[1];
+					const uint32_t c = u0.y & 255u, first = u0.x;
+					st_p++;
+					big = c == 255u;
+					if (!big && c) {
+						const uint64_t z[4] = {~(((uint64_t)u0.y << 32) | u0.x) & ~0xffffffffffull,
+						                       ~(((uint64_t)u0.w << 32) | u0.z), ~(((uint64_t)u1.y << 32) | u1.x),
+						                       ~(((uint64_t)u1.w << 32) | u1.z)};
+						const int k = (int)q;
+						const int fe = k ? code_zero(z, k - 1) - 40 - (k - 1) : 0;
+						const int ee = code_zero(z, k) - 40 - k;   // items with key_hi <= k
+						st_i += c;
+						if (ee > fe) {
+							const int le = ee - 1;
+							int lo = 0, hi = (int)c - 1, m;
+							for (;;) {
+								m = (lo + hi) >> 1;
+								if (m < fe) lo = m + 1;
+								else if (m > le) hi = m - 1;
+								else break;
+							}
+							rec = make_uint2(first + (uint32_t)m, (uint32_t)(le - m + 1) | ((uint32_t)(m - fe) << 16));
+							st_h += (unsigned)(ee - fe);
+						}
+					}
+					if (big) rec = make_uint2(key, 0xffffffffu);
+				} else if (!CODE && probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
 					const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
 					const uint32_t b = key - q * ix.nb;
 					// the bucket's 64-byte line: bounds and u8 keys in one random access
@@ -1806,10 +1867,10 @@ __global__ void __launch_bounds__(256) probe_big_kernel(PParams pp)
 			const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
 			const uint32_t b = key - q * ix.nb;
 			const uint16_t k16 = (uint16_t)q;
-			const uint2 l0 = *(const uint2 *)(ix.bline + 4 * (size_t)b);
+			const uint2 l0 = ix.bcode ? *(const uint2 *)(ix.bcode + 2 * (size_t)b) : *(const uint2 *)(ix.bline + 4 * (size_t)b);
 			const uint32_t first = l0.x;
 			uint32_t nn = l0.y & 255u;
-			if (nn == 255u) nn = ix.bstart[b + 1] - first;   // 255 = 255 or more items
+			if (nn == 255u) nn = ix.bstart[b + 1] - first;   // 255 = not in the image (or 255+ items)
 			const int16_t *K = ix.keys + first;
 			const uint4 *W = (const uint4 *)((uintptr_t)K & ~(uintptr_t)15);
 			const int sh = (int)(((uintptr_t)K & 15) >> 1);   // item 0 is halfword sh of word 0
@@ -1928,6 +1989,39 @@ __global__ void __launch_bounds__(256) build_keys8(const int16_t *keys, uint64_t
 		keys8[i] = (uint8_t)keys[i];
 }
 
+// DevIndex::bcode: one 32-byte sector per bucket -- u32 first item, u8 item count (255 = not coded:
+// more than 216 - V items, or keys not sorted), then the bucket's sorted key_hi multiset as a
+// unary count code over bits 40..255: for v = 0 .. V-1, c_v one-bits then a zero (V = number of
+// possible key_hi values, key / nb <= 0xffffffff / nb; 47 at nb = 93,018,839), rest one-bits.
+// The equal-key run of key_hi k is then [ones before zero k-1, ones before zero k): a probe needs
+// one random 32-byte sector instead of a 64-byte line (HBM serves ~1.6x more of them per second).
+#define BCODE_BITS 216
+__global__ void __launch_bounds__(256) build_bcode(const uint32_t *bstart, const int16_t *keys, uint32_t nb, int V, uint4 *bcode)
+{
+	for (uint32_t b = blockIdx.x * 256u + threadIdx.x; b < nb; b += gridDim.x * 256u) {
+		const uint32_t first = bstart[b], n = bstart[b + 1] - first;
+		uint32_t w[8];
+#pragma unroll
+		for (int q = 0; q < 8; q++) w[q] = 0xffffffffu;   // unused tail: one-bits
+		w[0] = first;
+		bool ok = (int)n + V <= BCODE_BITS;
+		if (ok) {
+			int pos = 40, cur = 0;
+			for (uint32_t i = 0; i < n && ok; i++) {
+				const int v = keys[first + i];
+				if (v < cur || v >= V) { ok = false; break; }
+				while (cur < v) { w[pos >> 5] &= ~(1u << (pos & 31)); pos++; cur++; }   // zero: value cur closed
+				pos++;                                                            // one: an item of value v
+			}
+			while (ok && cur < V) { w[pos >> 5] &= ~(1u << (pos & 31)); pos++; cur++; }
+		}
+		w[1] = (w[1] & 0xffffff00u) | (ok ? n : 255u);
+		uint4 *d = bcode + 2 * (size_t)b;
+		d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+		d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+	}
+}
+
 // DevIndex::bline: one 64-byte line per bucket (first item, count, the u8 keys of <= 59 items)
 __global__ void __launch_bounds__(256) build_bline(const uint32_t *bstart, const int16_t *keys, uint32_t nb, uint4 *bline)
 {
@@ -1991,7 +2085,27 @@ int svg_index_finish_device(svg_index *h)
 	h->dix.bgrp = NULL;
 	h->dix.keys8 = NULL;
 	h->dix.bline = NULL;
-	if (x->nb >= 16843009u && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_BLINE")) {
+	h->dix.bcode = NULL;
+	{
+		// 32-byte bucket codes when the key_hi range is small enough for them to hold ordinary
+		// buckets (V = 47 at nb = 93,018,839, the -F -B full index): n + V <= 216 bits
+		const uint32_t V = 0xffffffffu / x->nb + 1u;
+		if (V <= 80u && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_BCODE")) {
+			if (dmalloc(h, &h->d_bcode, (size_t)x->nb * 32 + 64) == 0) {
+				uint64_t blocks = ((uint64_t)x->nb + 255) / 256, bmax = (uint64_t)h->n_cu * 64;
+				if (blocks > bmax) blocks = bmax;
+				hipLaunchKernelGGL(build_bcode, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
+				                   (const int16_t *)h->d_keys, x->nb, (int)V, (uint4 *)h->d_bcode);
+				HIPCHK(hipGetLastError());
+				HIPCHK(hipStreamSynchronize(h->stream));
+				h->dix.bcode = (const uint4 *)h->d_bcode;
+			} else {
+				h->d_bcode = NULL;
+				(void)hipGetLastError();
+			}
+		}
+	}
+	if (!h->dix.bcode && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_BLINE")) {
 		// (2^32-1)/nb <= 255: every key_hi fits a byte; 64 B per bucket (5.95 GB at nb = 93M)
 		// optional image: without the HBM for it the index still opens with the group/key images
 		if (dmalloc(h, &h->d_bline, (size_t)x->nb * 64 + 64) == 0) {
@@ -2007,7 +2121,7 @@ int svg_index_finish_device(svg_index *h)
 			(void)hipGetLastError();
 		}
 	}
-	if (!h->dix.bline && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT")) {
+	if (!h->dix.bline && !h->dix.bcode && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT")) {
 		// (2^32-1)/nb <= 255: every key_hi fits a byte
 		const size_t ng = ((size_t)x->nb + 15) / 16;
 		if ((rc = dmalloc(h, &h->d_bgrp, ng * 32 + 64)) || (rc = dmalloc(h, &h->d_keys8, x->items + 128))) return rc;
@@ -2116,7 +2230,7 @@ extern "C" void svg_index_close(svg_index *h)
 			for (int j = 0; j < 2; j++)
 				if (h->tev[k][i][j]) hipEventDestroy(h->tev[k][i][j]);
 	hipFree(h->d_bstart); hipFree(h->d_keys); hipFree(h->d_vals); hipFree(h->d_values); hipFree(h->d_chr);
-	hipFree(h->d_bgrp); hipFree(h->d_keys8); hipFree(h->d_bline);
+	hipFree(h->d_bgrp); hipFree(h->d_keys8); hipFree(h->d_bline); hipFree(h->d_bcode);
 	hipFree(h->d_scratch); hipFree(h->d_stats); hipFree(h->d_err);
 	if (h->ev_last) hipEventDestroy(h->ev_last);
 	if (h->stream) hipStreamDestroy(h->stream);
@@ -2460,7 +2574,7 @@ int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slo
 		}
 	}
 #define PROBE_LAUNCH(E, L, P) hipLaunchKernelGGL((probe_kernel<E, 8, L, P>), dim3((unsigned)pb), dim3(256), 0, st, pp)
-	if (h->dix.bline && !getenv("SVG_PROBE_V1")) {
+	if ((h->dix.bline || h->dix.bcode) && !getenv("SVG_PROBE_V1")) {
 		// bucket lines: grouped probe kernel + the big-bucket kernel on its list
 		pp.group = (uint32_t)(PROBE_GROUP_RECS / job->per_read);
 		if (pp.group > 64) pp.group = 64;
@@ -2476,13 +2590,15 @@ int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slo
 		pp.big_list = (uint32_t *)h->d_big[slot] + cnt_words;
 		pp.big_stride = (uint32_t)stride;
 		pp.big_regions = (uint32_t)gb;
-		if (pp.packed) {
-			if (pe) hipLaunchKernelGGL((probe_line_kernel<2, true>), dim3((unsigned)gb), dim3(256), 0, st, pp);
-			else hipLaunchKernelGGL((probe_line_kernel<1, true>), dim3((unsigned)gb), dim3(256), 0, st, pp);
+#define LINE_LAUNCH(E, P, C) hipLaunchKernelGGL((probe_line_kernel<E, P, C>), dim3((unsigned)gb), dim3(256), 0, st, pp)
+		if (h->dix.bcode) {
+			if (pp.packed) { if (pe) LINE_LAUNCH(2, true, true); else LINE_LAUNCH(1, true, true); }
+			else { if (pe) LINE_LAUNCH(2, false, true); else LINE_LAUNCH(1, false, true); }
 		} else {
-			if (pe) hipLaunchKernelGGL((probe_line_kernel<2, false>), dim3((unsigned)gb), dim3(256), 0, st, pp);
-			else hipLaunchKernelGGL((probe_line_kernel<1, false>), dim3((unsigned)gb), dim3(256), 0, st, pp);
+			if (pp.packed) { if (pe) LINE_LAUNCH(2, true, false); else LINE_LAUNCH(1, true, false); }
+			else { if (pe) LINE_LAUNCH(2, false, false); else LINE_LAUNCH(1, false, false); }
 		}
+#undef LINE_LAUNCH
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL(probe_big_kernel, dim3((unsigned)(h->n_cu * 8)), dim3(256), 0, st, pp);
 	} else if (h->dix.bline) {

@@ -171,32 +171,40 @@ def test_gpu_pipelines_match_oracle(mode, gpu_indexes, index_cache, monkeypatch)
 
 
 def test_gpu_probe_images_match_oracle(monkeypatch):
-    """The probe images picked at index load: 64-byte bucket lines (default for -F -B
-    indexes), 16-bucket groups + u8 keys (SVG_NO_BLINE=1), plain bounds + i16 keys
-    (SVG_NO_COMPACT=1).  The genome carries repeat families, so that buckets past a
-    line's 59 keys (count byte 60..254, and 255 = bounds from bstart) take the
-    fallback search."""
+    """The probe images picked at index load: 32-byte unary bucket codes (default for -F -B
+    indexes), 64-byte bucket lines (SVG_NO_BCODE=1), 16-bucket groups + u8 keys
+    (+ SVG_NO_BLINE=1), plain bounds + i16 keys (SVG_NO_COMPACT=1), and the one-kernel
+    probe of the previous build (SVG_PROBE_V1=1).  The genome carries repeat families, so
+    that buckets past a code's 169 keys / a line's 59 keys take the big-bucket search."""
     import subread_amd as sa
     from oracle.pyoracle import OracleIndex
     from subread_amd.abi import default_params, PROGRAM_ALIGN
     from subread_amd.sim import random_genome, simulate_reads
-    g = random_genome([3_000_000, 1_000_000], 77, repeats=(8000, 300, 10, 0.12))
+    g = random_genome([3_000_000, 1_000_000], 77, repeats=(8000, 300, 10, 0.05))   # ~350 copies of many 16-mers
     r1 = simulate_reads(g, 40000, 100, seed=5, sub=0.01, indel=0.001)
     p = default_params(PROGRAM_ALIGN, False)
     want = None
-    for env in ({}, {"SVG_NO_BLINE": "1"}, {"SVG_NO_COMPACT": "1"}):
+    for env in ({}, {"SVG_NO_BCODE": "1"}, {"SVG_NO_BCODE": "1", "SVG_NO_BLINE": "1"}, {"SVG_NO_COMPACT": "1"},
+                {"SVG_PROBE_V1": "1"}, {"SVG_PROBE_V1": "1", "SVG_NO_BCODE": "1"}):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
-        ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True, device=0)
-        for k in env:
-            monkeypatch.delenv(k)
+        # repeat threshold 400 (-f 400): keys with up to 400 occurrences stay, so some buckets
+        # exceed a code's 169 items too
+        ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True, repeat_threshold=400, device=0)
+        if "SVG_PROBE_V1" not in env:
+            for k in env:
+                monkeypatch.delenv(k)
         if want is None:
             a = ix.export()
-            assert (np.diff(a["bstart"].astype(np.int64)) > 59).sum() > 200   # the fallback is exercised
+            sizes = np.diff(a["bstart"].astype(np.int64))
+            assert (sizes > 59).sum() > 200       # big buckets of the line image
+            assert (sizes > 169).sum() > 0        # and of the code image
             ref, _, _, _ = OracleIndex(arrays=a).vote(p, r1, None, threads=16)
             want = pack_records(ref, None, None)
             del a
         out, _, _ = ix.vote(p, r1)
         ix.close()
+        for k in env:
+            monkeypatch.delenv(k, raising=False)
         got = pack_records(out, None, None)
         assert (got == want).all(), "%s: %s" % (env, describe_mismatch(got, want, 1, 3))
