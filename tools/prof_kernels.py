@@ -2,17 +2,17 @@
 """Per-kernel rocprofv3 summary of one bench.py workload -> profiles/.
 
 Inputs (rocprofv3 output directories, each from its own run):
-  --trace DIR   rocprofv3 --kernel-trace --stats of `bench.py --steps S --warmup W --no-cpu`
-  --fetch DIR   rocprofv3 --pmc FETCH_SIZE of `bench.py --steps 1 --warmup 0 --no-cpu --no-check`
+  --trace DIR   rocprofv3 --kernel-trace --stats of `tools/prof_run.py WL S` (1 warmup + S steps)
+  --fetch DIR   rocprofv3 --pmc FETCH_SIZE of `tools/prof_run.py WL 1`
   --write DIR   rocprofv3 --pmc WRITE_SIZE of the same command
 Outputs: OUT.json (per-kernel launch time and HBM traffic per launch / per read; bench.py
 reads traffic_bytes_per_read of the dominant kernel from it) and OUT.md.
 
-Dispatch accounting: every bench step launches each kernel L times (one per chunk of
-reads); bench.py then runs one extra step with the statistics counters on.  The trace
-therefore holds (W + S + 1) * L dispatches per kernel: the timed-region average drops the
-first W * L (warmup) and the last L (stats pass).  The PMC runs have W = 0, S = 1: the
-first half of each kernel's dispatches is the measured step.
+Dispatch accounting: every step launches each kernel L times (one per chunk of reads).
+The trace holds (W + S) * L dispatches per kernel: the timed-region average drops the first
+W * L (warmup).  The PMC runs are 1 warmup + 1 step: half of each kernel's dispatches is one
+step.  probe_kernel = probe_line_kernel + probe_big_kernel (one probe launch of the library's
+timing API brackets both), or the one-kernel probe when the index has no bucket codes/lines.
 
 Units and corrections (MI355X_MICROARCH.md, HBM / rocprofv3 section): FETCH_SIZE and
 WRITE_SIZE are in KiB.  The guide's x2 correction is for 16-B/lane coalesced streaming
@@ -25,15 +25,18 @@ import os
 import sqlite3
 from collections import defaultdict
 
-KERNELS = ("probe_kernel", "gather_kernel", "lane_kernel", "vote_kernel")
+KERNELS = ("probe_kernel", "probe_line_kernel", "probe_big_kernel", "gather_kernel", "lane_kernel", "vote_kernel",
+           "unpack_reads", "compact_records")
 
 
 def short(name):
     if "lane_pe_kernel" in name:      # bench.py times both lane kernels as "lane_kernel"
         return "lane_kernel"
-    for k in KERNELS:
+    for k in KERNELS[1:]:
         if k in name:
             return k
+    if "probe_kernel" in name:
+        return "probe_kernel"
     return None
 
 
@@ -88,7 +91,7 @@ def main():
         if k not in per:
             continue
         d = per[k]
-        L = len(d) // (a.warmup + a.steps + 1)
+        L = max(1, len(d) // (a.warmup + a.steps))
         timed = d[a.warmup * L:(a.warmup + a.steps) * L]
         f, w = fe.get(k, []), wr.get(k, [])
         nf = len(f) // 2
@@ -104,6 +107,17 @@ def main():
             ent["bench_launch_ms"] = bench[k]["launch_ms"]
         res["kernels"][k] = ent
         tot_traffic += fb + wb
+    # the library's "probe_kernel" timing kind = line kernel + big-bucket kernel
+    if "probe_line_kernel" in res["kernels"] and "probe_kernel" not in res["kernels"]:
+        pl, pb = res["kernels"]["probe_line_kernel"], res["kernels"].get("probe_big_kernel")
+        comb = dict(pl)
+        if pb:
+            for f in ("timed_avg_ms", "fetch_bytes_per_read", "write_bytes_per_read", "traffic_bytes_per_read",
+                      "traffic_bytes_per_launch"):
+                comb[f] = pl[f] + pb[f]
+        comb["name"] = "probe_line_kernel + probe_big_kernel"
+        comb["all_dispatch_avg_ms"] = None
+        res["kernels"]["probe_kernel"] = comb
     res["traffic_bytes_per_read"] = tot_traffic / a.reads
     json.dump(res, open(a.out + ".json", "w"), indent=1)
     M = ["# rocprofv3 summary: %s (bench.py, %d timed steps of %d reads)" % (a.workload, a.steps, a.reads), "",

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Profiling target (GPU box): the device-resident vote path of one bench workload, exactly
+1 warmup + STEPS timed steps and nothing else on the GPU, so that a rocprofv3 trace or PMC
+pass holds (1 + STEPS) x launches-per-step dispatches of every vote kernel.
+Usage: prof_run.py WORKLOAD [STEPS]   (WORKLOAD c3 | c4 | c5; reads per step as bench.py)"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import subread_amd as sa  # noqa: E402
+from subread_amd.abi import default_params, PROGRAM_SUBJUNC, MAPPING_DTYPE, BIG_MARGIN_WORDS, SvgPackedReads  # noqa: E402
+from subread_amd.sim import random_genome, simulate_reads, simulate_pairs, simulate_spliced_reads, c3_lengths  # noqa: E402
+
+
+def main():
+    wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))
+    ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True, device=0)
+    dev = torch.device("cuda", 0)
+    if wl == "c4":
+        n, L = 25_000_000, 150
+        r1, r2 = simulate_pairs(g, n, L, seed=4004)
+        p = default_params(paired=True)
+    elif wl == "c5":
+        n, L = 50_000_000, 100
+        r1, r2 = simulate_spliced_reads(g, n, L, seed=5005), None
+        p = default_params(PROGRAM_SUBJUNC)
+    else:
+        n, L = 50_000_000, 100
+        r1, r2 = simulate_reads(g, n, L, seed=20261015, sub=0.01, indel=0.001), None
+        p = default_params()
+    keep = []
+
+    def dq(rb):
+        pk = sa.pack_reads(rb, L, threads=16)
+        t = [torch.from_numpy(pk.bases.view(np.uint8)).to(dev), torch.from_numpy(rb.lens.view(np.uint8)).to(dev)]
+        keep.append(t)
+        q = SvgPackedReads()
+        q.bases, q.lens, q.xmask, q.starts, q.stride, q.n_reads = t[0].data_ptr(), t[1].data_ptr(), None, None, L, n
+        return q
+    q1 = dq(r1)
+    q2 = dq(r2) if r2 is not None else None
+    ends = 2 if r2 is not None else 1
+    out = torch.empty(n * ends * 3 * MAPPING_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    sj = wl == "c5"
+    jout = torch.empty(n * ends * 3 * 16, dtype=torch.uint8, device=dev) if sj else None
+    bm = torch.empty(n * ends * BIG_MARGIN_WORDS * 2, dtype=torch.uint8, device=dev) if sj else None
+    ix.set_max_read_length(L)
+    torch.cuda.synchronize()
+
+    def step():
+        ix.vote_packed_device(p, q1, q2, out.data_ptr(), jout.data_ptr() if sj else None, bm.data_ptr() if sj else None)
+    step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ix.device_status()
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t
+    print("%s: %d reads x %d ends, %.1f ms/step, %.1f Mreads/s" % (wl, n, ends, t / steps * 1e3, n * ends * steps / t / 1e6))
+
+
+if __name__ == "__main__":
+    main()
