@@ -164,7 +164,7 @@ typedef struct svg_packed_reads {
 int64_t svg_pack_reads(const svg_reads *in, uint64_t stride, uint32_t *bases, uint32_t *xmask, uint64_t *starts,
                        int threads);
 
-/* opaque index handle: owns the HBM copy of <prefix>.00.b.tab / .array / .reads */
+/* opaque index handle: owns the HBM copy of every <prefix>.NN.b.tab / .array block and .reads */
 typedef struct svg_index svg_index;
 
 typedef struct svg_index_info {
@@ -177,10 +177,15 @@ typedef struct svg_index_info {
 	uint64_t device_bytes;       /* HBM held by the handle                     */
 	int32_t  device;             /* HIP device ordinal                         */
 	uint32_t array_values_bytes; /* bytes of the packed .array image           */
+	int32_t  n_blocks;           /* index blocks (<prefix>.NN.b.*); the fields above
+	                                but device_bytes describe block 00           */
 } svg_index_info;
 
-/* Load "<prefix>.00.b.tab", "<prefix>.00.b.array", "<prefix>.reads" (single-block
- * base-space index, as written by subread-buildindex) into HBM of `device`. */
+/* Load a base-space index as written by subread-buildindex -- "<prefix>.NN.b.tab" and
+ * "<prefix>.NN.b.array" for every block NN = 00, 01, ... and "<prefix>.reads" -- into HBM of
+ * `device`.  All blocks stay resident; a vote runs them in order, each later block merging
+ * with the records the earlier ones left (read_chunk_circles, core.c:3567-3613), so a
+ * multi-block index gives the reference's records for the same reads. */
 int  svg_index_open(const char *prefix, int device, svg_index **out);
 void svg_index_close(svg_index *idx);
 int  svg_index_get_info(const svg_index *idx, svg_index_info *out);
@@ -195,7 +200,7 @@ int  svg_index_build(const char *fasta, int gap, int memory_mb, int force_one_bl
 int  svg_index_build_mem(const char *const *names, const char *const *seqs, const uint64_t *lens,
                          uint32_t n_contigs, int gap, int memory_mb, int force_one_block,
                          int repeat_threshold, int device, const char *save_prefix, svg_index **out);
-/* Copy the index back to host arrays (any pointer may be NULL): bstart[buckets+1],
+/* Copy block 00 of the index back to host arrays (any pointer may be NULL): bstart[buckets+1],
  * keys[items], vals[items], values[array_values_bytes], chr_end[n_chromosomes]. */
 int  svg_index_export(const svg_index *idx, uint32_t *bstart, int16_t *keys, uint32_t *vals,
                       uint8_t *values, uint32_t *chr_end);

@@ -48,7 +48,7 @@
 #define JCW 17               /* JUNCTION_CONFIRM_WINDOW */
 
 /* ------------------------------------------------------------------ index */
-typedef struct {
+typedef struct svo_index {
 	uint32_t nb;
 	uint64_t items;
 	int gap, padding;
@@ -62,6 +62,7 @@ typedef struct {
 	uint32_t n_chr;
 	uint32_t *chr_end;
 	int borrowed;          /* arrays owned by the caller (svo_index_from_arrays) */
+	struct svo_index *next;   /* next block of a multi-block index (<prefix>.NN.b.*) */
 } svo_index;
 
 static int rd(FILE *fp, void *p, size_t n) { return fread(p, 1, n, fp) == n ? 0 : -1; }
@@ -69,17 +70,18 @@ static int rd(FILE *fp, void *p, size_t n) { return fread(p, 1, n, fp) == n ? 0 
 void svo_index_close(svo_index *ix)
 {
 	if (!ix) return;
+	svo_index_close(ix->next);
 	if (!ix->borrowed) { free(ix->bstart); free(ix->keys); free(ix->vals); free(ix->values); free(ix->chr_end); }
 	free(ix);
 }
 
-svo_index *svo_index_open(const char *prefix)
+static svo_index *open_block(const char *prefix, int block)
 {
 	char fn[4096];
 	svo_index *ix = calloc(1, sizeof(*ix));
 	FILE *fp;
 	char magic[8];
-	snprintf(fn, sizeof fn, "%s.00.b.tab", prefix);
+	snprintf(fn, sizeof fn, "%s.%02d.b.tab", prefix, block);
 	fp = fopen(fn, "rb");
 	if (!fp) { free(ix); return NULL; }
 	if (rd(fp, magic, 8) || memcmp(magic, "2subindx", 8)) goto bad;
@@ -117,7 +119,7 @@ svo_index *svo_index_open(const char *prefix)
 	}
 	fclose(fp);
 
-	snprintf(fn, sizeof fn, "%s.00.b.array", prefix);
+	snprintf(fn, sizeof fn, "%s.%02d.b.array", prefix, block);
 	fp = fopen(fn, "rb");
 	if (!fp) goto bad2;
 	if (rd(fp, &ix->start_point, 4) || rd(fp, &ix->length, 4)) goto bad;
@@ -149,6 +151,23 @@ bad:
 bad2:
 	svo_index_close(ix);
 	return NULL;
+}
+
+/* every block: gehash_load / gvindex_load per block (core.c:3553-3582) */
+svo_index *svo_index_open(const char *prefix)
+{
+	svo_index *first = open_block(prefix, 0), *last = first;
+	int k;
+	char fn[4096];
+	for (k = 1; first && k < 100; k++) {
+		FILE *fp;
+		snprintf(fn, sizeof fn, "%s.%02d.b.tab", prefix, k);
+		if (!(fp = fopen(fn, "rb"))) break;
+		fclose(fp);
+		if (!(last->next = open_block(prefix, k))) { svo_index_close(first); return NULL; }
+		last = last->next;
+	}
+	return first;
 }
 
 /* wrap caller-owned arrays of an index that was never written to disk (bench C3) */
@@ -384,6 +403,7 @@ typedef struct {
 	const svo_index *ix;
 	const svg_params *p;
 	int ends;
+	int stored;            /* a later block of a multi-block index: res/jres/bm hold the stored records */
 	char text[2][SVG_MAX_READ_LENGTH + 1];
 	int rl[2];
 	vtab_t vt[2];
@@ -801,9 +821,11 @@ static void vote_read(readctx *c)
 	int tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
 	uint32_t low = ix->start_base_offset, high = ix->start_base_offset + ix->length;
 	static __thread uint32_t shift_locs[TAB_ROWS * TAB_SPACE];
-	memset(c->res, 0, sizeof c->res);
-	memset(c->jres, 0, sizeof c->jres);
-	memset(c->bm, 0, sizeof c->bm);
+	if (!c->stored) {   /* later blocks start from the records the earlier ones left */
+		memset(c->res, 0, sizeof c->res);
+		memset(c->jres, 0, sizeof c->jres);
+		memset(c->bm, 0, sizeof c->bm);
+	}
 	c->applied[0] = c->applied[1] = 0;
 	for (strand = 0; strand < 2; strand++) {
 		int applied = 0;
@@ -858,6 +880,7 @@ typedef struct {
 	svg_subjunc_result *jout;
 	uint16_t *bm;
 	uint64_t next;
+	int stored;
 	pthread_mutex_t lock;
 	probe_stats st;
 } batch_t;
@@ -869,7 +892,7 @@ static void *worker(void *arg)
 	batch_t *b = arg;
 	readctx *c = malloc(sizeof(readctx));
 	int ends = b->r2 ? 2 : 1;
-	c->ix = b->ix; c->p = b->p; c->ends = ends;
+	c->ix = b->ix; c->p = b->p; c->ends = ends; c->stored = b->stored;
 	memset(&c->st, 0, sizeof c->st);
 	for (;;) {
 		uint64_t s, r, n = b->r1->n_reads;
@@ -889,6 +912,15 @@ static void *worker(void *arg)
 				c->rl[e] = len;
 				if (rev) revcomp(c->text[e], len);
 			}
+			if (c->stored)
+				for (e = 0; e < ends; e++) {
+					for (k = 0; k < b->p->multi_best; k++) {
+						size_t o = ((size_t)r * ends + e) * b->p->multi_best + k;
+						c->res[e][k] = b->out[o];
+						if (b->jout) c->jres[e][k] = b->jout[o];
+					}
+					if (b->bm) memcpy(c->bm[e], b->bm + ((size_t)r * ends + e) * SVG_BIG_MARGIN_WORDS, sizeof(uint16_t) * SVG_BIG_MARGIN_WORDS);
+				}
 			vote_read(c);
 			for (e = 0; e < ends; e++)
 				for (k = 0; k < b->p->multi_best; k++) {
@@ -916,20 +948,27 @@ int svo_vote_batch(const svo_index *ix, const svg_params *p, const svg_reads *r1
 	batch_t b;
 	pthread_t th[256];
 	int t;
+	const svo_index *first = ix;
 	if (!ix || !p || !r1 || !out) return SVG_E_ARG;
 	if (r2 && r2->n_reads != r1->n_reads) return SVG_E_ARG;
 	if (p->multi_best < 1 || p->multi_best > 3 || p->top_scores < 1 || p->top_scores > 9) return SVG_E_UNSUPPORTED;
 	if (p->max_vote_combinations > 11 || p->max_vote_simples < 1) return SVG_E_UNSUPPORTED;
 	if (p->do_breakpoint_detection && !jout) return SVG_E_ARG;
 	if (p->do_big_margin_filtering_for_junctions && !bm) return SVG_E_ARG;
-	memset(&b, 0, sizeof b);
-	b.ix = ix; b.p = p; b.r1 = r1; b.r2 = r2; b.out = out; b.jout = jout; b.bm = bm;
-	pthread_mutex_init(&b.lock, NULL);
 	if (threads < 1) threads = 1;
 	if (threads > 256) threads = 256;
-	for (t = 0; t < threads; t++) pthread_create(&th[t], NULL, worker, &b);
-	for (t = 0; t < threads; t++) pthread_join(th[t], NULL);
-	pthread_mutex_destroy(&b.lock);
-	if (stats3) { stats3[0] = b.st.probes; stats3[1] = b.st.bucket_items; stats3[2] = b.st.hits; }
+	if (stats3) stats3[0] = stats3[1] = stats3[2] = 0;
+	/* blocks in order over the whole batch, later ones merging into the stored records
+	 * (read_chunk_circles, core.c:3567-3613) */
+	for (; ix; ix = ix->next) {
+		memset(&b, 0, sizeof b);
+		b.ix = ix; b.p = p; b.r1 = r1; b.r2 = r2; b.out = out; b.jout = jout; b.bm = bm;
+		b.stored = ix != first;
+		pthread_mutex_init(&b.lock, NULL);
+		for (t = 0; t < threads; t++) pthread_create(&th[t], NULL, worker, &b);
+		for (t = 0; t < threads; t++) pthread_join(th[t], NULL);
+		pthread_mutex_destroy(&b.lock);
+		if (stats3) { stats3[0] += b.st.probes; stats3[1] += b.st.bucket_items; stats3[2] += b.st.hits; }
+	}
 	return 0;
 }

@@ -124,7 +124,8 @@ def params_default(program=PROGRAM_ALIGN, paired=False):
 
 
 def build_index(fasta, prefix, gap=3, memory_mb=8000, force_one_block=False, repeat_threshold=100):
-    """Format-exact subread-buildindex (single block): -F => gap=1, -B => force_one_block."""
+    """Format-exact subread-buildindex: -F => gap=1, -B => force_one_block, -M => memory_mb
+    (a genome over the -M budget is split into .NN blocks as the reference splits it)."""
     rc = lib().svg_build_index(str(fasta).encode(), str(prefix).encode(), gap, memory_mb,
                                1 if force_one_block else 0, repeat_threshold)
     _check(rc, "svg_build_index")
@@ -192,8 +193,12 @@ class VoteIndex:
                "svg_index_build_mem")
         return cls(_handle=h)
 
+    @property
+    def n_blocks(self):
+        return self.info.n_blocks
+
     def export(self):
-        """Host copy of the index arrays (dict usable by the oracle's from_arrays)."""
+        """Host copy of the index arrays of block 00 (dict usable by the oracle's from_arrays)."""
         i = self.info
         a = dict(buckets=i.buckets, items=i.items, gap=i.index_gap, padding=i.padding, length=i.array_length,
                  values_bytes=i.array_values_bytes, n_chr=i.n_chromosomes,

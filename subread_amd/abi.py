@@ -99,6 +99,7 @@ class SvgIndexInfo(ctypes.Structure):
         ("device_bytes", ctypes.c_uint64),
         ("device", ctypes.c_int32),
         ("array_values_bytes", ctypes.c_uint32),
+        ("n_blocks", ctypes.c_int32),
     ]
 
 

@@ -1,6 +1,6 @@
 /*
  * svg_build.c -- format-exact builder of the Subread base-space index
- * (<prefix>.00.b.tab / .00.b.array / .reads / .files / .log), single block.
+ * (<prefix>.NN.b.tab / .NN.b.array / .reads / .files / .log), one block or several.
  *
  * Replaces subread-buildindex (index-builder.c:1014-1306) for the one-block
  * case: the bytes of .tab/.array/.reads equal the reference's (md5 known
@@ -25,6 +25,7 @@
 #include <string.h>
 #include <stdint.h>
 #include <ctype.h>
+#include <unistd.h>
 #include <zlib.h>
 #include "subread_vote.h"
 #include "svg_internal.h"
@@ -202,8 +203,8 @@ uint64_t svg_items_budget(int gap, int memory_mb, int force_one_block)
 	return (uint32_t)(memory_mb * 1024.0 / 8.) * 1024;
 }
 
-int svg_write_tab(const char *prefix, uint32_t nb, uint64_t items, int gap, const uint32_t *bstart,
-                  const int16_t *keys, const uint32_t *vals)
+static int write_tab_block(const char *prefix, int block, uint32_t nb, uint64_t items, int gap, const uint32_t *bstart,
+                           const int16_t *keys, const uint32_t *vals)
 {
 	char fn[4096];
 	FILE *fp;
@@ -211,7 +212,7 @@ int svg_write_tab(const char *prefix, uint32_t nb, uint64_t items, int gap, cons
 	size_t bufsz = 1 << 24, bl = 0;
 	uint32_t c;
 	int rc = 0;
-	snprintf(fn, sizeof fn, "%s.00.b.tab", prefix);
+	snprintf(fn, sizeof fn, "%s.%02d.b.tab", prefix, block);
 	fp = fopen(fn, "wb");
 	if (!fp) { svg_set_error("cannot write '%s'", fn); return SVG_E_IO; }
 	buf = malloc(bufsz);
@@ -243,6 +244,25 @@ int svg_write_tab(const char *prefix, uint32_t nb, uint64_t items, int gap, cons
 	return rc;
 }
 
+int svg_write_tab(const char *prefix, uint32_t nb, uint64_t items, int gap, const uint32_t *bstart,
+                  const int16_t *keys, const uint32_t *vals)
+{
+	return write_tab_block(prefix, 0, nb, items, gap, bstart, keys, vals);
+}
+
+/* blocks a previous build into the same prefix left behind (build_gene_index, index-builder.c:181-187) */
+static void unlink_blocks_from(const char *prefix, int first)
+{
+	char fn[4096];
+	int i;
+	for (i = first; i < 100; i++) {
+		snprintf(fn, sizeof fn, "%s.%02d.b.tab", prefix, i);
+		unlink(fn);
+		snprintf(fn, sizeof fn, "%s.%02d.b.array", prefix, i);
+		unlink(fn);
+	}
+}
+
 uint8_t *svg_pack_array(const genome_t *g, const uint64_t *O, uint32_t *length_out, uint32_t *vbytes_out)
 {
 	uint32_t last = g->nctg - 1, c;
@@ -263,22 +283,27 @@ uint8_t *svg_pack_array(const genome_t *g, const uint64_t *O, uint32_t *length_o
 	return arr;
 }
 
-int svg_write_array_reads(const char *prefix, const genome_t *g, const uint64_t *O, int gap, uint64_t nwin,
-                          uint64_t items, uint32_t nb, const char *source)
+static int write_array_block(const char *prefix, int block, uint32_t start, uint32_t length, const uint8_t *arr, size_t vb)
 {
 	char fn[4096];
 	FILE *fp;
-	uint32_t c, length, vb, start = 0;
 	int rc = 0;
-	uint8_t *arr = svg_pack_array(g, O, &length, &vb);
-	if (!arr) { svg_set_error("out of memory packing .array"); return SVG_E_NOMEM; }
-	snprintf(fn, sizeof fn, "%s.00.b.array", prefix);
+	snprintf(fn, sizeof fn, "%s.%02d.b.array", prefix, block);
 	fp = fopen(fn, "wb");
-	if (!fp) { free(arr); svg_set_error("cannot write '%s'", fn); return SVG_E_IO; }
+	if (!fp) { svg_set_error("cannot write '%s'", fn); return SVG_E_IO; }
 	if (write_all(fp, &start, 4) || write_all(fp, &length, 4) || write_all(fp, arr, vb)) rc = SVG_E_IO;
-	fclose(fp);
-	free(arr);
-	if (rc) { svg_set_error("write error on '%s'", fn); return rc; }
+	if (fclose(fp)) rc = SVG_E_IO;
+	if (rc) svg_set_error("write error on '%s'", fn);
+	return rc;
+}
+
+/* .reads / .files / .log (the genome-wide files of any build) */
+static int write_reads_files(const char *prefix, const genome_t *g, const uint64_t *O, int gap, uint64_t nwin,
+                             uint64_t items, uint32_t nb, int nblocks, const char *source)
+{
+	char fn[4096];
+	FILE *fp;
+	uint32_t c;
 	snprintf(fn, sizeof fn, "%s.reads", prefix);
 	fp = fopen(fn, "wb");
 	if (!fp) { svg_set_error("cannot write '%s'", fn); return SVG_E_IO; }
@@ -290,18 +315,178 @@ int svg_write_array_reads(const char *prefix, const genome_t *g, const uint64_t 
 	snprintf(fn, sizeof fn, "%s.log", prefix);
 	fp = fopen(fn, "wb");
 	if (fp) {
-		fprintf(fp, "svg index: %u contigs, %llu windows, %llu items, %u buckets, gap %d\n", g->nctg,
-		        (unsigned long long)nwin, (unsigned long long)items, nb, gap);
+		fprintf(fp, "svg index: %u contigs, %llu windows, %llu items, %u buckets, gap %d, %d block%s\n", g->nctg,
+		        (unsigned long long)nwin, (unsigned long long)items, nb, gap, nblocks, nblocks > 1 ? "s" : "");
 		fclose(fp);
 	}
 	return 0;
+}
+
+int svg_write_array_reads(const char *prefix, const genome_t *g, const uint64_t *O, int gap, uint64_t nwin,
+                          uint64_t items, uint32_t nb, const char *source)
+{
+	uint32_t length, vb;
+	int rc;
+	uint8_t *arr = svg_pack_array(g, O, &length, &vb);
+	if (!arr) { svg_set_error("out of memory packing .array"); return SVG_E_NOMEM; }
+	rc = write_array_block(prefix, 0, 0, length, arr, vb);
+	free(arr);
+	if (rc) return rc;
+	unlink_blocks_from(prefix, 1);
+	return write_reads_files(prefix, g, O, gap, nwin, items, nb, 1, source);
+}
+
+/* sorted (key << 32 | pa) items -> bucket layout -> <prefix>.NN.b.tab (gehash_dump,
+ * sorted-hashtable.c:1689-1908): a stable counting sort by bucket keeps the key/pa order */
+static int tab_from_sorted(const char *prefix, int block, uint32_t nb, const uint64_t *items, uint64_t n, int gap)
+{
+	uint64_t i;
+	uint32_t c;
+	int rc;
+	uint32_t *bstart = calloc((size_t)nb + 1, sizeof(uint32_t));
+	int16_t *keys = malloc(2 * n + 2);
+	uint32_t *vals = malloc(4 * n + 4);
+	uint32_t *cur = malloc(sizeof(uint32_t) * nb);
+	if (!bstart || !keys || !vals || !cur) {
+		free(bstart); free(keys); free(vals); free(cur);
+		svg_set_error("out of memory laying out the table");
+		return SVG_E_NOMEM;
+	}
+	for (i = 0; i < n; i++) bstart[(uint32_t)(items[i] >> 32) % nb + 1]++;
+	for (c = 0; c < nb; c++) bstart[c + 1] += bstart[c];
+	memcpy(cur, bstart, sizeof(uint32_t) * nb);
+	for (i = 0; i < n; i++) {
+		uint32_t key = (uint32_t)(items[i] >> 32), pa = (uint32_t)items[i];
+		uint32_t b = key % nb, d = cur[b]++;
+		keys[d] = (int16_t)(key / nb);
+		vals[d] = ((key % 791) % 2 == 0) ? pa : ~pa;
+	}
+	free(cur);
+	rc = write_tab_block(prefix, block, nb, n, gap, bstart, keys, vals);
+	free(bstart); free(keys); free(vals);
+	return rc;
+}
+
+static inline uint32_t window_key(const char *b)
+{
+	uint32_t key = 0;
+	int k;
+	for (k = 0; k < 16; k++) key |= b2i(b[k]) << (30 - 2 * k);
+	return key;
+}
+
+/* is_1_greater_than_2: equal keys ascending by pos if key%791 even, else descending */
+static inline uint64_t window_item(uint32_t key, uint32_t pos)
+{
+	return ((uint64_t)key << 32) | (((key % 791) % 2 == 0) ? pos : ~pos);
+}
+
+static int is_repeat(const uint32_t *rep, uint64_t nrep, uint32_t key)
+{
+	uint64_t lo = 0, hi = nrep;
+	while (lo < hi) {
+		uint64_t m = (lo + hi) / 2;
+		if (rep[m] < key) lo = m + 1; else hi = m;
+	}
+	return lo < nrep && rep[lo] == key;
+}
+
+/*
+ * Multi-block build (build_gene_index, index-builder.c:257-357): windows are inserted in genome
+ * order; once a block holds `budget` items it is closed at the next window whose read_len (16 +
+ * distance from the contig start) is < 32 -- the block then restarts that contig from its first
+ * base -- or > MIN_READ_SPLICING (2,000,000) -- the next block then starts 1,999,974 bases back,
+ * so both hold the overlap.  Every block has its own .tab (same bucket count) and its own .array
+ * (start_point = the block's first window; the bases its windows and contig-end writes covered,
+ * gvindex_set / gvindex_dump, gene-value-index.c:135-187).
+ */
+typedef struct { uint32_t c; uint64_t a, b; int ends; } seg_t;
+typedef struct { uint64_t start, last_set, items; uint32_t s0, ns; } blk_t;
+
+#define MIN_READ_SPLICING 2000000u
+#define SPLICE_BACK (MIN_READ_SPLICING - 10 - (MIN_READ_SPLICING - 10) % 3 + 1 - 16)
+
+static int build_blocks(const char *prefix, const genome_t *g, const uint64_t *O, int gap, uint32_t nb, uint64_t budget,
+                        const uint32_t *rep, uint64_t nrep, int *nblocks_out)
+{
+	seg_t *seg = NULL;
+	blk_t *blk = NULL;
+	uint32_t nseg = 0, segcap = 0, nblk = 0, blkcap = 0, c, k;
+	int rc = 0;
+#define PUSH_SEG(C, A, B, E) do { \
+		if (nseg == segcap) { segcap = segcap ? 2 * segcap : 64; seg = realloc(seg, sizeof(seg_t) * segcap); } \
+		seg[nseg].c = (C); seg[nseg].a = (A); seg[nseg].b = (B); seg[nseg].ends = (E); nseg++; blk[nblk - 1].ns++; } while (0)
+#define NEW_BLOCK(S) do { \
+		if (nblk == blkcap) { blkcap = blkcap ? 2 * blkcap : 16; blk = realloc(blk, sizeof(blk_t) * blkcap); } \
+		blk[nblk].start = (S); blk[nblk].items = 0; blk[nblk].s0 = nseg; blk[nblk].ns = 0; blk[nblk].last_set = 0; nblk++; } while (0)
+	NEW_BLOCK(0);
+	for (c = 0; c < g->nctg; c++) {
+		const char *base = g->bases + g->ctg[c].start;
+		const uint64_t last = O[c] + (uint64_t)((g->ctg[c].len - 16) / gap) * gap;
+		uint64_t p = O[c], a = O[c];
+		while (p <= last) {
+			const uint64_t rl = 16 + p - O[c];
+			if (!is_repeat(rep, nrep, window_key(base + (p - O[c])))) blk[nblk - 1].items++;
+			if (blk[nblk - 1].items >= budget && (rl > MIN_READ_SPLICING || rl < 32)) {
+				PUSH_SEG(c, a, p, 0);
+				blk[nblk - 1].last_set = p;
+				if (nblk == 100) {   /* a budget far below MIN_READ_SPLICING items can cycle forever */
+					rc = SVG_E_UNSUPPORTED;
+					svg_set_error("more than 100 index blocks: raise memory_mb");
+					goto out;
+				}
+				p = rl < 32 ? O[c] : p - SPLICE_BACK;
+				NEW_BLOCK(p);
+				a = p;
+				continue;
+			}
+			p += gap;
+		}
+		PUSH_SEG(c, a, last, 1);
+		blk[nblk - 1].last_set = O[c] + g->ctg[c].len - 16;
+	}
+#undef PUSH_SEG
+#undef NEW_BLOCK
+	for (k = 0; k < nblk && !rc; k++) {
+		const blk_t *B = &blk[k];
+		uint64_t *items = malloc(sizeof(uint64_t) * (B->items + 1)), *tmp = malloc(sizeof(uint64_t) * (B->items + 1)), n = 0;
+		const uint64_t sbo = B->start - B->start % 4;
+		const uint32_t length = (uint32_t)(B->last_set + 16 - B->start + PAD);
+		const size_t vb = (size_t)((length + B->start - sbo) >> 2) + 1;
+		uint8_t *arr = calloc(vb + 8, 1);
+		uint32_t s;
+		if (!items || !tmp || !arr) { free(items); free(tmp); free(arr); rc = SVG_E_NOMEM; svg_set_error("out of memory (block %u)", k); break; }
+		for (s = B->s0; s < B->s0 + B->ns; s++) {
+			const seg_t *S = &seg[s];
+			const char *base = g->bases + g->ctg[S->c].start;
+			const uint64_t set_end = S->ends ? O[S->c] + g->ctg[S->c].len : S->b + 16;
+			uint64_t p;
+			for (p = S->a; p <= S->b; p += gap) {
+				uint32_t key = window_key(base + (p - O[S->c]));
+				if (!is_repeat(rep, nrep, key)) items[n++] = window_item(key, (uint32_t)p);
+			}
+			for (p = S->a; p < set_end; p++) arr[(p - sbo) >> 2] |= (uint8_t)(b2i(base[p - O[S->c]]) << (2 * (p & 3)));
+		}
+		radix64(items, tmp, n);
+		free(tmp);
+		rc = tab_from_sorted(prefix, (int)k, nb, items, n, gap);
+		free(items);
+		if (!rc) rc = write_array_block(prefix, (int)k, (uint32_t)B->start, length, arr, vb);
+		free(arr);
+	}
+	if (!rc) unlink_blocks_from(prefix, (int)nblk);
+	*nblocks_out = (int)nblk;
+out:
+	free(seg); free(blk);
+	return rc;
 }
 
 int svg_build_index(const char *fasta, const char *prefix, int gap, int memory_mb, int force_one_block, int repeat_threshold)
 {
 	genome_t g;
 	uint64_t *O = NULL, nwin = 0, i, nkeep = 0;
-	uint64_t *items = NULL, *tmp = NULL;
+	uint64_t *items = NULL, *tmp = NULL, nrep = 0, repcap = 0;
+	uint32_t *rep = NULL;
 	uint32_t c, nb;
 	uint64_t budget;
 	int rc = 0;
@@ -339,7 +524,8 @@ int svg_build_index(const char *fasta, const char *prefix, int gap, int memory_m
 		}
 	}
 	radix64(items, tmp, nwin);
-	/* drop keys occurring more than repeat_threshold times */
+	/* drop keys occurring more than repeat_threshold times (the repeated keys are kept, in order,
+	 * for a multi-block build) */
 	for (i = 0; i < nwin;) {
 		uint64_t j = i;
 		uint32_t key = (uint32_t)(items[i] >> 32);
@@ -347,40 +533,31 @@ int svg_build_index(const char *fasta, const char *prefix, int gap, int memory_m
 		if (j - i <= (uint64_t)repeat_threshold) {
 			uint64_t k;
 			for (k = i; k < j; k++) items[nkeep++] = items[k];
+		} else {
+			if (nrep == repcap) { repcap = repcap ? 2 * repcap : 1024; rep = realloc(rep, sizeof(uint32_t) * repcap); }
+			rep[nrep++] = key;
 		}
 		i = j;
 	}
-	if (!force_one_block && nkeep >= budget) { rc = SVG_E_UNSUPPORTED; svg_set_error("index would need more than one block; use force_one_block"); goto out; }
+	if (!force_one_block && nkeep >= budget) {
+		/* may still come out as one block: splits happen only near contig starts or deep in contigs */
+		int nblocks = 0;
+		free(items); items = NULL;
+		free(tmp); tmp = NULL;
+		rc = build_blocks(prefix, &g, O, gap, nb, budget, rep, nrep, &nblocks);
+		if (!rc) rc = write_reads_files(prefix, &g, O, gap, nwin, nkeep, nb, nblocks, fasta);
+		goto out;
+	}
 	if (nkeep > 0xffffffffull) { rc = SVG_E_UNSUPPORTED; svg_set_error("more than 2^32-1 items"); goto out; }
 
 	/* 6. stable counting sort by bucket (within a bucket, key order == key_hi order) */
-	{
-		uint32_t *bstart = calloc((size_t)nb + 1, sizeof(uint32_t));
-		int16_t *keys = malloc(2 * nkeep + 2);
-		uint32_t *vals = malloc(4 * nkeep + 4);
-		if (!bstart || !keys || !vals) { free(bstart); free(keys); free(vals); rc = SVG_E_NOMEM; goto out; }
-		for (i = 0; i < nkeep; i++) bstart[(uint32_t)(items[i] >> 32) % nb + 1]++;
-		for (c = 0; c < nb; c++) bstart[c + 1] += bstart[c];
-		{
-			uint32_t *cur = malloc(sizeof(uint32_t) * nb);
-			memcpy(cur, bstart, sizeof(uint32_t) * nb);
-			for (i = 0; i < nkeep; i++) {
-				uint32_t key = (uint32_t)(items[i] >> 32), pa = (uint32_t)items[i];
-				uint32_t b = key % nb, d = cur[b]++;
-				keys[d] = (int16_t)(key / nb);
-				vals[d] = ((key % 791) % 2 == 0) ? pa : ~pa;
-			}
-			free(cur);
-		}
-		free(items); items = NULL;
-		free(tmp); tmp = NULL;
-		rc = svg_write_tab(prefix, nb, nkeep, gap, bstart, keys, vals);
-		free(bstart); free(keys); free(vals);
-		if (rc) goto out;
-	}
+	free(tmp); tmp = NULL;
+	rc = tab_from_sorted(prefix, 0, nb, items, nkeep, gap);
+	free(items); items = NULL;
+	if (rc) goto out;
 	rc = svg_write_array_reads(prefix, &g, O, gap, nwin, nkeep, nb, fasta);
 out:
-	free(items); free(tmp); free(O);
+	free(items); free(tmp); free(O); free(rep);
 	svg_genome_free(&g);
 	return rc;
 }

@@ -34,6 +34,8 @@ struct DevIndex {
 	const uint4 *bcode;
 };
 
+#define SVG_MAX_BLOCKS 64
+
 struct svg_index {
 	int device;
 	hipStream_t stream;
@@ -78,6 +80,11 @@ struct svg_index {
 	int last_pending;
 	// host-buffer entry points (svg_io.hip): record compaction slots, pinned staging, worker pool
 	struct svg_hostio *io;
+	// multi-block indexes (<prefix>.NN.b.tab, NN = 00, 01, ...): this handle holds block 0; blocks
+	// 1.. are handles of their own, voted after it in order with stored = 1
+	int nblocks;
+	struct svg_index *blk[SVG_MAX_BLOCKS];
+	int stored;
 };
 
 #define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) { svg_set_error("HIP error %s at %s:%d", hipGetErrorString(_e), __FILE__, __LINE__); return SVG_E_DEVICE; } } while (0)
@@ -129,6 +136,7 @@ struct KParams {
 	const uint32_t *idx;      // NULL: reads 0..n_reads-1; else the reads idx[0..*idx_count) (deferred by lane_kernel)
 	const uint32_t *idx_count;
 	uint32_t *work;           // indirect mode: zeroed work counter (waves grab deferred reads dynamically)
+	int stored;               // records already hold earlier index blocks' results (multi-block, block > 0)
 	uint32_t *err;            // sticky device error word (svg_device_status): bit 0 = a read needs more
 	                          // probes than the announced read-length bound provides, bit 1 = a read
 	                          // longer than the kernel variant's text buffer; such reads get zero records

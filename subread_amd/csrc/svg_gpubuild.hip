@@ -186,7 +186,7 @@ static int build_from_genome(svg_genome *g, int gap, int memory_mb, int force_on
 			if (kept64 > 0xffffffffull) { rc = SVG_E_UNSUPPORTED; svg_set_error("more than 2^32-1 items"); goto fail; }
 		}
 	}
-	if (!force_one_block && items >= budget) { rc = SVG_E_UNSUPPORTED; svg_set_error("index would need more than one block; use force_one_block"); goto fail; }
+	if (!force_one_block && items >= budget) { rc = SVG_E_UNSUPPORTED; svg_set_error("index would need more than one block: use force_one_block, or svg_build_index + svg_index_open for a multi-block index"); goto fail; }
 	GCHK(hipMalloc(&h->d_keys, 2 * items + 64));
 	GCHK(hipMalloc(&h->d_vals, 4 * items + 64));
 	h->device_bytes += 6 * items + 128;

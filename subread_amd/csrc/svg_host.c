@@ -168,22 +168,33 @@ static int load_tab(const char *fn, svg_host_index *ix, int threads)
 	return 0;
 }
 
-int svg_host_index_load(const char *prefix, svg_host_index *ix, int threads)
+/* index blocks <prefix>.00.b.tab, .01.b.tab, ... (load_global_context counts them the same
+ * way, core.c:4193-4205) */
+int svg_index_count_blocks(const char *prefix)
+{
+	char fn[4096];
+	int n = 0;
+	for (;;) {
+		snprintf(fn, sizeof fn, "%s.%02d.b.tab", prefix, n);
+		if (access(fn, F_OK) != 0) break;
+		n++;
+	}
+	return n;
+}
+
+/* one block: <prefix>.NN.b.tab and .NN.b.array (gehash_load / gvindex_load of read_chunk_circles,
+ * core.c:3553-3582), plus the chromosome table of <prefix>.reads */
+int svg_host_index_load_block(const char *prefix, int block, svg_host_index *ix, int threads)
 {
 	char fn[4096];
 	FILE *fp;
 	int rc;
 	memset(ix, 0, sizeof *ix);
-	snprintf(fn, sizeof fn, "%s.00.b.tab", prefix);
-	{
-		char fn1[4096];
-		snprintf(fn1, sizeof fn1, "%s.01.b.tab", prefix);
-		if (access(fn1, F_OK) == 0) { svg_set_error("multi-block index '%s' is outside the drop-in contract", prefix); return SVG_E_UNSUPPORTED; }
-	}
+	snprintf(fn, sizeof fn, "%s.%02d.b.tab", prefix, block);
 	rc = load_tab(fn, ix, threads);
 	if (rc) { svg_host_index_free(ix); return rc; }
 
-	snprintf(fn, sizeof fn, "%s.00.b.array", prefix);
+	snprintf(fn, sizeof fn, "%s.%02d.b.array", prefix, block);
 	fp = fopen(fn, "rb");
 	if (!fp) { svg_host_index_free(ix); svg_set_error("'%s' not found", fn); return SVG_E_IO; }
 	if (fread(&ix->start_point, 4, 1, fp) != 1 || fread(&ix->length, 4, 1, fp) != 1) {
@@ -227,4 +238,9 @@ int svg_host_index_load(const char *prefix, svg_host_index *ix, int threads)
 	fclose(fp);
 	if (!ix->n_chr) { svg_host_index_free(ix); svg_set_error("'%s' is empty", fn); return SVG_E_FORMAT; }
 	return 0;
+}
+
+int svg_host_index_load(const char *prefix, svg_host_index *ix, int threads)
+{
+	return svg_host_index_load_block(prefix, 0, ix, threads);
 }

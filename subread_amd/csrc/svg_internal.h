@@ -35,6 +35,8 @@ typedef struct svg_host_index {
 } svg_host_index;
 
 int  svg_host_index_load(const char *prefix, svg_host_index *out, int threads);
+int  svg_host_index_load_block(const char *prefix, int block, svg_host_index *out, int threads);
+int  svg_index_count_blocks(const char *prefix);
 void svg_host_index_free(svg_host_index *ix);
 
 uint32_t svg_bucket_count(uint64_t expected_items, int gap);

@@ -458,7 +458,12 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	const uint64_t nsub = (n + sub - 1) / sub;
 	hipStream_t st = h->stream;
 	if (h->last_pending) HIPCHK(hipStreamWaitEvent(st, h->ev_last, 0));
-	if (h->stats_on) HIPCHK(hipMemsetAsync(h->d_stats, 0, 32 * sizeof(unsigned long long), st));
+	for (int k = 0; k < h->nblocks; k++) {
+		svg_index *bk = k ? h->blk[k] : h;
+		bk->stats_on = h->stats_on;
+		if (bk->last_pending && k) HIPCHK(hipStreamWaitEvent(st, bk->ev_last, 0));
+		if (h->stats_on) HIPCHK(hipMemsetAsync(bk->d_stats, 0, 32 * sizeof(unsigned long long), st));
+	}
 
 	// SVG_PIPE_DEBUG=1: where the host thread waits (seconds per batch)
 	const bool dbg = getenv("SVG_PIPE_DEBUG") != NULL;
@@ -641,11 +646,24 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		                           jo ? (svg_subjunc_result *)(dout + o_j) : NULL, bmo ? (uint16_t *)(dout + o_bm) : NULL, &job)))
 			break;
 		if (packed && !sjm) set_packed(job, pk, ends, b);
-		const bool overlap = job.overlap_mode && nsub > 1 && m <= job.chunk;
+		// a multi-block index votes its blocks in order on one stream (each later block merges with
+		// the records the earlier ones left)
+		const bool overlap = job.overlap_mode && nsub > 1 && m <= job.chunk && h->nblocks < 2;
 		overlap_any = overlap_any || overlap;
 		hipStream_t st2 = overlap ? h->stream2 : st;
 		for (uint64_t c0 = 0; c0 < m && !rc; c0 += job.chunk)   // one chunk unless reads are long
 			rc = svg_vote_chunk(h, &job, c0, m - c0 < job.chunk ? m - c0 : job.chunk, s, st, st2);
+		for (int k = 1; k < h->nblocks && !rc; k++) {
+			svg_index *bk = h->blk[k];
+			bk->max_read_len = U.maxlen;
+			VoteJob jk;
+			if ((rc = svg_vote_prepare(bk, p, &dr[0], pe ? &dr[1] : NULL, (svg_mapping_result *)dout,
+			                           jo ? (svg_subjunc_result *)(dout + o_j) : NULL, bmo ? (uint16_t *)(dout + o_bm) : NULL, &jk)))
+				break;
+			if (packed && !sjm) set_packed(jk, pk, ends, b);
+			for (uint64_t c0 = 0; c0 < m && !rc; c0 += jk.chunk)
+				rc = svg_vote_chunk(bk, &jk, c0, m - c0 < jk.chunk ? m - c0 : jk.chunk, 0, st, st);
+		}
 		if (rc) break;
 		if (dbg) w_vote += now() - tu;
 		// ---- compaction into compact slot s3 (free once sub-batch i-3's download is done)
@@ -698,13 +716,17 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		return SVG_E_DEVICE;
 	}
 	if (h->stats_on) {
-		unsigned long long sv[5];
-		HIPCHK(hipMemcpy(sv, h->d_stats, sizeof sv, hipMemcpyDeviceToHost));
-		h->last_stats.probes = sv[0];
-		h->last_stats.bucket_items = sv[1];
-		h->last_stats.hits = sv[2];
-		h->last_stats.results = sv[3];
-		h->last_stats.deferred = sv[4];
+		svg_batch_stats acc = {};
+		for (int k = 0; k < h->nblocks; k++) {
+			unsigned long long sv[5];
+			HIPCHK(hipMemcpy(sv, (k ? h->blk[k] : h)->d_stats, sizeof sv, hipMemcpyDeviceToHost));
+			acc.probes += sv[0];
+			acc.bucket_items += sv[1];
+			acc.hits += sv[2];
+			acc.results = sv[3];   // the last block's records are the final ones
+			acc.deferred += sv[4];
+		}
+		h->last_stats = acc;
 	}
 	return svg_device_status(h);
 }

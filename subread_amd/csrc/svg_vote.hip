@@ -453,6 +453,7 @@ struct Wave {
 				const int m = (int)cn;
 				unsigned long long serial = m == 64 ? ~0ull : ((1ull << m) - 1ull);
 				if (round == 0 && kp->ii_end == 5 && m >= 8) serial = batch_create<E>(kvv, kov, m, high_b);
+				if constexpr (!SJ) STAMP(6);   // diagnostics: batch mode (align variants; SJ uses 6 for junctions)
 				if (kp->stats) { st_batch += (unsigned long long)(m - __popcll(serial)); st_serial += (unsigned long long)__popcll(serial); }
 				while (serial) {
 					const int j = __ffsll((long long)serial) - 1;
@@ -1260,9 +1261,23 @@ struct Wave {
 			}
 		}
 		for (int e = 0; e < ENDS; e++) {
-			for (int i = 0; i < 3; i++) rec_zero(L->res[e][i]);
-			if (lane < 12) L->jres[e][lane / 4][lane % 4] = 0;
-			if (lane < 10) L->bm[e][lane] = 0;
+			if (kp->stored) {
+				// multi-block index, block > 0: the bigtable already holds the previous blocks'
+				// results, and top-K merges this block's table with them (core.c:3567-3613)
+				const uint64_t q = (r * ENDS + e) * (uint64_t)p.multi_best;
+				const uint32_t *src = (const uint32_t *)(kp->out + q * 68);
+				if (lane < 51) L->res[e][lane / 17][lane % 17] = lane < 17 * p.multi_best ? src[lane] : 0u;
+				if constexpr (SJ) {
+					const uint32_t *js = kp->jout ? (const uint32_t *)(kp->jout + q * 16) : NULL;
+					const uint16_t *bs = kp->bm_out ? kp->bm_out + (r * ENDS + e) * (uint64_t)SVG_BIG_MARGIN_WORDS : NULL;
+					if (lane < 12) L->jres[e][lane / 4][lane % 4] = js && lane < 4 * p.multi_best ? js[lane] : 0u;
+					if (lane < 10) L->bm[e][lane] = bs && lane < SVG_BIG_MARGIN_WORDS ? bs[lane] : (uint16_t)0;
+				}
+			} else {
+				for (int i = 0; i < 3; i++) rec_zero(L->res[e][i]);
+				if (lane < 12) L->jres[e][lane / 4][lane % 4] = 0;
+				if (lane < 10) L->bm[e][lane] = 0;
+			}
 		}
 		wsync();
 		STAMP(0);
@@ -2049,6 +2064,7 @@ int svg_index_finish_device(svg_index *h)
 {
 	svg_host_index *x = &h->host;
 	int rc;
+	h->nblocks = 1;
 	HIPCHK(hipSetDevice(h->device));
 	if ((rc = dmalloc(h, &h->d_values, (size_t)x->values_bytes + 64)) || (rc = dmalloc(h, &h->d_chr, 4 * (size_t)x->n_chr + 64)))
 		return rc;
@@ -2151,17 +2167,13 @@ int svg_index_finish_device(svg_index *h)
 	return 0;
 }
 
-extern "C" int svg_index_open(const char *prefix, int device, svg_index **out)
+static int index_open_block(const char *prefix, int block, int device, svg_index **out)
 {
-	if (!prefix || !out) { svg_set_error("svg_index_open: NULL argument"); return SVG_E_ARG; }
 	*out = NULL;
-	int ndev = 0;
-	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { svg_set_error("no HIP device visible"); return SVG_E_DEVICE; }
-	if (device < 0 || device >= ndev) { svg_set_error("device %d out of range (%d visible)", device, ndev); return SVG_E_ARG; }
-	HIPCHK(hipSetDevice(device));
 	svg_index *h = (svg_index *)calloc(1, sizeof(svg_index));
 	h->device = device;
-	int rc = svg_host_index_load(prefix, &h->host, 16);
+	h->nblocks = 1;
+	int rc = svg_host_index_load_block(prefix, block, &h->host, 16);
 	if (rc) { free(h); return rc; }
 	svg_host_index *x = &h->host;
 	if ((rc = dmalloc(h, &h->d_bstart, 4 * ((size_t)x->nb + 1))) || (rc = dmalloc(h, &h->d_keys, 2 * x->items + 64)) ||
@@ -2185,6 +2197,32 @@ extern "C" int svg_index_open(const char *prefix, int device, svg_index **out)
 	return 0;
 }
 
+extern "C" int svg_index_open(const char *prefix, int device, svg_index **out)
+{
+	if (!prefix || !out) { svg_set_error("svg_index_open: NULL argument"); return SVG_E_ARG; }
+	*out = NULL;
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { svg_set_error("no HIP device visible"); return SVG_E_DEVICE; }
+	if (device < 0 || device >= ndev) { svg_set_error("device %d out of range (%d visible)", device, ndev); return SVG_E_ARG; }
+	HIPCHK(hipSetDevice(device));
+	const int nb = svg_index_count_blocks(prefix);
+	if (nb < 1) { svg_set_error("index table '%s.00.b.tab' not found", prefix); return SVG_E_IO; }
+	if (nb > SVG_MAX_BLOCKS) { svg_set_error("%d index blocks (at most %d)", nb, SVG_MAX_BLOCKS); return SVG_E_UNSUPPORTED; }
+	svg_index *h;
+	int rc = index_open_block(prefix, 0, device, &h);
+	if (rc) return rc;
+	// every block stays resident in HBM (a human index is ~18 GB in all); the vote runs them in order
+	for (int k = 1; k < nb; k++) {
+		if ((rc = index_open_block(prefix, k, device, &h->blk[k]))) { svg_index_close(h); return rc; }
+		h->blk[k]->stored = 1;
+		h->device_bytes += h->blk[k]->device_bytes;
+		h->nblocks = k + 1;
+	}
+	h->nblocks = nb;
+	*out = h;
+	return 0;
+}
+
 extern "C" int svg_index_export(const svg_index *h, uint32_t *bstart, int16_t *keys, uint32_t *vals, uint8_t *values,
                                 uint32_t *chr_end)
 {
@@ -2201,6 +2239,7 @@ extern "C" int svg_index_export(const svg_index *h, uint32_t *bstart, int16_t *k
 extern "C" void svg_index_close(svg_index *h)
 {
 	if (!h) return;
+	for (int k = 1; k < h->nblocks && k < SVG_MAX_BLOCKS; k++) svg_index_close(h->blk[k]);
 	hipSetDevice(h->device);
 	if (h->stream) hipStreamSynchronize(h->stream);
 	if (h->stream2) hipStreamSynchronize(h->stream2);
@@ -2253,6 +2292,7 @@ extern "C" int svg_index_get_info(const svg_index *h, svg_index_info *o)
 	o->device_bytes = h->device_bytes;
 	o->device = h->device;
 	o->array_values_bytes = h->host.values_bytes;
+	o->n_blocks = h->nblocks > 1 ? h->nblocks : 1;
 	return 0;
 }
 
@@ -2291,6 +2331,26 @@ extern "C" int svg_set_timing(svg_index *h, int enable)
 	}
 	h->timing = enable ? 1 : 0;
 	for (int k = 0; k < 4; k++) { h->tn[k] = 0; h->tcount[k] = 0; h->tms[k] = 0.0; }
+	for (int k = 1; k < h->nblocks; k++) {
+		int rc = svg_set_timing(h->blk[k], enable);
+		if (rc) return rc;
+	}
+	return 0;
+}
+
+// fold every block's pending events; per-kind totals over the blocks
+static int timing_total(svg_index *h, double ms[4], int launches[4])
+{
+	for (int k = 0; k < 4; k++) { ms[k] = 0.0; launches[k] = 0; }
+	for (int b = 0; b < h->nblocks; b++) {
+		svg_index *x = b ? h->blk[b] : h;
+		for (int k = 0; k < 4; k++) {
+			int rc = timing_fold(x, k);
+			if (rc) return rc;
+			ms[k] += x->tms[k];
+			launches[k] += x->tcount[k];
+		}
+	}
 	return 0;
 }
 
@@ -2300,12 +2360,15 @@ extern "C" int svg_get_timing(svg_index *h, double *probe_ms, double *vote_ms, i
 {
 	if (!h) { svg_set_error("svg_get_timing: NULL handle"); return SVG_E_ARG; }
 	HIPCHK(hipSetDevice(h->device));
-	for (int k = 0; k < 4; k++) { int rc = timing_fold(h, k); if (rc) return rc; }
+	double ms[4];
+	int n[4];
+	int rc = timing_total(h, ms, n);
+	if (rc) return rc;
 	// vote = everything after the probe kernel (gather, lane and the wave kernel)
-	if (probe_ms) *probe_ms = h->tms[0];
-	if (vote_ms) *vote_ms = h->tms[1] + h->tms[2] + h->tms[3];
-	if (probe_launches) *probe_launches = h->tcount[0];
-	if (vote_launches) *vote_launches = h->tcount[1];
+	if (probe_ms) *probe_ms = ms[0];
+	if (vote_ms) *vote_ms = ms[1] + ms[2] + ms[3];
+	if (probe_launches) *probe_launches = n[0];
+	if (vote_launches) *vote_launches = n[1];
 	return 0;
 }
 
@@ -2313,13 +2376,7 @@ extern "C" int svg_get_kernel_timing(svg_index *h, double ms[4], int launches[4]
 {
 	if (!h || !ms || !launches) { svg_set_error("svg_get_kernel_timing: NULL argument"); return SVG_E_ARG; }
 	HIPCHK(hipSetDevice(h->device));
-	for (int k = 0; k < 4; k++) {
-		int rc = timing_fold(h, k);
-		if (rc) return rc;
-		ms[k] = h->tms[k];
-		launches[k] = h->tcount[k];
-	}
-	return 0;
+	return timing_total(h, ms, launches);
 }
 
 extern "C" int svg_set_stats(svg_index *h, int enable)
@@ -2347,9 +2404,15 @@ extern "C" int svg_device_status(svg_index *h)
 	HIPCHK(hipSetDevice(h->device));
 	if (h->last_pending) HIPCHK(hipEventSynchronize(h->ev_last));
 	uint32_t e = 0;
-	HIPCHK(hipMemcpy(&e, h->d_err, 4, hipMemcpyDeviceToHost));
+	for (int k = 0; k < h->nblocks; k++) {
+		svg_index *b = k ? h->blk[k] : h;
+		if (k && b->last_pending) HIPCHK(hipEventSynchronize(b->ev_last));
+		uint32_t eb = 0;
+		HIPCHK(hipMemcpy(&eb, b->d_err, 4, hipMemcpyDeviceToHost));
+		if (eb) HIPCHK(hipMemset(b->d_err, 0, 4));
+		e |= eb;
+	}
 	if (!e) return 0;
-	HIPCHK(hipMemset(h->d_err, 0, 4));
 	if (e & 1u) svg_set_error("a read needs more subread probes than the read-length bound of svg_set_max_read_length "
 	                          "(%d) provides; its records were zeroed", h->max_read_len);
 	else svg_set_error("a read is longer than the kernel variant's text buffer; its records were zeroed");
@@ -2532,7 +2595,9 @@ int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, con
 	pp.stats = kp.stats;
 	// align mode, reads <= 160 bp: lane-per-read (SE) / lane-per-pair (PE) fast path
 	// (svg_lane.hip), probe records in SoA layout
-	job->lane = svg_lane_eligible(h, p, r2 != NULL, job->sj) != 0 && (!r2 || nps <= 10) && (!job->sj || nps <= 14);
+	job->lane = svg_lane_eligible(h, p, r2 != NULL, job->sj) != 0 && (!r2 || nps <= 10) && (!job->sj || nps <= 14) &&
+	            !h->stored;   // later blocks of a multi-block index merge with stored records: wave kernel
+	kp.stored = h->stored;
 	pp.soa = job->lane ? 1 : 0;
 	pp.window = h->dix.nb >= 131073u && !getenv("SVG_NO_WINDOW");   // key_hi <= 32767: int16 order == key order
 	{ const char *e = getenv("SVG_PROBE_MAP"); pp.readmajor = !(e && e[0] == '0'); }
@@ -2703,10 +2768,40 @@ static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads 
 	return 0;
 }
 
+// multi-block index: block 0 (this handle), then blocks 1.. in order on the same stream, each
+// merging with the records the previous blocks left (read_chunk_circles, core.c:3567-3613)
+static int vote_blocks(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                       const svg_packed_reads *pk, svg_mapping_result *out, svg_subjunc_result *jout,
+                       uint16_t *big_margin, void *stream)
+{
+	int rc = vote_batch_device(h, p, r1, r2, pk, out, jout, big_margin, stream);
+	if (rc || h->nblocks < 2) return rc;
+	svg_batch_stats acc = h->last_stats;
+	void *st = stream ? stream : (void *)h->stream;
+	for (int k = 1; k < h->nblocks && !rc; k++) {
+		svg_index *b = h->blk[k];
+		b->max_read_len = h->max_read_len;
+		b->stats_on = h->stats_on;
+		rc = vote_batch_device(b, p, r1, r2, pk, out, jout, big_margin, st);
+		if (!rc && h->stats_on) {
+			acc.probes += b->last_stats.probes; acc.bucket_items += b->last_stats.bucket_items;
+			acc.hits += b->last_stats.hits; acc.results = b->last_stats.results;
+			acc.deferred += b->last_stats.deferred;
+		}
+	}
+	if (h->stats_on) h->last_stats = acc;
+	// later calls on this handle wait for the last block's work
+	if (!rc) {
+		HIPCHK(hipEventRecord(h->ev_last, (hipStream_t)st));
+		h->last_pending = 1;
+	}
+	return rc;
+}
+
 extern "C" int svg_vote_batch_device(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
                                      svg_mapping_result *out, svg_subjunc_result *jout, uint16_t *big_margin, void *stream)
 {
-	return vote_batch_device(h, p, r1, r2, NULL, out, jout, big_margin, stream);
+	return vote_blocks(h, p, r1, r2, NULL, out, jout, big_margin, stream);
 }
 
 // align mode from 2-bit packed device reads: r1/r2 carry the lengths, pk[e] the codes
@@ -2714,5 +2809,5 @@ int svg_vote_batch_device_packed(svg_index *h, const svg_params *p, const svg_re
                                  const svg_packed_reads *pk, svg_mapping_result *out, svg_subjunc_result *jout,
                                  uint16_t *big_margin, hipStream_t stream)
 {
-	return vote_batch_device(h, p, r1, r2, pk, out, jout, big_margin, (void *)stream);
+	return vote_blocks(h, p, r1, r2, pk, out, jout, big_margin, (void *)stream);
 }

@@ -4,6 +4,7 @@ import gzip
 import hashlib
 import json
 import os
+import re
 import subprocess
 
 import numpy as np
@@ -43,6 +44,39 @@ def md5(p):
     return h.hexdigest()
 
 
+# seeded synthetic genomes: lengths, seed (repeats 2500 copies of 300-bp elements, 16 families, 4%)
+SYNTH_GENOMES = {
+    "synth4242": ([300000, 250000, 17, 200000, 120000], 4242),
+    # one 3 Mbp contig: a -M 17 / -M 6 build splits it deep inside (read_len > MIN_READ_SPLICING),
+    # so consecutive blocks overlap by ~2 Mbp
+    "long777": ([3000000, 150000, 900000], 777),
+}
+
+
+def synth_genome(gname):
+    from subread_amd.sim import random_genome
+    lengths, seed = SYNTH_GENOMES[gname]
+    return random_genome(lengths, seed, repeats=(2500, 300, 16, 0.04))
+
+
+def index_recipe(key):
+    """'<genome>_<mode>' -> (genome, gap, memory_mb, force_one_block).  full = -F -B -M 100,
+    gapped = the defaults (-M 8000), fullM<n> / gappedM<n> = -F -M <n> / -M <n> (multi-block)."""
+    gname, mode = key.rsplit("_", 1)
+    if mode == "full":
+        return gname, 1, 100, True
+    if mode == "gapped":
+        return gname, 3, 8000, False
+    m = re.fullmatch(r"(full|gapped)M(\d+)", mode)
+    if not m:
+        raise KeyError(key)
+    return gname, 1 if m.group(1) == "full" else 3, int(m.group(2)), False
+
+
+def is_multi_block_key(key):
+    return "M" in key.rsplit("_", 1)[1]
+
+
 class IndexCache:
     """Builds the fixture indexes with OUR builder and checks them against the
     reference's md5 known answers before anything votes on them."""
@@ -58,12 +92,10 @@ class IndexCache:
                 with gzip.open(os.path.join(GOLD, "chr901.fa.gz"), "rb") as f, open(path, "wb") as o:
                     o.write(f.read())
             return path
-        if gname == "synth4242":
-            from subread_amd.sim import random_genome
-            path = os.path.join(self.root, "synth4242.fa")
+        if gname in SYNTH_GENOMES:
+            path = os.path.join(self.root, gname + ".fa")
             if not os.path.exists(path):
-                random_genome([300000, 250000, 17, 200000, 120000], 4242,
-                              repeats=(2500, 300, 16, 0.04)).write_fasta(path)
+                synth_genome(gname).write_fasta(path)
             return path
         raise KeyError(gname)
 
@@ -71,13 +103,10 @@ class IndexCache:
         if key in self.built:
             return self.built[key]
         import subread_amd as sa
-        gname, mode = key.rsplit("_", 1)
+        gname, gap, memory_mb, force = index_recipe(key)
         fa = self.genome_fasta(gname)
         pre = os.path.join(self.root, key)
-        if mode == "full":
-            sa.build_index(fa, pre, gap=1, memory_mb=100, force_one_block=True)
-        else:
-            sa.build_index(fa, pre, gap=3, memory_mb=8000, force_one_block=False)
+        sa.build_index(fa, pre, gap=gap, memory_mb=memory_mb, force_one_block=force)
         want = index_md5()["md5"][key]
         for suf, m in want.items():
             got = md5(pre + suf)

@@ -13,6 +13,7 @@ test/subread-align/data/test-err-mut-r{1,2}.fq.gz,
 test/subjunc/data/junction-reads-{A,B}.fq) plus seeded synthetic reads made here.
 The fixtures are data (inputs + expected outputs); no reference source is stored.
 """
+import glob
 import gzip
 import hashlib
 import json
@@ -28,7 +29,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 from subread_amd.abi import (MAPPING_DTYPE, SUBJUNC_DTYPE, ReadBatch, read_fastq, default_params,  # noqa: E402
                              PROGRAM_ALIGN, PROGRAM_SUBJUNC)
-from subread_amd.sim import Genome, random_genome, write_fastq  # noqa: E402
+from subread_amd.sim import Genome, write_fastq  # noqa: E402
+from tests.common import SYNTH_GENOMES, index_recipe, synth_genome  # noqa: E402
 
 REF = "/root/reference"
 REFBIN = os.path.join(ROOT, "oracle", "_ref")
@@ -41,12 +43,16 @@ def md5(p):
     return hashlib.md5(open(p, "rb").read()).hexdigest()
 
 
-def build_ref_index(fasta, prefix, full):
-    args = [REFBIN + "/subread-buildindex", "-o", prefix]
-    if full:
-        args += ["-F", "-B", "-M", "100"]
+def build_ref_index(fasta, prefix, key):
+    _, gap, memory_mb, force = index_recipe(key)
+    args = [REFBIN + "/subread-buildindex", "-o", prefix, "-M", str(memory_mb)]
+    if gap == 1:
+        args += ["-F"]
+    if force:
+        args += ["-B"]
     subprocess.run(args + [fasta], check=True, capture_output=True)
-    return {s: md5(prefix + s) for s in [".00.b.tab", ".00.b.array", ".reads"]}
+    files = sorted(os.path.basename(p)[len(os.path.basename(prefix)):] for p in glob.glob(prefix + ".[0-9][0-9].b.*"))
+    return {s: md5(prefix + s) for s in files + [".reads"]}
 
 
 def run_ref(prog, prefix, f1, f2, dump, extra=()):
@@ -125,6 +131,9 @@ def save_case(name, prog, paired, index, params_over, r1, r2, raw, ends, note):
     print("case", name, "reads", n, "bytes/read", per)
 
 
+from subread_amd.sim import simulate_spliced_reads  # noqa: E402
+
+
 def main():
     tmp = tempfile.mkdtemp(prefix="svg_gold_")
     try:
@@ -134,22 +143,30 @@ def main():
         with gzip.open(os.path.join(GOLD, "chr901.fa.gz"), "wb", compresslevel=9) as f:
             f.write(fa)
         chr901 = REF + "/test/chr901.fa"
-        synth = random_genome([300000, 250000, 17, 200000, 120000], 4242, repeats=(2500, 300, 16, 0.04))
-        synth_fa = os.path.join(tmp, "synth.fa")
-        synth.write_fasta(synth_fa)
+        synth = synth_genome("synth4242")
+        long777 = synth_genome("long777")
+        gfas = {"chr901": chr901}
+        for gname, g in (("synth4242", synth), ("long777", long777)):
+            gfas[gname] = os.path.join(tmp, gname + ".fa")
+            g.write_fasta(gfas[gname])
         md5s = {}
         idx = {}
-        for gname, gfa in [("chr901", chr901), ("synth4242", synth_fa)]:
-            for full in (True, False):
-                key = "%s_%s" % (gname, "full" if full else "gapped")
-                pre = os.path.join(tmp, key)
-                md5s[key] = build_ref_index(gfa, pre, full)
-                idx[key] = pre
+        keys = ["chr901_full", "chr901_gapped", "synth4242_full", "synth4242_gapped",
+                # multi-block: split at contig starts (synth4242) and deep inside a 3 Mbp contig (long777)
+                "synth4242_fullM1", "synth4242_gappedM1", "long777_fullM17", "long777_gappedM6"]
+        for key in keys:
+            pre = os.path.join(tmp, key)
+            md5s[key] = build_ref_index(gfas[key.rsplit("_", 1)[0]], pre, key)
+            idx[key] = pre
+        recipes = {"chr901": "tests/golden/chr901.fa.gz"}
+        for gname, (lengths, seed) in SYNTH_GENOMES.items():
+            recipes[gname] = "subread_amd.sim.random_genome(%r, %d, repeats=(2500,300,16,0.04))" % (lengths, seed)
         with open(os.path.join(GOLD, "index_md5.json"), "w") as f:
-            json.dump({"recipes": {"chr901": "tests/golden/chr901.fa.gz",
-                                   "synth4242": "subread_amd.sim.random_genome([300000,250000,17,200000,120000], 4242, repeats=(2500,300,16,0.04))"},
+            json.dump({"recipes": recipes,
                        "full": "gap=1 force_one_block memory_mb=100 (subread-buildindex -F -B -M 100)",
                        "gapped": "gap=3 memory_mb=8000 (subread-buildindex, defaults)",
+                       "fullM<n>": "gap=1 memory_mb=n (subread-buildindex -F -M n), may be multi-block",
+                       "gappedM<n>": "gap=3 memory_mb=n (subread-buildindex -M n), may be multi-block",
                        "md5": md5s}, f, indent=1)
 
         # ---- reference test reads
@@ -238,7 +255,6 @@ def main():
                       ReadBatch.from_list(lr2), "chr901 pairs seed 15, 200/250/400 bp, fragments up to 700 bp"))
         # subjunc long reads (161-400 bp: 6 bp subread step; the junction search adds the indel
         # offsets of both halves); ~30% span a GT..AG intron of chr901
-        from subread_amd.sim import simulate_spliced_reads
         sj_long = [simulate_spliced_reads(g901, 200, L, seed=16 + L) for L in (170, 250, 400)]
         sj_long = ReadBatch.from_list([b.read(i) for b in sj_long for i in range(len(b))])
         cases.append(("sj_se_full_long", PROGRAM_SUBJUNC, False, "chr901_full", {}, sj_long, None,
@@ -249,6 +265,26 @@ def main():
                       ReadBatch.from_list([b.read(i) for b in sj_l1 for i in range(len(b))]),
                       ReadBatch.from_list([b.read(i) for b in sj_l2 for i in range(len(b))]),
                       "chr901 spliced read pairs 200/300 bp, seeds 230/330 and 240/340"))
+        # ---- multi-block indexes (blocks voted in order, later blocks merge with the stored records)
+        cases.append(("se_mb_synth_fullM1", PROGRAM_ALIGN, False, "synth4242_fullM1", {},
+                      mixed_reads(synth, 2500, 21, [50, 75, 100, 120, 150, 200], False), None,
+                      "synth4242 mixed reads seed 21 on the 4-block -F -M 1 index"))
+        cases.append(("pe_mb_synth_gappedM1", PROGRAM_ALIGN, True, "synth4242_gappedM1", {}, ReadBatch.from_list(sr1),
+                      ReadBatch.from_list(sr2), "synth4242 pairs seed 99 on the 2-block -M 1 index"))
+        cases.append(("sj_se_mb_synth_fullM1", PROGRAM_SUBJUNC, False, "synth4242_fullM1", {},
+                      simulate_spliced_reads(synth, 2000, 100, seed=22, max_intron=20000), None,
+                      "synth4242 spliced reads seed 22 (100 bp) on the 4-block -F -M 1 index"))
+        from subread_amd.sim import simulate_pairs
+        lp1, lp2 = simulate_pairs(long777, 2000, 150, seed=23, sub=0.01)
+        cases.append(("pe_mb_long_fullM17", PROGRAM_ALIGN, True, "long777_fullM17", {}, lp1, lp2,
+                      "long777 pairs seed 23 (150 bp) on the 6-block -F -M 17 index (blocks overlap ~2 Mbp)"))
+        cases.append(("se_mb_long_gappedM6", PROGRAM_ALIGN, False, "long777_gappedM6", {},
+                      mixed_reads(long777, 2500, 24, [36, 75, 100, 150, 250], True), None,
+                      "long777 mixed reads seed 24 on the 4-block -M 6 index"))
+        sj_lp1 = simulate_spliced_reads(long777, 1500, 150, seed=25, max_intron=20000)
+        sj_lp2 = simulate_spliced_reads(long777, 1500, 150, seed=26, max_intron=20000)
+        cases.append(("sj_pe_mb_long_gappedM6", PROGRAM_SUBJUNC, True, "long777_gappedM6", {}, sj_lp1, sj_lp2,
+                      "long777 spliced reads seeds 25/26 (150 bp) on the 4-block -M 6 index"))
         only = set(sys.argv[1:])
         if only:
             cases = [c for c in cases if c[0] in only]

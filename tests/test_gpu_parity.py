@@ -208,3 +208,52 @@ def test_gpu_probe_images_match_oracle(monkeypatch):
             monkeypatch.delenv(k, raising=False)
         got = pack_records(out, None, None)
         assert (got == want).all(), "%s: %s" % (env, describe_mismatch(got, want, 1, 3))
+
+
+@pytest.mark.parametrize("key,mode,n", [("long777_fullM17", "se", 40000), ("long777_fullM17", "pe", 15000),
+                                        ("long777_gappedM6", "sj", 20000), ("synth4242_fullM1", "pe", 15000)])
+def test_gpu_multi_block_matches_oracle(key, mode, n, gpu_indexes, index_cache, monkeypatch):
+    """Multi-block indexes: every block resident in HBM, voted in order, later blocks merging
+    into the records the earlier ones left (core.c:3567-3613).  long777's blocks overlap by
+    ~2 Mbp, so most reads are found again in several blocks.  Host pipeline with small
+    sub-batches and the device entry too."""
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.abi import default_params, PROGRAM_ALIGN, PROGRAM_SUBJUNC
+    from subread_amd.sim import Genome, simulate_reads, simulate_pairs, simulate_spliced_reads
+    pre = index_cache.get(key)
+    g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
+    if mode == "sj":
+        r1, r2 = simulate_spliced_reads(g, n, 100, seed=41, max_intron=20000), None
+    elif mode == "pe":
+        r1, r2 = simulate_pairs(g, n, 150, seed=42)
+    else:
+        r1, r2 = simulate_reads(g, n, 100, seed=43, sub=0.02, indel=0.02, nrate=0.002), None
+    p = default_params(PROGRAM_SUBJUNC if mode == "sj" else PROGRAM_ALIGN, mode == "pe")
+    ix = gpu_indexes(key)
+    assert ix.n_blocks > 1
+    ref, rj, rbm, _ = OracleIndex(pre).vote(p, r1, r2, threads=16)
+    sj = mode == "sj"
+    want = pack_records(ref, rj if sj else None, rbm if sj else None)
+    ends = 2 if mode == "pe" else 1
+    for env in ({}, {"SVG_HOST_SUB": "7001"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        out, jout, bm = ix.vote(p, r1, r2)
+        for k in env:
+            monkeypatch.delenv(k)
+        got = pack_records(out, jout if sj else None, bm if sj else None)
+        assert (got == want).all(), "%s: %s" % (env, describe_mismatch(got, want, ends, 3))
+    if not sj:
+        import torch
+        dev = torch.device("cuda", 0)
+        keep = []
+
+        def dr(b):
+            t = [torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).to(dev) for x in (b.seq, b.offsets, b.lens)]
+            keep.append(t)
+            return (t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), len(b))
+        d_out = torch.zeros(n * ends * p.multi_best * 68, dtype=torch.uint8, device=dev)
+        ix.vote_device(p, dr(r1), dr(r2) if r2 is not None else None, d_out.data_ptr())
+        ix.device_status()
+        got = d_out.cpu().numpy().reshape(n, -1)
+        assert (got == want).all(), "device: " + describe_mismatch(got, want, ends, 3)

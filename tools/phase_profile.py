@@ -46,12 +46,14 @@ def main():
     dt = time.time() - t
     c = (ctypes.c_ulonglong * 32)()
     sa.lib().svg_debug_counters(ix.h, c)
-    names = ["text+init", "probe", "gather", "vote", "topk", "output", "junction", "bigmargin"]
+    names = ["text+init", "probe", "gather", "vote(serial)", "topk", "output", "batch/junc", "bigmargin"]
     tot = sum(c[8 + k] for k in range(8))
     print("workload %s reads %d paired %s wall %.3fs probes %d items %d hits %d results %d" % (
         wl, n, paired, dt, c[0], c[1], c[2], c[3]))
+    nd = c[20] if c[20] else n   # reads the wave kernel voted (lane-path deferrals)
     for k in range(8):
-        print("  %-10s %6.2f%%  %8.0f cycles/read" % (names[k], 100.0 * c[8 + k] / max(1, tot), c[8 + k] / n))
+        print("  %-12s %6.2f%%  %8.0f cycles/read  %8.0f cycles per wave-kernel read" % (
+            names[k], 100.0 * c[8 + k] / max(1, tot), c[8 + k] / n, c[8 + k] / nd))
     print("  lane pass: defer cap/len %d, slots %d, shift %d, candidates %d, deferrals %d" % tuple(c[16:21]))
     print("  wave kernel: batch-settled %d, serially replayed %d" % (c[26], c[27]))
 
