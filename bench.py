@@ -8,6 +8,7 @@ PCIe both ways included; reads are packed once, before timing).  Secondary field
 the same kernels with reads and records already in HBM (device_path,
 svg_vote_batch_device) and the ASCII host entry point (svg_vote_batch).  Workloads
 (SURVEY.md §8(d)):
+  c3g: C3 with the gapped index (gap 3, the reference's default index type).
   c2: 10M x 100 bp SE reads per GPU vs a chr901-scale 1,000,000 bp
       i.i.d. genome (seed 901), full one-block index (subread-buildindex -F -B),
       1% substitutions, 0.1% reads with a 1-5 bp indel, read seed 20261015.
@@ -51,6 +52,11 @@ def workload(name):
     if name == "c3":
         return dict(c3, reads=50_000_000, read_len=100, kind="se",
                     desc="C3: 50M x 100bp SE reads vs 3.0 Gbp 24-contig genome, full one-block index")
+    if name == "c3g":
+        # the reference's default index type: gapped (-M 8000 default budget, one block at 3 Gbp),
+        # 3 probes per subread offset -> 60 probes per read
+        return dict(c3, reads=50_000_000, read_len=100, kind="se", gap=3,
+                    desc="C3g: 50M x 100bp SE reads vs the C3 genome, gapped index (subread-buildindex defaults)")
     if name == "c4":
         return dict(c3, reads=25_000_000, read_len=150, kind="pe",
                     desc="C4: 25M x 2 x 150bp PE pairs per GPU vs the C3 3.0 Gbp index (400M reads on 8 GPUs)")
@@ -141,7 +147,8 @@ def main():
     else:
         # 3 Gbp: build the same index straight into this GPU's HBM (replicated per rank)
         t1 = time.time()
-        ix = sa.VoteIndex.build_genome(genome, gap=1, force_one_block=True, device=local)
+        gap = W.get("gap", 1)
+        ix = sa.VoteIndex.build_genome(genome, gap=gap, memory_mb=8000, force_one_block=gap == 1, device=local)
     log("[bench] index in HBM (%.1f GB, %d items) in %.1fs" % (ix.info.device_bytes / 1e9, ix.info.items,
                                                             time.time() - t1))
 
@@ -384,8 +391,8 @@ def main():
                        "mode": {"se": "subread-align SE", "pe": "subread-align PE", "sj": "subjunc SE"}[kind],
                        "entry": "svg_vote_batch_packed: 2-bit packed reads in host-pinned memory -> mapping_result_t "
                                 "in host-pinned memory (H2D + vote + compacted D2H + host expansion)",
-                       "index": "full one-block (gap 1), %d buckets, %d items, %s" % (
-                           ix.info.buckets, ix.info.items,
+                       "index": "%s one-block (gap %d), %d buckets, %d items, %s" % (
+                           "full" if ix.info.index_gap == 1 else "gapped", ix.info.index_gap, ix.info.buckets, ix.info.items,
                            "reference-format files via svg_index_open" if prefix else "built in HBM by svg_index_build_mem"),
                        "parallelism": "reads sharded across %d GPU(s), index replicated, no collective" % world},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(vote_achieved, 2),

@@ -1,0 +1,108 @@
+/*
+ * subread_events.h -- host-side event detection on the vote records: the tail of the
+ * reference's final voting run (do_voting, core.c:3241-3290), which turns each read's
+ * mapping records into indel and junction events of a chromosome event table, and the
+ * per-thread table merge that follows the voting step (finalise_indel_and_junction_thread,
+ * core-indel.c:1012-1141).  This is the first stage of the host post-vote pipeline
+ * (SURVEY.md §8(f) row 2); it consumes svg_vote_batch's records unchanged and marks them
+ * CORE_IS_GAPPED_READ (flag 64) exactly where the reference does (mark_gapped_read,
+ * core.h:61).
+ *
+ * Covered (the configuration subread-align and subjunc run by default):
+ *   find_new_indels   core-indel.c:1831-2098, dynamic-programming path
+ *                     (use_dynamic_programming_indel = 1, core-interface-aligner.c:271,
+ *                     core-interface-subjunc.c:270; core_dynamic_align core-indel.c:4573)
+ *   find_new_junctions core-junction.c:3836-4137 (do_breakpoint_detection; reads <= 160 bp)
+ *   local_add_indel_event / put_new_event / search_event  core-indel.c:1385-1569
+ *   has_better_mapping core.c:3035, is_ambiguous_voting core-junction.c:3522,
+ *   locate_current_value_index core.c:2216 (multi-block indexes)
+ * Not covered (SVG_E_UNSUPPORTED): subjunc reads > 160 bp (core_search_short_exons and the
+ * fragile junction voting feed their events), fusion / long-deletion detection, the
+ * extending indel search (extending_search_indels = 0 in both programs).
+ *
+ * Threading: one table per host thread; svg_events_merge() combines tables the way
+ * finalise_indel_and_junction_thread combines the reference's per-thread tables.
+ */
+#ifndef SUBREAD_EVENTS_H
+#define SUBREAD_EVENTS_H
+
+#include <stdint.h>
+#include "subread_vote.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* event_type values (core-indel.h:35-41) */
+#define SVG_EVENT_INDEL     8
+#define SVG_EVENT_JUNCTION 64
+#define SVG_EVENT_FUSION  128
+
+/* one chromosome_event_t (core.h:274-346) with the inserted bases decoded */
+typedef struct svg_event {
+	uint32_t small_side;                  /* event_small_side (linear, padded coordinates) */
+	uint32_t large_side;                  /* event_large_side                               */
+	int16_t  indel_length;                /* >0 deletion, <0 insertion, 0 junction          */
+	int16_t  junction_flanking_left;
+	int16_t  junction_flanking_right;
+	int8_t   indel_at_junction;
+	int8_t   is_negative_strand;
+	int8_t   is_strand_jumped;
+	int8_t   is_donor_found_or_annotation;
+	int8_t   small_side_increasing_coordinate;
+	int8_t   large_side_increasing_coordinate;
+	int8_t   connected_next_event_distance;
+	int8_t   connected_previous_event_distance;
+	uint16_t supporting_reads;
+	uint16_t anti_supporting_reads;
+	uint16_t final_counted_reads;
+	uint16_t final_reads_mismatches;
+	uint8_t  event_type;                  /* SVG_EVENT_*                                    */
+	uint8_t  inserted_len;                /* bases in inserted_bases (insertions)           */
+	uint64_t critical_read_id;            /* 2 * read number + end, junctions               */
+	float    event_quality;
+	int32_t  critical_supporting_reads;
+	char     inserted_bases[40];          /* ACGT text of an insertion (not terminated)     */
+} svg_event;
+
+/* knobs of the event search with the reference's defaults (core-indel.c:4512-4515) */
+typedef struct svg_event_params {
+	int32_t dp_penalty_create_gap;        /* -1 */
+	int32_t dp_penalty_extend_gap;        /*  0 */
+	int32_t dp_match_score;               /*  2 */
+	int32_t dp_mismatch_penalty;          /*  0 */
+} svg_event_params;
+void svg_event_params_default(svg_event_params *e);
+
+/* host copy of the index's base arrays (every <prefix>.NN.b.array) and contig table */
+typedef struct svg_genome_arrays svg_genome_arrays;
+int  svg_genome_arrays_open(const char *prefix, svg_genome_arrays **out);
+void svg_genome_arrays_close(svg_genome_arrays *g);
+
+typedef struct svg_events svg_events;
+int  svg_events_create(svg_events **out);
+void svg_events_destroy(svg_events *t);
+
+/*
+ * Add the events of a batch of voted reads (read i of the batch is read number
+ * first_read + i of the reference's chunk numbering).  r1/r2/params are those given to
+ * the vote; out/jout/big_margin are its records (jout / big_margin as the vote required
+ * them).  Reads are processed in order, ends R1 then R2, records best 0..multi_best-1,
+ * like do_voting.  out's result_flags gain CORE_IS_GAPPED_READ where the reference sets it.
+ */
+int svg_events_add_batch(svg_events *t, const svg_genome_arrays *g, const svg_params *p, const svg_event_params *ep,
+                         const svg_reads *r1, const svg_reads *r2, uint64_t first_read, svg_mapping_result *out,
+                         const svg_subjunc_result *jout, const uint16_t *big_margin);
+
+/* Merge `n` tables (in order) into `dst` (created empty by the caller): the sort-and-sum of
+ * finalise_indel_and_junction_thread.  Also call it with n = 1 on a single table: the merged
+ * table is sorted by (small side, large side, indel length) as the reference's is. */
+int svg_events_merge(svg_events *dst, svg_events *const *tables, int n);
+
+int64_t svg_events_count(const svg_events *t);
+int     svg_events_get(const svg_events *t, svg_event *out);   /* svg_events_count() entries */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

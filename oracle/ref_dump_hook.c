@@ -31,6 +31,84 @@
 #include "subread.h"
 #include "core.h"
 #include "core-bigtable.h"
+#include "core-indel.h"
+
+/*
+ * Event-table dump (env SVG_REF_EVENTS=<file>, appended chunk after chunk): the indel /
+ * junction event table of the final voting run as finalise_indel_and_junction_thread left
+ * it (core-indel.c:1012-1141; run the aligner with -T 1 so that every event comes from one
+ * thread table in read order), then the raw result_flags (CORE_IS_GAPPED_READ included) of
+ * every mapping record, in the record order of the vote dump.
+ *   u64 n_events, then n_events x svg_ref_event (96 B, layout below),
+ *   u64 n_records, then n_records x u16 result_flags
+ */
+typedef struct {
+	unsigned int small_side, large_side;
+	short indel_length, junction_flanking_left, junction_flanking_right;
+	char indel_at_junction, is_negative_strand, is_strand_jumped, is_donor_found_or_annotation;
+	char small_side_increasing_coordinate, large_side_increasing_coordinate;
+	char connected_next_event_distance, connected_previous_event_distance;
+	unsigned short supporting_reads, anti_supporting_reads, final_counted_reads, final_reads_mismatches;
+	unsigned char event_type, inserted_len;
+	unsigned long long critical_read_id;
+	float event_quality;
+	int critical_supporting_reads;
+	char inserted_bases[40];
+} svg_ref_event;
+
+void get_insertion_sequence(global_context_t *global_context, thread_context_t *thread_context, char *binary_bases,
+                            char *read_text, int insertions);
+
+static void dump_events(global_context_t *gc, const char *fn)
+{
+	FILE *fp = fopen(fn, "ab");
+	if (!fp) return;
+	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
+	unsigned long long n = ic ? ic->total_events : 0, i, nrec;
+	fwrite(&n, 8, 1, fp);
+	for (i = 0; i < n; i++) {
+		chromosome_event_t *e = ic->event_space_dynamic + i;
+		svg_ref_event o;
+		memset(&o, 0, sizeof o);
+		o.small_side = e->event_small_side; o.large_side = e->event_large_side;
+		o.indel_length = e->indel_length;
+		o.junction_flanking_left = e->junction_flanking_left; o.junction_flanking_right = e->junction_flanking_right;
+		o.indel_at_junction = e->indel_at_junction; o.is_negative_strand = e->is_negative_strand;
+		o.is_strand_jumped = e->is_strand_jumped; o.is_donor_found_or_annotation = e->is_donor_found_or_annotation;
+		o.small_side_increasing_coordinate = e->small_side_increasing_coordinate;
+		o.large_side_increasing_coordinate = e->large_side_increasing_coordinate;
+		o.connected_next_event_distance = e->connected_next_event_distance;
+		o.connected_previous_event_distance = e->connected_previous_event_distance;
+		o.supporting_reads = e->supporting_reads; o.anti_supporting_reads = e->anti_supporting_reads;
+		o.final_counted_reads = e->final_counted_reads; o.final_reads_mismatches = e->final_reads_mismatches;
+		o.event_type = e->event_type;
+		o.critical_read_id = e->critical_read_id;
+		o.event_quality = e->event_quality;
+		o.critical_supporting_reads = e->critical_supporting_reads;
+		if (e->event_type == CHRO_EVENT_TYPE_INDEL && e->indel_length < 0 && e->inserted_bases) {
+			char buf[MAX_INSERTION_LENGTH + 2];
+			int k = -e->indel_length;
+			get_insertion_sequence(gc, NULL, e->inserted_bases, buf, k);
+			if (k > (int)sizeof o.inserted_bases) k = sizeof o.inserted_bases;
+			memcpy(o.inserted_bases, buf, k);
+			o.inserted_len = (unsigned char)k;
+		}
+		fwrite(&o, sizeof o, 1, fp);
+	}
+	{
+		long long r, nr = gc->processed_reads_in_chunk;
+		int ends = 1 + gc->input_reads.is_paired_end_reads, mb = gc->config.multi_best_reads, e, b;
+		nrec = (unsigned long long)nr * ends * mb;
+		fwrite(&nrec, 8, 1, fp);
+		for (r = 0; r < nr; r++)
+			for (e = 0; e < ends; e++)
+				for (b = 0; b < mb; b++) {
+					unsigned short f = (unsigned short)_global_retrieve_alignment_ptr(gc, r, e, b)->result_flags;
+					fwrite(&f, 2, 1, fp);
+				}
+	}
+	fclose(fp);
+}
 
 int __real_anti_supporting_read_scan(global_context_t *global_context);
 
@@ -42,6 +120,8 @@ int __wrap_anti_supporting_read_scan(global_context_t *gc)
 	if (getenv("SVG_REF_TIMING"))
 		fprintf(stderr, "SVG_REF_TIMECOST_VOTING %.6f %lld\n", gc->timecost_voting,
 		        (long long)gc->processed_reads_in_chunk);
+	const char *ef = getenv("SVG_REF_EVENTS");
+	if (ef && ef[0]) dump_events(gc, ef);
 	const char *fn = getenv("SVG_REF_DUMP");
 	if (fn && fn[0]) {
 		FILE *fp = fopen(fn, "ab");

@@ -31,6 +31,9 @@ EXPORTS = [
     "svg_set_max_read_length", "svg_sim_pairs", "svg_set_timing", "svg_get_timing",
     "svg_get_kernel_timing", "svg_device_status", "svg_pack_reads", "svg_vote_batch_packed",
     "svg_vote_batch_packed_device",
+    # host post-vote events (include/subread_events.h)
+    "svg_event_params_default", "svg_genome_arrays_open", "svg_genome_arrays_close", "svg_events_create",
+    "svg_events_destroy", "svg_events_add_batch", "svg_events_merge", "svg_events_count", "svg_events_get",
 ]
 
 _lib = None
@@ -107,6 +110,21 @@ def lib():
         L.svg_sim_pairs.argtypes = [vp, vp, vp, ctypes.c_uint32, u64, u64, i32, ctypes.c_double, ctypes.c_double,
                                     i32, ctypes.c_double, u64, vp, vp, i32]
         L.svg_sim_pairs.restype = i32
+        L.svg_event_params_default.argtypes = [vp]
+        L.svg_genome_arrays_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
+        L.svg_genome_arrays_open.restype = i32
+        L.svg_genome_arrays_close.argtypes = [vp]
+        L.svg_events_create.argtypes = [ctypes.POINTER(vp)]
+        L.svg_events_create.restype = i32
+        L.svg_events_destroy.argtypes = [vp]
+        L.svg_events_add_batch.argtypes = [vp, vp, vp, vp, vp, vp, u64, vp, vp, vp]
+        L.svg_events_add_batch.restype = i32
+        L.svg_events_merge.argtypes = [vp, vp, i32]
+        L.svg_events_merge.restype = i32
+        L.svg_events_count.argtypes = [vp]
+        L.svg_events_count.restype = ctypes.c_int64
+        L.svg_events_get.argtypes = [vp, vp]
+        L.svg_events_get.restype = i32
         _lib = L
     return _lib
 
@@ -129,6 +147,87 @@ def build_index(fasta, prefix, gap=3, memory_mb=8000, force_one_block=False, rep
     rc = lib().svg_build_index(str(fasta).encode(), str(prefix).encode(), gap, memory_mb,
                                1 if force_one_block else 0, repeat_threshold)
     _check(rc, "svg_build_index")
+
+
+class GenomeArrays:
+    """svg_genome_arrays: host copy of an index's base arrays (every .NN.b.array) and contig
+    table -- what the event search reads (gvindex_get, locate_gene_position)."""
+
+    def __init__(self, prefix):
+        h = ctypes.c_void_p()
+        _check(lib().svg_genome_arrays_open(str(prefix).encode(), ctypes.byref(h)), "svg_genome_arrays_open")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().svg_genome_arrays_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class EventTable:
+    """svg_events: the indel / junction events of voted reads (include/subread_events.h)."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        _check(lib().svg_events_create(ctypes.byref(h)), "svg_events_create")
+        self.h = h
+
+    def add_batch(self, genome, params, r1, r2, records, first_read=0, event_params=None):
+        """records = (mapping, subjunc|None, big_margin|None) as VoteIndex.vote returns them;
+        mapping's result_flags gain CORE_IS_GAPPED_READ (64) where the reference sets it."""
+        out, jout, bm = records
+        s1 = r1.struct()
+        s2 = r2.struct() if r2 is not None else None
+        rc = lib().svg_events_add_batch(self.h, genome.h, ctypes.byref(params),
+                                        ctypes.byref(event_params) if event_params is not None else None,
+                                        ctypes.byref(s1), ctypes.byref(s2) if s2 is not None else None,
+                                        int(first_read), out.ctypes.data,
+                                        jout.ctypes.data if jout is not None else None,
+                                        bm.ctypes.data if bm is not None else None)
+        _check(rc, "svg_events_add_batch")
+
+    @classmethod
+    def merge(cls, tables):
+        """finalise_indel_and_junction_thread over `tables` (in order) -> a new sorted table."""
+        t = cls()
+        arr = (ctypes.c_void_p * len(tables))(*[x.h.value for x in tables])
+        _check(lib().svg_events_merge(t.h, arr, len(tables)), "svg_events_merge")
+        return t
+
+    def events(self):
+        from .abi import EVENT_DTYPE
+        n = lib().svg_events_count(self.h)
+        a = np.zeros(max(0, n), dtype=EVENT_DTYPE)
+        _check(lib().svg_events_get(self.h, a.ctypes.data if n else None), "svg_events_get")
+        return a
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().svg_events_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def find_events(genome, params, r1, r2, records, first_read=0):
+    """Events of one batch, merged and sorted like the reference's table after the voting step."""
+    t = EventTable()
+    t.add_batch(genome, params, r1, r2, records, first_read)
+    m = EventTable.merge([t])
+    ev = m.events()
+    t.close()
+    m.close()
+    return ev
 
 
 def pack_reads(batch, stride=None, threads=8, alloc=None):

@@ -37,6 +37,28 @@ MAPPING_DTYPE = np.dtype([
 ])
 assert MAPPING_DTYPE.itemsize == 68
 
+# svg_event (include/subread_events.h): chromosome_event_t, core.h:274-346, bases decoded
+EVENT_DTYPE = np.dtype([
+    ("small_side", "<u4"), ("large_side", "<u4"), ("indel_length", "<i2"),
+    ("junction_flanking_left", "<i2"), ("junction_flanking_right", "<i2"),
+    ("indel_at_junction", "i1"), ("is_negative_strand", "i1"), ("is_strand_jumped", "i1"),
+    ("is_donor_found_or_annotation", "i1"), ("small_side_increasing_coordinate", "i1"),
+    ("large_side_increasing_coordinate", "i1"), ("connected_next_event_distance", "i1"),
+    ("connected_previous_event_distance", "i1"), ("supporting_reads", "<u2"), ("anti_supporting_reads", "<u2"),
+    ("final_counted_reads", "<u2"), ("final_reads_mismatches", "<u2"), ("event_type", "u1"),
+    ("inserted_len", "u1"), ("critical_read_id", "<u8"), ("event_quality", "<f4"),
+    ("critical_supporting_reads", "<i4"), ("inserted_bases", "S40"),
+], align=True)
+assert EVENT_DTYPE.itemsize == 88
+
+EVENT_INDEL, EVENT_JUNCTION, EVENT_FUSION = 8, 64, 128
+
+
+class SvgEventParams(ctypes.Structure):
+    _fields_ = [("dp_penalty_create_gap", ctypes.c_int32), ("dp_penalty_extend_gap", ctypes.c_int32),
+                ("dp_match_score", ctypes.c_int32), ("dp_mismatch_penalty", ctypes.c_int32)]
+
+
 SUBJUNC_DTYPE = np.dtype([
     ("split_point", "<i2"),
     ("minor_votes", "<i2"),

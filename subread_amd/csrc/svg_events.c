@@ -1,0 +1,743 @@
+/*
+ * svg_events.c -- host post-vote stage: indel and junction events from the vote records
+ * (the final-run tail of do_voting, core.c:3241-3290) and the table merge of
+ * finalise_indel_and_junction_thread (core-indel.c:1012-1141).  See include/subread_events.h.
+ *
+ * Event table: a growable array of events plus an open-addressing map from a coordinate to
+ * the ids of the events that have it as small or large side -- at most 8 per coordinate,
+ * like put_new_event's id lists (EVENT_ENTRIES_INIT_SIZE, core-indel.c:1385-1419).
+ */
+#define _GNU_SOURCE
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdint.h>
+#include "subread_vote.h"
+#include "subread_events.h"
+#include "svg_internal.h"
+
+#define EV_PER_SITE        8          /* id slots of an id list (EVENT_ENTRIES_INIT_SIZE - 1) */
+#define MAX_INDEL_SECT     7          /* MAX_INDEL_SECTIONS: the loop bound of find_new_indels */
+#define LONG_READ          160        /* EXON_LONG_READ_LENGTH */
+#define MAX_INSERTION      200        /* MAX_INSERTION_LENGTH */
+#define GAPPED_FLAG        64         /* CORE_IS_GAPPED_READ */
+#define JUMPED_FLAG        4          /* CORE_IS_STRAND_JUMPED */
+#define NEG_FLAG           SVG_NEGATIVE_STRAND_FLAG
+#define MASK_MATCH         0          /* INDEL_MASK_BY_*, core-indel.c:4560-4563 */
+#define MASK_INSERTION     1
+#define MASK_DELETION      2
+#define MASK_MISMATCH      3
+
+void svg_event_params_default(svg_event_params *e)
+{
+	e->dp_penalty_create_gap = -1;
+	e->dp_penalty_extend_gap = 0;
+	e->dp_match_score = 2;
+	e->dp_mismatch_penalty = 0;
+}
+
+/* ------------------------------------------------------------------ base arrays */
+typedef struct {
+	uint32_t start_point, length, start_base_offset, values_bytes;
+	uint8_t *values;
+} garray;
+
+struct svg_genome_arrays {
+	int nblocks;
+	garray *blk;
+	uint32_t n_chr;
+	uint32_t *chr_end;
+	int padding;
+};
+
+void svg_genome_arrays_close(svg_genome_arrays *g)
+{
+	int b;
+	if (!g) return;
+	for (b = 0; b < g->nblocks; b++) free(g->blk[b].values);
+	free(g->blk);
+	free(g->chr_end);
+	free(g);
+}
+
+/* gvindex_load (gene-value-index.c:190-228) per block; load_offsets' .reads table
+ * (gene-algorithms.c:1293-1370) with the .tab's padding option */
+int svg_genome_arrays_open(const char *prefix, svg_genome_arrays **out)
+{
+	char fn[4096];
+	svg_genome_arrays *g;
+	int b, nb;
+	FILE *fp;
+	if (!prefix || !out) { svg_set_error("svg_genome_arrays_open: NULL argument"); return SVG_E_ARG; }
+	*out = NULL;
+	nb = svg_index_count_blocks(prefix);
+	if (nb < 1) { svg_set_error("index table '%s.00.b.tab' not found", prefix); return SVG_E_IO; }
+	g = calloc(1, sizeof *g);
+	g->blk = calloc((size_t)nb, sizeof(garray));
+	g->padding = 1210;
+	for (b = 0; b < nb; b++) {
+		garray *a = &g->blk[b];
+		uint32_t useful;
+		snprintf(fn, sizeof fn, "%s.%02d.b.array", prefix, b);
+		if (!(fp = fopen(fn, "rb"))) { svg_genome_arrays_close(g); svg_set_error("cannot open '%s'", fn); return SVG_E_IO; }
+		if (fread(&a->start_point, 4, 1, fp) != 1 || fread(&a->length, 4, 1, fp) != 1) {
+			fclose(fp); svg_genome_arrays_close(g); svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT;
+		}
+		a->start_base_offset = a->start_point - a->start_point % 4;
+		useful = (a->length + a->start_point - a->start_base_offset) >> 2;
+		a->values_bytes = useful + 1;
+		a->values = calloc((size_t)a->values_bytes + 8, 1);
+		if (fread(a->values, 1, (size_t)useful + 1, fp) < useful) {
+			fclose(fp); svg_genome_arrays_close(g); svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT;
+		}
+		fclose(fp);
+		g->nblocks = b + 1;
+	}
+	/* the padding option of the first table (gehash_load_option, 0x0102) */
+	snprintf(fn, sizeof fn, "%s.00.b.tab", prefix);
+	if ((fp = fopen(fn, "rb"))) {
+		char magic[8];
+		if (fread(magic, 1, 8, fp) == 8 && !memcmp(magic, "2subindx", 8))
+			for (;;) {
+				int16_t k, l, v;
+				if (fread(&k, 2, 1, fp) != 1 || !k || fread(&l, 2, 1, fp) != 1) break;
+				if (k == 0x0102) { if (fread(&v, 2, 1, fp) == 1) g->padding = v; break; }
+				if (fseek(fp, l, SEEK_CUR)) break;
+			}
+		fclose(fp);
+	}
+	snprintf(fn, sizeof fn, "%s.reads", prefix);
+	if (!(fp = fopen(fn, "r"))) { svg_genome_arrays_close(g); svg_set_error("cannot open '%s'", fn); return SVG_E_IO; }
+	{
+		char line[4096];
+		uint32_t cap = 64;
+		g->chr_end = malloc(4 * cap);
+		while (fgets(line, sizeof line, fp)) {
+			if (strlen(line) < 2) continue;
+			if (g->n_chr == cap) { cap *= 2; g->chr_end = realloc(g->chr_end, 4 * cap); }
+			g->chr_end[g->n_chr++] = (uint32_t)strtoull(line, NULL, 10);
+		}
+	}
+	fclose(fp);
+	*out = g;
+	return 0;
+}
+
+/* gvindex_get, gene-value-index.c:96-107 */
+static inline char gv_get(const garray *a, uint32_t pos)
+{
+	uint32_t byte = (pos - a->start_base_offset) >> 2;
+	if (byte >= a->values_bytes - 1) return 'N';
+	return "AGCT"[(a->values[byte] >> (pos % 4 * 2)) & 3];
+}
+
+/* locate_current_value_index, core.c:2216-2249: the block holding the record, else the block
+ * of the final voting run (the thread's value index, restored after every record) */
+static const garray *value_index(const svg_genome_arrays *g, uint32_t pos, int rlen)
+{
+	int b;
+	if (g->nblocks < 2) return &g->blk[0];
+	for (b = 0; b < g->nblocks; b++) {
+		uint32_t begin = g->blk[b].start_base_offset, end = g->blk[b].start_base_offset + g->blk[b].length;
+		if ((b == 0 && pos >= begin && pos < end - 1000000u) ||
+		    (b > 0 && b < g->nblocks - 1 && pos >= begin + 1000000u && pos < end - 1000000u) ||
+		    (b == g->nblocks - 1 && pos >= begin + 1000000u && pos < end))
+			return &g->blk[b];
+	}
+	(void)rlen;
+	return &g->blk[g->nblocks - 1];
+}
+
+/* locate_gene_position (gene-algorithms.c:441-517 with rl = 0): the contig index of a linear
+ * position, or -1 where the reference returns no name (padding, past the contig end) */
+static int contig_of(const svg_genome_arrays *g, uint32_t linear)
+{
+	int lo = 0, hi = (int)g->n_chr, n;
+	while (hi > lo + 1) {
+		int mid = (lo + hi) / 2;
+		if (g->chr_end[mid] > linear) hi = mid; else lo = mid + 1;
+	}
+	n = lo - 2 > 0 ? lo - 2 : 0;
+	for (; n < (int)g->n_chr; n++)
+		if (g->chr_end[n] > linear) {
+			uint32_t pos = n == 0 ? linear : linear - g->chr_end[n - 1];
+			if (linear > g->chr_end[n] + 15u - (uint32_t)g->padding) return -1;
+			if ((int)pos < g->padding) return -1;
+			return n;
+		}
+	return -1;
+}
+
+/* ------------------------------------------------------------------ event table */
+typedef struct { uint32_t key; uint32_t ids[EV_PER_SITE]; } site_t;   /* ids: event id + 1, 0 = end */
+
+struct svg_events {
+	svg_event *ev;
+	uint64_t n, cap;
+	site_t *site;
+	uint64_t site_cap, site_used;    /* open addressing, key 0 = empty (coordinate 0 is never put) */
+};
+
+int svg_events_create(svg_events **out)
+{
+	svg_events *t;
+	if (!out) { svg_set_error("svg_events_create: NULL argument"); return SVG_E_ARG; }
+	t = calloc(1, sizeof *t);
+	t->site_cap = 1 << 12;
+	t->site = calloc(t->site_cap, sizeof(site_t));
+	*out = t;
+	return 0;
+}
+
+void svg_events_destroy(svg_events *t)
+{
+	if (!t) return;
+	free(t->ev);
+	free(t->site);
+	free(t);
+}
+
+int64_t svg_events_count(const svg_events *t) { return t ? (int64_t)t->n : SVG_E_ARG; }
+
+int svg_events_get(const svg_events *t, svg_event *out)
+{
+	if (!t || (!out && t->n)) { svg_set_error("svg_events_get: NULL argument"); return SVG_E_ARG; }
+	if (t->n) memcpy(out, t->ev, sizeof(svg_event) * t->n);
+	return 0;
+}
+
+static inline uint64_t site_hash(uint32_t k) { return (k * 0x9E3779B97F4A7C15ull) >> 20; }
+
+static site_t *site_find(const svg_events *t, uint32_t key)
+{
+	uint64_t m = t->site_cap - 1, i = site_hash(key) & m;
+	for (;; i = (i + 1) & m) {
+		if (t->site[i].key == key) return &t->site[i];
+		if (!t->site[i].key) return NULL;
+	}
+}
+
+static site_t *site_get(svg_events *t, uint32_t key)
+{
+	uint64_t m, i;
+	if (2 * (t->site_used + 1) > t->site_cap) {
+		site_t *old = t->site;
+		uint64_t oc = t->site_cap, j;
+		t->site_cap *= 2;
+		t->site = calloc(t->site_cap, sizeof(site_t));
+		for (j = 0; j < oc; j++)
+			if (old[j].key) {
+				uint64_t k = site_hash(old[j].key) & (t->site_cap - 1);
+				while (t->site[k].key) k = (k + 1) & (t->site_cap - 1);
+				t->site[k] = old[j];
+			}
+		free(old);
+	}
+	m = t->site_cap - 1;
+	for (i = site_hash(key) & m;; i = (i + 1) & m) {
+		if (t->site[i].key == key) return &t->site[i];
+		if (!t->site[i].key) {
+			t->site[i].key = key;
+			t->site_used++;
+			return &t->site[i];
+		}
+	}
+}
+
+/* a fresh zeroed event (reallocate_event_space + memset) */
+static uint64_t new_event(svg_events *t)
+{
+	if (t->n == t->cap) {
+		t->cap = t->cap ? t->cap * 2 : 1024;
+		t->ev = realloc(t->ev, sizeof(svg_event) * t->cap);
+	}
+	memset(&t->ev[t->n], 0, sizeof(svg_event));
+	return t->n++;
+}
+
+/* put_new_event, core-indel.c:1385-1419 */
+static void put_event(svg_events *t, uint64_t id)
+{
+	uint32_t sides[2] = {t->ev[id].small_side, t->ev[id].large_side};
+	int s, k;
+	for (s = 0; s < 2; s++) {
+		site_t *st;
+		if (!sides[s]) continue;
+		st = site_get(t, sides[s]);
+		for (k = 0; k < EV_PER_SITE; k++)
+			if (!st->ids[k]) { st->ids[k] = (uint32_t)id + 1; break; }
+	}
+}
+
+/* search_event by small side, core-indel.c:1420-1461: ids of the events of the given types
+ * whose small side is pos, in list order */
+static int search_small(const svg_events *t, uint32_t pos, int types, uint64_t *ids)
+{
+	const site_t *st;
+	int k, n = 0;
+	if (pos < 1 || pos > 0xffff0000u) return 0;
+	if (!(st = site_find(t, pos))) return 0;
+	for (k = 0; k < EV_PER_SITE && st->ids[k]; k++) {
+		const svg_event *e = &t->ev[st->ids[k] - 1];
+		if (!(e->event_type & types) || e->small_side != pos) continue;
+		ids[n++] = st->ids[k] - 1;
+	}
+	return n;
+}
+
+/* local_add_indel_event, core-indel.c:1498-1569: returns the id of a new event, or -1 when an
+ * event of this length at this side existed (its id in *old_id, its support + 1) */
+static int64_t add_indel_event(svg_events *t, const char *text, uint32_t left_edge, int indels, int64_t *old_id)
+{
+	uint64_t ids[EV_PER_SITE], id;
+	int k, n = search_small(t, left_edge, SVG_EVENT_INDEL | 16 /* LONG_INDEL */, ids);
+	svg_event *e;
+	for (k = 0; k < n; k++)
+		if (t->ev[ids[k]].indel_length == indels) {
+			if (old_id) *old_id = (int64_t)ids[k];
+			t->ev[ids[k]].supporting_reads++;
+			return -1;
+		}
+	id = new_event(t);
+	e = &t->ev[id];
+	if (indels < 0) {
+		/* set_insertion_sequence keeps base2int of each inserted base (2 bits); decoded here */
+		int i, L = -indels < (int)sizeof e->inserted_bases ? -indels : (int)sizeof e->inserted_bases;
+		for (i = 0; i < L; i++) {
+			char c = text[i];
+			e->inserted_bases[i] = "AGCT"[c < 'G' ? (c == 'A' ? 0 : 2) : (c == 'G' ? 1 : 3)];
+		}
+		e->inserted_len = (uint8_t)L;
+	}
+	e->small_side = left_edge;
+	e->large_side = left_edge + 1 + (indels > 0 ? indels : 0);
+	e->event_type = SVG_EVENT_INDEL;
+	e->indel_length = (int16_t)indels;
+	e->supporting_reads = 1;
+	e->event_quality = 1.0f;
+	put_event(t, id);
+	return (int64_t)id;
+}
+
+/* ------------------------------------------------------------------ per-record searches */
+typedef struct {
+	int16_t *dp;          /* (rl + 16) x rl score table, row-major */
+	uint8_t *mask;
+	int rows, cols;
+	char mv[SVG_MAX_READ_LENGTH * 10 / 7 + 64];
+} scratch_t;
+
+/* find_subread_end, input-files.c:1371-1387 */
+static int subread_end(int len, int total, int subread)
+{
+	int step;
+	if (len <= LONG_READ) {
+		step = ((len << 16) - (19 << 16)) / (total - 1);
+		return ((step * subread) >> 16) + 15;
+	}
+	step = 6 << 16;
+	if (((len - 18) << 16) / step > 62) step = ((len - 18) << 16) / 62;
+	return ((step * subread) >> 16) + 15;
+}
+
+/* core_dynamic_align, core-indel.c:4573-4787: banded global alignment of read[0..len) to the
+ * genome from begin; movements 0 match, 1 deletion, 2 insertion, 3 mismatch; 0 if the path's
+ * net offset is not expected_offset */
+static int dynamic_align(scratch_t *s, const garray *a, const svg_event_params *ep, int max_indel_length,
+                         const char *read, int len, uint32_t begin, int expected_offset)
+{
+	const int max_indel = max_indel_length < 16 ? max_indel_length : 16;
+	const int rows = len + expected_offset;
+	int i, j, out = 0, delta = 0, path_i;
+	if (len < 3 || abs(expected_offset) > max_indel) return 0;
+	if (expected_offset < 0 && len < 3 - expected_offset) return 0;
+#define T(i, j) s->dp[(size_t)(i) * s->cols + (j)]
+#define M(i, j) s->mask[(size_t)(i) * s->cols + (j)]
+	for (i = 0; i < rows; i++)
+		for (j = 0; j < len; j++) {
+			int16_t up, left, diag;
+			char ch;
+			int sc;
+			M(i, j) = 0;
+			if (j < i - max_indel || j > max_indel + i) { T(i, j) = -9999; continue; }
+			up = i > 0 ? (int16_t)(T(i - 1, j) + (M(i - 1, j) == MASK_DELETION ? ep->dp_penalty_extend_gap : ep->dp_penalty_create_gap)) : -9999;
+			left = j > 0 ? (int16_t)(T(i, j - 1) + (M(i, j - 1) == MASK_INSERTION ? ep->dp_penalty_extend_gap : ep->dp_penalty_create_gap)) : -9999;
+			ch = gv_get(a, begin + i);
+			sc = ch == read[j] ? ep->dp_match_score : ep->dp_mismatch_penalty;
+			if (i > 0 && j > 0) diag = (int16_t)(T(i - 1, j - 1) + sc);
+			else if (i == 0 && j == 0) diag = (int16_t)sc;
+			else diag = -9999;
+			if (diag == up && diag > left) { M(i, j) = MASK_DELETION; T(i, j) = up; }
+			else if (diag == left && diag > up) { M(i, j) = MASK_INSERTION; T(i, j) = left; }
+			else if (diag > left && diag > up) { M(i, j) = ch == read[j] ? MASK_MATCH : MASK_MISMATCH; T(i, j) = diag; }
+			else if (diag == left && diag == up) { M(i, j) = ch == read[j] ? MASK_MATCH : MASK_MISMATCH; T(i, j) = diag; }
+			else if (left > up) { M(i, j) = MASK_INSERTION; T(i, j) = left; }
+			else { M(i, j) = MASK_DELETION; T(i, j) = up; }
+		}
+	path_i = rows - 1;
+	j = len - 1;
+	for (;;) {
+		int m = M(path_i, j);
+		if (m == MASK_INSERTION) { j--; delta--; s->mv[out++] = 2; }
+		else if (m == MASK_DELETION) { path_i--; delta++; s->mv[out++] = 1; }
+		else { s->mv[out++] = m == MASK_MATCH ? 0 : 3; path_i--; j--; }
+		if (path_i == -1 && j == -1) break;
+		if (j < 0 || path_i < 0) return 0;
+	}
+#undef T
+#undef M
+	if (expected_offset != delta) return 0;
+	for (i = 0; i < out / 2; i++) { char x = s->mv[out - 1 - i]; s->mv[out - 1 - i] = s->mv[i]; s->mv[i] = x; }
+	return out;
+}
+
+static inline int8_t min_dist(int8_t cur, int dist)
+{
+	/* connected_*_event_distance: set when < 1, else the smaller (char fields) */
+	if (cur < 1) return (int8_t)dist;
+	return (int8_t)(dist < cur ? dist : cur);
+}
+
+/* find_new_indels, core-indel.c:1831-2098 (dynamic-programming path) */
+static void find_indels(svg_events *t, scratch_t *s, const garray *a, const svg_params *p, const svg_event_params *ep,
+                        svg_mapping_result *r, const char *text, int rl)
+{
+	const int16_t *rec = r->selected_indel_record;
+	const uint32_t vpos = r->selected_position;
+	int i, last_correct_subread = 0, last_indel = 0;
+	if (!rec[0]) return;
+	for (i = 0; rec[i] && i < MAX_INDEL_SECT; i += 3) {
+		const int indels = rec[i + 2] - last_indel;
+		const int next_correct_subread = rec[i] - 1;
+		if (indels) {
+			int last_cb = subread_end(rl, p->total_subreads, last_correct_subread) - 9;
+			int first_cb = subread_end(rl, p->total_subreads, next_correct_subread) - 16 + 9;
+			int steps, x, total_mm = 0, last_mv = 0, in_indel = 0, cur_len = 0;
+			int64_t last_event_id = -1;
+			uint32_t chr, left_boundary = 0;
+			int cursor_read;
+			last_cb = last_cb < 0 ? 0 : last_cb;
+			last_cb = last_cb < rl - 1 ? last_cb : rl - 1;
+			first_cb = first_cb < rl - 1 ? first_cb : rl - 1;
+			first_cb = first_cb > 0 ? first_cb : 0;
+			first_cb = first_cb > last_cb ? first_cb : last_cb;
+			first_cb = first_cb + 10 < rl ? first_cb + 10 : rl;
+			steps = dynamic_align(s, a, ep, p->max_indel_length, text + last_cb, first_cb - last_cb,
+			                      vpos + last_cb + last_indel, indels);
+			chr = vpos + last_cb + last_indel;
+			cursor_read = last_cb;
+			for (x = 0; x < steps; x++) total_mm += s->mv[x] == 3;
+			if (total_mm <= 2)
+				for (x = 0; x < steps; x++) {
+					const int mv = s->mv[x];
+					if (last_mv != mv) {
+						if ((mv == 1 || mv == 2) && !in_indel) {
+							left_boundary = chr;
+							in_indel = 1;
+							cur_len = 0;
+						} else if (in_indel && (mv == 0 || mv == 3)) {
+							if (abs(cur_len) <= p->max_indel_length) {
+								int64_t old_id = -1, nid;
+								nid = add_indel_event(t, text + cursor_read + (cur_len < 0 ? cur_len : 0), left_boundary - 1,
+								                      cur_len, &old_id);
+								r->result_flags |= GAPPED_FLAG;
+								if (last_event_id >= 0) {
+									svg_event *last = &t->ev[last_event_id], *cur = &t->ev[nid >= 0 ? nid : old_id];
+									const int dist = (int)(left_boundary - last->large_side);
+									last->connected_next_event_distance = min_dist(last->connected_next_event_distance, dist);
+									cur->connected_previous_event_distance = min_dist(cur->connected_previous_event_distance, dist);
+								}
+								last_event_id = nid >= 0 ? nid : old_id;
+							}
+						}
+						if (mv == 0 || mv == 3) in_indel = 0;
+					}
+					if (in_indel && mv == 1) cur_len++;
+					if (in_indel && mv == 2) cur_len--;
+					if (mv == 1 || mv == 3 || mv == 0) chr++;
+					if (mv == 2 || mv == 3 || mv == 0) cursor_read++;
+					last_mv = mv;
+				}
+		}
+		last_correct_subread = rec[i + 1] - 1;
+		last_indel = rec[i + 2];
+	}
+}
+
+/* is_ambiguous_voting, core-junction.c:3522-3566 */
+static int ambiguous_voting(const svg_params *p, const uint16_t *bm, int vote, int max_start, int max_end, int rl, int neg)
+{
+	int k, enc = 0;
+	if (p->big_margin_record_size < 3) return 0;
+	if (neg) { int x = max_start; max_start = rl - max_end; max_end = rl - x; }
+	for (k = 0; k < p->big_margin_record_size / 3; k++) {
+		if (!bm[k * 3]) break;
+		if (bm[k * 3] >= vote - 1) {
+			if (vote >= bm[k * 3]) { if (bm[k * 3 + 1] >= max_start - 4 && bm[k * 3 + 2] <= max_end + 4) enc++; }
+			else if (bm[k * 3 + 1] <= max_start + 4 && bm[k * 3 + 2] >= max_end - 4) enc++;
+		}
+	}
+	return enc > 1 ? enc : 0;
+}
+
+/* find_new_junctions, core-junction.c:3836-4137, reads <= 160 bp, no fusion detection */
+static void find_junctions(svg_events *t, const svg_genome_arrays *g, const svg_params *p, svg_mapping_result *r,
+                           const svg_subjunc_result *j, const uint16_t *bm, int rl, uint64_t read_no, int end)
+{
+	const int split = j->split_point;
+	uint32_t left_vh, right_vh, left_edge, right_edge;
+	int gtag, donor_found, jumped, cl, cr;
+	if (j->minor_votes < 1) return;
+	if (p->do_big_margin_filtering_for_junctions &&
+	    ambiguous_voting(p, bm, r->selected_votes, r->confident_coverage_start, r->confident_coverage_end, rl,
+	                     (r->result_flags & NEG_FLAG) ? 1 : 0))
+		return;
+	left_vh = r->selected_position < j->minor_position ? r->selected_position : j->minor_position;
+	right_vh = r->selected_position > j->minor_position ? r->selected_position : j->minor_position;
+	gtag = r->result_flags & 3;
+	donor_found = gtag < 3;
+	jumped = (r->result_flags & JUMPED_FLAG) ? 1 : 0;
+	if (split <= 0) return;
+	if (jumped) {
+		uint32_t major_small = r->selected_position + split, minor_small = j->minor_position + rl - split;
+		int abnormal = (j->minor_coverage_start > r->confident_coverage_start) + (minor_small > major_small) == 1;
+		int small_neg = ((r->result_flags & NEG_FLAG) ? 1 : 0) + (minor_small < major_small) == 1;
+		left_edge = major_small < minor_small ? major_small : minor_small;
+		right_edge = major_small > minor_small ? major_small : minor_small;
+		if (!(r->result_flags & NEG_FLAG)) abnormal = !abnormal;
+		if (small_neg != abnormal) { left_edge--; right_edge--; }
+	} else {
+		int sl = split, sr = split, minor_off = j->double_indel_offset & 0xf, major_off = (j->double_indel_offset >> 4) & 0xf;
+		if ((j->minor_coverage_start > r->confident_coverage_start) + (j->minor_position > r->selected_position) == 1) sr--;
+		else sl--;
+		if (major_off >= 8) major_off = -(16 - major_off);
+		left_edge = left_vh + sl + (r->selected_position > j->minor_position ? minor_off : major_off);
+		right_edge = right_vh + sr;
+	}
+	cl = contig_of(g, left_edge);
+	cr = contig_of(g, right_edge);
+	if (cl != cr) return;
+	{
+		uint64_t ids[EV_PER_SITE], id;
+		int k, n = search_small(t, left_edge, SVG_EVENT_INDEL | SVG_EVENT_JUNCTION | SVG_EVENT_FUSION, ids);
+		int64_t found = -1;
+		int type;
+		svg_event *e;
+		for (k = 0; k < n; k++)
+			if (t->ev[ids[k]].large_side == right_edge) { found = (int64_t)ids[k]; break; }
+		r->result_flags |= GAPPED_FLAG;
+		if (found >= 0) { t->ev[found].supporting_reads++; return; }
+		id = new_event(t);
+		e = &t->ev[id];
+		e->small_side = left_edge;
+		e->large_side = right_edge + j->indel_at_junction;
+		e->critical_read_id = 2ull * read_no + (uint64_t)end;
+		type = SVG_EVENT_JUNCTION;
+		if (jumped) type = SVG_EVENT_FUSION;
+		if ((j->minor_coverage_start > r->confident_coverage_start) + (j->minor_position > r->selected_position) == 1)
+			type = SVG_EVENT_FUSION;
+		if (right_edge - left_edge > (uint32_t)p->maximum_intron_length) type = 0;
+		{
+			const uint32_t dist = e->large_side - e->small_side;
+			if (dist > MAX_INSERTION && type == SVG_EVENT_FUSION) {
+				int cov_end = j->minor_coverage_end > r->confident_coverage_end ? j->minor_coverage_end : r->confident_coverage_end;
+				int cov_start = j->minor_coverage_start < r->confident_coverage_start ? j->minor_coverage_start : r->confident_coverage_start;
+				int major_cov = r->confident_coverage_end - r->confident_coverage_start;
+				if (cov_end - cov_start < rl - 15 || major_cov > rl - 15) type = 0;
+			}
+			if (dist > MAX_INSERTION && type == SVG_EVENT_FUSION && j->minor_votes < 2) type = 0;
+			else if (type == SVG_EVENT_FUSION && j->minor_votes < 1) type = 0;
+			if (dist > MAX_INSERTION && type == SVG_EVENT_FUSION && r->selected_votes < 2) type = 0;
+			else if (type == SVG_EVENT_FUSION && r->selected_votes < 1) type = 0;
+			if (dist > MAX_INSERTION && type == SVG_EVENT_FUSION && (split < rl * 0.2 || split >= rl * 0.8)) type = 0;
+		}
+		if (type == SVG_EVENT_JUNCTION) {
+			e->is_negative_strand = !gtag;
+			e->event_type = SVG_EVENT_JUNCTION;
+			e->supporting_reads = 1;
+			e->indel_at_junction = j->indel_at_junction;
+			e->is_donor_found_or_annotation = (int8_t)donor_found;
+			e->small_side_increasing_coordinate = j->small_side_increasing_coordinate;
+			e->large_side_increasing_coordinate = j->large_side_increasing_coordinate;
+			put_event(t, id);
+		}
+		/* fusions are recorded only with fusion / long-deletion detection: the slot stays
+		 * type 0 (CHRO_EVENT_TYPE_REMOVED) like the reference's */
+	}
+}
+
+/* reverse_read (input-files.c:1113-1189, base space) with its conversion table: A/C/G/T/U
+ * complemented, every other character -> 'N' */
+static inline char rc_char(char c)
+{
+	switch (c) { case 'A': return 'T'; case 'C': return 'G'; case 'G': return 'C'; case 'T': return 'A'; case 'U': return 'A'; }
+	return 'N';
+}
+static void reverse_read(char *s, int len)
+{
+	int i;
+	for (i = 0; i < len / 2; i++) { char x = s[len - 1 - i]; s[len - 1 - i] = rc_char(s[i]); s[i] = rc_char(x); }
+	if (i * 2 == len - 1) s[i] = rc_char(s[i]);
+}
+
+/* has_better_mapping, core.c:3035-3047 (unsigned position arithmetic as in the reference) */
+static int has_better_mapping(const svg_params *p, const svg_mapping_result *recs, int b)
+{
+	const svg_mapping_result *x = &recs[b];
+	int k;
+	for (k = 0; k < b; k++) {
+		const svg_mapping_result *y = &recs[k];
+		if (x->selected_position >= y->selected_position - (uint32_t)p->max_indel_length - 1u &&
+		    x->selected_position <= y->selected_position + (uint32_t)p->max_indel_length + 1u)
+			if (x->confident_coverage_start >= y->confident_coverage_start &&
+			    x->confident_coverage_end <= y->confident_coverage_end) return 1;
+	}
+	return 0;
+}
+
+int svg_events_add_batch(svg_events *t, const svg_genome_arrays *g, const svg_params *p, const svg_event_params *ep_in,
+                         const svg_reads *r1, const svg_reads *r2, uint64_t first_read, svg_mapping_result *out,
+                         const svg_subjunc_result *jout, const uint16_t *big_margin)
+{
+	const int ends = r2 ? 2 : 1, mb = p ? p->multi_best : 0;
+	svg_event_params epd;
+	const svg_event_params *ep = ep_in;
+	scratch_t *s;
+	uint64_t i;
+	if (!t || !g || !p || !r1 || !out) { svg_set_error("svg_events_add_batch: NULL argument"); return SVG_E_ARG; }
+	if (r2 && r2->n_reads != r1->n_reads) { svg_set_error("svg_events_add_batch: r1/r2 differ in length"); return SVG_E_ARG; }
+	if (mb < 1 || mb > 3 || p->total_subreads < 2) { svg_set_error("svg_events_add_batch: bad parameters"); return SVG_E_ARG; }
+	if (p->do_breakpoint_detection && !jout) { svg_set_error("svg_events_add_batch: subjunc records required"); return SVG_E_ARG; }
+	if (p->do_breakpoint_detection && p->do_big_margin_filtering_for_junctions && !big_margin) {
+		svg_set_error("svg_events_add_batch: big-margin records required"); return SVG_E_ARG;
+	}
+	if (!ep) { svg_event_params_default(&epd); ep = &epd; }
+	if (p->do_breakpoint_detection)
+		for (i = 0; i < r1->n_reads; i++)
+			if (r1->lens[i] > LONG_READ || (r2 && r2->lens[i] > LONG_READ)) {
+				svg_set_error("events of subjunc reads over %d bp (short-exon search, fragile junction voting) "
+				              "are not implemented", LONG_READ);
+				return SVG_E_UNSUPPORTED;
+			}
+	s = calloc(1, sizeof *s);
+	s->cols = SVG_MAX_READ_LENGTH;
+	s->rows = SVG_MAX_READ_LENGTH + 20;
+	s->dp = malloc(sizeof(int16_t) * (size_t)s->rows * s->cols);
+	s->mask = malloc((size_t)s->rows * s->cols);
+	if (!s->dp || !s->mask) { free(s->dp); free(s->mask); free(s); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	for (i = 0; i < r1->n_reads; i++) {
+		int e;
+		for (e = 0; e < ends; e++) {
+			const svg_reads *rr = e ? r2 : r1;
+			char text[SVG_MAX_READ_LENGTH + 2];
+			int rl = rr->lens[i], b, has_reversed;
+			svg_mapping_result *recs = out + ((size_t)i * ends + e) * mb;
+			if (rl > SVG_READ_KEEP) rl = SVG_READ_KEEP;
+			memcpy(text, rr->seq + rr->offsets[i], (size_t)rl);
+			text[rl] = 0;
+			/* -S reversal at fetch (core.c:1186-1198), then the strand loop's one reversal after
+			 * strand 0 (core.c:3229-3234): the text is in the reversed state afterwards */
+			if (e ? p->reverse_r2 : p->reverse_r1) reverse_read(text, rl);
+			reverse_read(text, rl);
+			has_reversed = 1;
+			for (b = 0; b < mb; b++) {
+				svg_mapping_result *r = &recs[b];
+				const garray *a;
+				int should;
+				if (r->selected_votes < 1) continue;
+				should = (r->result_flags & NEG_FLAG) ? 1 : 0;
+				if (should != has_reversed) { has_reversed = !has_reversed; reverse_read(text, rl); }
+				a = value_index(g, r->selected_position, rl);
+				if (!has_better_mapping(p, recs, b)) find_indels(t, s, a, p, ep, r, text, rl);
+				if (p->do_breakpoint_detection)
+					find_junctions(t, g, p, r, &jout[((size_t)i * ends + e) * mb + b],
+					               big_margin ? big_margin + ((size_t)i * ends + e) * SVG_BIG_MARGIN_WORDS : NULL, rl,
+					               first_read + i, e);
+			}
+		}
+	}
+	free(s->dp); free(s->mask); free(s);
+	return 0;
+}
+
+/* ------------------------------------------------------------------ merge (finalise) */
+typedef struct { const svg_event *e; uint64_t order; } mref_t;
+
+/* conc_sort_compare, core-indel.c:944-970 (|value| 2-3: different events, 0-1: same event) */
+static int conc_compare(const svg_event *l, const svg_event *r)
+{
+	if (l->small_side > r->small_side) return 3;
+	if (l->small_side < r->small_side) return -3;
+	if (l->large_side > r->large_side) return 3;
+	if (l->large_side < r->large_side) return -3;
+	if (abs(l->indel_length) < abs(r->indel_length)) return 2;
+	if (abs(l->indel_length) > abs(r->indel_length)) return -2;
+	if (l->indel_length > r->indel_length) return -2;
+	if (l->indel_length < r->indel_length) return 2;
+	if ((l->is_donor_found_or_annotation & 64) && !(r->is_donor_found_or_annotation & 64)) return 1;
+	if (!(l->is_donor_found_or_annotation & 64) && (r->is_donor_found_or_annotation & 64)) return -1;
+	if (l->supporting_reads > r->supporting_reads) return -1;
+	if (l->supporting_reads < r->supporting_reads) return 1;
+	return 0;
+}
+
+static int mref_cmp(const void *a, const void *b)
+{
+	const mref_t *x = a, *y = b;
+	int c = conc_compare(x->e, y->e);
+	if (c) return c;
+	return x->order < y->order ? -1 : x->order > y->order;
+}
+
+int svg_events_merge(svg_events *dst, svg_events *const *tables, int n)
+{
+	uint64_t total = 0, i, k = 0, start;
+	mref_t *refs;
+	int ti;
+	if (!dst || (n > 0 && !tables)) { svg_set_error("svg_events_merge: NULL argument"); return SVG_E_ARG; }
+	for (ti = 0; ti < n; ti++)
+		if (!tables[ti] || tables[ti] == dst) { svg_set_error("svg_events_merge: NULL table or dst among the inputs"); return SVG_E_ARG; }
+	for (ti = 0; ti < n; ti++) total += tables[ti]->n;
+	refs = malloc(sizeof(mref_t) * (total + 1));
+	for (ti = 0; ti < n; ti++)
+		for (i = 0; i < tables[ti]->n; i++)
+			if (tables[ti]->ev[i].event_type) { refs[k].e = &tables[ti]->ev[i]; refs[k].order = k; k++; }
+	qsort(refs, k, sizeof(mref_t), mref_cmp);
+	/* a group of records of one event: the merged body is a copy of the group's last record
+	 * plus the sums / maxima of the others (core-indel.c:1058-1111) */
+	for (start = 0; start < k;) {
+		uint64_t end = start + 1, m;
+		svg_event body;
+		while (end < k && abs(conc_compare(refs[end - 1].e, refs[end].e)) <= 1) end++;
+		body = *refs[end - 1].e;
+		for (m = start; m + 1 < end; m++) {
+			const svg_event *o = refs[m].e;
+			body.supporting_reads += o->supporting_reads;
+			body.anti_supporting_reads += o->anti_supporting_reads;
+			body.final_counted_reads += o->final_counted_reads;
+			body.final_reads_mismatches += o->final_reads_mismatches;
+			body.critical_supporting_reads += o->critical_supporting_reads;
+			if (o->junction_flanking_left > body.junction_flanking_left) body.junction_flanking_left = o->junction_flanking_left;
+			if (o->junction_flanking_right > body.junction_flanking_right) body.junction_flanking_right = o->junction_flanking_right;
+			body.is_donor_found_or_annotation |= o->is_donor_found_or_annotation;
+			if (body.connected_next_event_distance > 0 && o->connected_next_event_distance > 0)
+				body.connected_next_event_distance = body.connected_next_event_distance < o->connected_next_event_distance ?
+				                                     body.connected_next_event_distance : o->connected_next_event_distance;
+			else if (o->connected_next_event_distance > body.connected_next_event_distance)
+				body.connected_next_event_distance = o->connected_next_event_distance;
+			if (body.connected_previous_event_distance > 0 && o->connected_previous_event_distance > 0)
+				body.connected_previous_event_distance = body.connected_previous_event_distance < o->connected_previous_event_distance ?
+				                                         body.connected_previous_event_distance : o->connected_previous_event_distance;
+			else if (o->connected_previous_event_distance > body.connected_previous_event_distance)
+				body.connected_previous_event_distance = o->connected_previous_event_distance;
+		}
+		{
+			uint64_t id = new_event(dst);
+			dst->ev[id] = body;
+			put_event(dst, id);
+		}
+		start = end;
+	}
+	free(refs);
+	return 0;
+}

@@ -27,8 +27,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-from subread_amd.abi import (MAPPING_DTYPE, SUBJUNC_DTYPE, ReadBatch, read_fastq, default_params,  # noqa: E402
-                             PROGRAM_ALIGN, PROGRAM_SUBJUNC)
+from subread_amd.abi import (MAPPING_DTYPE, SUBJUNC_DTYPE, EVENT_DTYPE, ReadBatch, read_fastq,  # noqa: E402
+                             default_params, PROGRAM_ALIGN, PROGRAM_SUBJUNC)
 from subread_amd.sim import Genome, write_fastq  # noqa: E402
 from tests.common import SYNTH_GENOMES, index_recipe, synth_genome  # noqa: E402
 
@@ -69,6 +69,51 @@ def run_ref(prog, prefix, f1, f2, dump, extra=()):
     if r.returncode != 0:
         raise RuntimeError(r.stdout[-2000:] + r.stderr[-2000:])
     return np.fromfile(dump, dtype=np.uint8)
+
+
+def run_ref_events(prog, prefix, f1, f2, path, extra=()):
+    """The reference's event table after the voting step (-T 1: one thread table, events in
+    read order) and the raw result_flags of every record (ref_dump_hook.c, SVG_REF_EVENTS)."""
+    exe = REFBIN + ("/subjunc-dump" if prog == PROGRAM_SUBJUNC else "/subread-align-dump")
+    if os.path.exists(path):
+        os.remove(path)
+    args = [exe, "-T", "1", "-i", prefix, "-r", f1, "-o", path + ".sam"] + list(extra)
+    if prog == PROGRAM_ALIGN:
+        args += ["-t", "1"]
+    if f2:
+        args += ["-R", f2]
+    r = subprocess.run(args, env=dict(os.environ, SVG_REF_EVENTS=path), capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(r.stdout[-2000:] + r.stderr[-2000:])
+    b = open(path, "rb").read()
+    n = int(np.frombuffer(b[:8], np.uint64)[0])
+    ev = np.frombuffer(b[8:8 + EVENT_DTYPE.itemsize * n], EVENT_DTYPE)
+    rest = b[8 + EVENT_DTYPE.itemsize * n:]
+    nr = int(np.frombuffer(rest[:8], np.uint64)[0])
+    return ev, np.frombuffer(rest[8:8 + 2 * nr], np.uint16)
+
+
+def save_events(name, prog, idx_prefix, r1, r2, over, tmp):
+    """tests/golden/events/<case>.npz: the reference's events + raw record flags for the case's
+    reads (subjunc cases with reads over 160 bp are outside the event search's scope)."""
+    if prog == PROGRAM_SUBJUNC and (r1.lens.max() > 160 or (r2 is not None and r2.lens.max() > 160)):
+        return
+    extra = []
+    if "total_subreads" in over:
+        extra += ["-n", str(over["total_subreads"])]
+    if "max_indel_length" in over:
+        extra += ["-I", str(over["max_indel_length"])]
+    f1 = os.path.join(tmp, name + "_e1.fq")
+    write_fastq(f1, r1)
+    f2 = None
+    if r2 is not None:
+        f2 = os.path.join(tmp, name + "_e2.fq")
+        write_fastq(f2, r2)
+    ev, flags = run_ref_events(prog, idx_prefix, f1, f2, os.path.join(tmp, name + ".ev"), extra)
+    os.makedirs(os.path.join(GOLD, "events"), exist_ok=True)
+    np.savez_compressed(os.path.join(GOLD, "events", name + ".npz"), events=ev.view(np.uint8).reshape(len(ev), EVENT_DTYPE.itemsize),
+                        flags=flags)
+    print("events", name, len(ev), "events,", int((flags & 64 > 0).sum()), "gapped records")
 
 
 def take(batch, idx):
@@ -285,9 +330,16 @@ def main():
         sj_lp2 = simulate_spliced_reads(long777, 1500, 150, seed=26, max_intron=20000)
         cases.append(("sj_pe_mb_long_gappedM6", PROGRAM_SUBJUNC, True, "long777_gappedM6", {}, sj_lp1, sj_lp2,
                       "long777 spliced reads seeds 25/26 (150 bp) on the 4-block -M 6 index"))
-        only = set(sys.argv[1:])
+        only = set(a for a in sys.argv[1:] if not a.startswith("--"))
         if only:
             cases = [c for c in cases if c[0] in only]
+        if "--events-only" in sys.argv:
+            # event tables for the committed cases (reads from their fixtures)
+            from tests.common import Case
+            for name, prog, paired, ikey, over, r1, r2, note in cases:
+                cs = Case(name)
+                save_events(name, prog, idx[ikey], cs.r1, cs.r2, over, tmp)
+            return
 
         for name, prog, paired, ikey, over, r1, r2, note in cases:
             extra = []
@@ -299,6 +351,7 @@ def main():
             f2 = fq(r2, name + "_2") if r2 is not None else None
             raw = run_ref(prog, idx[ikey], f1, f2, os.path.join(tmp, name + ".bin"), extra)
             save_case(name, prog, paired, ikey, over, r1, r2, raw, 2 if paired else 1, note)
+            save_events(name, prog, idx[ikey], r1, r2, over, tmp)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

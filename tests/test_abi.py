@@ -1,5 +1,5 @@
-"""CPU: the C-ABI library loads, exports every symbol include/subread_vote.h
-declares, and its host-side pieces behave (no GPU compute here)."""
+"""CPU: the C-ABI library loads, exports every symbol include/subread_vote.h and
+include/subread_events.h declare, and its host-side pieces behave (no GPU compute here)."""
 import ctypes
 import re
 import os
@@ -14,9 +14,12 @@ ensure_built()
 
 
 def header_symbols():
-    txt = open(os.path.join(ROOT, "include", "subread_vote.h")).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(svg_[a-z_]+)\s*\(", txt)))
+    syms = set()
+    for h in ("subread_vote.h", "subread_events.h"):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        syms |= set(re.findall(r"\b(svg_[a-z_]+)\s*\(", txt))
+    return sorted(syms)
 
 
 def test_library_exports_every_header_symbol():

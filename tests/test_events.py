@@ -1,0 +1,117 @@
+"""Host post-vote events (include/subread_events.h): the indel / junction event table the
+reference builds from the vote records in its final voting run (find_new_indels,
+core-indel.c:1831; find_new_junctions, core-junction.c:3836; merged by
+finalise_indel_and_junction_thread, core-indel.c:1012) and the CORE_IS_GAPPED_READ marks on
+the records.  Known answers: tests/golden/events/<case>.npz, dumped from the reference run
+with -T 1 (tests/golden/make_golden.py, oracle/ref_dump_hook.c).
+
+CPU tests feed the reference's own records (the golden vote dump); the GPU test feeds the
+records of the HIP vote path."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from subread_amd.abi import EVENT_DTYPE, MAPPING_DTYPE, SUBJUNC_DTYPE, BIG_MARGIN_WORDS
+from tests.common import GOLD, Case, ensure_built
+
+ensure_built()
+
+EVENT_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "events", "*.npz")))
+
+
+def load_events(name):
+    z = np.load(os.path.join(GOLD, "events", name + ".npz"), allow_pickle=False)
+    return z["events"].copy().view(EVENT_DTYPE).reshape(-1), z["flags"]
+
+
+def split_records(c):
+    """golden vote dump -> (mapping, subjunc|None, big_margin|None) arrays"""
+    n, mb, e = len(c.r1), c.params.multi_best, c.ends
+    raw = c.expected
+    out = raw[:, :e * mb * 68].copy().view(MAPPING_DTYPE).reshape(n, e, mb)
+    o, jout, bm = e * mb * 68, None, None
+    if c.params.do_breakpoint_detection:
+        jout = raw[:, o:o + e * mb * 16].copy().view(SUBJUNC_DTYPE).reshape(n, e, mb)
+        o += e * mb * 16
+    if c.params.do_big_margin_filtering_for_junctions:
+        bm = raw[:, o:o + e * BIG_MARGIN_WORDS * 2].copy().view(np.uint16).reshape(n, e, BIG_MARGIN_WORDS)
+    return out, jout, bm
+
+
+def describe(got, want, limit=4):
+    if len(got) != len(want):
+        g = set((int(x["small_side"]), int(x["large_side"]), int(x["indel_length"])) for x in got)
+        w = set((int(x["small_side"]), int(x["large_side"]), int(x["indel_length"])) for x in want)
+        return "%d events, reference %d; only ours %s; only reference %s" % (len(got), len(want), sorted(g - w)[:5],
+                                                                           sorted(w - g)[:5])
+    bad = np.nonzero((got.view(np.uint8).reshape(len(got), -1) != want.view(np.uint8).reshape(len(want), -1)).any(1))[0]
+    return "\n".join(["%d of %d events differ" % (len(bad), len(got))] +
+                     ["  ours %s\n  ref  %s" % (got[i], want[i]) for i in bad[:limit]])
+
+
+def check(got, flags, want, wflags):
+    assert len(got) == len(want) and (got.view(np.uint8) == want.view(np.uint8)).all(), describe(got, want)
+    assert (flags == wflags).all(), "%d records' flags differ" % int((flags != wflags).sum())
+
+
+@pytest.mark.parametrize("name", EVENT_CASES)
+def test_events_match_reference(name, index_cache):
+    import subread_amd as sa
+    c = Case(name)
+    want, wflags = load_events(name)
+    g = sa.GenomeArrays(index_cache.get(c.index_key))
+    recs = split_records(c)
+    got = sa.find_events(g, c.params, c.r1, c.r2, recs)
+    check(got, recs[0]["result_flags"].reshape(-1).view(np.uint16), want, wflags)
+    g.close()
+
+
+def test_events_merge_of_shards_equals_one_table(index_cache):
+    """Per-shard tables merged like the reference's per-thread tables give the same support
+    counts and event set as one table over all reads (critical_read_id and inserted bases
+    come from the first record of a group, as in one table)."""
+    import subread_amd as sa
+    c = Case("sj_pe_gapped_junc")
+    g = sa.GenomeArrays(index_cache.get(c.index_key))
+    whole, _ = load_events(c.name)
+    out, jout, bm = split_records(c)
+    tables = []
+    cuts = [0, 333, 1000, len(c.r1)]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        t = sa.EventTable()
+        t.add_batch(g, c.params, c.r1.slice(a, b), c.r2.slice(a, b), (out[a:b], jout[a:b], bm[a:b]), first_read=a)
+        tables.append(t)
+    m = sa.EventTable.merge(tables).events()
+    key = ["small_side", "large_side", "indel_length", "supporting_reads", "event_type"]
+    assert len(m) == len(whole)
+    for k in key:
+        assert (m[k] == whole[k]).all(), k
+    g.close()
+
+
+def test_events_reject_long_subjunc_reads(index_cache):
+    import subread_amd as sa
+    c = Case("sj_se_full_long")
+    g = sa.GenomeArrays(index_cache.get(c.index_key))
+    with pytest.raises(sa.SvgError, match="not implemented"):
+        sa.find_events(g, c.params, c.r1, None, split_records(c))
+    g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", [n for n in EVENT_CASES if len(load_events(n)[0]) > 0])
+def test_gpu_records_give_reference_events(name, index_cache):
+    """The whole drop-in stage: HIP vote -> host events == the reference's event table."""
+    import subread_amd as sa
+    c = Case(name)
+    want, wflags = load_events(name)
+    pre = index_cache.get(c.index_key)
+    ix = sa.VoteIndex(pre, device=0)
+    out, jout, bm = ix.vote(c.params, c.r1, c.r2)
+    ix.close()
+    g = sa.GenomeArrays(pre)
+    got = sa.find_events(g, c.params, c.r1, c.r2, (out, jout, bm))
+    check(got, out["result_flags"].reshape(-1).view(np.uint16), want, wflags)
+    g.close()
