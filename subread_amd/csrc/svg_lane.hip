@@ -39,7 +39,7 @@
 #include "svg_device.h"
 
 #define LROWS 30
-#define CW 7                 // cold words per slot: cs | ce << 8, then rec[0..23] as bytes
+#define CW 7                 // cold words per slot: cs | rec[0] << 8, then rec[0..23] as bytes (once spilled)
 
 // ---------------------------------------------------------------------------------------------
 // gather: one thread per (strand, read) of a chunk
@@ -135,19 +135,37 @@ struct LParams {
 	int stat_base, final_pass;    // diagnostics at stats[stat_base..+4]: deferrals by reason (3), candidates, deferrals
 };
 
-// meta: votes [0,6) | last [6,12) | toli [12,17) | cursor [17,23) (6-bit signed) | next [23,29)
-__device__ __forceinline__ int lm_votes(uint32_t m) { return (int)(m & 63u); }
-__device__ __forceinline__ int lm_last(uint32_t m) { return (int)((m >> 6) & 63u); }
-__device__ __forceinline__ int lm_toli(uint32_t m) { return (int)((m >> 12) & 31u); }
-__device__ __forceinline__ int lm_cursor(uint32_t m) { return ((int)(m << 9)) >> 26; }
-__device__ __forceinline__ uint32_t lm_next(uint32_t m) { return (m >> 23) & 63u; }
+// meta: votes [0,5) | last [5,10) | toli [10,15) | cursor [15,21) (6-bit signed) | next [21,27) |
+// end [27] | spilled [28] | x [29,31).  votes and last (a subread number + 1) are <= 31 on this
+// path (applied <= 31).  end: the slot's read end (paired-end lanes share one slot pool between
+// the two tables).  spilled: the slot's indel recorder lives in the cold scratch; until its first
+// indel section opens, the recorder is (first kP1, last, 0) and stays implicit.  x: the gap slot
+// of the last vote, which with last gives coverage_end without a cold store per vote.
+#define LM_END   (1u << 27)
+#define LM_SPILL (1u << 28)
+__device__ __forceinline__ int lm_votes(uint32_t m) { return (int)(m & 31u); }
+__device__ __forceinline__ int lm_last(uint32_t m) { return (int)((m >> 5) & 31u); }
+__device__ __forceinline__ int lm_toli(uint32_t m) { return (int)((m >> 10) & 31u); }
+__device__ __forceinline__ int lm_cursor(uint32_t m) { return ((int)(m << 11)) >> 26; }
+__device__ __forceinline__ uint32_t lm_next(uint32_t m) { return (m >> 21) & 63u; }
+__device__ __forceinline__ int lm_x(uint32_t m) { return (int)(m >> 29); }
 __device__ __forceinline__ uint32_t lm_pack(int votes, int last, int toli, int cursor, uint32_t next)
 {
-	return (uint32_t)votes | ((uint32_t)last << 6) | ((uint32_t)toli << 12) | (((uint32_t)cursor & 63u) << 17) | (next << 23);
+	return (uint32_t)votes | ((uint32_t)last << 5) | ((uint32_t)toli << 10) | (((uint32_t)cursor & 63u) << 15) | (next << 21);
 }
-__device__ __forceinline__ uint32_t lm_set_next(uint32_t m, uint32_t next) { return (m & ~(63u << 23)) | (next << 23); }
-// bit 29: the slot's read end (paired-end lanes share one slot pool between the two tables)
-__device__ __forceinline__ uint32_t lm_endbit(uint32_t m) { return m & (1u << 29); }
+__device__ __forceinline__ uint32_t lm_set_next(uint32_t m, uint32_t next) { return (m & ~(63u << 21)) | (next << 21); }
+__device__ __forceinline__ uint32_t lm_endbit(uint32_t m) { return m & LM_END; }
+// the record-side summary of a slot: spilled | last << 1 | x << 6
+__device__ __forceinline__ uint32_t lm_ext(uint32_t m) { return ((m >> 28) & 1u) | ((uint32_t)lm_last(m) << 1) | ((uint32_t)lm_x(m) << 6); }
+// coverage_end of a slot: the last vote's subread offset + 16 (core.c:3169-3171; sorted-hashtable.c:1046)
+// the gap slot of a subread offset (off = base - base % gap + x); gap is 1 (-F) or 3 (default)
+__device__ __forceinline__ int lgap_x(int off, int gap) { return gap == 1 ? 0 : (gap == 3 ? off % 3 : off % gap); }
+__device__ __forceinline__ int lcov_end(int last, int x, int step, int gap)
+{
+	int off = (int)(((int64_t)step * (last - 1)) >> 16);
+	if (gap > 1) off -= lgap_x(off, gap) - x;
+	return off + 16;
+}
 
 __device__ __forceinline__ uint32_t lrow(uint32_t x) { return (x / 5u) % LROWS; }
 
@@ -237,7 +255,7 @@ struct Lane {
 
 	// gehash_go_X body for one candidate of end E (round 0; sorted-hashtable.c:995-1107)
 	template <int E>
-	__device__ __forceinline__ void vote(int st, uint32_t kv, int kP1, int off, uint32_t high_b)
+	__device__ __forceinline__ void vote(int st, uint32_t kv, int kP1, int off, uint32_t high_b, int gap)
 	{
 		const uint32_t r0 = lrow(kv), rp = lrow(kv + 5u), rm = lrow(kv - 5u);
 		uint32_t tail = NIL, tailM = 0;
@@ -263,11 +281,20 @@ struct Lane {
 				if (kP1 > last) {
 					votes += 1;
 					int cur = lm_cursor(M);
-					*((uint8_t *)cw(st, s, 0) + 1) = (uint8_t)(off + 16);   // coverage_end
-					if (d == cur) *recb(st, s, tl + 1) = (int8_t)kP1;
+					uint32_t spill = M & LM_SPILL;
+					// coverage_end = off + 16 follows from (kP1, x) in the meta (lcov_end)
+					if (d == cur) { if (spill) *recb(st, s, tl + 1) = (int8_t)kP1; }   // implicit rec[1] = last
 					else {
 						const int t2 = tl + 3;
-						if (t2 < 21) {
+						if (!spill) {
+							// first indel section (tl == 0): the recorder goes to the cold scratch,
+							// rec[0..7] = first kP1, last, 0, kP1, kP1, d, 0, -
+							const uint32_t r0 = (*cw(st, s, 0) >> 8) & 0xffu;
+							*cw(st, s, 1) = r0 | ((uint32_t)(uint8_t)last << 8) | ((uint32_t)(uint8_t)kP1 << 24);
+							*cw(st, s, 2) = (uint32_t)(uint8_t)kP1 | ((uint32_t)(uint8_t)(int8_t)d << 8);
+							tl = 3;
+							spill = LM_SPILL;
+						} else if (t2 < 21) {
 							tl = t2;
 							*recb(st, s, t2) = (int8_t)kP1;
 							*recb(st, s, t2 + 1) = (int8_t)kP1;
@@ -276,13 +303,13 @@ struct Lane {
 						}
 						cur = d;
 					}
-					M = lm_pack(votes, kP1, tl, cur, lm_next(M)) | lm_endbit(M);
+					M = lm_pack(votes, kP1, tl, cur, lm_next(M)) | lm_endbit(M) | spill | ((uint32_t)lgap_x(off, gap) << 29);
 					pm[s * 64 + lane].y = M;
 					if (max_vote[E] < votes) max_vote[E] = votes;
 					found = true;
 					break;
 				}
-				if (chg) { M = lm_pack(votes, last, tl, lm_cursor(M), lm_next(M)) | lm_endbit(M); pm[s * 64 + lane].y = M; }
+				if (chg) { M = lm_pack(votes, last, tl, lm_cursor(M), lm_next(M)) | (M & (LM_END | LM_SPILL | (3u << 29))); pm[s * 64 + lane].y = M; }
 			}
 			if (ri == 0) { tail = s; tailM = M; n0++; }
 			s = lm_next(M);
@@ -291,9 +318,8 @@ struct Lane {
 		if (!found && kv >= low && kv <= high_b && (K <= 24 || n0 < 24)) {
 			if (nslots == K) { dfr = true; why = 2; return; }
 			const uint32_t ns = (uint32_t)nslots++;
-			pm[ns * 64 + lane] = make_uint2(kv, lm_pack(1, kP1, 0, 0, NIL) | ((uint32_t)E << 29));
-			*cw(st, (int)ns, 0) = (uint32_t)off | ((uint32_t)(off + 16) << 8);
-			*cw(st, (int)ns, 1) = (uint32_t)kP1 | ((uint32_t)kP1 << 8);   // rec[0..3] = k+1, k+1, 0, 0
+			pm[ns * 64 + lane] = make_uint2(kv, lm_pack(1, kP1, 0, 0, NIL) | (E ? LM_END : 0u) | ((uint32_t)lgap_x(off, gap) << 29));
+			*cw(st, (int)ns, 0) = (uint32_t)off | ((uint32_t)kP1 << 8);   // coverage_start, rec[0] (first kP1)
 			if (tail == NIL) set_head<E>(r0, ns);
 			else pm[tail * 64 + lane].y = lm_set_next(tailM, ns);
 			if (max_vote[E] < 1) max_vote[E] = 1;
@@ -303,19 +329,30 @@ struct Lane {
 
 
 // mapping_result_t of a bigtable record (copy_vote_to_alignment_res, core-junction.c:1058-1071;
-// indel_recorder_copy, sorted-hashtable.c:1144) from its source slot's cold state
+// indel_recorder_copy, sorted-hashtable.c:1144) from its source slot's cold state and the slot's
+// record summary ext (lm_ext): coverage_end from (last, x); an unspilled recorder is
+// (first kP1, last, 0)
 template <class LT>
-__device__ __forceinline__ void write_record(const LT &L, int src, uint32_t pos, int v, int u, uint32_t (&w)[17])
+__device__ __forceinline__ void write_record(const LT &L, int src, uint32_t pos, int v, int u, uint32_t ext, int step,
+                                             int gap, uint32_t (&w)[17])
 {
 #pragma unroll
 	for (int k = 0; k < 17; k++) w[k] = 0;
 	w[2] = (uint32_t)(uint16_t)v | ((uint32_t)(uint16_t)u << 16);
 	if (src >= 0) {
 		const int st = src >> 6, s = src & 63;
+		const int lastk = (int)((ext >> 1) & 31u), xg = (int)(ext >> 6);
 		uint32_t rw[6];
+		const uint32_t w0 = *L.cw(st, s, 0);
+		if (ext & 1u) {
 #pragma unroll
-		for (int k = 0; k < 6; k++) rw[k] = *L.cw(st, s, 1 + k);
-		const uint32_t c0w = *L.cw(st, s, 0);
+			for (int k = 0; k < 6; k++) rw[k] = *L.cw(st, s, 1 + k);
+		} else {
+			rw[0] = ((w0 >> 8) & 0xffu) | ((uint32_t)lastk << 8);   // rec[3] = 0 ends it
+#pragma unroll
+			for (int k = 1; k < 6; k++) rw[k] = 0;
+		}
+		const uint32_t c0w = (w0 & 0xffu) | ((uint32_t)lcov_end(lastk, xg, step, gap) << 8);
 		int nrec = 0, last = 0;
 #pragma unroll
 		for (int t = 0; t < 7; t++) {
@@ -379,6 +416,7 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 		int rsrc0 = -1, rsrc1 = -1, rsrc2 = -1;
 		uint32_t rpos0 = 0, rpos1 = 0, rpos2 = 0;
 		int rv0 = 0, rv1 = 0, rv2 = 0, ru0 = 0, ru1 = 0, ru2 = 0;
+		uint32_t rx0 = 0, rx1 = 0, rx2 = 0;   // lm_ext of the records' slots
 		int nc_read = 0;
 		// subjunc: the read's big-margin records (insert_big_margin_record, core-junction.c:789-811):
 		// votes | start << 16 ... as (votes, start | end << 16) per record
@@ -404,7 +442,7 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				const uint32_t kv = kv_a, pk = pk_a;
 				kv_a = kv_b; pk_a = pk_b;
 				if (j + 2 < mycnt) { kv_b = cb[(size_t)(j + 2) * lp.cs]; pk_b = pb[(size_t)(j + 2) * lp.cs]; }
-				if (j < mycnt && !L.dfr) L.template vote<0>(st, kv, (int)(pk & 63u), (int)(pk >> 6), high_b);
+				if (j < mycnt && !L.dfr) L.template vote<0>(st, kv, (int)(pk & 63u), (int)(pk >> 6), high_b, lp.gap);
 			}
 			} else {
 			// ---- fused gather: the read's probe records of this strand in a register window
@@ -457,7 +495,7 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				q0 = q1; q1 = q2; q2 = q3;
 				k0 = k1; k1 = k2; k2 = k3;
 				if (j + 4 < mycnt) { next(it, pkn); q3 = lp.vals[it]; k3 = pkn; }
-				if (j < mycnt && !L.dfr) L.template vote<0>(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b);
+				if (j < mycnt && !L.dfr) L.template vote<0>(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b, lp.gap);
 			}
 			}
 			if (L.dfr) continue;
@@ -480,8 +518,8 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 								const uint32_t M = L.pm[q * 64 + L.lane].y;
 								const int v = lm_votes(M);
 								if (v >= t2) {
-									const uint32_t w0 = *L.cw(st, (int)q, 0);
-									const int rs = (int)(w0 & 0xffu), re = (int)((w0 >> 8) & 0xffu);
+									const int rs = (int)(*L.cw(st, (int)q, 0) & 0xffu);
+									const int re = lcov_end(lm_last(M), lm_x(M), step, lp.gap);
 									const uint32_t vv = (uint32_t)(v & 255);
 									const uint32_t se = st ? ((uint32_t)(uint16_t)(len - re) | ((uint32_t)(uint16_t)(len - rs) << 16))
 									                       : ((uint32_t)rs | ((uint32_t)re << 16));
@@ -534,18 +572,21 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				// single-end results: simples with >= min_votes_first votes, distinct positions
 				int cur = 0;
 				int ts0 = -1, ts1 = -1, ts2 = -1, tu0 = 0, tu1 = 0, tu2 = 0, tv0 = 0, tv1 = 0, tv2 = 0;
-				uint32_t tp0 = 0, tp1 = 0, tp2 = 0;
+				uint32_t tp0 = 0, tp1 = 0, tp2 = 0, tx0 = 0, tx1 = 0, tx2 = 0;
 				auto emit = [&](int kind, uint32_t pos, int v) __attribute__((always_inline)) {
 					if (cur >= mb || v < mvf) return;
 					if ((cur > 0 && tp0 == pos) || (cur > 1 && tp1 == pos)) return;
 					int src, u, vv = v;
-					if (kind & 128) { src = (st << 6) | (kind & 63); u = applied; }
+					uint32_t x;
+					if (kind & 128) { src = (st << 6) | (kind & 63); u = applied; x = lm_ext(L.pm[(kind & 63) * 64 + L.lane].y); }
 					else {
 						src = sel3(kind, rsrc0, rsrc1, rsrc2);
 						u = sel3(kind, ru0, ru1, ru2);
 						pos = sel3(kind, rpos0, rpos1, rpos2);
 						vv = sel3(kind, rv0, rv1, rv2);
+						x = sel3(kind, rx0, rx1, rx2);
 					}
+					PUT3(cur, tx0, tx1, tx2, x);
 					PUT3(cur, ts0, ts1, ts2, src);
 					PUT3(cur, tp0, tp1, tp2, pos);
 					PUT3(cur, tv0, tv1, tv2, vv);
@@ -566,16 +607,14 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 						const int sM = src & 63;
 						const uint2 eM = L.pm[sM * 64 + L.lane];
 						const int vM = lm_votes(eM.y);
-						const uint32_t wM = *L.cw(st, sM, 0);
-						const int csM = (int)(wM & 0xffu), ceM = (int)((wM >> 8) & 0xffu);
+						const int csM = (int)(*L.cw(st, sM, 0) & 0xffu), ceM = lcov_end(lm_last(eM.y), lm_x(eM.y), step, lp.gap);
 						for (int q = 0; q < L.nslots; q++) {
 							if (q == sM) continue;
 							const uint2 e2 = L.pm[q * 64 + L.lane];
 							if (vM < lm_votes(e2.y)) continue;
 							const long long dist = (long long)eM.x - (long long)e2.x;
 							if ((dist < 0 ? -dist : dist) > (long long)lp.max_intron) continue;
-							const uint32_t w2 = *L.cw(st, q, 0);
-							const int cs2 = (int)(w2 & 0xffu), ce2 = (int)((w2 >> 8) & 0xffu);
+							const int cs2 = (int)(*L.cw(st, q, 0) & 0xffu), ce2 = lcov_end(lm_last(e2.y), lm_x(e2.y), step, lp.gap);
 							if (csM == cs2 || ceM == ce2) continue;
 							if (csM > cs2 ? eM.x < e2.x : eM.x > e2.x) continue;
 							const int ov = csM > cs2 ? ce2 - csM : ceM - cs2;
@@ -587,9 +626,9 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 					}
 					if (L.dfr) continue;
 				}
-				if (cur > 0) { rsrc0 = ts0; rpos0 = tp0; rv0 = tv0; ru0 = tu0; } else rv0 = 0;
-				if (cur > 1) { rsrc1 = ts1; rpos1 = tp1; rv1 = tv1; ru1 = tu1; } else rv1 = 0;
-				if (cur > 2) { rsrc2 = ts2; rpos2 = tp2; rv2 = tv2; ru2 = tu2; } else rv2 = 0;
+				if (cur > 0) { rsrc0 = ts0; rpos0 = tp0; rv0 = tv0; ru0 = tu0; rx0 = tx0; } else rv0 = 0;
+				if (cur > 1) { rsrc1 = ts1; rpos1 = tp1; rv1 = tv1; ru1 = tu1; rx1 = tx1; } else rv1 = 0;
+				if (cur > 2) { rsrc2 = ts2; rpos2 = tp2; rv2 = tv2; ru2 = tu2; rx2 = tx2; } else rv2 = 0;
 			} else if (rv0 < 1) {
 				if (applied > ru0) ru0 = applied;   // used_subreads_in_vote (noninformative stays 0)
 			}
@@ -617,7 +656,7 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				const int v = sel3(i, rv0, rv1, rv2);
 				const int u = sel3(i, ru0, ru1, ru2);
 				uint32_t w[17];
-				write_record(L, src, pos, v, u, w);
+				write_record(L, src, pos, v, u, sel3(i, rx0, rx1, rx2), step, lp.gap, w);
 				if constexpr (SJ) {
 					// no minor half on the lane path: empty subjunc_result_t
 					uint4 *jd = (uint4 *)(lp.jout + ((size_t)r * mb + i) * 16);
@@ -712,7 +751,8 @@ __device__ __forceinline__ void pl_put(uint32_t (&w)[PLW], int i, uint32_t id)
 #define RM(src, v, u) ((uint32_t)((src) + 1) | ((uint32_t)(v) << 8) | ((uint32_t)(u) << 16))
 #define RM_SRC(m) ((int)((m) & 255u) - 1)
 #define RM_V(m) ((int)(((m) >> 8) & 255u))
-#define RM_U(m) ((int)((m) >> 16))
+#define RM_U(m) ((int)(((m) >> 16) & 63u))
+#define RM_EXT(m) ((m) >> 22)          // lm_ext of the record's slot, above used (<= 31)
 #define RM_SETV(m, v) (((m) & ~(255u << 8)) | ((uint32_t)(v) << 8))
 
 template <int K, int NPF>
@@ -805,7 +845,7 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 					q0 = q1; q1 = q2; q2 = q3;
 					k0 = k1; k1 = k2; k2 = k3;
 					if (j + 4 < mycnt) { next(it, pkn); q3 = lp.vals[it]; k3 = pkn; }
-					if (j < mycnt && !L.dfr) L.template vote<E>(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b[E]);
+					if (j < mycnt && !L.dfr) L.template vote<E>(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b[E], lp.gap);
 				}
 			};
 			vote_end(std::integral_constant<int, 0>());
@@ -917,7 +957,7 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 				uint32_t pos;
 				const int v = sv(E, id, pos);
 				uint32_t m;
-				if (id < 32u) m = RM((st << 6) | (int)id, v, applied[E]);
+				if (id < 32u) m = RM((st << 6) | (int)id, v, applied[E]) | (lm_ext(L.pm[id * 64 + L.lane].y) << 22);
 				else { const int i = (int)id - 32; m = E ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]); }
 				const int c = cur[E];
 				const uint32_t q0 = E ? tp1[0] : tp0[0], q1 = E ? tp1[1] : tp0[1];
@@ -970,7 +1010,7 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 					const uint32_t m = e ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]);
 					const uint32_t pos = e ? sel3(i, rp1[0], rp1[1], rp1[2]) : sel3(i, rp0[0], rp0[1], rp0[2]);
 					uint32_t w[17];
-					write_record(L, RM_SRC(m), pos, RM_V(m), RM_U(m), w);
+					write_record(L, RM_SRC(m), pos, RM_V(m), RM_U(m), RM_EXT(m), step[e], lp.gap, w);
 #pragma unroll
 					for (int k = 0; k < 17; k++) dst[i * 17 + k] = w[k];
 					nres += RM_V(m) > 0;
