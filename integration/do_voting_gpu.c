@@ -2,7 +2,7 @@
  * integration/do_voting_gpu.c -- the reference-side binding of include/subread_vote.h.
  *
  * What a Subread maintainer adds to subread-align / subjunc (v2.0.6) to run the voting
- * step on an MI355X: do_voting_gpu() replaces do_voting() (src/core.c:3049) for one-block
+ * step on an MI355X: do_voting_gpu() replaces do_voting() (src/core.c:3049) for one- and multi-block
  * indexes.  It is compiled here against the REFERENCE's own headers
  * (tests/test_boundary_ref.py: gcc -c -I/root/reference/src -Iinclude), so every field
  * name and type below is checked by a compiler; it is not linked into anything in this
@@ -149,7 +149,10 @@ int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
 		svg_packed_reads q = {bases[e], nx ? xmask[e] : NULL, starts[e], 0, c.len[e], c.n};
 		pk[e] = q;
 	}
-	if (!rc && c.n)
+	/* a multi-block index: the library votes every block (all resident in HBM) in the first
+	 * block's run of read_chunk_circles (core.c:3567-3613); the later runs only re-read the
+	 * chunk (go_chunk_start) and, in the final one, run step 3 */
+	if (!rc && c.n && gc->current_index_block_number == 0)
 		rc = svg_vote_batch_packed(svg_ix, &p, &pk[0], ends == 2 ? &pk[1] : NULL,
 		                           (svg_mapping_result *)_global_retrieve_alignment_ptr(gc, 0, 0, 0),
 		                           p.do_breakpoint_detection ? (svg_subjunc_result *)_global_retrieve_subjunc_ptr(gc, 0, 0, 0) : NULL,
@@ -161,12 +164,17 @@ int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
 	subread_read_number_t r;
 	for (r = 0; !rc && gc->is_final_voting_run && r < (subread_read_number_t)c.n; r++) {
 		for (e = 0; e < ends; e++) {
-			int has_reversed = 0;   /* the text as fetched (do_voting's copy is reversed after its strand loop) */
+			/* do_voting's text buffer is reversed once after strand 0 (core.c:3229-3234) and the
+			 * tail starts from that state (read_1_reversed = 1); reverse_read maps every
+			 * non-ACGTU character to 'N', so the state machine is kept exactly */
+			int has_reversed = 1;
 			char *rt = text[0], *rq = qual[0];
 			int rl = c.len[e][r];
 			memcpy(rt, c.text[e] + c.off[e][r], rl);
 			memcpy(rq, c.qual[e] + c.off[e][r], rl);
 			rt[rl] = rq[rl] = 0;
+			reverse_read(rt, rl, gc->config.space_type);
+			reverse_quality(rq, rl);
 			char *rn = c.name[e] + r * (MAX_READ_NAME_LEN + 1);
 			int b;
 			for (b = 0; b < gc->config.multi_best_reads; b++) {
