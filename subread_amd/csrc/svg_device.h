@@ -32,6 +32,14 @@ struct DevIndex {
 	//            sorted key_hi multiset as a unary count code (build_bcode); replaces bline when
 	//            the index's key_hi range is small (V = 0xffffffff / nb + 1 <= 80)
 	const uint4 *bcode;
+	//   khash: the probe records themselves, keyed by the full 32-bit key -- one 64-byte line
+	//            per lookup: keys of 5 entries (0xffffffff = empty), their records (mid item,
+	//            fwd | bwd << 16), an overflow word (continue at the next line).  Built when the
+	//            bucket code does not apply (wide key_hi range: gapped indexes); the key
+	//            0xffffffff itself lives in khash_ff = {present, mid, fwd | bwd << 16}
+	const uint32_t *khash;
+	const uint32_t *khash_ff;
+	uint64_t khash_lines;
 };
 
 #define SVG_MAX_BLOCKS 64
@@ -41,7 +49,7 @@ struct svg_index {
 	hipStream_t stream;
 	svg_host_index host;
 	DevIndex dix;
-	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr, *d_bgrp, *d_keys8, *d_bline, *d_bcode;
+	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr, *d_bgrp, *d_keys8, *d_bline, *d_bcode, *d_khash;
 	uint32_t *d_scratch;
 	size_t scratch_words;
 	unsigned long long *d_stats;

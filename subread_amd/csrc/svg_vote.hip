@@ -1727,7 +1727,17 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 //     dependent binary search plus a one-load-per-step run scan.
 // =============================================================================================
 #define PROBE_GROUP_RECS 2048
-template <int ENDS, bool PACKED, bool CODE>
+// DevIndex::khash line of a key: the key scrambled by an odd constant (a bijection), reduced to
+// [0, lines) by the high half of a 64-bit product
+__device__ __forceinline__ uint64_t khash_line(uint32_t key, uint64_t lines)
+{
+	return ((uint64_t)(key * 0x9E3779B1u) * lines) >> 32;
+}
+
+#define IMG_LINE  0
+#define IMG_CODE  1
+#define IMG_KHASH 2
+template <int ENDS, bool PACKED, int IMG>
 __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 {
 	__shared__ uint2 srec[PROBE_GROUP_RECS];
@@ -1755,7 +1765,34 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 				const int p = (int)(rem2 - (uint32_t)s * nps);
 				outidx = pp.soa ? rem * n + r : r * per_read + rem;
 				uint32_t key;
-				if (CODE && probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
+				constexpr bool CODE = IMG == IMG_CODE;
+				if (IMG == IMG_KHASH && probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
+					// the key's record from its 64-byte line (and the overflow chain)
+					st_p++;
+					if (pp.stats) {
+						const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic), b = key - q * ix.nb;
+						st_i += ix.bstart[b + 1] - ix.bstart[b];
+					}
+					if (key == 0xffffffffu) {
+						if (ix.khash_ff[0]) rec = make_uint2(ix.khash_ff[1], ix.khash_ff[2]);
+					} else {
+						uint64_t L = khash_line(key, ix.khash_lines);
+						for (;;) {
+							const uint4 *l4 = (const uint4 *)(ix.khash + 16 * L);
+							const uint4 a = l4[0], b4 = l4[1], c4 = l4[2], d4 = l4[3];
+							const uint32_t ks[5] = {a.x, a.y, a.z, a.w, b4.x};
+							const uint32_t px[5] = {b4.y, b4.w, c4.y, c4.w, d4.y};
+							const uint32_t py[5] = {b4.z, c4.x, c4.z, d4.x, d4.z};
+							bool found = false;
+#pragma unroll
+							for (int k = 0; k < 5; k++)
+								if (ks[k] == key) { rec = make_uint2(px[k], py[k]); found = true; }
+							if (found || !d4.w) break;
+							L = L + 1 == ix.khash_lines ? 0 : L + 1;
+						}
+					}
+					if (pp.stats) st_h += (rec.y & 0xffffu) + (rec.y >> 16);
+				} else if (CODE && probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
 					const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
 					const uint32_t b = key - q * ix.nb;
 					// the bucket's 32-byte code: first item, count, unary key_hi counts
@@ -1786,7 +1823,7 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 						}
 					}
 					if (big) rec = make_uint2(key, 0xffffffffu);
-				} else if (!CODE && probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
+				} else if (IMG == IMG_LINE && probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
 					const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
 					const uint32_t b = key - q * ix.nb;
 					// the bucket's 64-byte line: bounds and u8 keys in one random access
@@ -2037,6 +2074,60 @@ __global__ void __launch_bounds__(256) build_bcode(const uint32_t *bstart, const
 	}
 }
 
+__global__ void __launch_bounds__(256) clear_khash_overflow(uint32_t *kh, uint64_t lines)
+{
+	for (uint64_t L = blockIdx.x * 256ull + threadIdx.x; L < lines; L += gridDim.x * 256ull) kh[16 * L + 15] = 0u;
+}
+
+// DevIndex::khash: for every distinct key of every bucket, gehash_go_X's binary search
+// (sorted-hashtable.c:947-981) run here once -- first hit midpoint m, equal keys after / before
+// it -- and the resulting probe record stored under the full key.  A probe then costs one random
+// 64-byte line whatever the bucket's size (gapped indexes: ~87 items per bucket at 3 Gbp)
+__global__ void __launch_bounds__(256) build_khash(const uint32_t *bstart, const int16_t *keys, uint32_t nb, uint32_t *kh,
+                                                   uint64_t lines, uint32_t *ff)
+{
+	for (uint32_t b = blockIdx.x * 256u + threadIdx.x; b < nb; b += gridDim.x * 256u) {
+		const uint32_t first = bstart[b], n = bstart[b + 1] - first;
+		const int16_t *K = keys + first;
+		for (uint32_t j = 0; j < n; j++) {
+			const int16_t k16 = K[j];
+			if (j > 0 && K[j - 1] == k16) continue;   // the run's first item (a repeated run inserts once)
+			int lo = 0, hi = (int)n - 1, m = 0;
+			bool hit = false;
+			for (;;) {
+				m = (lo + hi) >> 1;
+				const int16_t kk = K[m];
+				if (kk > k16) hi = m - 1;
+				else if (kk < k16) lo = m + 1;
+				else { hit = true; break; }
+				if (hi < lo) break;
+			}
+			if (!hit) continue;   // an unsorted bucket can hide a key from the search: no record
+			int qq = m + 1;
+			while (qq < (int)n && K[qq] == k16) qq++;
+			const uint32_t fwd = (uint32_t)(qq - m);
+			qq = m - 1;
+			while (qq >= 0 && K[qq] == k16) qq--;
+			const uint32_t bwd = (uint32_t)(m - 1 - qq);
+			const uint32_t key = (uint32_t)(uint16_t)k16 * nb + b, rx = first + (uint32_t)m, ry = fwd | (bwd << 16);
+			if (key == 0xffffffffu) { ff[1] = rx; ff[2] = ry; ff[0] = 1u; continue; }
+			uint64_t L = khash_line(key, lines);
+			for (;;) {
+				uint32_t *w = kh + 16 * L;
+				int s = 0;
+				for (; s < 5; s++) {
+					const uint32_t old = atomicCAS(&w[s], 0xffffffffu, key);
+					if (old == 0xffffffffu) { w[5 + 2 * s] = rx; w[6 + 2 * s] = ry; break; }
+					if (old == key) break;
+				}
+				if (s < 5) break;
+				atomicOr(&w[15], 1u);   // full: lookups continue at the next line
+				L = L + 1 == lines ? 0 : L + 1;
+			}
+		}
+	}
+}
+
 // DevIndex::bline: one 64-byte line per bucket (first item, count, the u8 keys of <= 59 items)
 __global__ void __launch_bounds__(256) build_bline(const uint32_t *bstart, const int16_t *keys, uint32_t nb, uint4 *bline)
 {
@@ -2102,6 +2193,9 @@ int svg_index_finish_device(svg_index *h)
 	h->dix.keys8 = NULL;
 	h->dix.bline = NULL;
 	h->dix.bcode = NULL;
+	h->dix.khash = NULL;
+	h->dix.khash_ff = NULL;
+	h->dix.khash_lines = 0;
 	{
 		// 32-byte bucket codes when the key_hi range is small enough for them to hold ordinary
 		// buckets (V = 47 at nb = 93,018,839, the -F -B full index): n + V <= 216 bits
@@ -2121,7 +2215,33 @@ int svg_index_finish_device(svg_index *h)
 			}
 		}
 	}
-	if (!h->dix.bcode && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_BLINE")) {
+	if (!h->dix.bcode && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_KHASH")) {
+		// key-hash image of the probe records: lines ~ items / 3.5 (<= 57% of the 5 slots used)
+		const uint64_t lines = x->items / 3 + 1024;
+		if (dmalloc(h, &h->d_khash, lines * 64 + 64) == 0) {
+			HIPCHK(hipMemsetAsync(h->d_khash, 0xff, lines * 64, h->stream));
+			// overflow words start at 0 (memset 0xff above, cleared per line here)
+			uint32_t *ff = (uint32_t *)((uint8_t *)h->d_khash + lines * 64);
+			HIPCHK(hipMemsetAsync(ff, 0, 64, h->stream));
+			uint64_t blocks = (lines + 255) / 256, bmax = (uint64_t)h->n_cu * 64;
+			if (blocks > bmax) blocks = bmax;
+			hipLaunchKernelGGL(clear_khash_overflow, dim3((unsigned)blocks), dim3(256), 0, h->stream, (uint32_t *)h->d_khash, lines);
+			HIPCHK(hipGetLastError());
+			blocks = ((uint64_t)x->nb + 255) / 256;
+			if (blocks > bmax) blocks = bmax;
+			hipLaunchKernelGGL(build_khash, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
+			                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff);
+			HIPCHK(hipGetLastError());
+			HIPCHK(hipStreamSynchronize(h->stream));
+			h->dix.khash = (const uint32_t *)h->d_khash;
+			h->dix.khash_ff = ff;
+			h->dix.khash_lines = lines;
+		} else {
+			h->d_khash = NULL;
+			(void)hipGetLastError();
+		}
+	}
+	if (!h->dix.bcode && !h->dix.khash && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_BLINE")) {
 		// (2^32-1)/nb <= 255: every key_hi fits a byte; 64 B per bucket (5.95 GB at nb = 93M)
 		// optional image: without the HBM for it the index still opens with the group/key images
 		if (dmalloc(h, &h->d_bline, (size_t)x->nb * 64 + 64) == 0) {
@@ -2137,7 +2257,7 @@ int svg_index_finish_device(svg_index *h)
 			(void)hipGetLastError();
 		}
 	}
-	if (!h->dix.bline && !h->dix.bcode && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT")) {
+	if (!h->dix.bline && !h->dix.bcode && !h->dix.khash && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT")) {
 		// (2^32-1)/nb <= 255: every key_hi fits a byte
 		const size_t ng = ((size_t)x->nb + 15) / 16;
 		if ((rc = dmalloc(h, &h->d_bgrp, ng * 32 + 64)) || (rc = dmalloc(h, &h->d_keys8, x->items + 128))) return rc;
@@ -2269,7 +2389,7 @@ extern "C" void svg_index_close(svg_index *h)
 			for (int j = 0; j < 2; j++)
 				if (h->tev[k][i][j]) hipEventDestroy(h->tev[k][i][j]);
 	hipFree(h->d_bstart); hipFree(h->d_keys); hipFree(h->d_vals); hipFree(h->d_values); hipFree(h->d_chr);
-	hipFree(h->d_bgrp); hipFree(h->d_keys8); hipFree(h->d_bline); hipFree(h->d_bcode);
+	hipFree(h->d_bgrp); hipFree(h->d_keys8); hipFree(h->d_bline); hipFree(h->d_bcode); hipFree(h->d_khash);
 	hipFree(h->d_scratch); hipFree(h->d_stats); hipFree(h->d_err);
 	if (h->ev_last) hipEventDestroy(h->ev_last);
 	if (h->stream) hipStreamDestroy(h->stream);
@@ -2639,7 +2759,7 @@ int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slo
 		}
 	}
 #define PROBE_LAUNCH(E, L, P) hipLaunchKernelGGL((probe_kernel<E, 8, L, P>), dim3((unsigned)pb), dim3(256), 0, st, pp)
-	if ((h->dix.bline || h->dix.bcode) && !getenv("SVG_PROBE_V1")) {
+	if ((h->dix.bline || h->dix.bcode || h->dix.khash) && !getenv("SVG_PROBE_V1")) {
 		// bucket lines: grouped probe kernel + the big-bucket kernel on its list
 		pp.group = (uint32_t)(PROBE_GROUP_RECS / job->per_read);
 		if (pp.group > 64) pp.group = 64;
@@ -2656,16 +2776,20 @@ int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slo
 		pp.big_stride = (uint32_t)stride;
 		pp.big_regions = (uint32_t)gb;
 #define LINE_LAUNCH(E, P, C) hipLaunchKernelGGL((probe_line_kernel<E, P, C>), dim3((unsigned)gb), dim3(256), 0, st, pp)
-		if (h->dix.bcode) {
-			if (pp.packed) { if (pe) LINE_LAUNCH(2, true, true); else LINE_LAUNCH(1, true, true); }
-			else { if (pe) LINE_LAUNCH(2, false, true); else LINE_LAUNCH(1, false, true); }
+		if (h->dix.khash) {
+			if (pp.packed) { if (pe) LINE_LAUNCH(2, true, IMG_KHASH); else LINE_LAUNCH(1, true, IMG_KHASH); }
+			else { if (pe) LINE_LAUNCH(2, false, IMG_KHASH); else LINE_LAUNCH(1, false, IMG_KHASH); }
+		} else if (h->dix.bcode) {
+			if (pp.packed) { if (pe) LINE_LAUNCH(2, true, IMG_CODE); else LINE_LAUNCH(1, true, IMG_CODE); }
+			else { if (pe) LINE_LAUNCH(2, false, IMG_CODE); else LINE_LAUNCH(1, false, IMG_CODE); }
 		} else {
-			if (pp.packed) { if (pe) LINE_LAUNCH(2, true, false); else LINE_LAUNCH(1, true, false); }
-			else { if (pe) LINE_LAUNCH(2, false, false); else LINE_LAUNCH(1, false, false); }
+			if (pp.packed) { if (pe) LINE_LAUNCH(2, true, IMG_LINE); else LINE_LAUNCH(1, true, IMG_LINE); }
+			else { if (pe) LINE_LAUNCH(2, false, IMG_LINE); else LINE_LAUNCH(1, false, IMG_LINE); }
 		}
 #undef LINE_LAUNCH
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(probe_big_kernel, dim3((unsigned)(h->n_cu * 8)), dim3(256), 0, st, pp);
+		// (the key-hash image resolves every probe in the line kernel: no big-bucket list)
+		if (!h->dix.khash) hipLaunchKernelGGL(probe_big_kernel, dim3((unsigned)(h->n_cu * 8)), dim3(256), 0, st, pp);
 	} else if (h->dix.bline) {
 		if (pp.packed) { if (pe) PROBE_LAUNCH(2, true, true); else PROBE_LAUNCH(1, true, true); }
 		else { if (pe) PROBE_LAUNCH(2, true, false); else PROBE_LAUNCH(1, true, false); }
