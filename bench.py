@@ -60,6 +60,10 @@ def workload(name):
     if name == "c4":
         return dict(c3, reads=25_000_000, read_len=150, kind="pe",
                     desc="C4: 25M x 2 x 150bp PE pairs per GPU vs the C3 3.0 Gbp index (400M reads on 8 GPUs)")
+    if name == "c5pe":
+        # paired-end subjunc (SURVEY §8(d) lists C5 as SE; this is the PE shape of it)
+        return dict(c3, reads=25_000_000, read_len=100, kind="sjpe",
+                    desc="C5pe: subjunc PE, 25M x 2 x 100bp pairs per GPU (fragments N(300,50)) vs the C3 index")
     if name == "c5":
         return dict(c3, reads=50_000_000, read_len=100, kind="sj",
                     desc="C5: subjunc, 50M x 100bp spliced RNA-seq reads (30% span a GT..AG intron) vs the C3 index")
@@ -156,7 +160,7 @@ def main():
     t1 = time.time()
     kind = W["kind"]
     rb2 = None
-    if kind == "pe":
+    if kind in ("pe", "sjpe"):
         rb, rb2 = simulate_pairs(genome, n, L, seed=4004, first=rank * n)
     elif kind == "sj":
         rb = simulate_spliced_reads(genome, n, L, seed=5005 + rank)
@@ -165,9 +169,9 @@ def main():
     ends = 2 if rb2 is not None else 1
     log("[bench] simulated %d %s in %.1fs" % (n, "pairs" if ends == 2 else "reads", time.time() - t1))
     dev = torch.device("cuda", local)
-    p = default_params(PROGRAM_SUBJUNC if kind == "sj" else PROGRAM_ALIGN, ends == 2)
+    p = default_params(PROGRAM_SUBJUNC if kind in ("sj", "sjpe") else PROGRAM_ALIGN, ends == 2)
     mb = p.multi_best
-    sj = kind == "sj"
+    sj = kind in ("sj", "sjpe")
 
     # ---- host-pinned 2-bit packed reads and host-pinned output records
     keep = []
@@ -388,7 +392,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": W["desc"], "reads_per_gpu_per_step": n * ends, "read_len": L,
-                       "mode": {"se": "subread-align SE", "pe": "subread-align PE", "sj": "subjunc SE"}[kind],
+                       "mode": {"se": "subread-align SE", "pe": "subread-align PE", "sj": "subjunc SE",
+                                "sjpe": "subjunc PE"}[kind],
                        "entry": "svg_vote_batch_packed: 2-bit packed reads in host-pinned memory -> mapping_result_t "
                                 "in host-pinned memory (H2D + vote + compacted D2H + host expansion)",
                        "index": "%s one-block (gap %d), %d buckets, %d items, %s" % (

@@ -199,8 +199,8 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
                    int nps, uint8_t *out, uint8_t *jout, uint16_t *bm, unsigned long long *stats, uint32_t **defer_list,
                    uint32_t **defer_count, hipStream_t st);
 int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *len1, const uint16_t *len2, uint32_t n,
-                      const uint2 *precs, int nps, uint8_t *out, unsigned long long *stats, uint32_t **defer_list,
-                      uint32_t **defer_count, hipStream_t st);
+                      const uint2 *precs, int nps, uint8_t *out, uint8_t *jout, uint16_t *bm_out, unsigned long long *stats,
+                      uint32_t **defer_list, uint32_t **defer_count, hipStream_t st);
 int svg_timing_mark(svg_index *h, int k, int phase, hipStream_t st);
 
 #endif

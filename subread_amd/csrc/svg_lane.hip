@@ -755,7 +755,10 @@ __device__ __forceinline__ void pl_put(uint32_t (&w)[PLW], int i, uint32_t id)
 #define RM_EXT(m) ((m) >> 22)          // lm_ext of the record's slot, above used (<= 31)
 #define RM_SETV(m, v) (((m) & ~(255u << 8)) | ((uint32_t)(v) << 8))
 
-template <int K, int NPF>
+// SJ: subjunc pairs (process_voting_junction_PE_topK with copy_vote's junction part): big-margin
+// records per end as in lane_kernel; a pair with a result whose table holds a minor half that
+// would reach donor_score is deferred to the wave kernel
+template <int K, int NPF, bool SJ>
 __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 {
 	extern __shared__ __align__(16) uint8_t lds_raw[];
@@ -794,6 +797,9 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 		}
 		// bigtable records of both ends
 		uint32_t rm0[3] = {0, 0, 0}, rm1[3] = {0, 0, 0}, rp0[3] = {0, 0, 0}, rp1[3] = {0, 0, 0};
+		// subjunc: big-margin records of each end, (votes, start | end << 16)
+		uint32_t bv[2][3] = {{0, 0, 0}, {0, 0, 0}}, bs[2][3] = {{0, 0, 0}, {0, 0, 0}};
+		const int nbm = SJ ? (lp.bm_size >= 3 ? lp.bm_size / 3 : 0) : 0;
 		int nc_read = 0;
 		for (int st = 0; st < 2; st++) {
 			L.reset();
@@ -880,7 +886,34 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 				for (int tk = 0; tk < 3; tk++) {
 					const int N = ta[E][tk];
 					if (ns[E] >= mvs || N < 1 || ta[E][0] - N > cutoff) break;
-					if (N >= mvsec) {
+					if (SJ && tk == 0 && nbm > 0) {
+						// the first value's row-major scan, up to max_vote_simples simples: every slot it
+						// visits with votes >= the third top value is a big-margin record
+						// (core-junction.c:2276-2277; insert_big_margin_record :789-811)
+						for (uint32_t row = 0; row < LROWS && ns[E] < mvs; row++) {
+							uint32_t s = L.template head<E>(row);
+							while (s != Lane<K, 2>::NIL && ns[E] < mvs) {
+								const uint32_t M = L.pm[s * 64 + L.lane].y;
+								const int v = lm_votes(M);
+								if (v >= ta[E][2]) {
+									const int rs = (int)(*L.cw(st, (int)s, 0) & 0xffu);
+									const int re = lcov_end(lm_last(M), lm_x(M), step[E], lp.gap);
+									const uint32_t vv = (uint32_t)(v & 255);
+									const uint32_t se = st ? ((uint32_t)(uint16_t)(len[E] - re) | ((uint32_t)(uint16_t)(len[E] - rs) << 16))
+									                       : ((uint32_t)rs | ((uint32_t)re << 16));
+									const int x1 = vv >= bv[E][0] ? 0 : (nbm > 1 && vv >= bv[E][1]) ? 1 : (nbm > 2 && vv >= bv[E][2]) ? 2 : 3;
+									if (x1 < nbm) {
+										if (x1 <= 1 && nbm > 2) { bv[E][2] = bv[E][1]; bs[E][2] = bs[E][1]; }
+										if (x1 == 0 && nbm > 1) { bv[E][1] = bv[E][0]; bs[E][1] = bs[E][0]; }
+										PUT3(x1, bv[E][0], bv[E][1], bv[E][2], vv);
+										PUT3(x1, bs[E][0], bs[E][1], bs[E][2], se);
+									}
+								}
+								if (v == N && N >= mvsec) { pl_put(pl[E], ns[E], s); ns[E]++; }
+								s = lm_next(M);
+							}
+						}
+					} else if (N >= mvsec) {
 						for (uint32_t row = 0; row < LROWS; row++) {
 							uint32_t s = L.template head<E>(row);
 							while (s != Lane<K, 2>::NIL) {
@@ -959,6 +992,30 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 				uint32_t m;
 				if (id < 32u) m = RM((st << 6) | (int)id, v, applied[E]) | (lm_ext(L.pm[id * 64 + L.lane].y) << 22);
 				else { const int i = (int)id - 32; m = E ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]); }
+				if constexpr (SJ) {
+					// copy_vote_to_alignment_res's junction part (core-junction.c:1073-1334) for a
+					// result taken from this table: a minor half of the same end that passes
+					// test_junction_minor and the overlap / distance tests would go to donor_score
+					if (id < 32u && !L.dfr) {
+						const uint2 eM = L.pm[id * 64 + L.lane];
+						const int csM = (int)(*L.cw(st, (int)id, 0) & 0xffu), ceM = lcov_end(lm_last(eM.y), lm_x(eM.y), step[E], lp.gap);
+						for (int q = 0; q < L.nslots; q++) {
+							if (q == (int)id) continue;
+							const uint2 e2 = L.pm[q * 64 + L.lane];
+							if ((lm_endbit(e2.y) != 0) != (E != 0) || v < lm_votes(e2.y)) continue;
+							const long long dist = (long long)eM.x - (long long)e2.x;
+							if ((dist < 0 ? -dist : dist) > (long long)lp.max_intron) continue;
+							const int cs2 = (int)(*L.cw(st, q, 0) & 0xffu), ce2 = lcov_end(lm_last(e2.y), lm_x(e2.y), step[E], lp.gap);
+							if (csM == cs2 || ceM == ce2) continue;
+							if (csM > cs2 ? eM.x < e2.x : eM.x > e2.x) continue;
+							const int ov = csM > cs2 ? ce2 - csM : ceM - cs2;
+							if (ov > 14 || abs((int)dist) < 6) continue;
+							L.dfr = true;
+							L.why = 2;
+							break;
+						}
+					}
+				}
 				const int c = cur[E];
 				const uint32_t q0 = E ? tp1[0] : tp0[0], q1 = E ? tp1[1] : tp0[1];
 				if ((c > 0 && q0 == pos) || (c > 1 && q1 == pos)) return;
@@ -996,6 +1053,7 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 			}
 #pragma unroll
 			for (int i = 0; i < 3; i++) {
+				if (SJ && L.dfr) break;
 				if (i < cur[0]) { rm0[i] = tm0[i]; rp0[i] = tp0[i]; } else rm0[i] = RM_SETV(rm0[i], 0);
 				if (i < cur[1]) { rm1[i] = tm1[i]; rp1[i] = tp1[i]; } else rm1[i] = RM_SETV(rm1[i], 0);
 			}
@@ -1014,6 +1072,22 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 #pragma unroll
 					for (int k = 0; k < 17; k++) dst[i * 17 + k] = w[k];
 					nres += RM_V(m) > 0;
+					if constexpr (SJ) {
+						// no minor half on the lane path: empty subjunc_result_t
+						uint4 *jd = (uint4 *)(lp.jout + (((size_t)r * 2 + e) * mb + i) * 16);
+						*jd = make_uint4(0u, 0u, 0u, 0u);
+					}
+				}
+				if constexpr (SJ) {
+					if (lp.bm_out) {
+						uint16_t *bd = lp.bm_out + ((size_t)r * 2 + e) * SVG_BIG_MARGIN_WORDS;
+#pragma unroll
+						for (int k = 0; k < 3; k++) {
+							bd[3 * k] = (uint16_t)bv[e][k];
+							bd[3 * k + 1] = (uint16_t)(bs[e][k] & 0xffffu);
+							bd[3 * k + 2] = (uint16_t)(bs[e][k] >> 16);
+						}
+					}
 				}
 			}
 		}
@@ -1105,9 +1179,9 @@ int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int s
 	const char *e = getenv("SVG_LANE");
 	if (e && e[0] == '0') return 0;
 	if (h->max_read_len > 160) return 0;
-	// subjunc: single end, junction search on (the lane path carries big-margin records and
-	// defers every read that needs donor scoring)
-	if (sj && (paired || !p->do_breakpoint_detection || p->max_insertion_at_junctions)) return 0;
+	// subjunc: junction search on (the lane paths carry big-margin records and defer every read
+	// or pair that needs donor scoring)
+	if (sj && (!p->do_breakpoint_detection || p->max_insertion_at_junctions)) return 0;
 	int tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
 	if (tol > 5 || p->total_subreads > 31 || p->multi_best > 3 || p->top_scores != 3) return 0;
 	if (!paired && p->max_vote_simples > 3) return 0;
@@ -1120,8 +1194,8 @@ int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int s
 
 // paired-end: lane_pe_kernel over every pair of the chunk; deferred pairs listed for vote_kernel
 int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *len1, const uint16_t *len2, uint32_t n,
-                      const uint2 *precs, int nps, uint8_t *out, unsigned long long *stats, uint32_t **defer_list,
-                      uint32_t **defer_count, hipStream_t st)
+                      const uint2 *precs, int nps, uint8_t *out, uint8_t *jout, uint16_t *bm_out, unsigned long long *stats,
+                      uint32_t **defer_list, uint32_t **defer_count, hipStream_t st)
 {
 	const char *e = getenv("SVG_LANE");
 	const size_t o_l1 = 0, o_cnt = (o_l1 + (size_t)4 * n + 255) & ~(size_t)255, need = o_cnt + 256;
@@ -1135,7 +1209,7 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	uint8_t *b = (uint8_t *)h->d_lane[slot];
 	uint32_t *cnt = (uint32_t *)(b + o_cnt);   // [0] deferrals, [2] wave-kernel work counter
 	HIPCHK(hipMemsetAsync(cnt, 0, 16, st));
-	if (nps > LANE_NPF) { svg_set_error("lane_pe: %d probes per strand", nps); return SVG_E_UNSUPPORTED; }
+	if (nps > (jout ? LANE_NPF_SJ : LANE_NPF)) { svg_set_error("lane_pe: %d probes per strand", nps); return SVG_E_UNSUPPORTED; }
 	LParams lp;
 	memset(&lp, 0, sizeof lp);
 	lp.len = len1; lp.len2 = len2; lp.n = n; lp.cap = LANE_PE_CAP;
@@ -1149,6 +1223,10 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	lp.chr_end = h->dix.chr_end; lp.n_chr = (int)h->dix.n_chr; lp.padding = h->dix.padding;
 	lp.min_pair = p->min_pair_distance; lp.max_pair = p->max_pair_distance; lp.mvc = p->max_vote_combinations;
 	lp.out = out;
+	lp.jout = jout;
+	lp.bm_out = jout ? bm_out : NULL;
+	lp.bm_size = p->do_big_margin_filtering_for_junctions ? p->big_margin_record_size : 0;
+	lp.max_intron = p->maximum_intron_length;
 	lp.defer_list = (uint32_t *)(b + o_l1);
 	lp.defer_count = cnt;
 	lp.defer_all = e && e[0] == '2';
@@ -1174,7 +1252,8 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	lp.cold = h->d_lscratch;
 	int rc = svg_timing_mark(h, 3, 0, st);
 	if (rc) return rc;
-	hipLaunchKernelGGL((lane_pe_kernel<K, LANE_NPF>), dim3((unsigned)blocks), dim3(64), lds, st, lp);
+	if (jout) hipLaunchKernelGGL((lane_pe_kernel<K, LANE_NPF_SJ, true>), dim3((unsigned)blocks), dim3(64), lds, st, lp);
+	else hipLaunchKernelGGL((lane_pe_kernel<K, LANE_NPF, false>), dim3((unsigned)blocks), dim3(64), lds, st, lp);
 	HIPCHK(hipGetLastError());
 	if ((rc = svg_timing_mark(h, 3, 1, st))) return rc;
 	*defer_list = lp.defer_list;

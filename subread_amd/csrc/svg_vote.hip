@@ -2715,7 +2715,7 @@ int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, con
 	pp.stats = kp.stats;
 	// align mode, reads <= 160 bp: lane-per-read (SE) / lane-per-pair (PE) fast path
 	// (svg_lane.hip), probe records in SoA layout
-	job->lane = svg_lane_eligible(h, p, r2 != NULL, job->sj) != 0 && (!r2 || nps <= 10) && (!job->sj || nps <= 14) &&
+	job->lane = svg_lane_eligible(h, p, r2 != NULL, job->sj) != 0 && (!r2 || nps <= (job->sj ? 14 : 10)) && (!job->sj || nps <= 14) &&
 	            !h->stored;   // later blocks of a multi-block index merge with stored records: wave kernel
 	kp.stored = h->stored;
 	pp.soa = job->lane ? 1 : 0;
@@ -2813,7 +2813,8 @@ int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slo
 		// gather + lane kernels vote every read they can; the rest (deferral list) go to
 		// vote_kernel below, which reads the SoA probe records of the deferred reads
 		uint32_t *dl = NULL, *dc = NULL;
-		rc = pe ? svg_lane_pe_chunk(h, slot, p, kc.len1, kc.len2, (uint32_t)cn, kc.precs, nps, kc.out, kp.stats, &dl, &dc, st)
+		rc = pe ? svg_lane_pe_chunk(h, slot, p, kc.len1, kc.len2, (uint32_t)cn, kc.precs, nps, kc.out, job->sj ? kc.jout : NULL,
+		                            kc.bm_out, kp.stats, &dl, &dc, st)
 		        : svg_lane_chunk(h, slot, p, kc.len1, (uint32_t)cn, kc.precs, nps, kc.out, job->sj ? kc.jout : NULL, kc.bm_out,
 		                         kp.stats, &dl, &dc, st);
 		if (rc) return rc;

@@ -198,3 +198,54 @@ def test_lane_sj_modes_match_oracle(key, n, length, params, mode, gpu_indexes, i
         assert st["deferred"] == n
     elif mode == "1" and key.startswith("chr901"):
         assert st["deferred"] < n * 3 // 4, st
+
+
+SJ_PE = [n for n in golden_names() if n.startswith("sj_pe_")]
+
+
+@pytest.mark.parametrize("mode", PE_MODES)
+@pytest.mark.parametrize("name", SJ_PE)
+def test_lane_sj_pe_modes_match_reference_golden(name, mode, gpu_indexes, monkeypatch):
+    """Subjunc PE on the paired lane path (lane_pe_kernel<SJ>: big-margin records per end,
+    pairs whose results have a donor-scoring minor half deferred) on the reference's records."""
+    monkeypatch.setenv("SVG_LANE", mode)
+    c = Case(name)
+    ix = gpu_indexes(c.index_key)
+    out, jout, bm = ix.vote(c.params, c.r1, c.r2)
+    got = pack_records(out, jout, bm)
+    assert (got == c.expected).all(), describe_mismatch(got, c.expected, c.ends, c.params.multi_best)
+
+
+@pytest.mark.parametrize("mode", PE_MODES)
+@pytest.mark.parametrize("key,n,length,params", [("chr901_full", 40000, 100, {}), ("synth4242_gapped", 20000, 120, {}),
+                                                 ("chr901_full", 20000, 150, {"big_margin_record_size": 6,
+                                                                              "maximum_intron_length": 3000})])
+def test_lane_sj_pe_modes_match_oracle(key, n, length, params, mode, gpu_indexes, index_cache, monkeypatch):
+    """Subjunc pairs: simulated fragments (no splicing) for half of the pairs, spliced reads for
+    the other half (R2 unrelated), vs the oracle."""
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.abi import default_params, PROGRAM_SUBJUNC, ReadBatch
+    from subread_amd.sim import Genome, simulate_pairs, simulate_spliced_reads
+    monkeypatch.setenv("SVG_LANE", mode)
+    pre = index_cache.get(key)
+    g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
+    a1, a2 = simulate_pairs(g, n, length, seed=71, insert_max=700)
+    s1 = simulate_spliced_reads(g, n, length, seed=72)
+    s2 = simulate_spliced_reads(g, n, length, seed=73)
+    r1 = ReadBatch.from_list([a1.read(i) if i % 2 else s1.read(i) for i in range(n)])
+    r2 = ReadBatch.from_list([a2.read(i) if i % 2 else s2.read(i) for i in range(n)])
+    p = default_params(PROGRAM_SUBJUNC, True, **params)
+    ix = gpu_indexes(key)
+    ix.set_stats(True)
+    out, jout, bm = ix.vote(p, r1, r2)
+    st = ix.stats()
+    ix.set_stats(False)
+    ref, rj, rbm, _ = OracleIndex(pre).vote(p, r1, r2, threads=16)
+    got, want = pack_records(out, jout, bm), pack_records(ref, rj, rbm)
+    assert (got == want).all(), describe_mismatch(got, want, 2, p.multi_best)
+    # (a gapped index has 3 probes per subread offset: 42 per strand at -n 14, beyond the lane
+    # path's 14, so those pairs are voted by the wave kernel from the start)
+    if mode == "2" and key.endswith("_full"):
+        assert st["deferred"] == n
+    elif mode == "1":
+        assert st["deferred"] < n, st
