@@ -40,6 +40,7 @@ struct DevIndex {
 	const uint32_t *khash;
 	const uint32_t *khash_ff;
 	uint64_t khash_lines;
+	int32_t khash_sec;        // 1: 32-byte sectors of 3 entries (8-bit run counts), 0: 64-byte lines
 };
 
 #define SVG_MAX_BLOCKS 64

@@ -1777,7 +1777,20 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 						if (ix.khash_ff[0]) rec = make_uint2(ix.khash_ff[1], ix.khash_ff[2]);
 					} else {
 						uint64_t L = khash_line(key, ix.khash_lines);
-						for (;;) {
+						if (ix.khash_sec) {
+							for (;;) {
+								const uint4 *l4 = (const uint4 *)(ix.khash + 8 * L);
+								const uint4 a = l4[0], b4 = l4[1];
+								const uint32_t ks[3] = {a.x, a.y, a.z}, mid[3] = {a.w, b4.x, b4.y};
+								const uint32_t fb[3] = {b4.z & 0xffffu, b4.z >> 16, b4.w & 0xffffu};
+								bool found = false;
+#pragma unroll
+								for (int k = 0; k < 3; k++)
+									if (ks[k] == key) { rec = make_uint2(mid[k], (fb[k] & 0xffu) | ((fb[k] >> 8) << 16)); found = true; }
+								if (found || !(b4.w >> 16)) break;
+								L = L + 1 == ix.khash_lines ? 0 : L + 1;
+							}
+						} else for (;;) {
 							const uint4 *l4 = (const uint4 *)(ix.khash + 16 * L);
 							const uint4 a = l4[0], b4 = l4[1], c4 = l4[2], d4 = l4[3];
 							const uint32_t ks[5] = {a.x, a.y, a.z, a.w, b4.x};
@@ -2074,15 +2087,23 @@ __global__ void __launch_bounds__(256) build_bcode(const uint32_t *bstart, const
 	}
 }
 
-__global__ void __launch_bounds__(256) clear_khash_overflow(uint32_t *kh, uint64_t lines)
+// the payload words of every line start at 0 (the keys at 0xffffffff: empty)
+template <bool SEC>
+__global__ void __launch_bounds__(256) clear_khash_payload(uint32_t *kh, uint64_t lines)
 {
-	for (uint64_t L = blockIdx.x * 256ull + threadIdx.x; L < lines; L += gridDim.x * 256ull) kh[16 * L + 15] = 0u;
+	for (uint64_t L = blockIdx.x * 256ull + threadIdx.x; L < lines; L += gridDim.x * 256ull) {
+		if (SEC) { uint32_t *w = kh + 8 * L; w[3] = w[4] = w[5] = w[6] = w[7] = 0u; }
+		else kh[16 * L + 15] = 0u;
+	}
 }
 
 // DevIndex::khash: for every distinct key of every bucket, gehash_go_X's binary search
 // (sorted-hashtable.c:947-981) run here once -- first hit midpoint m, equal keys after / before
 // it -- and the resulting probe record stored under the full key.  A probe then costs one random
-// 64-byte line whatever the bucket's size (gapped indexes: ~87 items per bucket at 3 Gbp)
+// sector (SEC: 32 bytes, 3 entries with 8-bit run counts) or line (64 bytes, 5 entries) whatever
+// the bucket's size (gapped indexes: ~87 items per bucket at 3 Gbp).  ff[3] is set when a run
+// count does not fit 8 bits (the sector image is then not used).
+template <bool SEC>
 __global__ void __launch_bounds__(256) build_khash(const uint32_t *bstart, const int16_t *keys, uint32_t nb, uint32_t *kh,
                                                    uint64_t lines, uint32_t *ff)
 {
@@ -2111,17 +2132,28 @@ __global__ void __launch_bounds__(256) build_khash(const uint32_t *bstart, const
 			const uint32_t bwd = (uint32_t)(m - 1 - qq);
 			const uint32_t key = (uint32_t)(uint16_t)k16 * nb + b, rx = first + (uint32_t)m, ry = fwd | (bwd << 16);
 			if (key == 0xffffffffu) { ff[1] = rx; ff[2] = ry; ff[0] = 1u; continue; }
+			if (SEC && (fwd > 255u || bwd > 255u)) { atomicOr(&ff[3], 1u); continue; }
 			uint64_t L = khash_line(key, lines);
 			for (;;) {
-				uint32_t *w = kh + 16 * L;
+				uint32_t *w = kh + (SEC ? 8 : 16) * L;
+				const int slots = SEC ? 3 : 5;
 				int s = 0;
-				for (; s < 5; s++) {
+				for (; s < slots; s++) {
 					const uint32_t old = atomicCAS(&w[s], 0xffffffffu, key);
-					if (old == 0xffffffffu) { w[5 + 2 * s] = rx; w[6 + 2 * s] = ry; break; }
+					if (old == 0xffffffffu) {
+						if (SEC) {
+							w[3 + s] = rx;
+							atomicOr(&w[6 + (s >> 1)], (fwd | (bwd << 8)) << (16 * (s & 1)));
+						} else {
+							w[5 + 2 * s] = rx;
+							w[6 + 2 * s] = ry;
+						}
+						break;
+					}
 					if (old == key) break;
 				}
-				if (s < 5) break;
-				atomicOr(&w[15], 1u);   // full: lookups continue at the next line
+				if (s < slots) break;
+				atomicOr(SEC ? &w[7] : &w[15], SEC ? 1u << 16 : 1u);   // full: lookups continue at the next line
 				L = L + 1 == lines ? 0 : L + 1;
 			}
 		}
@@ -2196,6 +2228,7 @@ int svg_index_finish_device(svg_index *h)
 	h->dix.khash = NULL;
 	h->dix.khash_ff = NULL;
 	h->dix.khash_lines = 0;
+	h->dix.khash_sec = 0;
 	{
 		// 32-byte bucket codes when the key_hi range is small enough for them to hold ordinary
 		// buckets (V = 47 at nb = 93,018,839, the -F -B full index): n + V <= 216 bits
@@ -2216,29 +2249,45 @@ int svg_index_finish_device(svg_index *h)
 		}
 	}
 	if (!h->dix.bcode && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_KHASH")) {
-		// key-hash image of the probe records: lines ~ items / 3.5 (<= 57% of the 5 slots used)
-		const uint64_t lines = x->items / 3 + 1024;
-		if (dmalloc(h, &h->d_khash, lines * 64 + 64) == 0) {
-			HIPCHK(hipMemsetAsync(h->d_khash, 0xff, lines * 64, h->stream));
-			// overflow words start at 0 (memset 0xff above, cleared per line here)
-			uint32_t *ff = (uint32_t *)((uint8_t *)h->d_khash + lines * 64);
+		// key-hash image of the probe records: 32-byte sectors of 3 entries (lines ~ items / 1.8),
+		// or 64-byte lines of 5 entries (~ items / 3) when a run count needs more than 8 bits
+		for (int sec = getenv("SVG_KHASH64") ? 0 : 1; sec >= 0 && !h->dix.khash; sec--) {
+			const uint64_t lines = (sec ? x->items * 5 / 9 : x->items / 3) + 1024, lb = sec ? 32 : 64;
+			if (dmalloc(h, &h->d_khash, lines * lb + 64) != 0) {
+				h->d_khash = NULL;
+				(void)hipGetLastError();
+				break;
+			}
+			uint32_t *ff = (uint32_t *)((uint8_t *)h->d_khash + lines * lb);
+			HIPCHK(hipMemsetAsync(h->d_khash, 0xff, lines * lb, h->stream));
 			HIPCHK(hipMemsetAsync(ff, 0, 64, h->stream));
 			uint64_t blocks = (lines + 255) / 256, bmax = (uint64_t)h->n_cu * 64;
 			if (blocks > bmax) blocks = bmax;
-			hipLaunchKernelGGL(clear_khash_overflow, dim3((unsigned)blocks), dim3(256), 0, h->stream, (uint32_t *)h->d_khash, lines);
+			if (sec) hipLaunchKernelGGL(clear_khash_payload<true>, dim3((unsigned)blocks), dim3(256), 0, h->stream, (uint32_t *)h->d_khash, lines);
+			else hipLaunchKernelGGL(clear_khash_payload<false>, dim3((unsigned)blocks), dim3(256), 0, h->stream, (uint32_t *)h->d_khash, lines);
 			HIPCHK(hipGetLastError());
 			blocks = ((uint64_t)x->nb + 255) / 256;
 			if (blocks > bmax) blocks = bmax;
-			hipLaunchKernelGGL(build_khash, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
-			                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff);
+			if (sec)
+				hipLaunchKernelGGL(build_khash<true>, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
+				                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff);
+			else
+				hipLaunchKernelGGL(build_khash<false>, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
+				                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff);
 			HIPCHK(hipGetLastError());
+			uint32_t wide = 0;
+			HIPCHK(hipMemcpyAsync(&wide, ff + 3, 4, hipMemcpyDeviceToHost, h->stream));
 			HIPCHK(hipStreamSynchronize(h->stream));
+			if (sec && wide) {   // a run of more than 255 equal keys (repeat threshold > 255): 64-byte lines
+				h->device_bytes -= lines * lb + 64;
+				HIPCHK(hipFree(h->d_khash));
+				h->d_khash = NULL;
+				continue;
+			}
 			h->dix.khash = (const uint32_t *)h->d_khash;
 			h->dix.khash_ff = ff;
 			h->dix.khash_lines = lines;
-		} else {
-			h->d_khash = NULL;
-			(void)hipGetLastError();
+			h->dix.khash_sec = sec;
 		}
 	}
 	if (!h->dix.bcode && !h->dix.khash && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_BLINE")) {

@@ -172,8 +172,9 @@ def test_gpu_pipelines_match_oracle(mode, gpu_indexes, index_cache, monkeypatch)
 
 def test_gpu_probe_images_match_oracle(monkeypatch):
     """The probe images picked at index load: 32-byte unary bucket codes (default for -F -B
-    indexes), the key-hash of probe records (SVG_NO_BCODE=1; the default of every index the
-    code does not fit, e.g. gapped ones), 64-byte bucket lines (+ SVG_NO_KHASH=1), 16-bucket
+    indexes), the key-hash of probe records in 32-byte sectors (SVG_NO_BCODE=1; the default of
+    every index the code does not fit, e.g. gapped ones) or 64-byte lines (+ SVG_KHASH64=1),
+    64-byte bucket lines (+ SVG_NO_KHASH=1), 16-bucket
     groups + u8 keys (+ SVG_NO_BLINE=1), plain bounds + i16 keys (SVG_NO_COMPACT=1), and the
     one-kernel probe of the previous build (SVG_PROBE_V1=1).  The genome carries repeat families, so
     that buckets past a code's 169 keys / a line's 59 keys take the big-bucket search."""
@@ -185,7 +186,7 @@ def test_gpu_probe_images_match_oracle(monkeypatch):
     r1 = simulate_reads(g, 40000, 100, seed=5, sub=0.01, indel=0.001)
     p = default_params(PROGRAM_ALIGN, False)
     want = None
-    for env in ({}, {"SVG_NO_BCODE": "1"}, {"SVG_NO_BCODE": "1", "SVG_NO_KHASH": "1"},
+    for env in ({}, {"SVG_NO_BCODE": "1"}, {"SVG_NO_BCODE": "1", "SVG_KHASH64": "1"}, {"SVG_NO_BCODE": "1", "SVG_NO_KHASH": "1"},
                 {"SVG_NO_BCODE": "1", "SVG_NO_KHASH": "1", "SVG_NO_BLINE": "1"}, {"SVG_NO_COMPACT": "1"},
                 {"SVG_PROBE_V1": "1"}, {"SVG_PROBE_V1": "1", "SVG_NO_BCODE": "1"}):
         for k, v in env.items():
