@@ -16,6 +16,7 @@
  *   local_add_indel_event / put_new_event / search_event  core-indel.c:1385-1569
  *   has_better_mapping core.c:3035, is_ambiguous_voting core-junction.c:3522,
  *   locate_current_value_index core.c:2216 (multi-block indexes)
+ *   anti_supporting_read_scan core-indel.c:177-330
  * Not covered (SVG_E_UNSUPPORTED): subjunc reads > 160 bp (core_search_short_exons and the
  * fragile junction voting feed their events), fusion / long-deletion detection, the
  * extending indel search (extending_search_indels = 0 in both programs).
@@ -71,6 +72,7 @@ typedef struct svg_event_params {
 	int32_t dp_penalty_extend_gap;        /*  0 */
 	int32_t dp_match_score;               /*  2 */
 	int32_t dp_mismatch_penalty;          /*  0 */
+	int32_t report_multi_mapping_reads;   /*  0 (--multiMapping: 1) */
 } svg_event_params;
 void svg_event_params_default(svg_event_params *e);
 
@@ -98,6 +100,16 @@ int svg_events_add_batch(svg_events *t, const svg_genome_arrays *g, const svg_pa
  * finalise_indel_and_junction_thread.  Also call it with n = 1 on a single table: the merged
  * table is sorted by (small side, large side, indel length) as the reference's is. */
 int svg_events_merge(svg_events *dst, svg_events *const *tables, int n);
+
+/*
+ * anti_supporting_read_scan (core-indel.c:177-330) on a merged table: every record of the
+ * batch (n_reads x ends x multi_best, as the vote wrote them) that covers an event's side
+ * strictly inside its covered range (5 bases in from both ends) counts one anti-supporting
+ * read for it.  Run it once per chunk after svg_events_merge, as the reference does after
+ * its voting step.
+ */
+int svg_events_anti_support(svg_events *t, const svg_params *p, const svg_event_params *ep, uint64_t n_reads, int ends,
+                            const svg_mapping_result *out);
 
 int64_t svg_events_count(const svg_events *t);
 int     svg_events_get(const svg_events *t, svg_event *out);   /* svg_events_count() entries */

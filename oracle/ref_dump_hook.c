@@ -37,8 +37,9 @@
  * Event-table dump (env SVG_REF_EVENTS=<file>, appended chunk after chunk): the indel /
  * junction event table of the final voting run as finalise_indel_and_junction_thread left
  * it (core-indel.c:1012-1141; run the aligner with -T 1 so that every event comes from one
- * thread table in read order), then the raw result_flags (CORE_IS_GAPPED_READ included) of
- * every mapping record, in the record order of the vote dump.
+ * thread table in read order) and anti_supporting_read_scan then counted (core-indel.c:268),
+ * then the raw result_flags (CORE_IS_GAPPED_READ included) of every mapping record, in the
+ * record order of the vote dump.
  *   u64 n_events, then n_events x svg_ref_event (96 B, layout below),
  *   u64 n_records, then n_records x u16 result_flags
  */
@@ -120,8 +121,6 @@ int __wrap_anti_supporting_read_scan(global_context_t *gc)
 	if (getenv("SVG_REF_TIMING"))
 		fprintf(stderr, "SVG_REF_TIMECOST_VOTING %.6f %lld\n", gc->timecost_voting,
 		        (long long)gc->processed_reads_in_chunk);
-	const char *ef = getenv("SVG_REF_EVENTS");
-	if (ef && ef[0]) dump_events(gc, ef);
 	const char *fn = getenv("SVG_REF_DUMP");
 	if (fn && fn[0]) {
 		FILE *fp = fopen(fn, "ab");
@@ -152,5 +151,9 @@ int __wrap_anti_supporting_read_scan(global_context_t *gc)
 			fclose(fp);
 		}
 	}
-	return __real_anti_supporting_read_scan(gc);
+	int rc = __real_anti_supporting_read_scan(gc);
+	/* the event table after the anti-supporting read scan (supporting counts unchanged by it) */
+	const char *ef = getenv("SVG_REF_EVENTS");
+	if (ef && ef[0]) dump_events(gc, ef);
+	return rc;
 }

@@ -34,6 +34,7 @@ EXPORTS = [
     # host post-vote events (include/subread_events.h)
     "svg_event_params_default", "svg_genome_arrays_open", "svg_genome_arrays_close", "svg_events_create",
     "svg_events_destroy", "svg_events_add_batch", "svg_events_merge", "svg_events_count", "svg_events_get",
+    "svg_events_anti_support",
 ]
 
 _lib = None
@@ -121,6 +122,8 @@ def lib():
         L.svg_events_add_batch.restype = i32
         L.svg_events_merge.argtypes = [vp, vp, i32]
         L.svg_events_merge.restype = i32
+        L.svg_events_anti_support.argtypes = [vp, vp, vp, u64, i32, vp]
+        L.svg_events_anti_support.restype = i32
         L.svg_events_count.argtypes = [vp]
         L.svg_events_count.restype = ctypes.c_int64
         L.svg_events_get.argtypes = [vp, vp]
@@ -200,6 +203,12 @@ class EventTable:
         _check(lib().svg_events_merge(t.h, arr, len(tables)), "svg_events_merge")
         return t
 
+    def anti_support(self, params, n_reads, ends, mapping, event_params=None):
+        """svg_events_anti_support over a merged table and the batch's mapping records."""
+        _check(lib().svg_events_anti_support(self.h, ctypes.byref(params),
+                                             ctypes.byref(event_params) if event_params is not None else None,
+                                             int(n_reads), int(ends), mapping.ctypes.data), "svg_events_anti_support")
+
     def events(self):
         from .abi import EVENT_DTYPE
         n = lib().svg_events_count(self.h)
@@ -219,11 +228,14 @@ class EventTable:
             pass
 
 
-def find_events(genome, params, r1, r2, records, first_read=0):
-    """Events of one batch, merged and sorted like the reference's table after the voting step."""
+def find_events(genome, params, r1, r2, records, first_read=0, anti_support=True):
+    """Events of one batch, merged and sorted like the reference's table after the voting step,
+    with the anti-supporting read counts of the scan that follows it."""
     t = EventTable()
     t.add_batch(genome, params, r1, r2, records, first_read)
     m = EventTable.merge([t])
+    if anti_support:
+        m.anti_support(params, len(r1), 2 if r2 is not None else 1, records[0])
     ev = m.events()
     t.close()
     m.close()

@@ -56,7 +56,8 @@ EVENT_INDEL, EVENT_JUNCTION, EVENT_FUSION = 8, 64, 128
 
 class SvgEventParams(ctypes.Structure):
     _fields_ = [("dp_penalty_create_gap", ctypes.c_int32), ("dp_penalty_extend_gap", ctypes.c_int32),
-                ("dp_match_score", ctypes.c_int32), ("dp_mismatch_penalty", ctypes.c_int32)]
+                ("dp_match_score", ctypes.c_int32), ("dp_mismatch_penalty", ctypes.c_int32),
+                ("report_multi_mapping_reads", ctypes.c_int32)]
 
 
 SUBJUNC_DTYPE = np.dtype([

@@ -34,6 +34,7 @@ void svg_event_params_default(svg_event_params *e)
 	e->dp_penalty_extend_gap = 0;
 	e->dp_match_score = 2;
 	e->dp_mismatch_penalty = 0;
+	e->report_multi_mapping_reads = 0;
 }
 
 /* ------------------------------------------------------------------ base arrays */
@@ -739,5 +740,97 @@ int svg_events_merge(svg_events *dst, svg_events *const *tables, int n)
 		start = end;
 	}
 	free(refs);
+	return 0;
+}
+
+/* ------------------------------------------------------------------ anti-supporting reads */
+typedef struct { uint32_t pos; uint32_t id; } side_t;
+
+static int side_cmp(const void *a, const void *b)
+{
+	const side_t *x = a, *y = b;
+	if (x->pos != y->pos) return x->pos < y->pos ? -1 : 1;
+	return x->id < y->id ? -1 : x->id > y->id;
+}
+
+/* BINsearch_event, core-indel.c:132-157: an index of pos, else the last index below it (-1) */
+static int64_t side_search(const side_t *v, int64_t n, uint32_t pos)
+{
+	int64_t lo = 0, hi = n - 1;
+	for (;;) {
+		const int64_t mid = (lo + hi) / 2;
+		if (v[mid].pos == pos) return mid;
+		if (v[mid].pos < pos) lo = mid + 1; else hi = mid - 1;
+		if (lo > hi) return hi;
+	}
+}
+
+#define ANTI_LIMIT 100   /* ANTI_SUPPORTING_READ_LIMIT, core-indel.c:241 */
+
+/*
+ * anti_supporting_read_scan, core-indel.c:177-330, over a (merged) event table: every record
+ * with votes (>= min_votes_first; a record with no votes ends the read's list) counts against
+ * each event whose small or large side lies strictly inside its covered range shrunk by 5 bases
+ * at both ends (an event once per record; at most 100 small-side events per record).
+ */
+int svg_events_anti_support(svg_events *t, const svg_params *p, const svg_event_params *ep_in, uint64_t n_reads, int ends,
+                            const svg_mapping_result *out)
+{
+	const int mb = p ? p->multi_best : 0;
+	svg_event_params epd;
+	const svg_event_params *ep = ep_in;
+	side_t *sm, *lg;
+	uint32_t *cnt;
+	int64_t ne, i;
+	uint64_t r;
+	if (!t || !p || !out || ends < 1 || ends > 2 || mb < 1 || mb > 3) { svg_set_error("svg_events_anti_support: bad argument"); return SVG_E_ARG; }
+	if (!ep) { svg_event_params_default(&epd); ep = &epd; }
+	ne = (int64_t)t->n;
+	if (ne < 1) return 0;
+	sm = malloc(sizeof(side_t) * (size_t)ne);
+	lg = malloc(sizeof(side_t) * (size_t)ne);
+	cnt = calloc((size_t)ne, sizeof(uint32_t));
+	if (!sm || !lg || !cnt) { free(sm); free(lg); free(cnt); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	for (i = 0; i < ne; i++) {
+		sm[i].pos = t->ev[i].small_side; sm[i].id = (uint32_t)i;
+		lg[i].pos = t->ev[i].large_side; lg[i].id = (uint32_t)i;
+	}
+	qsort(sm, (size_t)ne, sizeof(side_t), side_cmp);
+	qsort(lg, (size_t)ne, sizeof(side_t), side_cmp);
+	for (r = 0; r < n_reads; r++) {
+		int e, b;
+		for (e = 0; e < ends; e++)
+			for (b = 0; b < mb; b++) {
+				const svg_mapping_result *m = &out[(r * (uint64_t)ends + (uint64_t)e) * (uint64_t)mb + (uint64_t)b];
+				uint32_t cancelled[ANTI_LIMIT];
+				int nc = 0;
+				int64_t x, l0, l1, r0, r1;
+				uint32_t cs, ce;
+				if (m->selected_votes < 1) break;
+				if (!ep->report_multi_mapping_reads && (m->result_flags & 32)) continue;   /* CORE_IS_BREAKEVEN */
+				if (m->selected_votes < p->min_votes_first) continue;
+				cs = m->selected_position + m->confident_coverage_start;
+				ce = m->selected_position + m->confident_coverage_end;
+				l0 = side_search(sm, ne, cs - 1) + 1;
+				l1 = side_search(lg, ne, cs - 1) + 1;
+				r0 = side_search(sm, ne, ce) + 20;
+				r1 = side_search(lg, ne, ce) + 20;
+				for (x = l0; x <= r0 && x < ne && nc < ANTI_LIMIT; x++) {
+					const uint32_t pos = sm[x].pos;
+					if (pos <= cs + 5 || pos >= ce - 5) continue;
+					cnt[sm[x].id]++;
+					cancelled[nc++] = sm[x].id;
+				}
+				for (x = l1; x <= r1 && x < ne; x++) {
+					const uint32_t pos = lg[x].pos;
+					int k, dup = 0;
+					if (pos <= cs + 5 || pos >= ce - 5) continue;
+					for (k = 0; k < nc; k++) if (cancelled[k] == lg[x].id) { dup = 1; break; }
+					if (!dup) cnt[lg[x].id]++;
+				}
+			}
+	}
+	for (i = 0; i < ne; i++) t->ev[i].anti_supporting_reads = (uint16_t)(t->ev[i].anti_supporting_reads + cnt[i]);
+	free(sm); free(lg); free(cnt);
 	return 0;
 }
