@@ -40,6 +40,12 @@
 
 #define LROWS 30
 #define CW 7                 // cold words per slot: cs | rec[0] << 8, then rec[0..23] as bytes (once spilled)
+#define LJW 4                // subjunc: words of a slot's subjunc_result_t (junction of the result it became)
+#define LCODEW 10            // subjunc: 2-bit codes of the current strand's read text (<= 160 bases)
+#define LJCW 17              // JUNCTION_CONFIRM_WINDOW (subread.h)
+// per-wave cold scratch words (x 64 lanes)
+#define LJLIST 24            // subjunc: minor-half candidates of a strand's results (more: the read is deferred)
+__host__ __device__ constexpr int lane_cold_words(int K, bool sj) { return 2 * K * CW + (sj ? 2 * K * LJW + LCODEW + LJLIST : 0); }
 
 // ---------------------------------------------------------------------------------------------
 // gather: one thread per (strand, read) of a chunk
@@ -127,6 +133,12 @@ struct LParams {
 	uint8_t *jout;                // subjunc_result_t records of the chunk
 	uint16_t *bm_out;             // big-margin records of the chunk
 	int bm_size, max_intron;
+	// subjunc donor scoring on the lane (SE): read text in HBM, the .array, donor-test switches
+	const char *seq;
+	const uint64_t *off;
+	const uint8_t *values;
+	uint32_t v_sbo, v_len, v_start, v_bytes;
+	int need_donor, prefer_donor, allow_mm, rev;
 	// paired-end (lane_pe_kernel)
 	const uint16_t *len2;
 	const uint32_t *chr_end;
@@ -233,6 +245,10 @@ struct Lane {
 		for (int k = 0; k < NHW; k++) h[E][k] = pick(q == (uint32_t)k, (h[E][k] & clr) | v, h[E][k]);
 	}
 	__device__ __forceinline__ uint32_t *cw(int st, int s, int w) const { return cold + ((st * K + s) * CW + w) * 64; }
+	// subjunc scratch after the slot words: the junction record of result slot (st, s), read codes
+	__device__ __forceinline__ uint32_t *jw(int st, int s) const { return cold + (2 * K * CW + (st * K + s) * LJW) * 64; }
+	__device__ __forceinline__ uint32_t *codes() const { return cold + (2 * K * CW + 2 * K * LJW) * 64; }
+	__device__ __forceinline__ uint32_t *jlist() const { return cold + (2 * K * CW + 2 * K * LJW + LCODEW) * 64; }
 	__device__ __forceinline__ int8_t *recb(int st, int s, int i) const
 	{
 		return (int8_t *)cw(st, s, 1 + (i >> 2)) + (i & 3);
@@ -341,7 +357,7 @@ __device__ __forceinline__ void write_record(const LT &L, int src, uint32_t pos,
 	w[2] = (uint32_t)(uint16_t)v | ((uint32_t)(uint16_t)u << 16);
 	if (src >= 0) {
 		const int st = src >> 6, s = src & 63;
-		const int lastk = (int)((ext >> 1) & 31u), xg = (int)(ext >> 6);
+		const int lastk = (int)((ext >> 1) & 31u), xg = (int)((ext >> 6) & 7u);
 		uint32_t rw[6];
 		const uint32_t w0 = *L.cw(st, s, 0);
 		if (ext & 1u) {
@@ -377,6 +393,118 @@ __device__ __forceinline__ void write_record(const LT &L, int src, uint32_t pos,
 	}
 }
 
+// ---------------------------------------------------------------------------------------------
+// subjunc junction search on the lane (copy_vote_to_alignment_res's junction part, no fusion /
+// long-del, max_insertion_at_junctions 0; reads <= 160 bp so both halves' indel offsets are 0)
+// ---------------------------------------------------------------------------------------------
+// base codes: A 0, G 1, C 2, T 3 (the .array's "AGCT"), 4 = 'N' past the array
+#define LB_A 0
+#define LB_G 1
+#define LB_C 2
+#define LB_T 3
+__device__ __forceinline__ uint32_t labs32u(uint32_t x) { return x > 0x7fffffffu ? (0xffffffffu - x) + 1 : x; }
+
+// gvindex_get via gvindex_get_string (gene-value-index.c:1118-1136)
+__device__ __forceinline__ int lgv(const LParams &lp, uint32_t pos)
+{
+	const uint32_t byte = (pos - lp.v_sbo) >> 2;
+	if (byte >= lp.v_bytes - 1) return 4;
+	return (int)((lp.values[byte] >> ((pos & 3u) * 2u)) & 3u);
+}
+
+// is_donor_chars + paired_chars of donor_score (core-junction.c:3717-3731): GT..AG or CT..AC
+__device__ __forceinline__ bool ldonor_ok(int l0, int l1, int r0, int r1)
+{
+	return (l0 == LB_G && l1 == LB_T && r0 == LB_A && r1 == LB_G) || (l0 == LB_C && l1 == LB_T && r0 == LB_A && r1 == LB_C);
+}
+__device__ __forceinline__ bool ldonor_chars(int a, int b)
+{
+	return (a == LB_G && b == LB_T) || (a == LB_A && b == LB_G) || (a == LB_A && b == LB_C) || (a == LB_C && b == LB_T);
+}
+
+// match_chro (gene-value-index.c:856-959, base space) over JUNCTION_CONFIRM_WINDOW bases: the read's
+// 2-bit codes at `at` (rc: LCODEW words, stride 64) against the array at pos, as one 34-bit XOR
+__device__ __forceinline__ int lmatch(const LParams &lp, const uint32_t *rc, int at, uint32_t pos)
+{
+	if ((uint32_t)(pos + LJCW) >= lp.v_len + lp.v_start) return 0;
+	if (pos > 0xffff0000u) return 0;
+	const uint32_t byte = (pos - lp.v_sbo) >> 2, bit = (pos & 3u) * 2u;
+	if (byte >= lp.v_bytes) return 0;
+	if (byte + (bit / 2 + LJCW) / 4 >= lp.v_bytes) return 0;   // the walk would hit the end
+	const uint32_t *gw = (const uint32_t *)lp.values + (byte >> 2);   // the array is padded by 64 bytes
+	const uint64_t g = ((uint64_t)gw[0] | ((uint64_t)gw[1] << 32)) >> ((byte & 3u) * 8u + bit);
+	const int wi = at >> 4;
+	const uint64_t rr = ((uint64_t)rc[wi * 64] | ((uint64_t)rc[(wi + 1) * 64] << 32)) >> ((at & 15) * 2);
+	const uint64_t x = (g ^ rr) & ((1ull << (2 * LJCW)) - 1ull);
+	return LJCW - __popcll((x | (x >> 1)) & 0x155555555ull);
+}
+
+// the current strand's read text as 2-bit codes (LSB-first, 16 per word) in the lane's scratch:
+// strand text = the read (flip 0) or reverse_read of it (flip 1; input-files.c:1111 table, 'U' as
+// 'T', anything else 'N'); match_chro counts A/G/C against 0/1/2 and every other character as T
+__device__ void lcodes(const LParams &lp, uint32_t r, int len, int flip, uint32_t *rc)
+{
+	const uint8_t *b = (const uint8_t *)(lp.seq + lp.off[r]);
+	for (int w = 0; w < LCODEW; w++) {
+		if (16 * w >= len) { rc[w * 64] = 0u; continue; }
+		uint32_t acc = 0;
+#pragma unroll 4   // (full unroll: 178 VGPRs, 2 waves/SIMD)
+		for (int k = 0; k < 16; k++) {
+			const int i = 16 * w + k;
+			const int j = i < len ? (flip ? len - 1 - i : i) : 0;
+			const int c = b[j];
+			const uint32_t code = flip ? (c == 'A' ? 3u : c == 'C' ? 1u : c == 'G' ? 2u : (c == 'T' || c == 'U') ? 0u : 3u)
+			                           : (c == 'A' ? 0u : c == 'G' ? 1u : c == 'C' ? 2u : 3u);
+			acc |= (i < len ? code : 0u) << (2 * k);
+		}
+		rc[w * 64] = acc;
+	}
+}
+
+// donor_score (core-junction.c:3675-3834) in one lane: split points mid-outward, the first strictly
+// best score kept; returns the raw best score (> 0: found) with its split point and strand.  The four
+// donor bases of a split point are independent loads (one round trip); the match windows follow only
+// where the donor test passes.
+__device__ int ldonor(const LParams &lp, const uint32_t *rc, int rl, uint32_t left, uint32_t right, int normal, int gs,
+                      int ge, int &split, int &gtag)
+{
+	int best = -111111, dr1 = 4;   // dr1: the last fetched donor_right[1] (the reference's buffer)
+	const int mid = (gs + ge) / 2, n = ge - gs;
+	const uint32_t A = normal ? left : right, B = normal ? right : left;   // donor_left / donor_right sides
+	for (int i = 0; i < n; i++) {
+		const int sp = mid + ((i & 1) ? -((i + 1) >> 1) : ((i + 1) >> 1));
+		if (sp > rl - LJCW || sp < LJCW) continue;
+		const uint32_t u = (uint32_t)sp;
+		const int g0 = lgv(lp, A + u), g1 = lgv(lp, A + u + 1u), g2 = lgv(lp, B + u - 2u), g3 = lgv(lp, B + u - 1u);
+		bool ok = false;
+		int dl0 = 4;
+		if (lp.prefer_donor) {
+			dl0 = g0;
+			// normal: donor_right is fetched only after a donor pair on the left
+			if (!normal || ldonor_chars(g0, g1)) { dr1 = g3; ok = ldonor_ok(g0, g1, g2, g3); }
+		}
+		if (!ok && lp.need_donor) continue;
+		// (with the donor test, the default, only split points at a GT..AG / CT..AC pair get here)
+		const int mLa = lmatch(lp, rc, sp - LJCW, left + u - LJCW), mLb = lmatch(lp, rc, sp, left + u);
+		const int mRa = lmatch(lp, rc, sp - LJCW, right + u - LJCW), mRb = lmatch(lp, rc, sp, right + u);
+		int lm, rm, ln, rn;
+		if (normal) {
+			lm = mLa; rm = mRb; ln = mLb; rn = mRa;
+			if (lm <= LJCW - 2 || rm < 2 * LJCW - lm - lp.allow_mm || ln > LJCW - 5 || rn > LJCW - 5) continue;
+		} else {
+			rm = mRa; lm = mLb; rn = mRb; ln = mLa;
+			if (lm + rm < 2 * LJCW - lp.allow_mm || ln > LJCW - 5 || rn > LJCW - 5) continue;
+		}
+		const int sc = 100 * ((ok ? 3000 : 0) + lm + rm - ln - rn);
+		if (sc > best) {
+			best = sc;
+			split = sp;
+			gtag = (dl0 == LB_G || dr1 == LB_G) ? 1 : 0;
+		}
+	}
+	return best;
+}
+
 template <int K, int NPF, bool SJ>
 __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 {
@@ -387,7 +515,7 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 	L.low = lp.low;
 	L.lane = (int)__lane_id();
 	L.pm = reinterpret_cast<uint2 *>(lds_raw);
-	L.cold = lp.cold + (size_t)gw * (2 * K * CW * 64) + L.lane;
+	L.cold = lp.cold + (size_t)gw * (lane_cold_words(K, SJ) * 64) + L.lane;
 	const int mb = lp.multi_best, mvs = lp.max_vote_simples, mvf = lp.min_votes_first, mvsec = lp.min_votes_second;
 	const int cutoff = lp.cutoff;
 	unsigned long long nres = 0, ndef = 0, nwhy1 = 0, nwhy2 = 0, nwhy3 = 0, ncand = 0;
@@ -598,9 +726,15 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				if (ns > 2) emit(sk2, sp2, sv2);
 				if constexpr (SJ) {
 					// junction part of copy_vote_to_alignment_res (core-junction.c:1073-1334) for each
-					// result taken from this table: a minor half that passes test_junction_minor and
-					// the overlap / distance tests would go to donor_score -- such reads are voted by
-					// the wave kernel; for every other read the junction records stay empty
+					// result taken from this table: every other slot, in the table's row-major order, is
+					// a minor-half candidate -- test_junction_minor, the overlap / distance tests,
+					// is_better_inner (core-junction.c:961) against the minor kept so far, then
+					// donor_score.  The junction record goes to the result slot's scratch; the result's
+					// ext carries bit 12 (record present) and the result_flags bits 0-1 (bits 13-14)
+					// phase 1: the candidates that pass the J-independent tests, per result in row-major
+					// order, into the lane's list (c << 6 | slot)
+					uint32_t *lst = L.jlist();
+					int nl = 0;
 					for (int c = 0; c < cur && !L.dfr; c++) {
 						const int src = sel3(c, ts0, ts1, ts2);
 						if (src < 0 || (src >> 6) != st) continue;
@@ -608,23 +742,74 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 						const uint2 eM = L.pm[sM * 64 + L.lane];
 						const int vM = lm_votes(eM.y);
 						const int csM = (int)(*L.cw(st, sM, 0) & 0xffu), ceM = lcov_end(lm_last(eM.y), lm_x(eM.y), step, lp.gap);
-						for (int q = 0; q < L.nslots; q++) {
-							if (q == sM) continue;
-							const uint2 e2 = L.pm[q * 64 + L.lane];
-							if (vM < lm_votes(e2.y)) continue;
-							const long long dist = (long long)eM.x - (long long)e2.x;
-							if ((dist < 0 ? -dist : dist) > (long long)lp.max_intron) continue;
-							const int cs2 = (int)(*L.cw(st, q, 0) & 0xffu), ce2 = lcov_end(lm_last(e2.y), lm_x(e2.y), step, lp.gap);
-							if (csM == cs2 || ceM == ce2) continue;
-							if (csM > cs2 ? eM.x < e2.x : eM.x > e2.x) continue;
-							const int ov = csM > cs2 ? ce2 - csM : ceM - cs2;
-							if (ov > 14 || abs((int)dist) < 6) continue;
-							L.dfr = true;
-							L.why = 2;
-							break;
+						for (uint32_t row = 0; row < LROWS && !L.dfr; row++) {
+							uint32_t q = L.template head<0>(row);
+							while (q != Lane<K>::NIL) {
+								const uint2 e2 = L.pm[q * 64 + L.lane];
+								const uint32_t qs = q;
+								q = lm_next(e2.y);
+								if ((int)qs == sM || vM < lm_votes(e2.y)) continue;
+								const long long dist = (long long)eM.x - (long long)e2.x;
+								if ((dist < 0 ? -dist : dist) > (long long)lp.max_intron) continue;
+								const int cs2 = (int)(*L.cw(st, (int)qs, 0) & 0xffu), ce2 = lcov_end(lm_last(e2.y), lm_x(e2.y), step, lp.gap);
+								if (csM == cs2 || ceM == ce2) continue;
+								if (csM > cs2 ? eM.x < e2.x : eM.x > e2.x) continue;   // test_junction_minor
+								const int ov = csM > cs2 ? ce2 - csM : ceM - cs2;
+								if (ov > 14 || abs((int)dist) < 6) continue;
+								if (nl == LJLIST) { L.dfr = true; L.why = 2; break; }
+								lst[nl * 64] = ((uint32_t)c << 6) | qs;
+								nl++;
+							}
 						}
 					}
 					if (L.dfr) continue;
+					// phase 2: every lane walks its list at the same step k, so the wave scores its
+					// lanes' candidates together: is_better_inner against the minor kept so far for
+					// that result, then donor_score
+					if (nl > 0) lcodes(lp, r, len, st ^ lp.rev, L.codes());
+					int Jc = -1, Jv = 0, Jcs = 0, Jce = 0, Jsplit = 0, Jnormal = 0, Jf = -1;
+					uint32_t Jpos = 0, Mpos = 0;
+					int Mcs = 0, Mce = 0, sM = 0;
+					auto flush = [&]() __attribute__((always_inline)) {
+						if (Jf < 0) return;
+						uint32_t *jw = L.jw(st, sM);
+						jw[0] = (uint32_t)(uint16_t)Jsplit | ((uint32_t)(uint16_t)Jv << 16);
+						jw[64] = ((uint32_t)(Jnormal ? 0 : 1) << 16) | ((uint32_t)(Jnormal ? 1 : 0) << 24);
+						jw[128] = Jpos;
+						jw[192] = (uint32_t)(uint16_t)Jcs | ((uint32_t)(uint16_t)Jce << 16);
+						PUT3(Jc, tx0, tx1, tx2, sel3(Jc, tx0, tx1, tx2) | (1u << 12) | ((uint32_t)Jf << 13));
+					};
+					for (int k = 0; k < nl; k++) {
+						const uint32_t ent = lst[k * 64];
+						const int c = (int)(ent >> 6), qs = (int)(ent & 63u);
+						if (c != Jc) {
+							flush();
+							Jc = c; Jv = 0; Jcs = 0; Jce = 0; Jsplit = 0; Jnormal = 0; Jf = -1; Jpos = 0;
+							sM = sel3(c, ts0, ts1, ts2) & 63;
+							const uint2 eM = L.pm[sM * 64 + L.lane];
+							Mpos = eM.x;
+							Mcs = (int)(*L.cw(st, sM, 0) & 0xffu);
+							Mce = lcov_end(lm_last(eM.y), lm_x(eM.y), step, lp.gap);
+						}
+						const uint2 e2 = L.pm[qs * 64 + L.lane];
+						const int V = lm_votes(e2.y);
+						const int cs2 = (int)(*L.cw(st, qs, 0) & 0xffu), ce2 = lcov_end(lm_last(e2.y), lm_x(e2.y), step, lp.gap);
+						// is_better_inner (core-junction.c:961)
+						const int oldi = (int)labs32u(Mpos - Jpos), intr = (int)labs32u(Mpos - e2.x);
+						const int cl = ce2 - cs2, jl = Jce - Jcs;
+						if (!(V > Jv || (V == Jv && cl > jl) || (V == Jv && cl == jl && intr < oldi))) continue;
+						const int gs = Mcs > cs2 ? ce2 - 8 : Mce - 8;
+						const int ge = Mcs < cs2 ? cs2 + 8 : Mcs + 8;
+						const int normal = 1 != (int)(Mcs > cs2) + (int)(Mpos > e2.x);
+						int split = 0, gtag = 0;
+						const int best = ldonor(lp, L.codes(), len, Mpos < e2.x ? Mpos : e2.x, Mpos > e2.x ? Mpos : e2.x, normal,
+						                        gs > 0 ? gs : 0, ge < len ? ge : len, split, gtag);
+						if (best > 0) {
+							Jpos = e2.x; Jv = V; Jcs = cs2; Jce = ce2; Jsplit = split; Jnormal = normal;
+							Jf = best < 290000 ? 3 : (gtag ? 1 : 0);   // is_donor_found_or_annotation, GT/AG strand
+						}
+					}
+					flush();
 				}
 				if (cur > 0) { rsrc0 = ts0; rpos0 = tp0; rv0 = tv0; ru0 = tu0; rx0 = tx0; } else rv0 = 0;
 				if (cur > 1) { rsrc1 = ts1; rpos1 = tp1; rv1 = tv1; ru1 = tu1; rx1 = tx1; } else rv1 = 0;
@@ -656,11 +841,18 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 				const int v = sel3(i, rv0, rv1, rv2);
 				const int u = sel3(i, ru0, ru1, ru2);
 				uint32_t w[17];
-				write_record(L, src, pos, v, u, sel3(i, rx0, rx1, rx2), step, lp.gap, w);
+				const uint32_t x = sel3(i, rx0, rx1, rx2);
+				write_record(L, src, pos, v, u, x, step, lp.gap, w);
 				if constexpr (SJ) {
-					// no minor half on the lane path: empty subjunc_result_t
-					uint4 *jd = (uint4 *)(lp.jout + ((size_t)r * mb + i) * 16);
-					*jd = make_uint4(0u, 0u, 0u, 0u);
+					// the result's subjunc_result_t (empty without a minor half); a zero-vote record
+					// keeps the stale one with minor_votes 0 (topk's reset of unused results)
+					uint4 jr = make_uint4(0u, 0u, 0u, 0u);
+					if (src >= 0 && ((x >> 12) & 1u)) {
+						const uint32_t *jw = L.jw(src >> 6, src & 63);
+						jr = make_uint4(v > 0 ? jw[0] : (jw[0] & 0xffffu), jw[64], jw[128], jw[192]);
+						w[1] |= (x >> 13) & 3u;
+					}
+					*(uint4 *)(lp.jout + ((size_t)r * mb + i) * 16) = jr;
 				}
 #pragma unroll
 				for (int k = 0; k < 17; k++) dst[i * 17 + k] = w[k];
@@ -1145,7 +1337,7 @@ static int lane_launch(svg_index *h, LParams &lp, uint32_t **cold, size_t *cold_
 	uint64_t blocks = (uint64_t)h->n_cu * per_cu, need_b = (lp.n + 63) / 64;
 	if (blocks > need_b) blocks = need_b;
 	if (blocks < 1) blocks = 1;
-	const size_t words = blocks * (size_t)(2 * K * CW * 64);
+	const size_t words = blocks * (size_t)(lane_cold_words(K, lp.jout != NULL) * 64);
 	if (words > *cold_words) {
 		hipFree(*cold);
 		*cold = NULL;
@@ -1262,8 +1454,8 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 }
 
 int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *len, uint32_t n, const uint2 *precs, int nps,
-                   uint8_t *out, uint8_t *jout, uint16_t *bm, unsigned long long *stats, uint32_t **defer_list,
-                   uint32_t **defer_count, hipStream_t st)
+                   uint8_t *out, uint8_t *jout, uint16_t *bm, const char *seq, const uint64_t *off,
+                   unsigned long long *stats, uint32_t **defer_list, uint32_t **defer_count, hipStream_t st)
 {
 	const uint32_t n2 = n / 4 + 64;   // heavy-pass columns
 	const char *e = getenv("SVG_LANE");
@@ -1310,6 +1502,15 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 	lp.bm_out = p->do_big_margin_filtering_for_junctions ? bm : NULL;
 	lp.bm_size = p->do_big_margin_filtering_for_junctions ? p->big_margin_record_size : 0;
 	lp.max_intron = p->maximum_intron_length;
+	// donor scoring (subjunc): the chunk's read text and the .array
+	lp.seq = seq; lp.off = off;
+	lp.values = h->dix.values;
+	lp.v_sbo = h->dix.start_base_offset; lp.v_len = h->dix.length; lp.v_start = h->dix.start_point;
+	lp.v_bytes = h->dix.values_bytes;
+	lp.need_donor = p->check_donor_at_junctions != 0;
+	lp.prefer_donor = p->prefer_donor_receptor_junctions != 0;
+	lp.allow_mm = p->more_accurate_fusions ? 0 : 1;
+	lp.rev = p->reverse_r1 != 0;
 	lp.defer_list = (uint32_t *)(b + o_l1);
 	lp.defer_count = cnt;
 	lp.defer_all = e && e[0] == '2';
