@@ -200,7 +200,8 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
                    int nps, uint8_t *out, uint8_t *jout, uint16_t *bm, const char *seq, const uint64_t *off,
                    unsigned long long *stats, uint32_t **defer_list, uint32_t **defer_count, hipStream_t st);
 int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *len1, const uint16_t *len2, uint32_t n,
-                      const uint2 *precs, int nps, uint8_t *out, uint8_t *jout, uint16_t *bm_out, unsigned long long *stats,
+                      const uint2 *precs, int nps, uint8_t *out, uint8_t *jout, uint16_t *bm_out, const char *seq1,
+                      const uint64_t *off1, const char *seq2, const uint64_t *off2, unsigned long long *stats,
                       uint32_t **defer_list, uint32_t **defer_count, hipStream_t st);
 int svg_timing_mark(svg_index *h, int k, int phase, hipStream_t st);
 

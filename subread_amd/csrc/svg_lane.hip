@@ -45,7 +45,7 @@
 #define LJCW 17              // JUNCTION_CONFIRM_WINDOW (subread.h)
 // per-wave cold scratch words (x 64 lanes)
 #define LJLIST 24            // subjunc: minor-half candidates of a strand's results (more: the read is deferred)
-__host__ __device__ constexpr int lane_cold_words(int K, bool sj) { return 2 * K * CW + (sj ? 2 * K * LJW + LCODEW + LJLIST : 0); }
+__host__ __device__ constexpr int lane_cold_words(int K, bool sj, int ends = 1) { return 2 * K * CW + (sj ? 2 * K * LJW + ends * LCODEW + LJLIST : 0); }
 
 // ---------------------------------------------------------------------------------------------
 // gather: one thread per (strand, read) of a chunk
@@ -134,11 +134,11 @@ struct LParams {
 	uint16_t *bm_out;             // big-margin records of the chunk
 	int bm_size, max_intron;
 	// subjunc donor scoring on the lane (SE): read text in HBM, the .array, donor-test switches
-	const char *seq;
-	const uint64_t *off;
+	const char *seq, *seq2;
+	const uint64_t *off, *off2;
 	const uint8_t *values;
 	uint32_t v_sbo, v_len, v_start, v_bytes;
-	int need_donor, prefer_donor, allow_mm, rev;
+	int need_donor, prefer_donor, allow_mm, rev, rev2;
 	// paired-end (lane_pe_kernel)
 	const uint16_t *len2;
 	const uint32_t *chr_end;
@@ -247,8 +247,8 @@ struct Lane {
 	__device__ __forceinline__ uint32_t *cw(int st, int s, int w) const { return cold + ((st * K + s) * CW + w) * 64; }
 	// subjunc scratch after the slot words: the junction record of result slot (st, s), read codes
 	__device__ __forceinline__ uint32_t *jw(int st, int s) const { return cold + (2 * K * CW + (st * K + s) * LJW) * 64; }
-	__device__ __forceinline__ uint32_t *codes() const { return cold + (2 * K * CW + 2 * K * LJW) * 64; }
-	__device__ __forceinline__ uint32_t *jlist() const { return cold + (2 * K * CW + 2 * K * LJW + LCODEW) * 64; }
+	__device__ __forceinline__ uint32_t *codes(int e = 0) const { return cold + (2 * K * CW + 2 * K * LJW + e * LCODEW) * 64; }
+	__device__ __forceinline__ uint32_t *jlist() const { return cold + (2 * K * CW + 2 * K * LJW + ENDS * LCODEW) * 64; }
 	__device__ __forceinline__ int8_t *recb(int st, int s, int i) const
 	{
 		return (int8_t *)cw(st, s, 1 + (i >> 2)) + (i & 3);
@@ -442,9 +442,9 @@ __device__ __forceinline__ int lmatch(const LParams &lp, const uint32_t *rc, int
 // the current strand's read text as 2-bit codes (LSB-first, 16 per word) in the lane's scratch:
 // strand text = the read (flip 0) or reverse_read of it (flip 1; input-files.c:1111 table, 'U' as
 // 'T', anything else 'N'); match_chro counts A/G/C against 0/1/2 and every other character as T
-__device__ void lcodes(const LParams &lp, uint32_t r, int len, int flip, uint32_t *rc)
+__device__ void lcodes(const char *seq, const uint64_t *off, uint32_t r, int len, int flip, uint32_t *rc)
 {
-	const uint8_t *b = (const uint8_t *)(lp.seq + lp.off[r]);
+	const uint8_t *b = (const uint8_t *)(seq + off[r]);
 	for (int w = 0; w < LCODEW; w++) {
 		if (16 * w >= len) { rc[w * 64] = 0u; continue; }
 		uint32_t acc = 0;
@@ -505,8 +505,10 @@ __device__ int ldonor(const LParams &lp, const uint32_t *rc, int rl, uint32_t le
 	return best;
 }
 
+// (waves_per_eu 4: the subjunc variant needs 154 VGPRs unconstrained, i.e. 3 waves/SIMD; capped at
+// 128 it spills 48 B/lane and the C5 lane kernel runs 3.6 -> 2.5 ms per 1M reads)
 template <int K, int NPF, bool SJ>
-__global__ void __launch_bounds__(64) lane_kernel(LParams lp)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) lane_kernel(LParams lp)
 {
 	extern __shared__ __align__(16) uint8_t lds_raw[];
 	const uint32_t gw = blockIdx.x, nw = gridDim.x;
@@ -766,7 +768,7 @@ __global__ void __launch_bounds__(64) lane_kernel(LParams lp)
 					// phase 2: every lane walks its list at the same step k, so the wave scores its
 					// lanes' candidates together: is_better_inner against the minor kept so far for
 					// that result, then donor_score
-					if (nl > 0) lcodes(lp, r, len, st ^ lp.rev, L.codes());
+					if (nl > 0) lcodes(lp.seq, lp.off, r, len, st ^ lp.rev, L.codes());
 					int Jc = -1, Jv = 0, Jcs = 0, Jce = 0, Jsplit = 0, Jnormal = 0, Jf = -1;
 					uint32_t Jpos = 0, Mpos = 0;
 					int Mcs = 0, Mce = 0, sM = 0;
@@ -948,10 +950,11 @@ __device__ __forceinline__ void pl_put(uint32_t (&w)[PLW], int i, uint32_t id)
 #define RM_SETV(m, v) (((m) & ~(255u << 8)) | ((uint32_t)(v) << 8))
 
 // SJ: subjunc pairs (process_voting_junction_PE_topK with copy_vote's junction part): big-margin
-// records per end as in lane_kernel; a pair with a result whose table holds a minor half that
-// would reach donor_score is deferred to the wave kernel
+// records per end and the junction search / donor scoring of every record taken from a table, as
+// in lane_kernel
+// (waves_per_eu 3: the subjunc variant needs 179 VGPRs unconstrained, 168 without spills at 3 waves)
 template <int K, int NPF, bool SJ>
-__global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) lane_pe_kernel(LParams lp)
 {
 	extern __shared__ __align__(16) uint8_t lds_raw[];
 	const uint32_t gw = blockIdx.x, nw = gridDim.x;
@@ -960,7 +963,7 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 	L.low = lp.low;
 	L.lane = (int)__lane_id();
 	L.pm = reinterpret_cast<uint2 *>(lds_raw);
-	L.cold = lp.cold + (size_t)gw * (2 * K * CW * 64) + L.lane;
+	L.cold = lp.cold + (size_t)gw * (lane_cold_words(K, SJ, 2) * 64) + L.lane;
 	const int mb = lp.multi_best, mvs = lp.max_vote_simples, mvf = lp.min_votes_first, mvsec = lp.min_votes_second;
 	const int cutoff = lp.cutoff, mvc = lp.mvc;
 	unsigned long long nres = 0, ndef = 0, nwhy1 = 0, nwhy2 = 0, nwhy3 = 0, ncand = 0;
@@ -993,6 +996,9 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 		uint32_t bv[2][3] = {{0, 0, 0}, {0, 0, 0}}, bs[2][3] = {{0, 0, 0}, {0, 0, 0}};
 		const int nbm = SJ ? (lp.bm_size >= 3 ? lp.bm_size / 3 : 0) : 0;
 		int nc_read = 0;
+		// subjunc: a nibble per (end, record) at (end * 3 + i) * 4: bit 0 = the record has a junction
+		// record in the scratch of its slot, bits 1-2 = its result_flags bits 0-1
+		uint32_t jm = 0;
 		for (int st = 0; st < 2; st++) {
 			L.reset();
 			// ---- both ends' tables: fused gather as in lane_kernel, records of (end, strand)
@@ -1178,41 +1184,28 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 			// (4) results of each end
 			uint32_t tm0[3] = {0, 0, 0}, tm1[3] = {0, 0, 0}, tp0[3] = {0, 0, 0}, tp1[3] = {0, 0, 0};
 			int cur[2] = {0, 0};
+			uint32_t tjm = 0, needj = 0;   // subjunc: the new records' nibbles; records needing a junction search
 			auto emit = [&](int E, uint32_t id) __attribute__((always_inline)) {
 				uint32_t pos;
 				const int v = sv(E, id, pos);
 				uint32_t m;
 				if (id < 32u) m = RM((st << 6) | (int)id, v, applied[E]) | (lm_ext(L.pm[id * 64 + L.lane].y) << 22);
 				else { const int i = (int)id - 32; m = E ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]); }
-				if constexpr (SJ) {
-					// copy_vote_to_alignment_res's junction part (core-junction.c:1073-1334) for a
-					// result taken from this table: a minor half of the same end that passes
-					// test_junction_minor and the overlap / distance tests would go to donor_score
-					if (id < 32u && !L.dfr) {
-						const uint2 eM = L.pm[id * 64 + L.lane];
-						const int csM = (int)(*L.cw(st, (int)id, 0) & 0xffu), ceM = lcov_end(lm_last(eM.y), lm_x(eM.y), step[E], lp.gap);
-						for (int q = 0; q < L.nslots; q++) {
-							if (q == (int)id) continue;
-							const uint2 e2 = L.pm[q * 64 + L.lane];
-							if ((lm_endbit(e2.y) != 0) != (E != 0) || v < lm_votes(e2.y)) continue;
-							const long long dist = (long long)eM.x - (long long)e2.x;
-							if ((dist < 0 ? -dist : dist) > (long long)lp.max_intron) continue;
-							const int cs2 = (int)(*L.cw(st, q, 0) & 0xffu), ce2 = lcov_end(lm_last(e2.y), lm_x(e2.y), step[E], lp.gap);
-							if (csM == cs2 || ceM == ce2) continue;
-							if (csM > cs2 ? eM.x < e2.x : eM.x > e2.x) continue;
-							const int ov = csM > cs2 ? ce2 - csM : ceM - cs2;
-							if (ov > 14 || abs((int)dist) < 6) continue;
-							L.dfr = true;
-							L.why = 2;
-							break;
-						}
-					}
-				}
 				const int c = cur[E];
 				const uint32_t q0 = E ? tp1[0] : tp0[0], q1 = E ? tp1[1] : tp0[1];
 				if ((c > 0 && q0 == pos) || (c > 1 && q1 == pos)) return;
 				if (E) { PUT3(c, tm1[0], tm1[1], tm1[2], m); PUT3(c, tp1[0], tp1[1], tp1[2], pos); }
 				else { PUT3(c, tm0[0], tm0[1], tm0[2], m); PUT3(c, tp0[0], tp0[1], tp0[2], pos); }
+				if constexpr (SJ) {
+					// a stored record keeps its junction record; one taken from this table gets the
+					// junction search below (copy_vote_to_alignment_res runs after the position test,
+					// core-junction.c:2413-2425)
+					const int b = (E * 3 + c) * 4;
+					uint32_t nib = 0;
+					if (id >= 32u) nib = (jm >> ((E * 3 + (int)id - 32) * 4)) & 15u;
+					else needj |= 1u << (E * 3 + c);
+					tjm = (tjm & ~(15u << b)) | (nib << b);
+				}
 				cur[E] = c + 1;
 			};
 			if (ncomb > 0) {
@@ -1243,11 +1236,102 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 						emit(e, id);
 					}
 			}
+			if constexpr (SJ) {
+				// junction part of copy_vote_to_alignment_res (core-junction.c:1073-1334) for every
+				// record taken from this strand's tables, in lane_kernel's two phases; a minor half is
+				// a slot of the same end's table.  List entries: end << 7 | record << 5 | slot.
+				uint32_t *lst = L.jlist();
+				int nl = 0;
+				uint32_t ends_used = 0;
+				for (int E = 0; E < 2 && !L.dfr; E++)
+					for (int c = 0; c < cur[E] && !L.dfr; c++) {
+						if (!((needj >> (E * 3 + c)) & 1u)) continue;
+						const int sM = RM_SRC(E ? sel3(c, tm1[0], tm1[1], tm1[2]) : sel3(c, tm0[0], tm0[1], tm0[2])) & 63;
+						const uint2 eM = L.pm[sM * 64 + L.lane];
+						const int vM = lm_votes(eM.y), stE = E ? step[1] : step[0];
+						const int csM = (int)(*L.cw(st, sM, 0) & 0xffu), ceM = lcov_end(lm_last(eM.y), lm_x(eM.y), stE, lp.gap);
+						for (uint32_t row = 0; row < LROWS && !L.dfr; row++) {
+							uint32_t q = E ? L.template head<1>(row) : L.template head<0>(row);
+							while (q != Lane<K, 2>::NIL) {
+								const uint2 e2 = L.pm[q * 64 + L.lane];
+								const uint32_t qs = q;
+								q = lm_next(e2.y);
+								if ((int)qs == sM || vM < lm_votes(e2.y)) continue;
+								const long long dist = (long long)eM.x - (long long)e2.x;
+								if ((dist < 0 ? -dist : dist) > (long long)lp.max_intron) continue;
+								const int cs2 = (int)(*L.cw(st, (int)qs, 0) & 0xffu), ce2 = lcov_end(lm_last(e2.y), lm_x(e2.y), stE, lp.gap);
+								if (csM == cs2 || ceM == ce2) continue;
+								if (csM > cs2 ? eM.x < e2.x : eM.x > e2.x) continue;   // test_junction_minor
+								const int ov = csM > cs2 ? ce2 - csM : ceM - cs2;
+								if (ov > 14 || abs((int)dist) < 6) continue;
+								if (nl == LJLIST) { L.dfr = true; L.why = 2; break; }
+								lst[nl * 64] = ((uint32_t)E << 7) | ((uint32_t)c << 5) | qs;
+								nl++;
+								ends_used |= 1u << E;
+							}
+						}
+					}
+				if (L.dfr) continue;
+				if (ends_used & 1u) lcodes(lp.seq, lp.off, r, len[0], st ^ lp.rev, L.codes(0));
+				if (ends_used & 2u) lcodes(lp.seq2, lp.off2, r, len[1], st ^ lp.rev2, L.codes(1));
+				int Jk = -1, JE = 0, Jc = 0, Jv = 0, Jcs = 0, Jce = 0, Jsplit = 0, Jnormal = 0, Jf = -1;
+				uint32_t Jpos = 0, Mpos = 0;
+				int Mcs = 0, Mce = 0, sM = 0, stE = 0, rl = 0;
+				auto flush = [&]() __attribute__((always_inline)) {
+					if (Jf < 0) return;
+					uint32_t *jw = L.jw(st, sM);
+					jw[0] = (uint32_t)(uint16_t)Jsplit | ((uint32_t)(uint16_t)Jv << 16);
+					jw[64] = ((uint32_t)(Jnormal ? 0 : 1) << 16) | ((uint32_t)(Jnormal ? 1 : 0) << 24);
+					jw[128] = Jpos;
+					jw[192] = (uint32_t)(uint16_t)Jcs | ((uint32_t)(uint16_t)Jce << 16);
+					const int b = (JE * 3 + Jc) * 4;
+					tjm = (tjm & ~(15u << b)) | ((1u | ((uint32_t)Jf << 1)) << b);
+				};
+				for (int k = 0; k < nl; k++) {
+					const uint32_t ent = lst[k * 64];
+					const int key = (int)(ent >> 5), qs = (int)(ent & 31u);
+					if (key != Jk) {
+						flush();
+						Jk = key; JE = key >> 2; Jc = key & 3;
+						Jv = 0; Jcs = 0; Jce = 0; Jsplit = 0; Jnormal = 0; Jf = -1; Jpos = 0;
+						sM = RM_SRC(JE ? sel3(Jc, tm1[0], tm1[1], tm1[2]) : sel3(Jc, tm0[0], tm0[1], tm0[2])) & 63;
+						stE = JE ? step[1] : step[0];
+						rl = JE ? len[1] : len[0];
+						const uint2 eM = L.pm[sM * 64 + L.lane];
+						Mpos = eM.x;
+						Mcs = (int)(*L.cw(st, sM, 0) & 0xffu);
+						Mce = lcov_end(lm_last(eM.y), lm_x(eM.y), stE, lp.gap);
+					}
+					const uint2 e2 = L.pm[qs * 64 + L.lane];
+					const int V = lm_votes(e2.y);
+					const int cs2 = (int)(*L.cw(st, qs, 0) & 0xffu), ce2 = lcov_end(lm_last(e2.y), lm_x(e2.y), stE, lp.gap);
+					// is_better_inner (core-junction.c:961)
+					const int oldi = (int)labs32u(Mpos - Jpos), intr = (int)labs32u(Mpos - e2.x);
+					const int cl = ce2 - cs2, jl = Jce - Jcs;
+					if (!(V > Jv || (V == Jv && cl > jl) || (V == Jv && cl == jl && intr < oldi))) continue;
+					const int gs = Mcs > cs2 ? ce2 - 8 : Mce - 8;
+					const int ge = Mcs < cs2 ? cs2 + 8 : Mcs + 8;
+					const int normal = 1 != (int)(Mcs > cs2) + (int)(Mpos > e2.x);
+					int split = 0, gtag = 0;
+					const int best = ldonor(lp, L.codes(JE), rl, Mpos < e2.x ? Mpos : e2.x, Mpos > e2.x ? Mpos : e2.x, normal,
+					                        gs > 0 ? gs : 0, ge < rl ? ge : rl, split, gtag);
+					if (best > 0) {
+						Jpos = e2.x; Jv = V; Jcs = cs2; Jce = ce2; Jsplit = split; Jnormal = normal;
+						Jf = best < 290000 ? 3 : (gtag ? 1 : 0);
+					}
+				}
+				flush();
+			}
 #pragma unroll
 			for (int i = 0; i < 3; i++) {
-				if (SJ && L.dfr) break;
-				if (i < cur[0]) { rm0[i] = tm0[i]; rp0[i] = tp0[i]; } else rm0[i] = RM_SETV(rm0[i], 0);
-				if (i < cur[1]) { rm1[i] = tm1[i]; rp1[i] = tp1[i]; } else rm1[i] = RM_SETV(rm1[i], 0);
+				if (i < cur[0]) {
+					rm0[i] = tm0[i]; rp0[i] = tp0[i];
+					if (SJ) jm = (jm & ~(15u << (i * 4))) | (tjm & (15u << (i * 4)));
+				} else rm0[i] = RM_SETV(rm0[i], 0);
+				if (i < cur[1]) {
+					rm1[i] = tm1[i]; rp1[i] = tp1[i];
+					if (SJ) jm = (jm & ~(15u << ((3 + i) * 4))) | (tjm & (15u << ((3 + i) * 4)));
+				} else rm1[i] = RM_SETV(rm1[i], 0);
 			}
 		}
 		if (!L.dfr) ncand += (unsigned long long)nc_read;
@@ -1261,14 +1345,22 @@ __global__ void __launch_bounds__(64) lane_pe_kernel(LParams lp)
 					const uint32_t pos = e ? sel3(i, rp1[0], rp1[1], rp1[2]) : sel3(i, rp0[0], rp0[1], rp0[2]);
 					uint32_t w[17];
 					write_record(L, RM_SRC(m), pos, RM_V(m), RM_U(m), RM_EXT(m), step[e], lp.gap, w);
+					if constexpr (SJ) {
+						// the record's subjunc_result_t (empty without a minor half; a zero-vote record
+						// keeps the stale one with minor_votes 0)
+						const uint32_t nib = (jm >> ((e * 3 + i) * 4)) & 15u;
+						uint4 jr = make_uint4(0u, 0u, 0u, 0u);
+						const int src = RM_SRC(m);
+						if (src >= 0 && (nib & 1u)) {
+							const uint32_t *jw = L.jw(src >> 6, src & 63);
+							jr = make_uint4(RM_V(m) > 0 ? jw[0] : (jw[0] & 0xffffu), jw[64], jw[128], jw[192]);
+							w[1] |= (nib >> 1) & 3u;
+						}
+						*(uint4 *)(lp.jout + (((size_t)r * 2 + e) * mb + i) * 16) = jr;
+					}
 #pragma unroll
 					for (int k = 0; k < 17; k++) dst[i * 17 + k] = w[k];
 					nres += RM_V(m) > 0;
-					if constexpr (SJ) {
-						// no minor half on the lane path: empty subjunc_result_t
-						uint4 *jd = (uint4 *)(lp.jout + (((size_t)r * 2 + e) * mb + i) * 16);
-						*jd = make_uint4(0u, 0u, 0u, 0u);
-					}
 				}
 				if constexpr (SJ) {
 					if (lp.bm_out) {
@@ -1386,7 +1478,8 @@ int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int s
 
 // paired-end: lane_pe_kernel over every pair of the chunk; deferred pairs listed for vote_kernel
 int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *len1, const uint16_t *len2, uint32_t n,
-                      const uint2 *precs, int nps, uint8_t *out, uint8_t *jout, uint16_t *bm_out, unsigned long long *stats,
+                      const uint2 *precs, int nps, uint8_t *out, uint8_t *jout, uint16_t *bm_out, const char *seq1,
+                      const uint64_t *off1, const char *seq2, const uint64_t *off2, unsigned long long *stats,
                       uint32_t **defer_list, uint32_t **defer_count, hipStream_t st)
 {
 	const char *e = getenv("SVG_LANE");
@@ -1419,6 +1512,16 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	lp.bm_out = jout ? bm_out : NULL;
 	lp.bm_size = p->do_big_margin_filtering_for_junctions ? p->big_margin_record_size : 0;
 	lp.max_intron = p->maximum_intron_length;
+	// donor scoring (subjunc): both ends' read text and the .array
+	lp.seq = seq1; lp.off = off1; lp.seq2 = seq2; lp.off2 = off2;
+	lp.values = h->dix.values;
+	lp.v_sbo = h->dix.start_base_offset; lp.v_len = h->dix.length; lp.v_start = h->dix.start_point;
+	lp.v_bytes = h->dix.values_bytes;
+	lp.need_donor = p->check_donor_at_junctions != 0;
+	lp.prefer_donor = p->prefer_donor_receptor_junctions != 0;
+	lp.allow_mm = p->more_accurate_fusions ? 0 : 1;
+	lp.rev = p->reverse_r1 != 0;
+	lp.rev2 = p->reverse_r2 != 0;
 	lp.defer_list = (uint32_t *)(b + o_l1);
 	lp.defer_count = cnt;
 	lp.defer_all = e && e[0] == '2';
@@ -1433,7 +1536,7 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	uint64_t blocks = (uint64_t)h->n_cu * per_cu, need_b = (n + 63) / 64;
 	if (blocks > need_b) blocks = need_b;
 	if (blocks < 1) blocks = 1;
-	const size_t words = blocks * (size_t)(2 * K * CW * 64);
+	const size_t words = blocks * (size_t)(lane_cold_words(K, jout != NULL, 2) * 64);
 	if (words > h->lscratch_words) {
 		hipFree(h->d_lscratch);
 		h->d_lscratch = NULL;

@@ -2863,7 +2863,7 @@ int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slo
 		// vote_kernel below, which reads the SoA probe records of the deferred reads
 		uint32_t *dl = NULL, *dc = NULL;
 		rc = pe ? svg_lane_pe_chunk(h, slot, p, kc.len1, kc.len2, (uint32_t)cn, kc.precs, nps, kc.out, job->sj ? kc.jout : NULL,
-		                            kc.bm_out, kp.stats, &dl, &dc, st)
+		                            kc.bm_out, kc.seq1, kc.off1, kc.seq2, kc.off2, kp.stats, &dl, &dc, st)
 		        : svg_lane_chunk(h, slot, p, kc.len1, (uint32_t)cn, kc.precs, nps, kc.out, job->sj ? kc.jout : NULL, kc.bm_out,
 		                         kc.seq1, kc.off1, kp.stats, &dl, &dc, st);
 		if (rc) return rc;
