@@ -162,8 +162,8 @@ SJ_SE = [n for n in golden_names() if n.startswith("sj_se_")]
 @pytest.mark.parametrize("mode", PE_MODES)
 @pytest.mark.parametrize("name", SJ_SE)
 def test_lane_sj_modes_match_reference_golden(name, mode, gpu_indexes, monkeypatch):
-    """Subjunc SE on the lane path (big-margin records, junction pre-filter deferring
-    every read that needs donor scoring) on the reference's subjunc records."""
+    """Subjunc SE on the lane path (big-margin records, junction search and donor scoring in
+    the lane kernel) on the reference's subjunc records."""
     monkeypatch.setenv("SVG_LANE", mode)
     c = Case(name)
     ix = gpu_indexes(c.index_key)
@@ -206,8 +206,8 @@ SJ_PE = [n for n in golden_names() if n.startswith("sj_pe_")]
 @pytest.mark.parametrize("mode", PE_MODES)
 @pytest.mark.parametrize("name", SJ_PE)
 def test_lane_sj_pe_modes_match_reference_golden(name, mode, gpu_indexes, monkeypatch):
-    """Subjunc PE on the paired lane path (lane_pe_kernel<SJ>: big-margin records per end,
-    pairs whose results have a donor-scoring minor half deferred) on the reference's records."""
+    """Subjunc PE on the paired lane path (lane_pe_kernel<SJ>: big-margin records, junction
+    search and donor scoring per end) on the reference's records."""
     monkeypatch.setenv("SVG_LANE", mode)
     c = Case(name)
     ix = gpu_indexes(c.index_key)
