@@ -244,6 +244,20 @@ int svg_vote_batch_packed_device(svg_index *idx, const svg_params *p,
                                  svg_mapping_result *out, svg_subjunc_result *jout,
                                  uint16_t *big_margin, void *hip_stream);
 
+/*
+ * Equal-key runs of arbitrary subread keys in one index block: cellCounts' hit-list lookup
+ * (prefill_votes, cell-counts.c:432-491) on the GPU.  For key i: bucket b = key % buckets,
+ * binary search of (short)(key / buckets) in the bucket's keys, then prefill_votes' step-down
+ * widening, exactly.  first[i] = bucket-local index of the run's first item (the reference's
+ * start_location_in_index = bucket->item_values + first[i]), count[i] = run length (its
+ * votes[i]; 0 = absent, first[i] = 0).  svg_probe_keys takes host buffers (synchronous);
+ * svg_probe_keys_device device buffers, asynchronous on hip_stream (NULL: the handle's).
+ */
+int svg_probe_keys(svg_index *idx, int block, const uint32_t *keys, uint64_t n,
+                   uint32_t *first, uint32_t *count);
+int svg_probe_keys_device(svg_index *idx, int block, const uint32_t *keys, uint64_t n,
+                          uint32_t *first, uint32_t *count, void *hip_stream);
+
 /* Per-batch statistics of the last svg_vote_batch* call on this handle
  * (filled only when the handle was opened with SVG_STATS=1 in the environment
  * or after svg_set_stats(idx,1)); used for the algorithmic-byte roofline. */

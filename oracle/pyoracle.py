@@ -37,6 +37,8 @@ def lib():
         L.svo_index_open.argtypes = [ctypes.c_char_p]
         L.svo_index_close.argtypes = [ctypes.c_void_p]
         L.svo_index_info.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
+        L.svo_prefill.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                  ctypes.c_void_p]
         L.svo_index_from_arrays.restype = ctypes.c_void_p
         L.svo_index_from_arrays.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
@@ -67,6 +69,14 @@ class OracleIndex:
                              ctypes.byref(pad), ctypes.byref(nchr))
         self.buckets, self.items, self.gap, self.padding, self.n_chr = (
             nb.value, items.value, gap.value, pad.value, nchr.value)
+
+    def prefill(self, keys, block=0):
+        """prefill_votes (cell-counts.c:432-491) per key: (bucket-local first item, run length)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        first = np.empty(len(keys), np.uint32)
+        count = np.empty(len(keys), np.uint32)
+        lib().svo_prefill(self.h, int(block), keys.ctypes.data, len(keys), first.ctypes.data, count.ctypes.data)
+        return first, count
 
     def close(self):
         if self.h:

@@ -28,6 +28,7 @@
  *                     insert_big_margin_record      core-junction.c:789-811
  *                     match_chro / gvindex_get      gene-value-index.c:856-959, 96-107
  *   index files       gehash_load                   sorted-hashtable.c:1390-1625
+ *   cellCounts lists  prefill_votes                 cell-counts.c:432-491
  *                     gvindex_load                  gene-value-index.c:190-228
  *                     load_offsets                  gene-algorithms.c:1293-1370
  */
@@ -187,6 +188,43 @@ svo_index *svo_index_from_arrays(uint32_t nb, uint64_t items, int gap, int paddi
 void svo_index_info(const svo_index *ix, uint32_t *nb, uint64_t *items, int *gap, int *padding, uint32_t *n_chr)
 {
 	*nb = ix->nb; *items = ix->items; *gap = ix->gap; *padding = ix->padding; *n_chr = ix->n_chr;
+}
+
+/* ------------------------------------------------------------------ cellCounts hit lists */
+/* prefill_votes, cell-counts.c:432-491: bucket-local first item and length of the equal-key run
+ * of each key in block `block` (binary search on short keys, step-down widening, single steps) */
+void svo_prefill(const svo_index *ix0, int block, const uint32_t *in, uint64_t n, uint32_t *first, uint32_t *count)
+{
+	const svo_index *ix = ix0;
+	for (int b = 0; b < block && ix; b++) ix = ix->next;
+	for (uint64_t t = 0; t < n; t++) {
+		first[t] = 0; count[t] = 0;
+		if (!ix) continue;
+		const uint32_t sub = in[t], bk = sub % ix->nb;
+		const int items = (int)(ix->bstart[bk + 1] - ix->bstart[bk]);
+		const int16_t *keys = ix->keys + ix->bstart[bk];
+		const int16_t key = (int16_t)(sub / ix->nb);
+		if (!items) continue;
+		int imin = 0, imax = items - 1, last, found = 1;
+		while (1) {
+			last = (imin + imax) / 2;
+			if (keys[last] > key) imax = last - 1;
+			else if (keys[last] < key) imin = last + 1;
+			else break;
+			if (imax < imin) { found = 0; break; }
+		}
+		if (!found) continue;
+		imax -= imin;
+		int start = last, stoploc, step;
+		for (step = imax / 4; step > 1; step /= 3)
+			while (1) { int tl = last + step; if (tl >= items || keys[tl] != key) break; last = tl; }
+		while (1) { last++; if (last == items || keys[last] != key) { stoploc = last; last = start; break; } }
+		for (step = imax / 4; step > 1; step /= 3)
+			while (1) { int tl = last - step; if (tl < imin || keys[tl] != key) break; last = tl; }
+		while (1) { if (last == imin || keys[last - 1] != key) break; last--; }
+		first[t] = (uint32_t)last;
+		count[t] = (uint32_t)(stoploc - last);
+	}
 }
 
 /* ------------------------------------------------------------------ read text */

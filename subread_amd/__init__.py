@@ -30,7 +30,7 @@ EXPORTS = [
     "svg_sim_repeats", "svg_sim_reads", "svg_index_build", "svg_index_build_mem", "svg_index_export",
     "svg_set_max_read_length", "svg_sim_pairs", "svg_set_timing", "svg_get_timing",
     "svg_get_kernel_timing", "svg_device_status", "svg_pack_reads", "svg_vote_batch_packed",
-    "svg_vote_batch_packed_device",
+    "svg_vote_batch_packed_device", "svg_probe_keys", "svg_probe_keys_device",
     # host post-vote events (include/subread_events.h)
     "svg_event_params_default", "svg_genome_arrays_open", "svg_genome_arrays_close", "svg_events_create",
     "svg_events_destroy", "svg_events_add_batch", "svg_events_merge", "svg_events_count", "svg_events_get",
@@ -93,6 +93,10 @@ def lib():
         L.svg_vote_batch_packed.restype = i32
         L.svg_vote_batch_packed_device.argtypes = [vp] * 8
         L.svg_vote_batch_packed_device.restype = i32
+        L.svg_probe_keys.argtypes = [vp, i32, vp, u64, vp, vp]
+        L.svg_probe_keys.restype = i32
+        L.svg_probe_keys_device.argtypes = [vp, i32, vp, u64, vp, vp, vp]
+        L.svg_probe_keys_device.restype = i32
         L.svg_last_error.restype = ctypes.c_char_p
         L.svg_index_build.argtypes = [ctypes.c_char_p, i32, i32, i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
         L.svg_index_build.restype = i32
@@ -330,6 +334,16 @@ class VoteIndex:
             self.close()
         except Exception:
             pass
+
+    def probe_keys(self, keys, block=0):
+        """svg_probe_keys: cellCounts' prefill_votes lookup for a batch of 32-bit subread keys;
+        returns (first, count) -- bucket-local index of each key's equal-key run and its length."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        first = np.empty(len(keys), np.uint32)
+        count = np.empty(len(keys), np.uint32)
+        _check(lib().svg_probe_keys(self.h, int(block), keys.ctypes.data, len(keys), first.ctypes.data,
+                                    count.ctypes.data), "svg_probe_keys")
+        return first, count
 
     def set_max_read_length(self, n):
         _check(lib().svg_set_max_read_length(self.h, int(n)), "svg_set_max_read_length")
