@@ -208,8 +208,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
+    step_ends = []
     for _ in range(args.steps):
         host_step()
+        step_ends.append(time.perf_counter())   # host call returns when its records are in host memory
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -225,8 +227,9 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    log("[bench] packed host path: %.1f Mreads/s (%.1f ms/step)" % (n * ends * args.steps / elapsed / 1e6,
-                                                                  elapsed / args.steps * 1e3))
+    step_ms = [round((b - a) * 1e3, 1) for a, b in zip([t_start] + step_ends[:-1], step_ends)]
+    log("[bench] packed host path: %.1f Mreads/s (%.1f ms/step; steps %s ms)" % (
+        n * ends * args.steps / elapsed / 1e6, elapsed / args.steps * 1e3, step_ms))
 
     # ---- secondary: the same kernels with reads and records already in HBM
     def upload(b):
@@ -410,6 +413,7 @@ def main():
                          "deferred_reads": st.get("deferred", 0),
                          "path": {"achieved": round(achieved, 2), "algorithmic_bytes_per_read": round(algo_bytes / n, 1),
                                   "step_ms": round(step_s * 1e3, 3), "frac": round(achieved / HBM_PEAK_GBS, 5)}},
+            "host_step_ms": step_ms,
             "device_path": device_path,
             "ascii_host_path": ascii_host,
             "cpu_baseline": cpu_base,
