@@ -24,6 +24,7 @@
 #include <functional>
 #include <vector>
 #include <chrono>
+#include <emmintrin.h>
 #include "subread_vote.h"
 #include "svg_internal.h"
 #include "svg_device.h"
@@ -78,6 +79,13 @@ __global__ void __launch_bounds__(256) unpack_reads(UnpackParams u)
 		}
 		u.text[t] = o;
 	}
+}
+
+// 16-byte streaming stores of n bytes (dst and n 16-byte aligned, src 16-byte aligned)
+static inline void stream_out(uint8_t *dst, const uint8_t *src, size_t n)
+{
+	for (size_t i = 0; i < n; i += 16)
+		_mm_stream_si128((__m128i *)(dst + i), _mm_load_si128((const __m128i *)(src + i)));
 }
 
 // ============================================================================ record compaction
@@ -501,32 +509,45 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		for (uint32_t t0 = 0; t0 < tiles; t0 += per_job) {
 			const uint32_t t1 = t0 + per_job < tiles ? t0 + per_job : tiles;
 			io->pool->post(s3, [=]() {
+				// a tile's records are assembled in a cache-resident buffer and leave with streaming
+				// stores: the caller's array is written once and never read, so plain stores would
+				// also read every line first (read-for-ownership) -- twice the host memory traffic
+				alignas(64) uint8_t tbuf[64 * 6 * 68];
 				const uint8_t *flags = stg + C.o_flags;
 				const uint32_t *tb = (const uint32_t *)(stg + C.o_tile);
 				for (uint32_t t = t0; t < t1; t++) {
 					const uint64_t r0 = (uint64_t)t * 64, r1 = r0 + 64 < m ? r0 + 64 : m;
 					const uint8_t *rec = stg + C.o_rec + (size_t)tb[t] * 68;
-					uint8_t *o = (uint8_t *)out + (b + r0) * rec_b;
+					uint8_t *const od = (uint8_t *)out + (b + r0) * rec_b;
+					const size_t tbytes = (size_t)(r1 - r0) * rec_b;
+					const bool nt = tbytes <= sizeof tbuf && (((uintptr_t)od | tbytes) & 15) == 0;
+					uint8_t *o = nt ? tbuf : od;
 					for (uint64_t r = r0; r < r1; r++) {
 						const uint32_t f = flags[r];
 						for (int q = 0; q < R; q++, o += 68)
 							if ((f >> q) & 1u) { memcpy(o, rec, 68); rec += 68; }
 							else memset(o, 0, 68);
 					}
+					if (nt) stream_out(od, tbuf, tbytes);
 					if (jo) {
 						const uint8_t *jf = stg + C.o_jflags;
 						const uint32_t *jt = (const uint32_t *)(stg + C.o_jtile);
 						const uint8_t *jr = stg + C.o_jrec + (size_t)jt[t] * 16;
-						uint8_t *jd = (uint8_t *)jout + (b + r0) * j_b;
+						uint8_t *const jdd = (uint8_t *)jout + (b + r0) * j_b;
+						const size_t jbytes = (size_t)(r1 - r0) * j_b;
+						const bool jnt = jbytes <= sizeof tbuf && (((uintptr_t)jdd | jbytes) & 15) == 0;
+						uint8_t *jd = jnt ? tbuf : jdd;
 						for (uint64_t r = r0; r < r1; r++) {
 							const uint32_t f = jf[r];
 							for (int q = 0; q < R; q++, jd += 16)
 								if ((f >> q) & 1u) { memcpy(jd, jr, 16); jr += 16; }
 								else memset(jd, 0, 16);
 						}
+						if (jnt) stream_out(jdd, tbuf, jbytes);
 					}
 					if (bmo) memcpy((uint8_t *)big_margin + (b + r0) * bm_b, stg + C.o_bm + r0 * bm_b, (r1 - r0) * bm_b);
 				}
+				_mm_sfence();   // streaming stores visible before the job counts as done
 			});
 		}
 		return 0;
