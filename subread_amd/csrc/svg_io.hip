@@ -200,8 +200,10 @@ static int host_threads()
 {
 	const char *e = getenv("SVG_HOST_THREADS");
 	if (e && atoi(e) > 0) return atoi(e);
+	// 12: measured at C3 on one box in one call (profiles/r02_host_variance/ab_threads_*.log):
+	// 8 threads 371.7 / 264.8, 12 threads 399.1 / 402.2, 16 threads 399.8 / 383.7 Mreads/s
 	unsigned hw = std::thread::hardware_concurrency();
-	return hw == 0 ? 4 : (hw < 8 ? (int)hw : 8);
+	return hw == 0 ? 4 : (hw < 12 ? (int)hw : 12);
 }
 
 // ============================================================================ per-handle state
