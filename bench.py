@@ -352,7 +352,7 @@ def main():
             check = check and ok
             log("[bench] parity check on reads %d..%d: %s" % (a, b, "IDENTICAL" if ok else "MISMATCH"))
     ascii_host = None
-    if rank == 0 and args.ascii_reads:
+    if rank == 0 and world == 1 and args.ascii_reads:
         # the ASCII host entry point (svg_vote_batch, pageable numpy reads, pinned records)
         m = min(n, args.ascii_reads)
         h1, h2 = rb.slice(0, m), (rb2.slice(0, m) if rb2 is not None else None)
@@ -364,7 +364,7 @@ def main():
         ascii_host = {"value": round(m * ends / ta / 1e6, 3), "unit": "Mreads/s", "reads": m * ends,
                       "entry": "svg_vote_batch: ASCII reads (pageable) in, records (pinned) out, PCIe both ways"}
     cpu_base = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:   # the CPU baseline is an N=1 figure
         # bounded CPU sample: chunks of the same reads until >= 10 s of CPU work
         done, cs, chunk = 0, 0.0, 200000
         while cs < 10.0 and done < min(n, args.cpu_sample):
