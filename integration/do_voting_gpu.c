@@ -2,22 +2,26 @@
  * integration/do_voting_gpu.c -- the reference-side binding of include/subread_vote.h.
  *
  * What a Subread maintainer adds to subread-align / subjunc (v2.0.6) to run the voting
- * step on an MI355X: do_voting_gpu() replaces do_voting() (src/core.c:3049) for one- and multi-block
- * indexes.  It is compiled here against the REFERENCE's own headers
- * (tests/test_boundary_ref.py: gcc -c -I/root/reference/src -Iinclude), so every field
- * name and type below is checked by a compiler; it is not linked into anything in this
- * repository.
+ * step on an MI355X: do_voting_gpu() replaces do_voting() (src/core.c:3049) for one- and
+ * multi-block indexes.  tests/test_boundary_ref.py compiles it against the REFERENCE's own
+ * headers, and oracle/Makefile links it into the reference's own subread-align / subjunc
+ * (built from /root/reference/src, `make -C oracle dropin`), whose run_in_thread call to
+ * do_voting (core.c:3366-3368) then lands here; tests/test_gpu_dropin.py compares the SAM,
+ * VCF and junction BED of that binary with the stock reference's, byte for byte.
  *
  *   svg_attach           once, after load_global_context (core.c:4013) has the index prefix
- *   do_voting_gpu        per chunk, from ONE host thread per GPU (run_in_thread, core.c:3366)
+ *   do_voting_gpu        per chunk and index block, from ONE host thread per GPU
+ *                        (run_in_thread, core.c:3366)
  *
  * The chunk's reads come from fetch_next_read_pair (core.c:1121) exactly as do_voting
  * reads them -- that function already applies the -S reversal (core.c:1186-1198), so the
  * library is told not to reverse again (reverse_r1 = reverse_r2 = 0).  Reads are 2-bit
  * packed on the host (svg_pack_reads) and voted with svg_vote_batch_packed straight into
- * the chunk's bigtable (core-bigtable.c:84-131).  The final-voting-run block of do_voting
- * (core.c:3240-3290: find_new_indels / find_new_junctions per record) then runs on the
- * host unchanged, from the same records.
+ * the chunk's bigtable (core-bigtable.c:84-131).  The per-read host work of do_voting that is
+ * not voting then runs unchanged, in do_voting's order:
+ *   - subjunc reads > 160 bp: core_fragile_junction_voting (core.c:3138-3142), per strand and
+ *     end, in every index block's run (it only adds events to the event tables);
+ *   - the final voting run: find_new_indels / find_new_junctions per record (core.c:3240-3290).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -80,7 +84,7 @@ static void svg_fill_params(global_context_t *gc, svg_params *p)
 	p->more_accurate_fusions = gc->config.more_accurate_fusions;
 }
 
-/* the chunk's reads as the reference reads them: text, names, qualities, lengths */
+/* the chunk's reads as fetch_next_read_pair hands them to do_voting: text, names, qualities */
 typedef struct {
 	char *text[2], *qual[2], *name[2];
 	uint16_t *len[2];
@@ -105,76 +109,141 @@ static int chunk_push(svg_chunk_reads *c, int e, const char *text, const char *q
 	return 0;
 }
 
-int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
+static void chunk_free(svg_chunk_reads *c)
+{
+	int e;
+	for (e = 0; e < 2; e++) {
+		free(c->text[e]); free(c->qual[e]); free(c->name[e]); free(c->len[e]); free(c->off[e]);
+	}
+}
+
+/* 1. the chunk's reads, in chunk read-number order (one thread: numbers are sequential) */
+static int read_chunk(global_context_t *gc, thread_context_t *tc, int ends, svg_chunk_reads *c)
 {
 	gene_input_t *ginp1 = NULL, *ginp2 = NULL;
 	char text[2][MAX_READ_LENGTH + 1], qual[2][MAX_READ_LENGTH + 1], name[2][MAX_READ_NAME_LEN + 1];
-	int len[2] = {0, 0}, ends = 1 + gc->input_reads.is_paired_end_reads, rc = 0, e;
+	int len[2] = {0, 0}, e;
 	subread_read_number_t rno = 0;
-	svg_chunk_reads c;
-	memset(&c, 0, sizeof c);
 	init_chunk_scanning_parameters(gc, tc, &ginp1, &ginp2);
-
-	/* 1. the chunk's reads, in chunk read-number order (one thread: numbers are sequential) */
 	for (;;) {
-		fetch_next_read_pair(gc, tc, ginp1, ginp2, &len[0], &len[1], name[0], name[1], text[0], text[1], qual[0], qual[1], 1, &rno);
+		fetch_next_read_pair(gc, tc, ginp1, ginp2, &len[0], &len[1], name[0], name[1], text[0], text[1], qual[0],
+		                     qual[1], 1, &rno);
 		if (rno < 0) break;
-		if (c.n == c.cap) {
-			c.cap = c.cap ? 2 * c.cap : 1 << 16;
+		if ((uint64_t)rno != c->n) {
+			SUBREADprintf("do_voting_gpu: read numbers are not sequential (%lld after %llu reads)\n",
+			              (long long)rno, (unsigned long long)c->n);
+			return 1;
+		}
+		if (c->n == c->cap) {
+			c->cap = c->cap ? 2 * c->cap : 1 << 16;
 			for (e = 0; e < ends; e++) {
-				c.len[e] = realloc(c.len[e], c.cap * sizeof(uint16_t));
-				c.off[e] = realloc(c.off[e], c.cap * sizeof(uint64_t));
-				c.name[e] = realloc(c.name[e], c.cap * (MAX_READ_NAME_LEN + 1));
-				if (!c.len[e] || !c.off[e] || !c.name[e]) return 1;
+				c->len[e] = realloc(c->len[e], c->cap * sizeof(uint16_t));
+				c->off[e] = realloc(c->off[e], c->cap * sizeof(uint64_t));
+				c->name[e] = realloc(c->name[e], c->cap * (MAX_READ_NAME_LEN + 1));
+				if (!c->len[e] || !c->off[e] || !c->name[e]) return 1;
 			}
 		}
 		for (e = 0; e < ends; e++)
-			if (chunk_push(&c, e, text[e], qual[e], name[e], len[e])) return 1;
-		c.n++;
+			if (chunk_push(c, e, text[e], qual[e], name[e], len[e])) return 1;
+		c->n++;
 	}
+	return 0;
+}
 
-	/* 2. one packed call for the whole chunk, records into the bigtable */
+/* 2. one packed call for the whole chunk, records into the bigtable */
+static int vote_chunk(global_context_t *gc, int ends, const svg_chunk_reads *c)
+{
 	svg_params p;
 	svg_fill_params(gc, &p);
 	svg_packed_reads pk[2];
 	uint32_t *bases[2] = {NULL, NULL}, *xmask[2] = {NULL, NULL};
 	uint64_t *starts[2] = {NULL, NULL};
+	uint16_t *bm = NULL;
+	int rc = 0, e;
 	for (e = 0; e < ends && !rc; e++) {
-		svg_reads r = {c.text[e], c.off[e], c.len[e], c.n};
-		bases[e] = malloc(4 * (c.bytes[e] / 16 + 1));
-		xmask[e] = malloc(4 * (c.bytes[e] / 32 + 1));
-		starts[e] = malloc(8 * (c.n + 1));
+		svg_reads r = {c->text[e], c->off[e], c->len[e], c->n};
+		bases[e] = malloc(4 * (c->bytes[e] / 16 + 1));
+		xmask[e] = malloc(4 * (c->bytes[e] / 32 + 1));
+		starts[e] = malloc(8 * (c->n + 1));
+		if (!bases[e] || !xmask[e] || !starts[e]) { rc = SVG_E_NOMEM; break; }
 		int64_t nx = svg_pack_reads(&r, 0, bases[e], xmask[e], starts[e], gc->config.all_threads);
 		if (nx < 0) { rc = (int)nx; break; }
-		svg_packed_reads q = {bases[e], nx ? xmask[e] : NULL, starts[e], 0, c.len[e], c.n};
+		svg_packed_reads q = {bases[e], nx ? xmask[e] : NULL, starts[e], 0, c->len[e], c->n};
 		pk[e] = q;
 	}
-	/* a multi-block index: the library votes every block (all resident in HBM) in the first
-	 * block's run of read_chunk_circles (core.c:3567-3613); the later runs only re-read the
-	 * chunk (go_chunk_start) and, in the final one, run step 3 */
-	if (!rc && c.n && gc->current_index_block_number == 0)
+	/* big-margin records live inside each bigtable_cached_result_t (core.h:453), not in one
+	 * array: the library writes them to a staging array, copied into the entries below */
+	if (!rc && p.do_big_margin_filtering_for_junctions) {
+		bm = malloc(sizeof(uint16_t) * SVG_BIG_MARGIN_WORDS * ends * (c->n + 1));
+		if (!bm) rc = SVG_E_NOMEM;
+	}
+	if (!rc)
 		rc = svg_vote_batch_packed(svg_ix, &p, &pk[0], ends == 2 ? &pk[1] : NULL,
 		                           (svg_mapping_result *)_global_retrieve_alignment_ptr(gc, 0, 0, 0),
 		                           p.do_breakpoint_detection ? (svg_subjunc_result *)_global_retrieve_subjunc_ptr(gc, 0, 0, 0) : NULL,
-		                           p.do_big_margin_filtering_for_junctions ? _global_retrieve_big_margin_ptr(gc, 0, 0) : NULL);
+		                           bm);
 	if (rc) SUBREADprintf("svg_vote_batch_packed: %s\n", svg_last_error());
+	else if (bm) {
+		uint64_t r;
+		int words = gc->config.big_margin_record_size;
+		for (r = 0; r < c->n; r++)
+			for (e = 0; e < ends; e++)
+				memcpy(_global_retrieve_big_margin_ptr(gc, r, e), bm + (r * ends + e) * SVG_BIG_MARGIN_WORDS,
+				       sizeof(uint16_t) * words);
+	}
+	for (e = 0; e < 2; e++) { free(bases[e]); free(xmask[e]); free(starts[e]); }
+	free(bm);
+	return rc;
+}
 
-	/* 3. unchanged host step: the final-voting-run block of do_voting (core.c:3240-3290) */
+int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
+{
+	int ends = 1 + gc->input_reads.is_paired_end_reads, rc = 0, e, s;
+	svg_chunk_reads c;
+	memset(&c, 0, sizeof c);
+	/* do_voting's per-run state (core.c:3081-3089) */
+	unsigned int low_border = gc->current_value_index->start_base_offset;
+	unsigned int high_border = gc->current_value_index->start_base_offset + gc->current_value_index->length;
+	if (tc) tc->current_value_index = gc->current_value_index;
 	int need_junction_step = gc->config.do_breakpoint_detection || gc->config.do_fusion_detection || gc->config.do_long_del_detection;
+	gene_vote_t *vote_fg = gc->config.do_breakpoint_detection ? malloc(sizeof(gene_vote_t)) : NULL;
+	if (gc->config.do_breakpoint_detection && !vote_fg) return 1;
+
+	rc = read_chunk(gc, tc, ends, &c);
+	/* a multi-block index: the library votes every block (all resident in HBM) in the first
+	 * block's run of read_chunk_circles (core.c:3567-3613); the later runs re-read the chunk
+	 * for the per-block host work below */
+	if (!rc && c.n && gc->current_index_block_number == 0) rc = vote_chunk(gc, ends, &c);
+
+	/* 3. do_voting's per-read host work, in its order */
+	char text[MAX_READ_LENGTH + 1], qual[MAX_READ_LENGTH + 1];
 	subread_read_number_t r;
-	for (r = 0; !rc && gc->is_final_voting_run && r < (subread_read_number_t)c.n; r++) {
+	for (r = 0; !rc && r < (subread_read_number_t)c.n; r++) {
+		/* core_fragile_junction_voting (core.c:3138-3142): strand 0 on the fetched text, strand 1
+		 * on its reverse_read, R1 then R2; the quality is never reversed inside the strand loop */
+		for (s = 0; gc->config.do_breakpoint_detection && s < 2; s++)
+			for (e = 0; e < ends; e++) {
+				int rl = c.len[e][r];
+				if (rl <= EXON_LONG_READ_LENGTH) continue;
+				memcpy(text, c.text[e] + c.off[e][r], rl);
+				memcpy(qual, c.qual[e] + c.off[e][r], rl);
+				text[rl] = qual[rl] = 0;
+				if (s) reverse_read(text, rl, gc->config.space_type);
+				core_fragile_junction_voting(gc, tc, c.name[0] + r * (MAX_READ_NAME_LEN + 1), text, qual, rl, s,
+				                             gc->config.space_type, low_border, high_border - rl, vote_fg);
+			}
+		if (!gc->is_final_voting_run) continue;
+		/* the final-voting-run block (core.c:3240-3290) */
 		for (e = 0; e < ends; e++) {
-			/* do_voting's text buffer is reversed once after strand 0 (core.c:3229-3234) and the
-			 * tail starts from that state (read_1_reversed = 1); reverse_read maps every
-			 * non-ACGTU character to 'N', so the state machine is kept exactly */
+			/* do_voting leaves the text reversed once (core.c:3229-3234) and the quality as fetched;
+			 * the tail starts from that state (read_1_reversed = 1) and reverses both together when a
+			 * record's strand needs it, so text and quality stay in opposite orientations, as there */
 			int has_reversed = 1;
-			char *rt = text[0], *rq = qual[0];
 			int rl = c.len[e][r];
-			memcpy(rt, c.text[e] + c.off[e][r], rl);
-			memcpy(rq, c.qual[e] + c.off[e][r], rl);
-			rt[rl] = rq[rl] = 0;
-			reverse_read(rt, rl, gc->config.space_type);
-			reverse_quality(rq, rl);
+			memcpy(text, c.text[e] + c.off[e][r], rl);
+			memcpy(qual, c.qual[e] + c.off[e][r], rl);
+			text[rl] = qual[rl] = 0;
+			reverse_read(text, rl, gc->config.space_type);
 			char *rn = c.name[e] + r * (MAX_READ_NAME_LEN + 1);
 			int b;
 			for (b = 0; b < gc->config.multi_best_reads; b++) {
@@ -183,21 +252,37 @@ int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
 				int should = (cur->result_flags & CORE_IS_NEGATIVE_STRAND) ? 1 : 0;
 				if (should != has_reversed) {
 					has_reversed = !has_reversed;
-					reverse_read(rt, rl, gc->config.space_type);
-					reverse_quality(rq, rl);
+					reverse_read(text, rl, gc->config.space_type);
+					reverse_quality(qual, rl);
 				}
 				gene_value_index_t *saved = tc ? tc->current_value_index : gc->current_value_index;
 				locate_current_value_index(gc, tc, cur, rl);
-				if (!has_better_mapping(gc, tc, r, e, b)) find_new_indels(gc, tc, r, rn, rt, rq, rl, e, b);
-				if (need_junction_step) find_new_junctions(gc, tc, r, rn, rt, rq, rl, e, b);
+				if (!has_better_mapping(gc, tc, r, e, b)) find_new_indels(gc, tc, r, rn, text, qual, rl, e, b);
+				if (need_junction_step) find_new_junctions(gc, tc, r, rn, text, qual, rl, e, b);
 				if (tc) tc->current_value_index = saved;
 				else gc->current_value_index = saved;
 			}
 		}
 	}
-	for (e = 0; e < 2; e++) {
-		free(bases[e]); free(xmask[e]); free(starts[e]);
-		free(c.text[e]); free(c.qual[e]); free(c.name[e]); free(c.len[e]); free(c.off[e]);
-	}
+	chunk_free(&c);
+	free(vote_fg);
 	return rc ? 1 : 0;
 }
+
+#ifdef SVG_DROPIN_DO_VOTING
+/*
+ * Harness build only (oracle/Makefile `dropin`): the reference's core.o is compiled with
+ * do_voting weak, so this definition takes run_in_thread's call (core.c:3366-3368).  Thread 0
+ * (or the single -T 1 caller) feeds the whole chunk to the GPU; the other voting threads
+ * fetch nothing, so read numbers stay sequential.  The device is SVG_DEVICE (default 0).
+ */
+int do_voting(global_context_t *gc, thread_context_t *tc)
+{
+	if (tc && tc->thread_id != 0) return 0;
+	if (!svg_ix) {
+		const char *d = getenv("SVG_DEVICE");
+		if (svg_attach(gc, d ? atoi(d) : 0)) return 1;
+	}
+	return do_voting_gpu(gc, tc);
+}
+#endif

@@ -1,0 +1,69 @@
+"""GPU: the reference's own subread-align / subjunc with integration/do_voting_gpu.c as its
+voting step (votes by libsubread_amd.so on the GPU) gives the stock reference's outputs byte
+for byte: SAM (iteration two and the SAM writer of the reference consume the GPU records),
+.indel.vcf, .junction.bed, plus the vote records and the event table after the voting step
+(oracle/ref_dump_hook.c in both binaries).  Cases: the golden fixtures' reads (test-err-mut
+PE, junction-reads A/B, long subjunc reads with fragile junction voting, -n 14 -I 16, multi-block
+indexes, -T 4) and 200k C2 reads (1 Mbp seed-901 genome, full one-block index)."""
+import os
+
+import numpy as np
+import pytest
+
+from tests.common import Case, IndexCache
+from tests.dropin import check_case, compare, fastq_pair, have, run
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cache(tmp_path_factory):
+    return IndexCache(str(tmp_path_factory.mktemp("gpu_dropin_idx")))
+
+
+def _need(program):
+    if not have(program, "dropin"):
+        pytest.fail("oracle/_ref drop-in binaries missing: build them in the survey container (make -C oracle dropin)")
+
+
+@pytest.mark.parametrize("name,threads", [
+    ("pe_gapped_errmut", 1),            # PE align, test-err-mut pairs 8000..9999
+    ("pe_full_errmut", 1),              # PE align, full index
+    ("sj_pe_gapped_junc", 1),           # subjunc PE, junction-reads A/B
+    ("sj_se_full_junc", 1),             # subjunc SE, big-margin records, full index
+    ("sj_pe_gapped_long", 1),           # subjunc PE > 160 bp (fragile junction voting, host)
+    ("sj_se_full_long", 1),             # subjunc SE 170-400 bp
+    ("se_gapped_mixed_n14_I16", 4),     # -n 14 -I 16, N / lowercase / IUPAC, -T 4
+    ("se_mb_synth_fullM1", 1),          # 4-block full index
+    ("pe_mb_synth_gappedM1", 1),        # 2-block gapped index
+    ("sj_pe_mb_long_gappedM6", 1),      # subjunc PE, 4-block index, blocks overlapping ~2 Mbp
+])
+def test_gpu_dropin_matches_stock_reference(name, threads, cache, tmp_path):
+    c = Case(name)
+    _need(c.meta["program"])
+    rep = check_case(c, cache.get(c.index_key), str(tmp_path), "dropin", threads)
+    assert rep["mapped"] > 0
+    print(name, rep)
+
+
+@pytest.mark.timeout(600)
+def test_gpu_dropin_c2_200k(tmp_path):
+    """200k C2 reads (bench.py workload c2's genome and read generator) through the drop-in, -T 8."""
+    _need(0)
+    import subread_amd as sa
+    from subread_amd.sim import random_genome, simulate_reads
+    g = random_genome([1_000_000], 901)
+    fa = str(tmp_path / "c2.fa")
+    g.write_fasta(fa)
+    pre = str(tmp_path / "c2_full")
+    sa.build_index(fa, pre, gap=1, force_one_block=True)
+    rb = simulate_reads(g, 200_000, 100, seed=20261015, first=0, sub=0.01, indel=0.001)
+    f1, _ = fastq_pair(str(tmp_path), "c2", rb, None)
+    so, do = str(tmp_path / "c2.stock.sam"), str(tmp_path / "c2.dropin.sam")
+    run(0, "dump", pre, f1, None, so, threads=8)
+    run(0, "dropin", pre, f1, None, do, threads=8)
+    rep = compare(so, do)
+    votes = np.fromfile(do + ".votes", dtype=np.uint8)
+    assert votes.size == 200_000 * 3 * 68
+    assert rep["sam_records"] >= 200_000 and rep["mapped"] > 190_000, rep
+    print("c2", rep)
