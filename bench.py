@@ -114,11 +114,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # one rank per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share devices round-robin
+    ndev = torch.cuda.device_count()
+    device = local % ndev if ndev else local
+    torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # the vote path has no exchange step: the process group only carries the timing barrier and
+        # the max of one float, so it runs on gloo (host TCP) unless SVG_DIST_BACKEND asks for RCCL
+        backend = os.environ.get("SVG_DIST_BACKEND", "gloo")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     import subread_amd as sa
     from subread_amd.abi import default_params, PROGRAM_ALIGN, PROGRAM_SUBJUNC, MAPPING_DTYPE, SUBJUNC_DTYPE, \
@@ -147,12 +156,12 @@ def main():
         if dist is not None:
             dist.barrier()
         t1 = time.time()
-        ix = sa.VoteIndex(prefix, device=local)
+        ix = sa.VoteIndex(prefix, device=device)
     else:
         # 3 Gbp: build the same index straight into this GPU's HBM (replicated per rank)
         t1 = time.time()
         gap = W.get("gap", 1)
-        ix = sa.VoteIndex.build_genome(genome, gap=gap, memory_mb=8000, force_one_block=gap == 1, device=local)
+        ix = sa.VoteIndex.build_genome(genome, gap=gap, memory_mb=8000, force_one_block=gap == 1, device=device)
     log("[bench] index in HBM (%.1f GB, %d items) in %.1fs" % (ix.info.device_bytes / 1e9, ix.info.items,
                                                             time.time() - t1))
 
@@ -168,7 +177,7 @@ def main():
         rb = simulate_reads(genome, n, L, seed=20261015, first=rank * n, sub=0.01, indel=0.001)
     ends = 2 if rb2 is not None else 1
     log("[bench] simulated %d %s in %.1fs" % (n, "pairs" if ends == 2 else "reads", time.time() - t1))
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", device)
     p = default_params(PROGRAM_SUBJUNC if kind in ("sj", "sjpe") else PROGRAM_ALIGN, ends == 2)
     mb = p.multi_best
     sj = kind in ("sj", "sjpe")
@@ -224,7 +233,7 @@ def main():
     kt = ix.kernel_timing()
     ix.set_timing(False)
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     step_ms = [round((b - a) * 1e3, 1) for a, b in zip([t_start] + step_ends[:-1], step_ends)]
@@ -402,7 +411,8 @@ def main():
                        "index": "%s one-block (gap %d), %d buckets, %d items, %s" % (
                            "full" if ix.info.index_gap == 1 else "gapped", ix.info.index_gap, ix.info.buckets, ix.info.items,
                            "reference-format files via svg_index_open" if prefix else "built in HBM by svg_index_build_mem"),
-                       "parallelism": "reads sharded across %d GPU(s), index replicated, no collective" % world},
+                       "parallelism": "reads sharded across %d GPU(s), index replicated, no collective" % world,
+                       "host_threads_per_rank": int(sa.lib().svg_host_threads())},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(vote_achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(vote_achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_unit": "GB per launch",

@@ -220,9 +220,10 @@ int svg_vote_batch(svg_index *idx, const svg_params *p,
                    svg_mapping_result *out, svg_subjunc_result *jout,
                    uint16_t *big_margin);
 /* The same from 2-bit packed reads (host buffers).  Both host entry points run a sub-batch
- * pipeline: upload of sub-batch i+1, vote of i, download of i-1 (only the non-zero records,
- * compacted on the GPU) and expansion of i-2 into `out` by worker threads overlap
- * (SVG_HOST_THREADS, default min(8, cores)).  Pinned caller buffers copy fastest. */
+ * pipeline: upload of sub-batch i+1, vote of i (probe + lane kernels) beside the wave kernel and
+ * compaction of i-1, download of i-2 (only the non-zero records, compacted on the GPU) and
+ * expansion of i-3 into `out` by worker threads overlap.  Workers: SVG_HOST_THREADS, else
+ * svg_host_threads().  Pinned caller buffers copy fastest. */
 int svg_vote_batch_packed(svg_index *idx, const svg_params *p,
                           const svg_packed_reads *r1, const svg_packed_reads *r2,
                           svg_mapping_result *out, svg_subjunc_result *jout,
@@ -298,6 +299,10 @@ int svg_get_kernel_timing(svg_index *idx, double ms[4], int launches[4]);
 
 const char *svg_last_error(void);
 int svg_abi_version(void);
+/* Expansion worker threads the host entry points use: SVG_HOST_THREADS if set, else the CPUs
+ * this process may run on (affinity mask capped by the cgroup CPU quota) divided by
+ * LOCAL_WORLD_SIZE (one rank per GPU on the node), clamped to 2..12. */
+int svg_host_threads(void);
 
 /*
  * Index builder (replaces subread-buildindex for a single-block index,

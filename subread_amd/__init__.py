@@ -30,7 +30,7 @@ EXPORTS = [
     "svg_sim_repeats", "svg_sim_reads", "svg_index_build", "svg_index_build_mem", "svg_index_export",
     "svg_set_max_read_length", "svg_sim_pairs", "svg_set_timing", "svg_get_timing",
     "svg_get_kernel_timing", "svg_device_status", "svg_pack_reads", "svg_vote_batch_packed",
-    "svg_vote_batch_packed_device", "svg_probe_keys", "svg_probe_keys_device",
+    "svg_vote_batch_packed_device", "svg_probe_keys", "svg_probe_keys_device", "svg_host_threads",
     # host post-vote events (include/subread_events.h)
     "svg_event_params_default", "svg_genome_arrays_open", "svg_genome_arrays_close", "svg_events_create",
     "svg_events_destroy", "svg_events_add_batch", "svg_events_merge", "svg_events_count", "svg_events_get",
@@ -98,6 +98,7 @@ def lib():
         L.svg_probe_keys_device.argtypes = [vp, i32, vp, u64, vp, vp, vp]
         L.svg_probe_keys_device.restype = i32
         L.svg_last_error.restype = ctypes.c_char_p
+        L.svg_host_threads.restype = i32
         L.svg_index_build.argtypes = [ctypes.c_char_p, i32, i32, i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
         L.svg_index_build.restype = i32
         L.svg_index_build_mem.argtypes = [vp, vp, vp, ctypes.c_uint32, i32, i32, i32, i32, i32, ctypes.c_char_p,

@@ -196,6 +196,8 @@ int svg_vote_batch_device_packed(svg_index *h, const svg_params *p, const svg_re
 
 // svg_lane.hip
 int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int sj);
+// the parameter contract of every vote entry point (multi_best 1..3, top_scores 3, ...)
+int svg_check_params(const svg_index *h, const svg_params *p, int paired);
 int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *len, uint32_t n, const uint2 *precs,
                    int nps, uint8_t *out, uint8_t *jout, uint16_t *bm, const char *seq, const uint64_t *off,
                    unsigned long long *stats, uint32_t **defer_list, uint32_t **defer_count, hipStream_t st);

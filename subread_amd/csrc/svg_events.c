@@ -325,7 +325,9 @@ typedef struct {
 	int16_t *dp;          /* (rl + 16) x rl score table, row-major */
 	uint8_t *mask;
 	int rows, cols;
-	char mv[SVG_MAX_READ_LENGTH * 10 / 7 + 64];
+	/* a traceback takes at most rows + len <= 2 * len + 16 steps (the reference sizes its stack
+	 * buffer len * 10 / 7, core-indel.c; here the walk also stops at the end of the buffer) */
+	char mv[2 * (SVG_MAX_READ_LENGTH + 16) + 64];
 } scratch_t;
 
 /* find_subread_end, input-files.c:1371-1387 */
@@ -379,6 +381,7 @@ static int dynamic_align(scratch_t *s, const garray *a, const svg_event_params *
 	j = len - 1;
 	for (;;) {
 		int m = M(path_i, j);
+		if (out >= (int)sizeof s->mv) return 0;
 		if (m == MASK_INSERTION) { j--; delta--; s->mv[out++] = 2; }
 		else if (m == MASK_DELETION) { path_i--; delta++; s->mv[out++] = 1; }
 		else { s->mv[out++] = m == MASK_MATCH ? 0 : 3; path_i--; j--; }

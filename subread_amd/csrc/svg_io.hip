@@ -25,6 +25,7 @@
 #include <vector>
 #include <chrono>
 #include <emmintrin.h>
+#include <sched.h>
 #include "subread_vote.h"
 #include "svg_internal.h"
 #include "svg_device.h"
@@ -196,15 +197,54 @@ struct SvgPool {
 	}
 };
 
+// CPUs this process may run on: its affinity mask, capped by a cgroup CPU quota (v2 cpu.max or
+// v1 cfs_quota/cfs_period) -- hardware_concurrency() reports the whole machine (256 on the
+// GPU boxes, of which a 1-GPU job gets 16)
+static int usable_cpus()
+{
+	int n = 0;
+	cpu_set_t cs;
+	if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+	if (n <= 0) n = (int)std::thread::hardware_concurrency();
+	if (n <= 0) n = 4;
+	long quota = -1, period = 0;
+	if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+		char q[32];
+		if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0) quota = atol(q);
+		fclose(f);
+	} else if (FILE *f1 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+		if (fscanf(f1, "%ld", &quota) != 1) quota = -1;
+		fclose(f1);
+		if (FILE *f2 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+			if (fscanf(f2, "%ld", &period) != 1) period = 0;
+			fclose(f2);
+		}
+	}
+	if (quota > 0 && period > 0) {
+		int c = (int)(quota / period);
+		if (c < 1) c = 1;
+		if (c < n) n = c;
+	}
+	return n;
+}
+
+// expansion workers of one handle: SVG_HOST_THREADS, else this rank's share of the usable CPUs
+// (one rank per GPU: LOCAL_WORLD_SIZE ranks share the node's CPUs), at most 12 -- measured at
+// C3 on one box in one call (profiles/r02_host_variance/ab_threads_*.log): 8 threads 371.7 /
+// 264.8, 12 threads 399.1 / 402.2, 16 threads 399.8 / 383.7 Mreads/s -- and at least 2
 static int host_threads()
 {
 	const char *e = getenv("SVG_HOST_THREADS");
 	if (e && atoi(e) > 0) return atoi(e);
-	// 12: measured at C3 on one box in one call (profiles/r02_host_variance/ab_threads_*.log):
-	// 8 threads 371.7 / 264.8, 12 threads 399.1 / 402.2, 16 threads 399.8 / 383.7 Mreads/s
-	unsigned hw = std::thread::hardware_concurrency();
-	return hw == 0 ? 4 : (hw < 12 ? (int)hw : 12);
+	int n = usable_cpus();
+	const char *lw = getenv("LOCAL_WORLD_SIZE");
+	int ranks = lw ? atoi(lw) : 1;
+	if (ranks > 1) n /= ranks;
+	if (n < 2) n = 2;
+	return n < 12 ? n : 12;
 }
+
+extern "C" int svg_host_threads(void) { return host_threads(); }
 
 // ============================================================================ per-handle state
 struct svg_hostio {
@@ -433,6 +473,9 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	if (p->do_breakpoint_detection && !jout) { svg_set_error("do_breakpoint_detection needs jout"); return SVG_E_ARG; }
 	if (p->do_big_margin_filtering_for_junctions && !big_margin) { svg_set_error("big-margin filtering needs big_margin"); return SVG_E_ARG; }
 	int rc;
+	// before anything is sized from multi_best (staging slots, compaction flags: ends * multi_best
+	// bits of a uint8 per read)
+	if ((rc = svg_check_params(h, p, pe))) return rc;
 	if (packed && ((rc = check_packed(q1, who)) || (q2 && (rc = check_packed(q2, who))))) return rc;
 	if (!n) return 0;
 	const int ends = pe ? 2 : 1, mb = p->multi_best, R = ends * mb;

@@ -64,3 +64,30 @@ def test_index_open_without_gpu_fails_loudly(tmp_path):
             "try:\n sa.VoteIndex('/nonexistent/x')\nexcept sa.SvgError as e:\n print('ERR', e)\n")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT)
     assert "ERR" in r.stdout
+
+
+def _usable_cpus():
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def test_host_threads_follow_affinity_quota_and_ranks(monkeypatch):
+    """svg_host_threads: SVG_HOST_THREADS wins; else this process's usable CPUs (affinity capped by
+    the cgroup quota) shared among LOCAL_WORLD_SIZE ranks, clamped to 2..12 (svg_io.hip)."""
+    L = sa.lib()
+    monkeypatch.delenv("SVG_HOST_THREADS", raising=False)
+    monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    u = _usable_cpus()
+    assert L.svg_host_threads() == max(2, min(12, u))
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert L.svg_host_threads() == max(2, min(12, u // 2))
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "64")
+    assert L.svg_host_threads() == 2
+    monkeypatch.setenv("SVG_HOST_THREADS", "5")
+    assert L.svg_host_threads() == 5

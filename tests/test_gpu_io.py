@@ -82,6 +82,51 @@ def test_compacted_pipeline_small_subbatches(mode, entry, gpu_indexes, index_cac
         assert (got == want).all(), "sub %s: %s" % (sub, describe_mismatch(got, want, 2 if mode == "pe" else 1, 3))
 
 
+@pytest.mark.parametrize("name", ["se_mb_long_gappedM6", "sj_pe_mb_long_gappedM6", "pe_mb_long_fullM17"])
+@pytest.mark.parametrize("entry", ["ascii", "packed"])
+def test_compacted_pipeline_multi_block(name, entry, gpu_indexes, index_cache, monkeypatch):
+    """Multi-block indexes through the host pipeline with many sub-batches: later blocks run on
+    the first block's stream from the stored records of each sub-batch, device and staging slots
+    are reused; golden records (4-6 blocks) and the oracle on 15k simulated reads of the genome."""
+    import subread_amd as sa
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.sim import Genome, simulate_pairs, simulate_spliced_reads, simulate_reads
+    c = Case(name)
+    ix = gpu_indexes(c.index_key)
+    assert ix.n_blocks > 1
+    for sub, th in (("97", "2"), ("1000", "5")):
+        monkeypatch.setenv("SVG_HOST_SUB", sub)
+        monkeypatch.setenv("SVG_HOST_THREADS", th)
+        if entry == "ascii":
+            out, jout, bm = ix.vote(c.params, c.r1, c.r2)
+        else:
+            out, jout, bm = ix.vote_packed(c.params, sa.pack_reads(c.r1, None),
+                                           sa.pack_reads(c.r2, None) if c.r2 is not None else None)
+        got = pack_records(out, jout, bm)
+        assert (got == c.expected).all(), "sub %s: %s" % (sub, describe_mismatch(got, c.expected, c.ends, 3))
+    g = Genome.read_fasta(index_cache.genome_fasta(c.index_key.rsplit("_", 1)[0]))
+    n = 15013
+    if c.params.do_breakpoint_detection:
+        r1, r2 = simulate_spliced_reads(g, n, 150, seed=61, max_intron=20000), None
+        if c.r2 is not None:
+            r2 = simulate_spliced_reads(g, n, 150, seed=62, max_intron=20000)
+    elif c.r2 is not None:
+        r1, r2 = simulate_pairs(g, n, 150, seed=63, sub=0.01)
+    else:
+        r1, r2 = simulate_reads(g, n, 100, seed=64, sub=0.02, indel=0.02, nrate=0.002), None
+    ref, rj, rbm, _ = OracleIndex(index_cache.get(c.index_key)).vote(c.params, r1, r2, threads=16)
+    sj = bool(c.params.do_breakpoint_detection)
+    want = pack_records(ref, rj if sj else None, rbm if sj else None)
+    monkeypatch.setenv("SVG_HOST_SUB", "3001")
+    monkeypatch.setenv("SVG_HOST_THREADS", "3")
+    if entry == "ascii":
+        out, jout, bm = ix.vote(c.params, r1, r2)
+    else:
+        out, jout, bm = ix.vote_packed(c.params, sa.pack_reads(r1, None), sa.pack_reads(r2, None) if r2 is not None else None)
+    got = pack_records(out, jout if sj else None, bm if sj else None)
+    assert (got == want).all(), describe_mismatch(got, want, c.ends, 3)
+
+
 def _to_dev(a, dev):
     import torch
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).to(dev)
