@@ -37,6 +37,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "Mreads/s aligned, 100bp SE vs 3Gbp index; 1/2/4/8-GPU scaling + HBM GB/s"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+RANDOM_SECTOR_RATE = 26.4e9   # random 32-B sectors/s chip-wide, measured (profiles/r02_calib_random.txt)
 
 
 def log(*a):
@@ -320,20 +321,41 @@ def main():
     step_s = elapsed / args.steps
     achieved = algo_bytes / step_s / 1e9
 
-    # HBM traffic of the dominant kernel from the committed PMC passes of this workload
-    # (tools/profile_workload.sh -> profiles/r*_<workload>_kernels*.json; rocprofv3 cannot run
-    # inside this process), per launch, scaled to this run's reads per launch
+    # HBM traffic per kernel from the committed PMC passes of this workload's host path (the path
+    # `value` measures: tools/profile_workload.sh ... host -> profiles/r*_<workload>_kernels_host*.json;
+    # rocprofv3 cannot run inside this process), per launch, scaled to this run's reads per launch
     traffic, traffic_src = None, None
     import glob
-    tj = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_kernels*.json" % args.workload)))
-    if tj:
-        t = json.load(open(tj[-1]))
-        kd = t.get("kernels", {}).get(dom)
-        if kd:
-            per_read = kd["traffic_bytes_per_read"]
-            traffic = round(per_read * n / launches_per_step / 1e9, 3)
-            traffic_src = "%s (%s FETCH_SIZE+WRITE_SIZE, %.0f B/read, GB per launch)" % (
-                os.path.relpath(tj[-1], ROOT), dom, per_read)
+    tj = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_%s_kernels_host*.json" % args.workload)))
+    pmc = json.load(open(tj[-1])).get("kernels", {}) if tj else {}
+    for k, kd in kernels.items():
+        if k in pmc:
+            per_read = pmc[k]["traffic_bytes_per_read"]
+            kd["traffic_bytes_per_read"] = round(per_read, 1)
+            # the HBM bandwidth the kernel really draws (counter bytes / its HIP-event launch time)
+            kd["traffic_gbs"] = round(per_read * n / kd["launches_per_step"] / (kd["launch_ms"] / 1e3) / 1e9, 1)
+    if dom in pmc:
+        per_read = pmc[dom]["traffic_bytes_per_read"]
+        traffic = round(per_read * n / launches_per_step / 1e9, 3)
+        traffic_src = "%s (%s FETCH_SIZE+WRITE_SIZE, %.0f B/read, GB per launch)" % (
+            os.path.relpath(tj[-1], ROOT), dom, per_read)
+    # the probe kernels are bound by the HBM random-access rate, not by bytes: one random 32-B
+    # sector per probe (bucket code / key-hash image) against the measured chip-wide ceiling
+    if "probe_kernel" in kernels:
+        kd = kernels["probe_kernel"]
+        rate = st["probes"] / kd["launches_per_step"] / (kd["launch_ms"] / 1e3)
+        kd["probes_per_s"] = round(rate / 1e9, 2)
+        kd["random_sector_ceiling_per_s"] = RANDOM_SECTOR_RATE / 1e9
+        kd["random_sector_frac"] = round(rate / RANDOM_SECTOR_RATE, 3)
+    # the regime of each kernel from its own numbers
+    for k, kd in kernels.items():
+        bw = kd.get("traffic_gbs", kd["achieved"])
+        if bw >= 0.5 * HBM_PEAK_GBS:
+            kd["regime"] = "hbm-bandwidth"
+        elif kd.get("random_sector_frac", 0) >= 0.6:
+            kd["regime"] = "hbm-random-access-rate"
+        else:
+            kd["regime"] = "latency/issue-bound (%.0f GB/s of HBM traffic, %.1f%% of peak)" % (bw, 100 * bw / HBM_PEAK_GBS)
 
     check = None
     oi = None
@@ -413,7 +435,7 @@ def main():
                            "reference-format files via svg_index_open" if prefix else "built in HBM by svg_index_build_mem"),
                        "parallelism": "reads sharded across %d GPU(s), index replicated, no collective" % world,
                        "host_threads_per_rank": int(sa.lib().svg_host_threads())},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(vote_achieved, 2),
+            "roofline": {"bound": "hbm", "regime": kernels[dom]["regime"], "kernel": dom, "achieved": round(vote_achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(vote_achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_unit": "GB per launch",
                          "traffic_source": traffic_src,

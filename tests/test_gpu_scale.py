@@ -7,6 +7,10 @@ oracle restatement on the same index arrays:
     the wave kernel -- through the packed and the ASCII host entry points;
   * C4 shape: 150 bp PE pairs (fragments N(300,50));
   * C5 shape: subjunc on spliced RNA-seq-like reads.
+  * C3g: the same genome with the reference's DEFAULT index type (gapped, subread-buildindex
+    defaults, index-builder.c:1173; ~87 items per bucket), probed through the key-hash image --
+    32-byte sectors with overflow chains, and the 64-byte-line form (SVG_KHASH64) that indexes
+    with run counts over 255 use.
 Reference semantics: sorted-hashtable.c:937-1123 (probe + tally), core-junction.c:2199-2530
 (top-K), core-junction.c:1073-1334,3675-3834 (junction voting)."""
 import numpy as np
@@ -19,11 +23,16 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
-def c3():
+def c3_genome():
+    from subread_amd.sim import random_genome, c3_lengths
+    return random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))   # bench.py's C3 genome
+
+
+@pytest.fixture(scope="module")
+def c3(c3_genome):
     import subread_amd as sa
     from oracle.pyoracle import OracleIndex
-    from subread_amd.sim import random_genome, c3_lengths
-    g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))   # bench.py's C3 genome
+    g = c3_genome
     ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True, device=0)
     assert ix.info.buckets == 93018839 and ix.info.items > 2_900_000_000
     oi = OracleIndex(arrays=ix.export())
@@ -85,3 +94,35 @@ def test_c5_subjunc_spliced(c3):
     assert (rj["minor_votes"] > 0).sum() > 10_000      # the junction branch is exercised
     out, jout, bm = ix.vote_packed(p, sa.pack_reads(r, 100))
     _check(pack_records(out, jout, bm), pack_records(ref, rj, rbm), 1)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("image", ["khash32", "khash64"])
+def test_c3g_gapped_index_se_100bp(c3_genome, image, monkeypatch):
+    import subread_amd as sa
+    from oracle.pyoracle import OracleIndex
+    from subread_amd.abi import default_params, ReadBatch
+    from subread_amd.sim import simulate_reads
+    if image == "khash64":
+        monkeypatch.setenv("SVG_KHASH64", "1")
+    ix = sa.VoteIndex.build_genome(c3_genome, gap=3, memory_mb=8000, force_one_block=False, device=0)
+    monkeypatch.delenv("SVG_KHASH64", raising=False)
+    try:
+        assert ix.info.index_gap == 3 and ix.n_blocks == 1 and ix.info.items > 900_000_000
+        oi = OracleIndex(arrays=ix.export())
+        a = simulate_reads(c3_genome, 100_000, 100, seed=20261015, first=11_000_000, sub=0.01, indel=0.001)
+        b = simulate_reads(c3_genome, 20_000, 100, seed=77, sub=0.03, indel=0.02, nrate=0.003)
+        r = ReadBatch(np.concatenate([a.seq, b.seq]), np.arange(120_000, dtype=np.uint64) * 100,
+                      np.full(120_000, 100, np.uint16))
+        p = default_params()
+        ref, _, _, _ = oi.vote(p, r, None, threads=16)
+        want = pack_records(ref, None, None)
+        ix.set_stats(True)
+        out, _, _ = ix.vote_packed(p, sa.pack_reads(r, 100))
+        st = ix.stats()
+        ix.set_stats(False)
+        _check(pack_records(out, None, None), want, 1)
+        assert st["deferred"] > 0.05 * len(r), st        # repeat-family reads took the wave-kernel path
+        oi.close()
+    finally:
+        ix.close()

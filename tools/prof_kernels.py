@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--reads", type=int, default=50_000_000, help="reads per step (all chunks)")
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--bench-json", help="bench.py line of the traced run (launch_ms to compare)")
+    ap.add_argument("--cmd", default="python3 tools/prof_run.py WL STEPS host", help="the profiled command")
     a = ap.parse_args()
 
     per, stats = trace(a.trace)
@@ -119,12 +120,12 @@ def main():
         comb["all_dispatch_avg_ms"] = None
         res["kernels"]["probe_kernel"] = comb
     res["traffic_bytes_per_read"] = tot_traffic / a.reads
+    res["command"] = a.cmd
     json.dump(res, open(a.out + ".json", "w"), indent=1)
-    M = ["# rocprofv3 summary: %s (bench.py, %d timed steps of %d reads)" % (a.workload, a.steps, a.reads), "",
-         "Kernel trace: `rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu` (warmup %d, steps %d, "
-         "then one statistics pass).  PMC: separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs of "
-         "`bench.py --steps 1 --warmup 0` (no correction: random gathers, see tools/calib_fetch.hip)." % (
-             a.warmup, a.steps), "",
+    M = ["# rocprofv3 summary: %s (%d timed steps of %d reads)" % (a.workload, a.steps, a.reads), "",
+         "Kernel trace: `rocprofv3 --kernel-trace --stats -- %s` (STEPS = %d after %d warmup step).  PMC: "
+         "separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs of the same command with STEPS = 1 (no correction: "
+         "random gathers, see tools/calib_fetch.hip)." % (a.cmd, a.steps, a.warmup), "",
          "| kernel | launches/step | timed avg ms (trace) | bench.py HIP-event ms | rocprof --stats avg ms (all dispatches) "
          "| FETCH B/read | WRITE B/read | HBM traffic B/read |", "|---|---|---|---|---|---|---|---|"]
     for k, e in res["kernels"].items():
@@ -133,8 +134,7 @@ def main():
             "%.3f" % e["all_dispatch_avg_ms"] if e["all_dispatch_avg_ms"] is not None else "-",
             e["fetch_bytes_per_read"], e["write_bytes_per_read"], e["traffic_bytes_per_read"]))
     M += ["", "Total HBM traffic per read (all kernels of a step): %.1f B" % res["traffic_bytes_per_read"], "",
-          "The `--stats` average includes the warmup step and the statistics pass (counters on); the timed "
-          "average is the one bench.py's HIP events measure."]
+          "The `--stats` average includes the warmup step; the timed average drops it."]
     open(a.out + ".md", "w").write("\n".join(M) + "\n")
     print("\n".join(M))
 

@@ -1,8 +1,13 @@
 #!/usr/bin/env python3
-"""Profiling target (GPU box): the device-resident vote path of one bench workload, exactly
-1 warmup + STEPS timed steps and nothing else on the GPU, so that a rocprofv3 trace or PMC
-pass holds (1 + STEPS) x launches-per-step dispatches of every vote kernel.
-Usage: prof_run.py WORKLOAD [STEPS]   (WORKLOAD c3 | c4 | c5; reads per step as bench.py)"""
+"""Profiling target (GPU box): one bench workload's vote path, exactly 1 warmup + STEPS timed
+steps and nothing else on the GPU, so that a rocprofv3 trace or PMC pass holds
+(1 + STEPS) x launches-per-step dispatches of every vote kernel.
+  MODE host   (default): the path bench.py's `value` measures -- svg_vote_batch_packed from
+              2-bit packed reads in pinned host memory to records in pinned host memory
+              (1M-read sub-batches: 48 launches per kernel per 50M-read step)
+  MODE device: svg_vote_batch_packed_device, reads and records resident in HBM (bench.py's
+              device_path figure; 6.25M-read chunks)
+Usage: prof_run.py WORKLOAD [STEPS] [MODE]   (WORKLOAD c3 | c3g | c4 | c5; reads per step as bench.py)"""
 import os
 import sys
 import time
@@ -19,8 +24,10 @@ from subread_amd.sim import random_genome, simulate_reads, simulate_pairs, simul
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    mode = sys.argv[3] if len(sys.argv) > 3 else "host"
     g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))
-    ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True, device=0)
+    gap = 3 if wl == "c3g" else 1
+    ix = sa.VoteIndex.build_genome(g, gap=gap, memory_mb=8000, force_one_block=gap == 1, device=0)
     dev = torch.device("cuda", 0)
     if wl == "c4":
         n, L = 25_000_000, 150
@@ -35,6 +42,36 @@ def main():
         r1, r2 = simulate_reads(g, n, L, seed=20261015, sub=0.01, indel=0.001), None
         p = default_params()
     keep = []
+    ends = 2 if r2 is not None else 1
+    sj = wl == "c5"
+    if mode == "host":
+        # exactly bench.py's host step: pinned packed reads (stride L), pinned records
+        def pinned(count, dt):
+            dt = np.dtype(dt)
+            t = torch.empty(max(1, count * dt.itemsize), dtype=torch.uint8, pin_memory=True)
+            keep.append(t)
+            return t.numpy()[:count * dt.itemsize].view(dt)
+        from subread_amd.abi import SUBJUNC_DTYPE
+        pk1 = sa.pack_reads(r1, L, threads=16, alloc=pinned)
+        pk2 = sa.pack_reads(r2, L, threads=16, alloc=pinned) if r2 is not None else None
+        for pk, rb in ((pk1, r1), (pk2, r2)):
+            if pk is not None:
+                pk.lens = pinned(n, np.uint16)
+                pk.lens[:] = rb.lens
+        bufs = (pinned(n * ends * 3, MAPPING_DTYPE).reshape(n, ends, 3),
+                pinned(n * ends * 3, SUBJUNC_DTYPE).reshape(n, ends, 3) if sj else None,
+                pinned(n * ends * BIG_MARGIN_WORDS, np.uint16).reshape(n, ends, BIG_MARGIN_WORDS) if sj else None)
+
+        def step():
+            ix.vote_packed(p, pk1, pk2, bufs=bufs)
+        step()
+        t = time.perf_counter()
+        for _ in range(steps):
+            step()
+        t = time.perf_counter() - t
+        print("%s host: %d reads x %d ends, %.1f ms/step, %.1f Mreads/s" % (wl, n, ends, t / steps * 1e3,
+                                                                          n * ends * steps / t / 1e6))
+        return
 
     def dq(rb):
         pk = sa.pack_reads(rb, L, threads=16)
@@ -45,9 +82,7 @@ def main():
         return q
     q1 = dq(r1)
     q2 = dq(r2) if r2 is not None else None
-    ends = 2 if r2 is not None else 1
     out = torch.empty(n * ends * 3 * MAPPING_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    sj = wl == "c5"
     jout = torch.empty(n * ends * 3 * 16, dtype=torch.uint8, device=dev) if sj else None
     bm = torch.empty(n * ends * BIG_MARGIN_WORDS * 2, dtype=torch.uint8, device=dev) if sj else None
     ix.set_max_read_length(L)
@@ -63,7 +98,7 @@ def main():
     ix.device_status()
     torch.cuda.synchronize()
     t = time.perf_counter() - t
-    print("%s: %d reads x %d ends, %.1f ms/step, %.1f Mreads/s" % (wl, n, ends, t / steps * 1e3, n * ends * steps / t / 1e6))
+    print("%s device: %d reads x %d ends, %.1f ms/step, %.1f Mreads/s" % (wl, n, ends, t / steps * 1e3, n * ends * steps / t / 1e6))
 
 
 if __name__ == "__main__":
