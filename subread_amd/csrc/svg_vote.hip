@@ -115,17 +115,38 @@ __device__ __forceinline__ char comp(char c)
 	return c == 'A' ? 'T' : c == 'C' ? 'G' : c == 'G' ? 'C' : (c == 'T' || c == 'U') ? 'A' : 'N';
 }
 
-// meta packing
-__device__ __forceinline__ int m_votes(uint32_t m) { return m & 0xff; }
-__device__ __forceinline__ int m_last(uint32_t m) { return (m >> 8) & 0xff; }
-__device__ __forceinline__ int m_toli(uint32_t m) { return (m >> 16) & 0x7f; }
-__device__ __forceinline__ int m_shift(uint32_t m) { return (m >> 23) & 1; }
-__device__ __forceinline__ int m_cursor(uint32_t m) { return (int)(int8_t)(m >> 24); }
-__device__ __forceinline__ uint32_t m_pack(int votes, int last, int toli, int shift, int cursor)
+// meta packing: votes [0,7) | last [7,14) | shift [14] | x [15,17) | spill [17] | then
+//   unspilled: first [18,25) | fx [25,27)      spilled: toli [18,23) | cursor [23,29) (signed)
+// votes and last (a subread number + 1) are <= 64 (applied subreads).  x / fx: the gap slot of the
+// last / first vote, so coverage_end (last vote's offset + 16) and coverage_start (first vote's
+// offset) follow from the meta.  Until a slot opens its first indel section its recorder is
+// (first, last, 0) with toli = cursor = 0 (sorted-hashtable.c:1049-1063,1096-1102) and it has no
+// cold state at all; the first section spills coverage_start and the recorder to the cold scratch
+// (HBM), and the same bits then hold toli and cursor.
+#define M_SPILL (1u << 17)
+__device__ __forceinline__ int m_votes(uint32_t m) { return m & 0x7f; }
+__device__ __forceinline__ int m_last(uint32_t m) { return (m >> 7) & 0x7f; }
+__device__ __forceinline__ int m_shift(uint32_t m) { return (m >> 14) & 1; }
+__device__ __forceinline__ int m_x(uint32_t m) { return (m >> 15) & 3; }
+__device__ __forceinline__ bool m_spilled(uint32_t m) { return (m & M_SPILL) != 0; }
+__device__ __forceinline__ int m_first(uint32_t m) { return (m >> 18) & 0x7f; }
+__device__ __forceinline__ int m_fx(uint32_t m) { return (m >> 25) & 3; }
+__device__ __forceinline__ int m_toli(uint32_t m) { return m_spilled(m) ? (int)((m >> 18) & 31u) : 0; }
+__device__ __forceinline__ int m_cursor(uint32_t m) { return m_spilled(m) ? ((int)(m << 3)) >> 26 : 0; }
+// a spilled slot's meta
+__device__ __forceinline__ uint32_t m_pack_s(int votes, int last, int shift, int x, int toli, int cursor)
 {
-	return (uint32_t)(votes & 0xff) | ((uint32_t)(last & 0xff) << 8) | ((uint32_t)((toli & 0x7f) | (shift << 7)) << 16) |
-	       ((uint32_t)(uint8_t)(int8_t)cursor << 24);
+	return (uint32_t)(votes & 0x7f) | ((uint32_t)(last & 0x7f) << 7) | ((uint32_t)shift << 14) | ((uint32_t)x << 15) | M_SPILL |
+	       ((uint32_t)(toli & 31) << 18) | (((uint32_t)cursor & 63u) << 23);
 }
+// an unspilled slot's meta
+__device__ __forceinline__ uint32_t m_pack_u(int votes, int last, int shift, int x, int first, int fx)
+{
+	return (uint32_t)(votes & 0x7f) | ((uint32_t)(last & 0x7f) << 7) | ((uint32_t)shift << 14) | ((uint32_t)x << 15) |
+	       ((uint32_t)(first & 0x7f) << 18) | ((uint32_t)fx << 25);
+}
+// the gap slot of a subread offset (off = base - base % gap + x; gap 1 (-F) or 3 (default))
+__device__ __forceinline__ int gap_x(int off, int gap) { return gap == 1 ? 0 : off % gap; }
 
 // record field offsets in mapping_result_t (byte offsets)
 #define MR_POS 0
@@ -149,7 +170,8 @@ __device__ __forceinline__ void rec_set_noninf(uint32_t *r, int v) { r[3] = (r[3
 __device__ __forceinline__ int rec_cs(const uint32_t *r) { return r[15] & 0xffff; }
 
 // ---------------------------------------------------------------------------------------------
-// cold per-slot state in HBM scratch: word 0 = cs | ce<<16, bytes 4..24 = indel recorder
+// cold per-slot state in HBM scratch, spilled slots only: word 0 = coverage_start, bytes 4..24 =
+// indel recorder
 __device__ __forceinline__ uint32_t *cold_slot(uint32_t *cold, int slot) { return cold + slot * COLD_WORDS; }
 __device__ __forceinline__ int cold_rec(const uint32_t *cs, int i) { return (int)((const int8_t *)(cs + 1))[i]; }
 __device__ __forceinline__ void cold_set_rec(uint32_t *cs, int i, int v) { ((int8_t *)(cs + 1))[i] = (int8_t)v; }
@@ -200,6 +222,28 @@ struct Wave {
 		return off;
 	}
 
+	// offset of subread kP1 - 1 at gap slot x (core.c:3169-3171)
+	__device__ __forceinline__ int sub_off(int e, int kP1, int x) const
+	{
+		const int gap = kp->ix.gap;
+		int off = (int)(((int64_t)rc.step[e] * (kP1 - 1)) >> 16);
+		if (gap > 1) off -= off % gap - x;
+		return off;
+	}
+	// confident_coverage_start | confident_coverage_end << 16 of a slot (meta M)
+	__device__ __forceinline__ uint32_t slot_cw(int e, int slot, uint32_t M) const
+	{
+		const int ce = sub_off(e, m_last(M), m_x(M)) + 16;
+		const int cs = m_spilled(M) ? (int)(cold_slot(cold[e], slot)[0] & 0xffffu) : sub_off(e, m_first(M), m_fx(M));
+		return (uint32_t)(uint16_t)cs | ((uint32_t)(uint16_t)ce << 16);
+	}
+	// indel recorder entry i of a slot (meta M)
+	__device__ __forceinline__ int slot_rec(int e, int slot, uint32_t M, int i) const
+	{
+		if (m_spilled(M)) return cold_rec(cold_slot(cold[e], slot), i);
+		return i == 0 ? m_first(M) : (i == 1 ? m_last(M) : 0);
+	}
+
 	// ---------------------------------------------------------------- vote-table reset (init_gene_vote)
 	template <int E>
 	__device__ __forceinline__ void table_reset()
@@ -226,7 +270,7 @@ struct Wave {
 		int votes = m_votes(M), last = m_last(M), tl = m_toli(M), cur = m_cursor(M);
 		bool sev = match && round == 0 && tl > 0 && d == 0 && !sh;
 		bool rb = false;
-		if (match && last == kP1 && tl > 0) {    // roll-back test (sorted-hashtable.c:1027-1039)
+		if (match && last == kP1 && tl > 0) {    // roll-back test (sorted-hashtable.c:1027-1039); tl > 0: spilled
 			const uint32_t *cs = cold_slot(cold[E], slot);
 			int md = tl >= 3 ? cold_rec(cs, tl - 1) : 0;
 			int nd = md - d;
@@ -243,16 +287,28 @@ struct Wave {
 		nshift[E] += __popcll(smask);
 		int nvotes = votes;
 		if (apply) {
-			int nlast = last, ntl = tl, nsh = sh | (sev ? 1 : 0), ncur = cur;
+			int nlast = last, ntl = tl, nsh = sh | (sev ? 1 : 0), ncur = cur, nx = m_x(M);
+			bool spill = m_spilled(M);
 			if (rb) { ntl -= 3; nlast -= 1; nvotes -= 1; }
 			if (lane == wl) {
-				uint32_t *cs = cold_slot(cold[E], slot);
 				nvotes += 1;
-				// coverage_end = max(coverage_end, off+16): off rises strictly along the probe
-				// order of a round (step >= gap<<16), so the new value is always off+16
-				((uint16_t *)cs)[1] = (uint16_t)(off + 16);
-				if (d == ncur) cold_set_rec(cs, ntl + 1, kP1);
-				else {
+				// coverage_end = max(coverage_end, off+16): off rises strictly along the probe order
+				// of a round (step >= gap<<16), so it is this vote's off+16 -- kept as (last, x)
+				nx = gap_x(off, kp->ix.gap);
+				if (d == ncur) {
+					if (spill) cold_set_rec(cold_slot(cold[E], slot), ntl + 1, kP1);   // implicit: rec[1] = last
+				} else if (!spill) {
+					// first indel section (toli 0): coverage_start and the recorder go to the cold
+					// scratch, rec[0..7] = first, last, 0, kP1, kP1, d, 0, 0
+					uint32_t *cs = cold_slot(cold[E], slot);
+					cs[0] = (uint32_t)(uint16_t)sub_off(E, m_first(M), m_fx(M));
+					cs[1] = (uint32_t)(uint8_t)m_first(M) | ((uint32_t)(uint8_t)last << 8) | ((uint32_t)(uint8_t)kP1 << 24);
+					cs[2] = (uint32_t)(uint8_t)kP1 | ((uint32_t)(uint8_t)(int8_t)d << 8);
+					ntl = 3;
+					ncur = (int)(int8_t)d;
+					spill = true;
+				} else {
+					uint32_t *cs = cold_slot(cold[E], slot);
 					int t2 = ntl + 3;
 					if (t2 < REC_LEN) {
 						ntl = t2;
@@ -265,7 +321,7 @@ struct Wave {
 				}
 				nlast = kP1;
 			}
-			L->pm[slot].y = m_pack(nvotes, nlast, ntl, nsh, ncur);
+			L->pm[slot].y = spill ? m_pack_s(nvotes, nlast, nsh, nx, ntl, ncur) : m_pack_u(nvotes, nlast, nsh, nx, m_first(M), m_fx(M));
 		}
 		wsync();
 		if (wm) {
@@ -326,11 +382,9 @@ struct Wave {
 				sh = ballot(any) ? 1 : 0;
 			}
 			if (lane == 0) {
-				int slot = (int)r0 * SPACE + n0;
-				uint32_t *cs = cold_slot(cold[E], slot);
-				L->pm[slot] = make_uint2(kv, m_pack(1, kP1, 0, sh, 0));
-				*(uint2 *)cs = make_uint2((uint32_t)(uint16_t)off | ((uint32_t)(uint16_t)(off + 16) << 16),
-				                          (uint32_t)(uint8_t)kP1 | ((uint32_t)(uint8_t)kP1 << 8));   // rec[0..3] = k+1, k+1, 0, 0
+				// a new slot: recorder (k+1, k+1, 0), coverage off..off+16, all in the meta
+				const int x = gap_x(off, kp->ix.gap);
+				L->pm[(int)r0 * SPACE + n0] = make_uint2(kv, m_pack_u(1, kP1, sh, x, kP1, x));
 			}
 			if (lane == E * 32 + (int)r0) items_v = n0 + 1;
 			if (max_vote[E] == 0) max_vote[E] = 1;
@@ -387,11 +441,8 @@ struct Wave {
 		if (lane < 32) L->rnew[lane] = 0xff;
 		wsync();
 		if (mk) {
-			const int slot = (int)r0 * SPACE + n0 + rank;
-			uint32_t *cs = cold_slot(cold[E], slot);
-			L->pm[slot] = make_uint2(kv, m_pack(1, kP1, 0, 0, 0));
-			*(uint2 *)cs = make_uint2((uint32_t)(uint16_t)off | ((uint32_t)(uint16_t)(off + 16) << 16),
-			                          (uint32_t)(uint8_t)kP1 | ((uint32_t)(uint8_t)kP1 << 8));   // rec[0..3] = k+1, k+1, 0, 0
+			const int x = gap_x(off, kp->ix.gap);
+			L->pm[(int)r0 * SPACE + n0 + rank] = make_uint2(kv, m_pack_u(1, kP1, 0, x, kP1, x));   // no cold state
 		}
 		if (inr && (same & cm & ~le) == 0ull) L->rnew[r0] = (uint8_t)(n0 + rank + 1 < SPACE ? n0 + rank + 1 : SPACE);
 		wsync();
@@ -517,10 +568,10 @@ struct Wave {
 		uint32_t P, M;
 		int slot;
 		ent_h(e, h, P, M, slot);
-		const uint32_t *cs = cold_slot(cold[e], slot);
 		// indel_recorder_copy (sorted-hashtable.c:1144): triples while rec[3t] != 0 and 3t < 19
 		int v = 0;
-		if (lane < REC_LEN) v = cold_rec(cs, lane);
+		if (lane < REC_LEN) v = slot_rec(e, slot, M, lane);
+		const uint32_t cw = slot_cw(e, slot, M);
 		unsigned long long z = ballot(lane < 19 && (lane % 3) == 0 && v == 0);
 		int T = z ? (__ffsll((long long)z) - 1) / 3 : 7;   // number of triples copied
 		int nrec = 3 * T;
@@ -533,7 +584,7 @@ struct Wave {
 			r[0] = P;
 			r[2] = (uint32_t)(uint16_t)m_votes(M) | ((uint32_t)(uint16_t)rc.applied[e] << 16);
 			r[3] = (uint32_t)(uint8_t)(int8_t)(nrec > 0 ? last_ind : 0) << 8;   // noninf 0, indels
-			r[15] = cs[0];   // confident_coverage_start | confident_coverage_end << 16
+			r[15] = cw;      // confident_coverage_start | confident_coverage_end << 16
 			r[16] = 0;
 		}
 	}
@@ -727,14 +778,14 @@ struct Wave {
 		int ms;
 		ent_h(e, mh, Mpos, MM, ms);
 		const int Mv = m_votes(MM);
-		const uint32_t mw = cold_slot(cold[e], ms)[0];
+		const uint32_t mw = slot_cw(e, ms, MM);
 		const int Mcs = (int)(mw & 0xffff), Mce = (int)(mw >> 16);
 		const int rl = rc.rl[e];
 		int Jv = 0, Jcs = 0, Jce = 0, Jsplit = 0, Jnormal = 0, Jdio = 0;
 		// long reads (core-junction.c, curr_read_len > EXON_LONG_READ_LENGTH): the indel offsets
 		// accumulated over each half's indel recorder shift the smaller half's donor tests
 		int major_ind = 0;
-		if (rl > 160) {
+		if (rl > 160 && m_spilled(MM)) {   // an unspilled recorder is (first, last, 0): offset 0
 			const uint32_t *mcs = cold_slot(cold[e], ms);
 			for (int kx = 0; kx < SVG_MAX_INDEL_SECTIONS; kx++) {
 				if (!cold_rec(mcs, kx * 3)) break;
@@ -748,12 +799,11 @@ struct Wave {
 			int f = f0 + lane;
 			int hh = handle_of(e, rs_v, f);   // all lanes active
 			bool ok = f < U && hh != mh;
-			uint32_t P = 0;
+			uint32_t P = 0, MMv = 0;
 			int V = 0, cs = 0, ce = 0;
 			int sl = 0;
 			long long dist = 0;
 			if (ok) {
-				uint32_t MMv;
 				ent_h(e, hh, P, MMv, sl);
 				V = m_votes(MMv);
 				dist = (long long)Mpos - (long long)P;
@@ -762,7 +812,7 @@ struct Wave {
 			// the coverage (cold state, HBM) only for slots within intron distance -- usually none
 			if (!ballot(ok)) continue;
 			if (ok) {
-				uint32_t w = cold_slot(cold[e], sl)[0];
+				uint32_t w = slot_cw(e, sl, MMv);
 				cs = (int)(w & 0xffff); ce = (int)(w >> 16);
 				ok = cs != Mcs && ce != Mce;
 				if (ok) ok = (Mcs > cs) ? (Mpos >= P) : (Mpos <= P);   // test_junction_minor
@@ -788,8 +838,9 @@ struct Wave {
 				int split = 0, gtag = 0, found = 0;
 				int minor_ind = 0, lio = 0;
 				if (rl > 160) {
+					const uint32_t Mb = (uint32_t)rd((int)MMv, b);
 					const uint32_t *ncs = cold_slot(cold[e], rd(sl, b));
-					for (int kx = 0; kx < SVG_MAX_INDEL_SECTIONS; kx++) {
+					for (int kx = 0; kx < SVG_MAX_INDEL_SECTIONS && m_spilled(Mb); kx++) {
 						if (!cold_rec(ncs, kx * 3)) break;
 						minor_ind += cold_rec(ncs, kx * 3 + 2);
 					}
@@ -905,7 +956,7 @@ struct Wave {
 							STAMP(4);
 							const bool elig = f < U[e] && at < p.max_vote_simples && v >= top[e][TS - 1];
 							if (ballot(elig)) {
-								const uint32_t cw = elig ? cold_slot(cold[e], slot)[0] : 0u;
+								const uint32_t cw = elig ? slot_cw(e, slot, M) : 0u;
 								big_margin_merge(e, elig, v, cw);
 							}
 							STAMP(7);
@@ -2616,7 +2667,7 @@ extern "C" int svg_set_max_read_length(svg_index *h, int max_len)
 	return 0;
 }
 
-static int check_params(const svg_index *h, const svg_params *p, int paired)
+int svg_check_params(const svg_index *h, const svg_params *p, int paired)
 {
 	if (p->multi_best < 1 || p->multi_best > 3) { svg_set_error("multi_best must be 1..3"); return SVG_E_UNSUPPORTED; }
 	if (p->top_scores != 3) { svg_set_error("top_scores must be 3 (reference runtime value)"); return SVG_E_UNSUPPORTED; }
@@ -2707,7 +2758,7 @@ int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, con
 {
 	if (!h || !p || !r1 || !out) { svg_set_error("svg_vote_batch_device: NULL argument"); return SVG_E_ARG; }
 	if (r2 && r2->n_reads != r1->n_reads) { svg_set_error("R1/R2 read counts differ"); return SVG_E_ARG; }
-	int rc = check_params(h, p, r2 != NULL);
+	int rc = svg_check_params(h, p, r2 != NULL);
 	if (rc) return rc;
 	if (p->do_breakpoint_detection && !jout) { svg_set_error("do_breakpoint_detection needs jout"); return SVG_E_ARG; }
 	if (p->do_big_margin_filtering_for_junctions && !big_margin) { svg_set_error("big-margin filtering needs big_margin"); return SVG_E_ARG; }
