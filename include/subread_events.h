@@ -12,14 +12,16 @@
  *   find_new_indels   core-indel.c:1831-2098, dynamic-programming path
  *                     (use_dynamic_programming_indel = 1, core-interface-aligner.c:271,
  *                     core-interface-subjunc.c:270; core_dynamic_align core-indel.c:4573)
- *   find_new_junctions core-junction.c:3836-4137 (do_breakpoint_detection; reads <= 160 bp)
+ *   find_new_junctions core-junction.c:3836-4137 (do_breakpoint_detection), with
+ *                     core_search_short_exons (core-junction.c:4386-4731) for reads > 160 bp
+ *   the events of fragile junction voting (core-junction.c:5211-5419) for subjunc reads
+ *                     > 160 bp, from svg_fragile_batch's windows (svg_events_add_batch2)
  *   local_add_indel_event / put_new_event / search_event  core-indel.c:1385-1569
  *   has_better_mapping core.c:3035, is_ambiguous_voting core-junction.c:3522,
  *   locate_current_value_index core.c:2216 (multi-block indexes)
  *   anti_supporting_read_scan core-indel.c:177-330
- * Not covered (SVG_E_UNSUPPORTED): subjunc reads > 160 bp (core_search_short_exons and the
- * fragile junction voting feed their events), fusion / long-deletion detection, the
- * extending indel search (extending_search_indels = 0 in both programs).
+ * Not covered (SVG_E_UNSUPPORTED): fusion / long-deletion detection, the extending indel
+ * search (extending_search_indels = 0 in both programs).
  *
  * Threading: one table per host thread; svg_events_merge() combines tables the way
  * finalise_indel_and_junction_thread combines the reference's per-thread tables.
@@ -73,6 +75,8 @@ typedef struct svg_event_params {
 	int32_t dp_match_score;               /*  2 */
 	int32_t dp_mismatch_penalty;          /*  0 */
 	int32_t report_multi_mapping_reads;   /*  0 (--multiMapping: 1) */
+	int32_t quality_base;                 /* '#' (35): FASTQ_PHRED33; 'B' (66) with -P 6 (read_quality_score) */
+	int32_t maximise_sensitivity_indel;   /*  0 (the fragile votes' indels: < 2 mismatches, else <= 2) */
 } svg_event_params;
 void svg_event_params_default(svg_event_params *e);
 
@@ -95,6 +99,21 @@ void svg_events_destroy(svg_events *t);
 int svg_events_add_batch(svg_events *t, const svg_genome_arrays *g, const svg_params *p, const svg_event_params *ep,
                          const svg_reads *r1, const svg_reads *r2, uint64_t first_read, svg_mapping_result *out,
                          const svg_subjunc_result *jout, const uint16_t *big_margin);
+
+/*
+ * The same with what subjunc reads longer than 160 bases need as well (svg_events_add_batch
+ * refuses those with SVG_E_UNSUPPORTED):
+ *   q1 / q2 : the reads' quality strings (same offsets and lengths as r1 / r2; NULL = no
+ *             qualities, as FASTA input) -- core_search_short_exons tests the head / tail quality;
+ *   frag    : svg_fragile_batch's result for the same reads and parameters.
+ * The events come in the reference's order: the fragile windows of every index block but the
+ * last (the earlier runs of the block loop, core.c:3567-3613), then read by read the last
+ * block's windows of the read followed by its final-run tail.
+ */
+int svg_events_add_batch2(svg_events *t, const svg_genome_arrays *g, const svg_params *p, const svg_event_params *ep,
+                          const svg_reads *r1, const svg_reads *r2, const svg_reads *q1, const svg_reads *q2,
+                          uint64_t first_read, svg_mapping_result *out, const svg_subjunc_result *jout,
+                          const uint16_t *big_margin, const svg_fragile_result *frag);
 
 /* Merge `n` tables (in order) into `dst` (created empty by the caller): the sort-and-sum of
  * finalise_indel_and_junction_thread.  Also call it with n = 1 on a single table: the merged

@@ -259,6 +259,55 @@ int svg_probe_keys(svg_index *idx, int block, const uint32_t *keys, uint64_t n,
 int svg_probe_keys_device(svg_index *idx, int block, const uint32_t *keys, uint64_t n,
                           uint32_t *first, uint32_t *count, void *hip_stream);
 
+/*
+ * Fragile junction voting of subjunc reads longer than 160 bases (core_fragile_junction_voting,
+ * core-junction.c:5151-5422; do_voting runs it for every index block, strand and read end,
+ * core.c:3138-3142).  The read (strand 0: as fetched after the -S reversal, strand 1: its
+ * reverse_read) is cut into ~60-base windows; each window is voted with gehash_go_q
+ * (sorted-hashtable.c:515-933: every item of the key's equal-key run from the first one, the
+ * go_X tally without shift-indel rounds, tolerance 5) over subreads every 3.00001 bases, then:
+ *   - every slot with the top vote count whose indel recorder has a second section is reported
+ *     (svg_fragile_slot) -- the reference aligns those on the host (core_dynamic_align) into
+ *     indel events;
+ *   - select_best_vote + core_select_best_matching_halves pick a second half, and
+ *     core13_test_donor (GT..AG / CT..AC donors, 17-base match windows) decides whether the
+ *     window supports a junction (small_side, large_side, is_GTAG).
+ * svg_fragile_batch runs all of it on the GPU for a batch (host buffers, synchronous; reads as
+ * svg_vote_batch takes them, p must be subjunc parameters); the result arrays are owned by the
+ * library until svg_fragile_free.  The events are made on the host by svg_events_add_batch2
+ * (include/subread_events.h), in the reference's order.
+ */
+typedef struct svg_fragile_window {
+	uint32_t read;             /* read (pair) number in the batch */
+	uint8_t  block;            /* index block */
+	uint8_t  strand;           /* 0: the read as fetched, 1: reverse_read of it */
+	uint8_t  end;              /* 0: R1, 1: R2 */
+	uint8_t  window;           /* window number */
+	uint16_t start, length;    /* window_cursor and read_len of the window */
+	uint8_t  junction;         /* 1: core13_test_donor accepted a split point */
+	uint8_t  gtag;             /* its is_GTAG */
+	uint16_t n_slots;          /* reported slots: slots[first_slot .. first_slot + n_slots) */
+	uint32_t small_side;       /* junction event: min(split + pos1, split + pos2) - 1 */
+	uint32_t large_side;       /*                 max(split + pos1, split + pos2) */
+	uint32_t first_slot;
+} svg_fragile_window;          /* 28 bytes */
+
+typedef struct svg_fragile_slot {
+	uint32_t position;         /* the slot's voting position */
+	int16_t  rec[9];           /* indel_recorder[0..8], zero after the first empty section */
+	uint16_t _pad;
+} svg_fragile_slot;            /* 24 bytes */
+
+typedef struct svg_fragile_result {
+	uint64_t n_windows, n_slots;
+	svg_fragile_window *windows;   /* (block, read, strand, end, window) order: do_voting's */
+	svg_fragile_slot *slots;       /* window by window, each window's in row-major slot order */
+} svg_fragile_result;
+
+int  svg_fragile_batch(svg_index *idx, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                       svg_fragile_result *out);
+void svg_fragile_free(svg_fragile_result *r);
+
 /* Per-batch statistics of the last svg_vote_batch* call on this handle
  * (filled only when the handle was opened with SVG_STATS=1 in the environment
  * or after svg_set_stats(idx,1)); used for the algorithmic-byte roofline. */

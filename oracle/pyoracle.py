@@ -45,6 +45,9 @@ def lib():
                                             ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
         L.svo_vote_batch.restype = ctypes.c_int
         L.svo_vote_batch.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int, ctypes.c_void_p]
+        L.svo_fragile_batch.restype = ctypes.c_int
+        L.svo_fragile_batch.argtypes = [ctypes.c_void_p] * 5
+        L.svo_fragile_free.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -110,3 +113,18 @@ class OracleIndex:
         if rc != 0:
             raise RuntimeError("svo_vote_batch failed: %d" % rc)
         return out, jout, bm, st
+
+    def fragile(self, params, r1, r2=None):
+        """svo_fragile_batch: the fragile junction voting windows (svg_fragile_batch's form)."""
+        from subread_amd.abi import SvgFragileResult
+        s1 = r1.struct()
+        s2 = r2.struct() if r2 is not None else None
+        res = SvgFragileResult()
+        rc = lib().svo_fragile_batch(self.h, ctypes.byref(params), ctypes.byref(s1),
+                                     ctypes.byref(s2) if s2 is not None else None, ctypes.byref(res))
+        if rc != 0:
+            raise RuntimeError("svo_fragile_batch failed: %d" % rc)
+        try:
+            return res.arrays()
+        finally:
+            lib().svo_fragile_free(ctypes.byref(res))

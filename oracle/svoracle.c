@@ -1010,3 +1010,355 @@ int svo_vote_batch(const svo_index *ix, const svg_params *p, const svg_reads *r1
 	}
 	return 0;
 }
+
+/* ------------------------------------------------------------------ fragile junction voting */
+/*
+ * core_fragile_junction_voting, core-junction.c:5151-5422: the part that votes and decides
+ * (gehash_go_q windows, select_best_vote, core_select_best_matching_halves,
+ * core13_test_donor), in the form svg_fragile_batch returns it (include/subread_vote.h);
+ * the events it implies are made by svg_events_add_batch2 in the product.
+ */
+#define FRAG_WIN 60       /* EXON_LARGE_WINDOW, core-junction.c:5148 */
+#define FRAG_TOL 5        /* the indel tolerance of the fragile votes (core-junction.c:5205) */
+
+/* gehash_go_q VER_2, sorted-hashtable.c:750-932: binary search, back to the run's first item,
+ * then the go_X round-0 tally over the run in item order (no shift-indel marks) */
+static void probe_Q(const svo_index *ix, uint32_t key, int off, int strand, vtab_t *v, int tol, int subread_no,
+                    uint32_t low, uint32_t high)
+{
+	uint32_t b = key % ix->nb;
+	int16_t k16 = (int16_t)(key / ix->nb);
+	uint32_t first = ix->bstart[b];
+	int n = (int)(ix->bstart[b + 1] - first);
+	const int16_t *K = ix->keys + first;
+	const uint32_t *V = ix->vals + first;
+	int lo = 0, hi = n - 1, idx;
+	int kP1 = subread_no + 1, ofp16 = off + 16, mask = strand ? NEG_MASK : 0;
+	int ii_end = SEG;
+	if (!n) return;
+	for (;;) {
+		idx = (lo + hi) / 2;
+		if (K[idx] > k16) hi = idx - 1;
+		else if (K[idx] < k16) lo = idx + 1;
+		else break;
+		if (hi < lo) return;
+	}
+	while (idx && K[idx - 1] == k16) idx--;
+	if (tol > 5) ii_end = (tol % SEG) ? (tol - tol % SEG + SEG) : tol;
+	for (; idx < n && K[idx] == k16; idx++) {
+		uint32_t kv = V[idx] - (uint32_t)off;
+		uint32_t r0 = vrow(kv);
+		int n0 = v->items[r0];
+		int found = 0, iix;
+		for (iix = 0; iix <= ii_end; iix = iix > 0 ? -iix : (-iix + SEG)) {
+			uint32_t r = r0; int cnt = n0, s;
+			if (iix) { r = vrow(kv + (uint32_t)iix); cnt = v->items[r]; }
+			if (!cnt) continue;
+			for (s = 0; s < cnt; s++) {
+				int d = (int)(kv - v->pos[r][s]);
+				int tl;
+				if (!(d >= -tol && d <= tol && mask == v->masks[r][s])) continue;
+				tl = v->toli[r][s];
+				if (kP1 == v->last[r][s] && tl > 0) {
+					int md = 0, nd;
+					if (tl >= 3) md = v->rec[r][s][tl - 1];
+					nd = md;
+					md -= v->rec[r][s][tl + 2];
+					nd -= d;
+					if (abs(md) > abs(nd)) { tl -= 3; v->toli[r][s] = tl; v->last[r][s]--; v->votes[r][s]--; }
+				}
+				if (kP1 <= v->last[r][s]) continue;
+				{
+					int16_t nv = v->votes[r][s] + 1;
+					v->votes[r][s] = nv;
+					if (off + 16 > v->ce[r][s]) v->ce[r][s] = ofp16;
+					if (d == v->cursor[r][s]) v->rec[r][s][tl + 1] = kP1;
+					else {
+						tl += 3;
+						if (tl < REC_LEN) {
+							v->toli[r][s] = tl;
+							v->rec[r][s][tl] = kP1;
+							v->rec[r][s][tl + 1] = kP1;
+							v->rec[r][s][tl + 2] = d;
+							if (tl < REC_LEN - 3) v->rec[r][s][tl + 3] = 0;
+						}
+						v->cursor[r][s] = (int8_t)d;
+					}
+					v->last[r][s] = kP1;
+					if (v->max_vote < nv) v->max_vote = nv;
+				}
+				found = 1;
+				break;
+			}
+			if (found) break;
+		}
+		if (found) continue;
+		if (kv < low || kv > high) continue;
+		if (n0 < TAB_SPACE) {
+			int s = n0;
+			v->items[r0]++;
+			v->pos[r0][s] = kv;
+			v->masks[r0][s] = mask;
+			v->votes[r0][s] = 1;
+			v->toli[r0][s] = 0;
+			v->rec[r0][s][0] = v->rec[r0][s][1] = kP1;
+			v->rec[r0][s][2] = 0;
+			v->rec[r0][s][3] = 0;
+			v->cursor[r0][s] = 0;
+			v->cs[r0][s] = off;
+			v->ce[r0][s] = ofp16;
+			v->last[r0][s] = kP1;
+			if (v->max_vote == 0) v->max_vote = 1;
+		}
+	}
+}
+
+/* gvindex_get_string(buf, ix, pos, 2, neg), gene-value-index.c:1118-1136 */
+static void chro_2base(const svo_index *ix, uint32_t pos, int neg, char h[2])
+{
+	if (!neg) { h[0] = gv_get(ix, pos); h[1] = gv_get(ix, pos + 1); return; }
+	for (int i = 1; i >= 0; i--) {
+		char c = gv_get(ix, pos + 1 - i);
+		h[i] = c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'G' ? 'C' : c == 'C' ? 'G' : c;
+	}
+}
+
+/* match_chro, gene-value-index.c:856-959, base space, either strand */
+static int match_chro_s(const char *read, const svo_index *ix, uint32_t pos, int len, int neg)
+{
+	int ret = 0, i;
+	if (!neg) return match_chro(read, ix, pos, len);
+	if ((uint32_t)(pos + len) >= ix->length + ix->start_point) return 0;
+	if (pos > 0xffff0000u) return 0;
+	for (i = len - 1; i >= 0; i--) {
+		switch (gv_get(ix, pos + len - 1 - i)) {
+		case 'A': ret += read[i] == 'T'; break;
+		case 'T': ret += read[i] == 'A'; break;
+		case 'G': ret += read[i] == 'C'; break;
+		case 'C': ret += read[i] == 'G'; break;
+		}
+	}
+	return ret;
+}
+
+#define CEQ(c, t) ((c)[0] == (t)[0] && (c)[1] == (t)[1])
+#define C2EQ(a, b, x, y) ((CEQ(a, x) && CEQ(b, y)) || (CEQ(a, y) && CEQ(b, x)))
+#define DONOR_PART(c) (CEQ(c, "GT") || CEQ(c, "AG") || CEQ(c, "AC") || CEQ(c, "CT"))
+
+/* paired_chars_part, core-junction.c:4366-4374 */
+static int paired_part(const char *a, const char *b, int rev)
+{
+	if (C2EQ(a, b, "GT", "AG") || C2EQ(a, b, "CT", "AC")) {
+		if (rev && (CEQ(a, "AG") || CEQ(a, "AC"))) return 1;
+		if (!rev && (CEQ(a, "CT") || CEQ(a, "GT"))) return 1;
+	}
+	return 0;
+}
+
+/* core13_test_donor, core-junction.c:5027-5141 (indel offsets 0, base space) */
+static int test_donor13(const svo_index *ix, const char *read, int rl, uint32_t pos1, uint32_t pos2, int guess, int range,
+                        int rev, int *real_bp, int *gtag)
+{
+	int x, start = guess - range, end = guess + range, best = -1, min_x = -9099;
+	if (start < 10) start = 10;
+	if (end > rl - 10) end = rl - 10;
+	for (x = start; x < end; x++) {
+		char h1[2], h2[2];
+		chro_2base(ix, pos1 + (uint32_t)x, rev, h1);
+		chro_2base(ix, pos2 - 2 + (uint32_t)x, rev, h2);
+		if (h1[0] == h2[0] && h1[1] == h2[1]) continue;
+		if (!(DONOR_PART(h1) && DONOR_PART(h2)) || !paired_part(h1, h2, rev)) continue;
+		{
+			int bph = rev ? rl - x : x, conf = bph < 17 ? bph : 17, m1, m2, x1, x2;
+			uint32_t fe, ss;
+			if (rl - bph < conf) conf = rl - bph;
+			if (rev) {
+				fe = pos2 + (uint32_t)x; ss = pos1 + (uint32_t)x;
+				m1 = match_chro_s(read + bph - conf, ix, fe, conf, 1);
+				m2 = match_chro_s(read + bph, ix, ss - (uint32_t)conf, conf, 1);
+				x1 = match_chro_s(read + bph, ix, fe - (uint32_t)conf, conf, 1);
+				x2 = match_chro_s(read + bph - conf, ix, ss, conf, 1);
+			} else {
+				fe = pos1 + (uint32_t)x; ss = pos2 + (uint32_t)x;
+				m1 = match_chro_s(read + bph - conf, ix, fe - (uint32_t)conf, conf, 0);
+				m2 = match_chro_s(read + bph, ix, ss, conf, 0);
+				x1 = match_chro_s(read + bph, ix, fe, conf, 0);
+				x2 = match_chro_s(read + bph - conf, ix, ss - (uint32_t)conf, conf, 0);
+			}
+			if (m1 >= conf - 1 && m2 >= conf - 1 && x1 < conf - 3 && x2 < conf - 3) {
+				int score = 3000 - (x1 + x2) + (m1 + m2);
+				if (min_x < score) {
+					min_x = score;
+					best = x;
+					*gtag = 1 == (rev + (h1[0] == 'G' || h1[1] == 'G'));
+				}
+			}
+		}
+	}
+	if (best > 0) { *real_bp = best; return 1; }
+	return 0;
+}
+
+/* the window layout of a read of rl > 160 bases (core-junction.c:5153-5180, float arithmetic) */
+static int fragile_windows(int rl, int *cursor, int *len)
+{
+	int windows = rl / FRAG_WIN + 1, ww;
+	float overlap = (1.0 * windows * FRAG_WIN - rl) / (windows - 1);
+	for (ww = 0; ww < windows; ww++) {
+		cursor[ww] = (int)(ww * FRAG_WIN - ww * overlap);
+		len[ww] = ww == windows - 1 ? rl - cursor[ww] : FRAG_WIN;
+	}
+	return windows;
+}
+
+typedef struct {
+	svg_fragile_window *w; uint64_t nw, cw;
+	svg_fragile_slot *s; uint64_t ns, cs;
+} frag_out;
+
+/* one (block, read, strand, end): every window of core_fragile_junction_voting */
+static void fragile_read(const svo_index *ix, int block, vtab_t *v, const char *text, int rl, int strand, uint32_t low,
+                         uint32_t high_full, uint32_t read, int end, frag_out *o)
+{
+	const int gap = ix->gap;
+	const float sstep = 3.00001f;
+	int cur[SVG_MAX_READ_LENGTH / FRAG_WIN + 2], len[SVG_MAX_READ_LENGTH / FRAG_WIN + 2];
+	int windows = fragile_windows(rl, cur, len), ww;
+	for (ww = 0; ww < windows; ww++) {
+		const char *in = text + cur[ww];
+		const int wl = len[ww];
+		const uint32_t hb = high_full - (uint32_t)wl;
+		int k, r, s;
+		svg_fragile_window *W;
+		if (o->nw == o->cw) { o->cw = o->cw ? 2 * o->cw : 1024; o->w = realloc(o->w, sizeof *o->w * o->cw); }
+		W = &o->w[o->nw++];
+		memset(W, 0, sizeof *W);
+		W->read = read; W->block = (uint8_t)block; W->strand = (uint8_t)strand; W->end = (uint8_t)end;
+		W->window = (uint8_t)ww; W->start = (uint16_t)cur[ww]; W->length = (uint16_t)wl;
+		W->first_slot = (uint32_t)o->ns;
+		vt_reset(v);
+		for (k = 0;; k++) {
+			int off1 = (int)(sstep * (k + 1)), i;
+			off1 -= off1 % gap;
+			off1 += gap - 1;
+			for (i = 0; i < gap; i++) {
+				int off = (int)(sstep * k);
+				off -= off % gap - i;
+				probe_Q(ix, pack16(in + off), off, strand, v, FRAG_TOL, k, low, hb);
+			}
+			if (off1 >= wl - 16) break;
+		}
+		/* top-vote slots with a second recorder section (core-junction.c:5211-5339: the slots
+		 * core_dynamic_align then works on), row-major */
+		for (r = 0; r < TAB_ROWS; r++)
+			for (s = 0; s < v->items[r]; s++) {
+				svg_fragile_slot *S;
+				int q;
+				if (v->votes[r][s] < v->max_vote || !v->rec[r][s][3]) continue;
+				if (o->ns == o->cs) { o->cs = o->cs ? 2 * o->cs : 1024; o->s = realloc(o->s, sizeof *o->s * o->cs); }
+				S = &o->s[o->ns++];
+				memset(S, 0, sizeof *S);
+				S->position = v->pos[r][s];
+				for (q = 0; q < 9; q++) S->rec[q] = v->rec[r][s][q];
+				if (!S->rec[6]) S->rec[7] = S->rec[8] = 0;
+				W->n_slots++;
+			}
+		/* select_best_vote (sorted-hashtable.c:1128): the last slot with the top count */
+		{
+			uint32_t max_pos = 0;
+			int max_cs = 0, max_ce = 0, have = 0;
+			for (r = 0; r < TAB_ROWS; r++)
+				for (s = 0; s < v->items[r]; s++)
+					if (v->votes[r][s] == v->max_vote) { max_pos = v->pos[r][s]; max_cs = v->cs[r][s]; max_ce = v->ce[r][s]; have = 1; }
+			if (!have) continue;   /* no slot: core_select_best_matching_halves returns 0 */
+			/* core_select_best_matching_halves_maxone, core-junction.c:4741-4896 (hint_pos -1) */
+			int best_sp = -1, selected = -1, v2 = 0;
+			uint32_t p2 = 0;
+			for (r = 0; r < TAB_ROWS; r++)
+				for (s = 0; s < v->items[r]; s++) {
+					int cs = v->cs[r][s], ce = v->ce[r][s];
+					int os = max_cs > cs ? max_cs : cs, oe = max_ce < ce ? max_ce : ce;
+					long long dist = (long long)v->pos[r][s] - (long long)max_pos;
+					int ad = abs((int)dist), c1, c2, q1, q2, tv;
+					if (oe - os >= 14) continue;
+					if (ad < 6) continue;
+					if (v->max_vote < 1 || v->votes[r][s] < 1) continue;
+					if ((cs < max_cs) + strand == 1) {
+						locate(ix, max_pos + (uint32_t)wl, &c1, &q1);
+						locate(ix, v->pos[r][s], &c2, &q2);
+					} else {
+						locate(ix, max_pos, &c1, &q1);
+						locate(ix, v->pos[r][s] + (uint32_t)wl, &c2, &q2);
+					}
+					if (c1 != c2) continue;
+					if (ad > 500000) continue;
+					tv = 8888888 + v->votes[r][s] * 1000000 - ad;
+					if (tv < selected) continue;
+					best_sp = ((cs < max_cs) ? ce : max_ce) + ((cs < max_cs) ? max_cs : cs);
+					best_sp /= 2;
+					p2 = v->pos[r][s];
+					v2 = v->votes[r][s];
+					selected = tv;
+				}
+			/* core_select_best_matching_halves: taken only above 1000000 */
+			if (selected + v->max_vote * 1000000 <= 1000000) continue;
+			if (best_sp > 0 && v->max_vote >= 1 && v2 >= 1) {
+				int bp = 0, gt = 0;
+				uint32_t lo_p = max_pos < p2 ? max_pos : p2, hi_p = max_pos < p2 ? p2 : max_pos;
+				if (test_donor13(ix, in, wl, lo_p, hi_p, best_sp, wl / 4, strand, &bp, &gt)) {
+					uint32_t a = (uint32_t)bp + max_pos, c = (uint32_t)bp + p2;
+					W->junction = 1;
+					W->gtag = (uint8_t)gt;
+					W->small_side = (a < c ? a : c) - 1;
+					W->large_side = a < c ? c : a;
+				}
+			}
+		}
+	}
+}
+
+/* every block, read, strand and end of a batch, in do_voting's order (svg_fragile_batch's
+ * result; the arrays are malloc'ed: free them with svo_fragile_free) */
+int svo_fragile_batch(const svo_index *ix0, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                      svg_fragile_result *out)
+{
+	frag_out o;
+	vtab_t *v;
+	const svo_index *ix;
+	int ends = r2 ? 2 : 1, block = 0;
+	memset(&o, 0, sizeof o);
+	memset(out, 0, sizeof *out);
+	if (!ix0 || !p || !r1 || (r2 && r2->n_reads != r1->n_reads)) return SVG_E_ARG;
+	v = malloc(sizeof *v);
+	for (ix = ix0; ix; ix = ix->next, block++) {
+		const uint32_t low = ix->start_base_offset, high = ix->start_base_offset + ix->length;
+		for (uint64_t r = 0; r < r1->n_reads; r++) {
+			char text[2][SVG_MAX_READ_LENGTH + 1];
+			int rl[2], e, strand;
+			for (e = 0; e < ends; e++) {
+				const svg_reads *rr = e ? r2 : r1;
+				rl[e] = rr->lens[r] > SVG_READ_KEEP ? SVG_READ_KEEP : rr->lens[r];
+				memcpy(text[e], rr->seq + rr->offsets[r], (size_t)rl[e]);
+				text[e][rl[e]] = 0;
+				if (e ? p->reverse_r2 : p->reverse_r1) revcomp(text[e], rl[e]);
+			}
+			for (strand = 0; strand < 2; strand++) {
+				for (e = 0; e < ends; e++)
+					if (rl[e] > LONG_READ)
+						fragile_read(ix, block, v, text[e], rl[e], strand, low, high - (uint32_t)rl[e], (uint32_t)r, e, &o);
+				for (e = 0; e < ends; e++) revcomp(text[e], rl[e]);
+			}
+		}
+	}
+	free(v);
+	out->windows = o.w; out->n_windows = o.nw;
+	out->slots = o.s; out->n_slots = o.ns;
+	return 0;
+}
+
+void svo_fragile_free(svg_fragile_result *r)
+{
+	if (!r) return;
+	free(r->windows); free(r->slots);
+	r->windows = NULL; r->slots = NULL; r->n_windows = r->n_slots = 0;
+}

@@ -16,6 +16,7 @@ import numpy as np
 
 from .abi import (MAPPING_DTYPE, SUBJUNC_DTYPE, BIG_MARGIN_WORDS, ERRORS, PROGRAM_ALIGN,
                   PROGRAM_SUBJUNC, SvgParams, SvgReads, SvgPackedReads, SvgIndexInfo, SvgBatchStats, ReadBatch,
+                  SvgFragileResult,
                   PackedBatch, default_params, read_fastq)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -31,10 +32,11 @@ EXPORTS = [
     "svg_set_max_read_length", "svg_sim_pairs", "svg_set_timing", "svg_get_timing",
     "svg_get_kernel_timing", "svg_device_status", "svg_pack_reads", "svg_vote_batch_packed",
     "svg_vote_batch_packed_device", "svg_probe_keys", "svg_probe_keys_device", "svg_host_threads",
+    "svg_fragile_batch", "svg_fragile_free",
     # host post-vote events (include/subread_events.h)
     "svg_event_params_default", "svg_genome_arrays_open", "svg_genome_arrays_close", "svg_events_create",
     "svg_events_destroy", "svg_events_add_batch", "svg_events_merge", "svg_events_count", "svg_events_get",
-    "svg_events_anti_support",
+    "svg_events_anti_support", "svg_events_add_batch2",
 ]
 
 _lib = None
@@ -99,6 +101,11 @@ def lib():
         L.svg_probe_keys_device.restype = i32
         L.svg_last_error.restype = ctypes.c_char_p
         L.svg_host_threads.restype = i32
+        L.svg_fragile_batch.argtypes = [vp] * 5
+        L.svg_fragile_batch.restype = i32
+        L.svg_fragile_free.argtypes = [vp]
+        L.svg_events_add_batch2.argtypes = [vp] * 8 + [u64] + [vp] * 4
+        L.svg_events_add_batch2.restype = i32
         L.svg_index_build.argtypes = [ctypes.c_char_p, i32, i32, i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
         L.svg_index_build.restype = i32
         L.svg_index_build_mem.argtypes = [vp, vp, vp, ctypes.c_uint32, i32, i32, i32, i32, i32, ctypes.c_char_p,
@@ -186,19 +193,35 @@ class EventTable:
         _check(lib().svg_events_create(ctypes.byref(h)), "svg_events_create")
         self.h = h
 
-    def add_batch(self, genome, params, r1, r2, records, first_read=0, event_params=None):
+    def add_batch(self, genome, params, r1, r2, records, first_read=0, event_params=None, quals=None, fragile=None):
         """records = (mapping, subjunc|None, big_margin|None) as VoteIndex.vote returns them;
-        mapping's result_flags gain CORE_IS_GAPPED_READ (64) where the reference sets it."""
+        mapping's result_flags gain CORE_IS_GAPPED_READ (64) where the reference sets it.
+        quals = (q1, q2|None) ReadBatches of quality strings; fragile = (windows, slots) of
+        VoteIndex.fragile (subjunc reads > 160 bp): svg_events_add_batch2."""
         out, jout, bm = records
         s1 = r1.struct()
         s2 = r2.struct() if r2 is not None else None
-        rc = lib().svg_events_add_batch(self.h, genome.h, ctypes.byref(params),
-                                        ctypes.byref(event_params) if event_params is not None else None,
-                                        ctypes.byref(s1), ctypes.byref(s2) if s2 is not None else None,
-                                        int(first_read), out.ctypes.data,
-                                        jout.ctypes.data if jout is not None else None,
-                                        bm.ctypes.data if bm is not None else None)
-        _check(rc, "svg_events_add_batch")
+        ep = ctypes.byref(event_params) if event_params is not None else None
+        if quals is None and fragile is None:
+            rc = lib().svg_events_add_batch(self.h, genome.h, ctypes.byref(params), ep,
+                                            ctypes.byref(s1), ctypes.byref(s2) if s2 is not None else None,
+                                            int(first_read), out.ctypes.data,
+                                            jout.ctypes.data if jout is not None else None,
+                                            bm.ctypes.data if bm is not None else None)
+            _check(rc, "svg_events_add_batch")
+            return
+        q1 = quals[0].struct() if quals is not None else None
+        q2 = quals[1].struct() if quals is not None and quals[1] is not None else None
+        fr = SvgFragileResult.from_arrays(*fragile) if fragile is not None else None
+        rc = lib().svg_events_add_batch2(self.h, genome.h, ctypes.byref(params), ep,
+                                         ctypes.byref(s1), ctypes.byref(s2) if s2 is not None else None,
+                                         ctypes.byref(q1) if q1 is not None else None,
+                                         ctypes.byref(q2) if q2 is not None else None,
+                                         int(first_read), out.ctypes.data,
+                                         jout.ctypes.data if jout is not None else None,
+                                         bm.ctypes.data if bm is not None else None,
+                                         ctypes.byref(fr) if fr is not None else None)
+        _check(rc, "svg_events_add_batch2")
 
     @classmethod
     def merge(cls, tables):
@@ -233,11 +256,11 @@ class EventTable:
             pass
 
 
-def find_events(genome, params, r1, r2, records, first_read=0, anti_support=True):
+def find_events(genome, params, r1, r2, records, first_read=0, anti_support=True, quals=None, fragile=None):
     """Events of one batch, merged and sorted like the reference's table after the voting step,
     with the anti-supporting read counts of the scan that follows it."""
     t = EventTable()
-    t.add_batch(genome, params, r1, r2, records, first_read)
+    t.add_batch(genome, params, r1, r2, records, first_read, quals=quals, fragile=fragile)
     m = EventTable.merge([t])
     if anti_support:
         m.anti_support(params, len(r1), 2 if r2 is not None else 1, records[0])
@@ -345,6 +368,20 @@ class VoteIndex:
         _check(lib().svg_probe_keys(self.h, int(block), keys.ctypes.data, len(keys), first.ctypes.data,
                                     count.ctypes.data), "svg_probe_keys")
         return first, count
+
+    def fragile(self, params, r1, r2=None):
+        """svg_fragile_batch: the fragile junction voting windows of the batch's subjunc reads
+        > 160 bp -> (windows, slots) numpy arrays."""
+        s1 = r1.struct()
+        s2 = r2.struct() if r2 is not None else None
+        res = SvgFragileResult()
+        rc = lib().svg_fragile_batch(self.h, ctypes.byref(params), ctypes.byref(s1),
+                                     ctypes.byref(s2) if s2 is not None else None, ctypes.byref(res))
+        _check(rc, "svg_fragile_batch")
+        try:
+            return res.arrays()
+        finally:
+            lib().svg_fragile_free(ctypes.byref(res))
 
     def set_max_read_length(self, n):
         _check(lib().svg_set_max_read_length(self.h, int(n)), "svg_set_max_read_length")

@@ -57,7 +57,8 @@ EVENT_INDEL, EVENT_JUNCTION, EVENT_FUSION = 8, 64, 128
 class SvgEventParams(ctypes.Structure):
     _fields_ = [("dp_penalty_create_gap", ctypes.c_int32), ("dp_penalty_extend_gap", ctypes.c_int32),
                 ("dp_match_score", ctypes.c_int32), ("dp_mismatch_penalty", ctypes.c_int32),
-                ("report_multi_mapping_reads", ctypes.c_int32)]
+                ("report_multi_mapping_reads", ctypes.c_int32), ("quality_base", ctypes.c_int32),
+                ("maximise_sensitivity_indel", ctypes.c_int32)]
 
 
 SUBJUNC_DTYPE = np.dtype([
@@ -124,6 +125,39 @@ class SvgIndexInfo(ctypes.Structure):
         ("array_values_bytes", ctypes.c_uint32),
         ("n_blocks", ctypes.c_int32),
     ]
+
+
+# svg_fragile_window / svg_fragile_slot (include/subread_vote.h): fragile junction voting windows
+FRAGILE_WINDOW_DTYPE = np.dtype([
+    ("read", "<u4"), ("block", "u1"), ("strand", "u1"), ("end", "u1"), ("window", "u1"),
+    ("start", "<u2"), ("length", "<u2"), ("junction", "u1"), ("gtag", "u1"), ("n_slots", "<u2"),
+    ("small_side", "<u4"), ("large_side", "<u4"), ("first_slot", "<u4")])
+FRAGILE_SLOT_DTYPE = np.dtype([("position", "<u4"), ("rec", "<i2", (9,)), ("_pad", "<u2")])
+assert FRAGILE_WINDOW_DTYPE.itemsize == 28 and FRAGILE_SLOT_DTYPE.itemsize == 24
+
+
+class SvgFragileResult(ctypes.Structure):
+    _fields_ = [("n_windows", ctypes.c_uint64), ("n_slots", ctypes.c_uint64),
+                ("windows", ctypes.c_void_p), ("slots", ctypes.c_void_p)]
+
+    def arrays(self):
+        """Copies of the windows and slots as numpy structured arrays."""
+        w = np.zeros(self.n_windows, dtype=FRAGILE_WINDOW_DTYPE)
+        sl = np.zeros(self.n_slots, dtype=FRAGILE_SLOT_DTYPE)
+        if self.n_windows:
+            ctypes.memmove(w.ctypes.data, self.windows, w.nbytes)
+        if self.n_slots:
+            ctypes.memmove(sl.ctypes.data, self.slots, sl.nbytes)
+        return w, sl
+
+    @classmethod
+    def from_arrays(cls, w, sl):
+        """A result struct over numpy arrays (keep them alive while it is used)."""
+        r = cls()
+        r.n_windows, r.n_slots = len(w), len(sl)
+        r.windows = w.ctypes.data if len(w) else None
+        r.slots = sl.ctypes.data if len(sl) else None
+        return r
 
 
 class SvgBatchStats(ctypes.Structure):

@@ -35,6 +35,8 @@ void svg_event_params_default(svg_event_params *e)
 	e->dp_match_score = 2;
 	e->dp_mismatch_penalty = 0;
 	e->report_multi_mapping_reads = 0;
+	e->quality_base = '#';
+	e->maximise_sensitivity_indel = 0;
 }
 
 /* ------------------------------------------------------------------ base arrays */
@@ -49,6 +51,7 @@ struct svg_genome_arrays {
 	uint32_t n_chr;
 	uint32_t *chr_end;
 	int padding;
+	int gap;               /* index_gap of the first table (1 full, 3 gapped): GENE_SLIDING_STEP */
 };
 
 void svg_genome_arrays_close(svg_genome_arrays *g)
@@ -94,7 +97,8 @@ int svg_genome_arrays_open(const char *prefix, svg_genome_arrays **out)
 		fclose(fp);
 		g->nblocks = b + 1;
 	}
-	/* the padding option of the first table (gehash_load_option, 0x0102) */
+	/* the padding and gap options of the first table (gehash_load_option, 0x0102 / 0x0101) */
+	g->gap = 1;
 	snprintf(fn, sizeof fn, "%s.00.b.tab", prefix);
 	if ((fp = fopen(fn, "rb"))) {
 		char magic[8];
@@ -102,7 +106,12 @@ int svg_genome_arrays_open(const char *prefix, svg_genome_arrays **out)
 			for (;;) {
 				int16_t k, l, v;
 				if (fread(&k, 2, 1, fp) != 1 || !k || fread(&l, 2, 1, fp) != 1) break;
-				if (k == 0x0102) { if (fread(&v, 2, 1, fp) == 1) g->padding = v; break; }
+				if (k == 0x0102 || k == 0x0101) {
+					if (fread(&v, 2, 1, fp) != 1) break;
+					if (k == 0x0102) g->padding = v; else g->gap = v;
+					if (l > 2 && fseek(fp, l - 2, SEEK_CUR)) break;
+					continue;
+				}
 				if (fseek(fp, l, SEEK_CUR)) break;
 			}
 		fclose(fp);
@@ -130,6 +139,115 @@ static inline char gv_get(const garray *a, uint32_t pos)
 	uint32_t byte = (pos - a->start_base_offset) >> 2;
 	if (byte >= a->values_bytes - 1) return 'N';
 	return "AGCT"[(a->values[byte] >> (pos % 4 * 2)) & 3];
+}
+
+/* gvindex_get_string(buf, a, pos, 2, neg), gene-value-index.c:1118-1136 */
+static void chro_2base(const garray *a, uint32_t pos, int neg, char h[2])
+{
+	int i;
+	if (!neg) { h[0] = gv_get(a, pos); h[1] = gv_get(a, pos + 1); return; }
+	for (i = 1; i >= 0; i--) {
+		char c = gv_get(a, pos + 1 - (uint32_t)i);
+		h[i] = c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'G' ? 'C' : c == 'C' ? 'G' : c;
+	}
+}
+
+/* match_chro, gene-value-index.c:856-959 (base space, positive strand) */
+static int match_chro(const char *read, const garray *a, uint32_t pos, int len)
+{
+	int ret = 0, i;
+	uint32_t byte, bit;
+	int8_t iv;
+	if ((uint32_t)(pos + (uint32_t)len) >= a->length + a->start_point) return 0;
+	if (pos > 0xffff0000u) return 0;
+	byte = (pos - a->start_base_offset) >> 2;
+	bit = pos % 4 * 2;
+	if (byte >= a->values_bytes) return 0;
+	iv = (int8_t)a->values[byte];
+	for (i = 0; i < len; i++) {
+		const int tt = (iv >> bit) & 3;
+		switch (read[i]) {
+		case 'A': ret += tt == 0; break;
+		case 'G': ret += tt == 1; break;
+		case 'C': ret += tt == 2; break;
+		case 0: break;
+		default: ret += tt == 3;
+		}
+		bit += 2;
+		if (bit == 8) {
+			byte++;
+			if (byte == a->values_bytes) return 0;
+			iv = (int8_t)a->values[byte];
+			bit = 0;
+		}
+	}
+	return ret;
+}
+
+/* match_chro_maxerror(read, a, pos, len, 0, base space, max_error 0), gene-value-index.c:1036-1088 */
+static int match_exact(const char *read, const garray *a, uint32_t pos, int len)
+{
+	int i;
+	for (i = 0; i < len; i++)
+		if (read[i] != gv_get(a, pos + (uint32_t)i)) return 0;
+	return len;
+}
+
+static inline int b2i(char c) { return c < 'G' ? (c == 'A' ? 0 : 2) : (c == 'G' ? 1 : 3); }
+
+/* match_chro_range, gene-value-index.c:982-1034: the nearest 8-base exact hit of read[j..j+7]
+ * (j < 4) at a byte-aligned 16-bit word of the array, searched byte by byte from pos (backwards
+ * or forwards), confirmed over read_len bases; 0xffffffff when none.  The reference reads out of
+ * the array for a search that starts within 500 bytes of its head (an unsigned underflow in the
+ * clamp); here the search stops at the array's head instead. */
+static uint32_t match_chro_range(const char *read, const garray *a, uint32_t pos, int read_len, uint32_t search_length, int back)
+{
+	int16_t key[4];
+	int i, j;
+	uint32_t offset_byte = (pos - a->start_base_offset) >> 2, dist = search_length / 4;
+	for (i = 0; i < 4; i++) {
+		int k = 0;
+		for (j = i + 7; j >= i; j--) k = (k << 2) | b2i(read[j]);
+		key[i] = (int16_t)k;
+	}
+	if (back) { if (dist > offset_byte - 500u) dist = offset_byte - 500u; }
+	else if (dist + offset_byte >= a->values_bytes - 500u) dist = a->values_bytes - offset_byte - 501u;
+	for (i = 2; (uint32_t)i < dist; i++) {
+		uint64_t t = back ? (uint64_t)offset_byte - (uint64_t)i : (uint64_t)offset_byte + (uint64_t)i;
+		int16_t tv;
+		if (t + 1 >= (uint64_t)a->values_bytes + 8) break;   /* (see above) */
+		tv = (int16_t)(a->values[t] | (a->values[t + 1] << 8));
+		for (j = 0; j < 4; j++)
+			if (tv == key[j]) {
+				uint32_t hit = (uint32_t)t * 4u + a->start_base_offset - (uint32_t)j;
+				if (match_exact(read, a, hit, read_len) > 0) return hit;
+			}
+	}
+	return 0xffffffffu;
+}
+
+#define CEQ(c, t) ((c)[0] == (t)[0] && (c)[1] == (t)[1])
+#define C2EQ(x, y, u, v) ((CEQ(x, u) && CEQ(y, v)) || (CEQ(x, v) && CEQ(y, u)))
+#define DONOR_PART(c) (CEQ(c, "GT") || CEQ(c, "AG") || CEQ(c, "AC") || CEQ(c, "CT"))
+/* paired_chars_part, core-junction.c:4366-4374 */
+static int paired_part(const char *x, const char *y, int rev)
+{
+	if (C2EQ(x, y, "GT", "AG") || C2EQ(x, y, "CT", "AC")) {
+		if (rev && (CEQ(x, "AG") || CEQ(x, "AC"))) return 1;
+		if (!rev && (CEQ(x, "CT") || CEQ(x, "GT"))) return 1;
+	}
+	return 0;
+}
+
+/* read_quality_score, gene-algorithms.c:130-152 */
+static float quality_score(const char *q, int rl, int base)
+{
+	int i, qual = 0, n = 0;
+	for (i = 0; i < rl; i++) {
+		const int v = q[i] - base;
+		if (v > 1) { qual += v; n++; }
+	}
+	return (float)(qual * 1. / n);
 }
 
 /* locate_current_value_index, core.c:2216-2249: the block holding the record, else the block
@@ -468,6 +586,208 @@ static void find_indels(svg_events *t, scratch_t *s, const garray *a, const svg_
 	}
 }
 
+/* a junction event at (small, large): another read for an existing one (any event type of the
+ * search) or a new junction (core-junction.c:4522-4566, 5372-5414) */
+static void add_junction_event(svg_events *t, uint32_t small, uint32_t large, int gtag)
+{
+	uint64_t ids[EV_PER_SITE], id;
+	int k, n = search_small(t, small, SVG_EVENT_JUNCTION | SVG_EVENT_FUSION, ids);
+	svg_event *e;
+	for (k = 0; k < n; k++)
+		if (t->ev[ids[k]].large_side == large) { t->ev[ids[k]].supporting_reads++; return; }
+	id = new_event(t);
+	e = &t->ev[id];
+	e->small_side = small;
+	e->large_side = large;
+	e->is_negative_strand = (int8_t)!gtag;
+	e->event_type = SVG_EVENT_JUNCTION;
+	e->supporting_reads = 1;
+	put_event(t, id);
+}
+
+/*
+ * The events of one fragile-voting window (core_fragile_junction_voting, core-junction.c:5211-5419):
+ * every reported top-vote slot's recorder sections go through core_dynamic_align on the window
+ * text (in, wl bases, NUL-terminated) and its movement walk; then the window's junction.
+ */
+static void fragile_window_events(svg_events *t, scratch_t *s, const garray *a, const svg_params *p,
+                                  const svg_event_params *ep, int gap, const svg_fragile_window *W,
+                                  const svg_fragile_slot *slots, const char *in)
+{
+	const int wl = W->length;
+	uint32_t q;
+	for (q = 0; q < W->n_slots; q++) {
+		const svg_fragile_slot *S = &slots[W->first_slot + q];
+		const int16_t *rec = S->rec;
+		int kk, last_correct_subread = 0;
+		for (kk = 0; kk < MAX_INDEL_SECT && rec[kk]; kk += 3) {
+			const int indels = rec[kk + 2];   /* last_indel stays 0 in the reference's loop */
+			int last_cb, first_cb, steps, x, total_mm = 0, last_mv = 0, in_indel = 0, cur_len = 0, cursor_read;
+			int64_t last_event_id = -1;
+			uint32_t chr, left_boundary = 0;
+			if (!indels) continue;
+			last_cb = subread_end(wl, p->total_subreads, last_correct_subread) - 9;
+			first_cb = subread_end(wl, p->total_subreads, rec[kk] - 1) - 16 + 9;
+			first_cb = first_cb + 10 < wl ? first_cb + 10 : wl;
+			last_cb = last_cb > 0 ? last_cb : 0;
+			last_cb = last_cb < wl - 1 ? last_cb : wl - 1;
+			steps = dynamic_align(s, a, ep, p->max_indel_length, in + last_cb, first_cb - last_cb, S->position + (uint32_t)last_cb,
+			                      indels);
+			chr = S->position + (uint32_t)last_cb;
+			cursor_read = last_cb;
+			for (x = 0; x < steps; x++) total_mm += s->mv[x] == 3;
+			if (total_mm < 2 || (ep->maximise_sensitivity_indel && total_mm <= 2))
+				for (x = 0; x < steps; x++) {
+					const int mv = s->mv[x];
+					if (last_mv != mv) {
+						if ((mv == 1 || mv == 2) && !in_indel) {
+							left_boundary = chr;
+							in_indel = 1;
+							cur_len = 0;
+						} else if (in_indel && (mv == 0 || mv == 3)) {
+							/* (the ambiguity count the reference computes here is not used) */
+							if (abs(cur_len) <= p->max_indel_length) {
+								int64_t nid = add_indel_event(t, in + cursor_read + (cur_len < 0 ? cur_len : 0), left_boundary - 1,
+								                              cur_len, NULL);
+								if (last_event_id >= 0 && nid >= 0) {
+									svg_event *last = &t->ev[last_event_id], *cur = &t->ev[nid];
+									const int dist = (int)(cur->small_side - last->large_side + 1);
+									cur->connected_previous_event_distance = (int8_t)dist;
+									last->connected_next_event_distance = (int8_t)dist;
+								}
+								last_event_id = nid;
+							}
+						}
+						if (mv == 0 || mv == 3) in_indel = 0;
+					}
+					if (in_indel && mv == 1) cur_len++;
+					if (in_indel && mv == 2) cur_len--;
+					if (mv == 1 || mv == 3 || mv == 0) chr++;
+					if (mv == 2 || mv == 3 || mv == 0) cursor_read++;
+					last_mv = mv;
+				}
+			/* the reference reads indel_recorder[i + 1] with the voting loop's i (== gap) here */
+			last_correct_subread = rec[gap + 1] - 1;
+		}
+	}
+	if (W->junction) add_junction_event(t, W->small_side, W->large_side, W->gtag);
+}
+
+#define SE_MIN 18        /* SHORT_EXON_MIN_LENGTH, core-junction.c:4381 */
+#define SE_WINDOW 6      /* SHORT_EXON_WINDOW */
+#define SE_EXTEND 5000u  /* SHORT_EXON_EXTEND */
+
+/* core_search_short_exons, core-junction.c:4386-4731 (reads > 160 bp): a short exon before the
+ * head or after the tail of the record's coverage, found by an exact 7-base search within 5 kbp
+ * and a GT..AG / CT..AC donor pair, becomes a junction event */
+static void short_exons(svg_events *t, const garray *a, const svg_event_params *ep, const char *read_text, const char *qual,
+                        int rl, uint32_t p1, uint32_t p2, int cov_start, int cov_end)
+{
+	const char *inb = read_text;
+	const uint32_t pos_small = p1 < p2 ? p1 : p2, pos_big = p1 < p2 ? p2 : p1;
+	uint32_t best_j1 = 0, best_j2 = 0;
+	int need_to_test = 0, max_score, max_gtag = 0;
+	/* the head */
+	if (cov_start > SE_MIN) {
+		int need_check2 = 1;
+		if (qual && qual[0] && quality_score(qual, SE_MIN, ep->quality_base) < 6) need_check2 = 0;
+		if (need_check2 && SE_MIN * 0.6 < match_chro(inb, a, pos_small, SE_MIN)) need_check2 = 0;
+		if (need_check2) {
+			int d, is_indel = 0, tp;
+			for (d = -3; d <= 3; d++)
+				if (match_chro(inb, a, pos_small + (uint32_t)d, SE_MIN) >= SE_MIN * .7) { is_indel = 1; break; }
+			if (!is_indel)
+				for (tp = SE_MIN; tp < cov_start; tp++) {
+					char cc[2];
+					chro_2base(a, pos_small + (uint32_t)tp, 0, cc);
+					if (DONOR_PART(cc)) { need_to_test = 1; break; }
+				}
+		}
+	}
+	max_score = -999;
+	if (need_to_test && pos_small >= SE_MIN) {
+		uint32_t test_end = pos_small - SE_EXTEND, new_pos = pos_small - SE_MIN;
+		if (SE_EXTEND > pos_small) test_end = 0;
+		for (;;) {
+			int sp;
+			new_pos = match_chro_range(inb, a, new_pos, 7, new_pos - test_end, 1);
+			if (new_pos == 0xffffffffu) break;
+			for (sp = SE_MIN; sp < cov_start; sp++) {
+				char cc[2], cc2[2];
+				chro_2base(a, pos_small + (uint32_t)sp - 2, 0, cc);
+				if (!DONOR_PART(cc)) continue;
+				chro_2base(a, new_pos + (uint32_t)sp, 0, cc2);
+				if (DONOR_PART(cc2) && paired_part(cc2, cc, 0)) {
+					const int m_old = match_chro(inb + sp, a, pos_small + (uint32_t)sp, SE_WINDOW);
+					const int m_new = match_chro(inb, a, new_pos, sp);
+					const int score = (int)(1000000u + (uint32_t)(m_new * 10000) + (uint32_t)(m_old * 1000) + new_pos - test_end);
+					if (score <= max_score) continue;
+					max_score = score;
+					if (m_new < sp || m_old < SE_WINDOW) continue;
+					max_gtag = cc2[0] == 'G' || cc2[1] == 'G';
+					best_j1 = new_pos + (uint32_t)sp - 1;
+					best_j2 = pos_small + (uint32_t)sp;
+				}
+			}
+		}
+	}
+	if (best_j1 > 0) add_junction_event(t, best_j1, best_j2, max_gtag);
+	/* the tail */
+	need_to_test = 0;
+	max_score = -999;
+	if (cov_end < rl - SE_MIN) {
+		int need_check2 = 1;
+		if (qual && qual[0] && quality_score(qual + rl - SE_MIN, SE_MIN, ep->quality_base) < 6) need_check2 = 0;
+		if (SE_MIN * 0.6 < match_chro(inb + rl - SE_MIN, a, pos_big + (uint32_t)(rl - SE_MIN), SE_MIN)) need_check2 = 0;
+		if (need_check2) {
+			int d, is_indel = 0, tp;
+			for (d = -3; d <= 3; d++)
+				if (match_chro(inb + rl - SE_MIN, a, pos_big + (uint32_t)(rl - SE_MIN) + (uint32_t)d, SE_MIN) >= SE_MIN * .7) {
+					is_indel = 1;
+					break;
+				}
+			if (!is_indel)
+				for (tp = cov_end; tp < rl; tp++) {
+					char cc[2];
+					chro_2base(a, pos_big + (uint32_t)tp, 0, cc);
+					if (DONOR_PART(cc)) { need_to_test = 1; break; }
+				}
+		}
+	}
+	best_j1 = 0;
+	max_gtag = 0;
+	if (need_to_test) {
+		uint32_t test_end = pos_big + SE_EXTEND, new_pos = pos_big + (uint32_t)rl - SE_MIN + 16;
+		if (test_end > a->length + a->start_point) test_end = a->length + a->start_point;
+		for (;;) {
+			int sp;
+			if (new_pos + test_end - new_pos < a->start_base_offset + a->length)
+				new_pos = match_chro_range(inb + rl - SE_MIN, a, new_pos, 7, test_end - new_pos, 0);
+			else break;
+			if (new_pos == 0xffffffffu) break;
+			for (sp = cov_end; sp < rl - SE_MIN; sp++) {
+				char cc[2], cc2[2];
+				const uint32_t tail = new_pos + SE_MIN - (uint32_t)rl + (uint32_t)sp;
+				chro_2base(a, pos_big + (uint32_t)sp, 0, cc);
+				if (!DONOR_PART(cc)) continue;
+				chro_2base(a, tail - 2, 0, cc2);
+				if (DONOR_PART(cc2) && paired_part(cc, cc2, 0)) {
+					const int m_new = match_chro(inb + sp, a, tail, rl - sp);
+					const int m_old = match_chro(inb + sp - SE_WINDOW, a, pos_big + (uint32_t)sp - SE_WINDOW, SE_WINDOW);
+					const int score = (int)(1000000u + (uint32_t)(m_new * 10000) + (uint32_t)(m_old * 1000) + test_end - new_pos);
+					if (score <= max_score) continue;
+					max_score = score;
+					if (m_new < rl - sp || m_old < SE_WINDOW) continue;
+					max_gtag = cc[0] == 'G' || cc[1] == 'G';
+					best_j1 = pos_big + (uint32_t)sp - 1;
+					best_j2 = tail;
+				}
+			}
+		}
+	}
+	if (best_j1 > 0) add_junction_event(t, best_j1, best_j2, max_gtag);
+}
+
 /* is_ambiguous_voting, core-junction.c:3522-3566 */
 static int ambiguous_voting(const svg_params *p, const uint16_t *bm, int vote, int max_start, int max_end, int rl, int neg)
 {
@@ -599,15 +919,62 @@ static int has_better_mapping(const svg_params *p, const svg_mapping_result *rec
 	return 0;
 }
 
-int svg_events_add_batch(svg_events *t, const svg_genome_arrays *g, const svg_params *p, const svg_event_params *ep_in,
-                         const svg_reads *r1, const svg_reads *r2, uint64_t first_read, svg_mapping_result *out,
-                         const svg_subjunc_result *jout, const uint16_t *big_margin)
+static void reverse_chars(char *s, int len)
+{
+	int i;
+	for (i = 0; i < len / 2; i++) { char x = s[i]; s[i] = s[len - 1 - i]; s[len - 1 - i] = x; }
+}
+
+/* the strand-s text of an end as do_voting sees it (-S reversal at fetch, then reverse_read for
+ * strand 1), NUL-terminated */
+static int strand_text(const svg_params *p, const svg_reads *rr, int e, uint64_t i, int strand, char *text)
+{
+	int rl = rr->lens[i];
+	if (rl > SVG_READ_KEEP) rl = SVG_READ_KEEP;
+	memcpy(text, rr->seq + rr->offsets[i], (size_t)rl);
+	text[rl] = 0;
+	if (e ? p->reverse_r2 : p->reverse_r1) reverse_read(text, rl);
+	if (strand) reverse_read(text, rl);
+	return rl;
+}
+
+/* the events of every window [*w, ...) of block `blk` and read `read` (or of every read when
+ * read == UINT64_MAX), in the windows' order */
+static void fragile_events(svg_events *t, scratch_t *s, const svg_genome_arrays *g, const svg_params *p,
+                           const svg_event_params *ep, const svg_reads *r1, const svg_reads *r2, const svg_fragile_result *fr,
+                           uint64_t *w, int blk, uint64_t read)
+{
+	char text[SVG_MAX_READ_LENGTH + 2];
+	uint64_t cur = UINT64_MAX;
+	int cur_key = -1;
+	while (*w < fr->n_windows) {
+		const svg_fragile_window *W = &fr->windows[*w];
+		const int key = W->strand * 2 + W->end;
+		char in[SVG_MAX_READ_LENGTH + 2];
+		if (W->block != blk || (read != UINT64_MAX && W->read != read)) break;
+		if (W->read != cur || key != cur_key) {
+			strand_text(p, W->end ? r2 : r1, W->end, W->read, W->strand, text);
+			cur = W->read;
+			cur_key = key;
+		}
+		memcpy(in, text + W->start, W->length);
+		in[W->length] = 0;
+		fragile_window_events(t, s, &g->blk[blk], p, ep, g->gap, W, fr->slots, in);
+		(*w)++;
+	}
+}
+
+int svg_events_add_batch2(svg_events *t, const svg_genome_arrays *g, const svg_params *p, const svg_event_params *ep_in,
+                          const svg_reads *r1, const svg_reads *r2, const svg_reads *q1, const svg_reads *q2,
+                          uint64_t first_read, svg_mapping_result *out, const svg_subjunc_result *jout,
+                          const uint16_t *big_margin, const svg_fragile_result *fr)
 {
 	const int ends = r2 ? 2 : 1, mb = p ? p->multi_best : 0;
 	svg_event_params epd;
 	const svg_event_params *ep = ep_in;
 	scratch_t *s;
-	uint64_t i;
+	uint64_t i, w = 0;
+	int long_reads = 0;
 	if (!t || !g || !p || !r1 || !out) { svg_set_error("svg_events_add_batch: NULL argument"); return SVG_E_ARG; }
 	if (r2 && r2->n_reads != r1->n_reads) { svg_set_error("svg_events_add_batch: r1/r2 differ in length"); return SVG_E_ARG; }
 	if (mb < 1 || mb > 3 || p->total_subreads < 2) { svg_set_error("svg_events_add_batch: bad parameters"); return SVG_E_ARG; }
@@ -617,31 +984,51 @@ int svg_events_add_batch(svg_events *t, const svg_genome_arrays *g, const svg_pa
 	}
 	if (!ep) { svg_event_params_default(&epd); ep = &epd; }
 	if (p->do_breakpoint_detection)
-		for (i = 0; i < r1->n_reads; i++)
-			if (r1->lens[i] > LONG_READ || (r2 && r2->lens[i] > LONG_READ)) {
-				svg_set_error("events of subjunc reads over %d bp (short-exon search, fragile junction voting) "
-				              "are not implemented", LONG_READ);
-				return SVG_E_UNSUPPORTED;
+		for (i = 0; i < r1->n_reads && !long_reads; i++)
+			if (r1->lens[i] > LONG_READ || (r2 && r2->lens[i] > LONG_READ)) long_reads = 1;
+	if (long_reads && !fr) {
+		svg_set_error("subjunc reads over %d bp need their fragile junction votes (svg_fragile_batch, svg_events_add_batch2)",
+		              LONG_READ);
+		return SVG_E_UNSUPPORTED;
+	}
+	if (fr) {
+		for (i = 0; i < fr->n_windows; i++)
+			if (fr->windows[i].block >= g->nblocks || fr->windows[i].read >= r1->n_reads ||
+			    (fr->windows[i].end && !r2) || fr->windows[i].first_slot + fr->windows[i].n_slots > fr->n_slots) {
+				svg_set_error("svg_events_add_batch2: fragile windows do not match the batch / index");
+				return SVG_E_ARG;
 			}
+	}
 	s = calloc(1, sizeof *s);
 	s->cols = SVG_MAX_READ_LENGTH;
 	s->rows = SVG_MAX_READ_LENGTH + 20;
 	s->dp = malloc(sizeof(int16_t) * (size_t)s->rows * s->cols);
 	s->mask = malloc((size_t)s->rows * s->cols);
 	if (!s->dp || !s->mask) { free(s->dp); free(s->mask); free(s); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	/* the earlier runs of the block loop: every read's fragile windows, block by block */
+	if (fr)
+		for (int b = 0; b + 1 < g->nblocks; b++) fragile_events(t, s, g, p, ep, r1, r2, fr, &w, b, UINT64_MAX);
 	for (i = 0; i < r1->n_reads; i++) {
 		int e;
+		/* the final run: this read's windows of the last block, then its tail (core.c:3240-3290) */
+		if (fr) fragile_events(t, s, g, p, ep, r1, r2, fr, &w, g->nblocks - 1, i);
 		for (e = 0; e < ends; e++) {
-			const svg_reads *rr = e ? r2 : r1;
-			char text[SVG_MAX_READ_LENGTH + 2];
+			const svg_reads *rr = e ? r2 : r1, *qq = e ? q2 : q1;
+			char text[SVG_MAX_READ_LENGTH + 2], qual[SVG_MAX_READ_LENGTH + 2];
 			int rl = rr->lens[i], b, has_reversed;
 			svg_mapping_result *recs = out + ((size_t)i * ends + e) * mb;
 			if (rl > SVG_READ_KEEP) rl = SVG_READ_KEEP;
 			memcpy(text, rr->seq + rr->offsets[i], (size_t)rl);
 			text[rl] = 0;
-			/* -S reversal at fetch (core.c:1186-1198), then the strand loop's one reversal after
-			 * strand 0 (core.c:3229-3234): the text is in the reversed state afterwards */
-			if (e ? p->reverse_r2 : p->reverse_r1) reverse_read(text, rl);
+			qual[0] = 0;
+			if (qq) {
+				memcpy(qual, qq->seq + qq->offsets[i], (size_t)rl);
+				qual[rl] = 0;
+			}
+			/* -S reversal at fetch (core.c:1186-1198: text and quality), then the strand loop's one
+			 * reversal of the text after strand 0 (core.c:3229-3234); the tail reverses text and
+			 * quality together, so they stay in opposite orientations */
+			if (e ? p->reverse_r2 : p->reverse_r1) { reverse_read(text, rl); if (qq) reverse_chars(qual, rl); }
 			reverse_read(text, rl);
 			has_reversed = 1;
 			for (b = 0; b < mb; b++) {
@@ -650,18 +1037,34 @@ int svg_events_add_batch(svg_events *t, const svg_genome_arrays *g, const svg_pa
 				int should;
 				if (r->selected_votes < 1) continue;
 				should = (r->result_flags & NEG_FLAG) ? 1 : 0;
-				if (should != has_reversed) { has_reversed = !has_reversed; reverse_read(text, rl); }
+				if (should != has_reversed) {
+					has_reversed = !has_reversed;
+					reverse_read(text, rl);
+					if (qq) reverse_chars(qual, rl);
+				}
 				a = value_index(g, r->selected_position, rl);
 				if (!has_better_mapping(p, recs, b)) find_indels(t, s, a, p, ep, r, text, rl);
-				if (p->do_breakpoint_detection)
-					find_junctions(t, g, p, r, &jout[((size_t)i * ends + e) * mb + b],
-					               big_margin ? big_margin + ((size_t)i * ends + e) * SVG_BIG_MARGIN_WORDS : NULL, rl,
-					               first_read + i, e);
+				if (p->do_breakpoint_detection) {
+					const svg_subjunc_result *j = &jout[((size_t)i * ends + e) * mb + b];
+					if (rl > LONG_READ)
+						short_exons(t, a, ep, text, qq ? qual : "", rl, r->selected_position,
+						            j->minor_votes < 1 ? r->selected_position : j->minor_position, r->confident_coverage_start,
+						            r->confident_coverage_end);
+					find_junctions(t, g, p, r, j, big_margin ? big_margin + ((size_t)i * ends + e) * SVG_BIG_MARGIN_WORDS : NULL,
+					               rl, first_read + i, e);
+				}
 			}
 		}
 	}
 	free(s->dp); free(s->mask); free(s);
 	return 0;
+}
+
+int svg_events_add_batch(svg_events *t, const svg_genome_arrays *g, const svg_params *p, const svg_event_params *ep,
+                         const svg_reads *r1, const svg_reads *r2, uint64_t first_read, svg_mapping_result *out,
+                         const svg_subjunc_result *jout, const uint16_t *big_margin)
+{
+	return svg_events_add_batch2(t, g, p, ep, r1, r2, NULL, NULL, first_read, out, jout, big_margin, NULL);
 }
 
 /* ------------------------------------------------------------------ merge (finalise) */

@@ -95,9 +95,8 @@ def run_ref_events(prog, prefix, f1, f2, path, extra=()):
 
 def save_events(name, prog, idx_prefix, r1, r2, over, tmp):
     """tests/golden/events/<case>.npz: the reference's events + raw record flags for the case's
-    reads (subjunc cases with reads over 160 bp are outside the event search's scope)."""
-    if prog == PROGRAM_SUBJUNC and (r1.lens.max() > 160 or (r2 is not None and r2.lens.max() > 160)):
-        return
+    reads (for subjunc reads over 160 bp these include the fragile junction voting's and the
+    short-exon search's events)."""
     extra = []
     if "total_subreads" in over:
         extra += ["-n", str(over["total_subreads"])]
@@ -330,6 +329,11 @@ def main():
         sj_lp2 = simulate_spliced_reads(long777, 1500, 150, seed=26, max_intron=20000)
         cases.append(("sj_pe_mb_long_gappedM6", PROGRAM_SUBJUNC, True, "long777_gappedM6", {}, sj_lp1, sj_lp2,
                       "long777 spliced reads seeds 25/26 (150 bp) on the 4-block -M 6 index"))
+        # subjunc long reads on a 4-block index: fragile junction voting in every block's run
+        sj_mbl = [simulate_spliced_reads(synth, 300, L, seed=27 + L, max_intron=20000) for L in (200, 300)]
+        cases.append(("sj_se_mb_synth_long_fullM1", PROGRAM_SUBJUNC, False, "synth4242_fullM1", {},
+                      ReadBatch.from_list([b.read(i) for b in sj_mbl for i in range(len(b))]), None,
+                      "synth4242 spliced reads 200/300 bp, seeds 227/327, on the 4-block -F -M 1 index"))
         only = set(a for a in sys.argv[1:] if not a.startswith("--"))
         if only:
             cases = [c for c in cases if c[0] in only]

@@ -18,7 +18,7 @@ def header_symbols():
     for h in ("subread_vote.h", "subread_events.h"):
         txt = open(os.path.join(ROOT, "include", h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-        syms |= set(re.findall(r"\b(svg_[a-z_]+)\s*\(", txt))
+        syms |= set(re.findall(r"\b(svg_[a-z0-9_]+)\s*\(", txt))
     return sorted(syms)
 
 

@@ -51,6 +51,24 @@ def describe(got, want, limit=4):
                      ["  ours %s\n  ref  %s" % (got[i], want[i]) for i in bad[:limit]])
 
 
+def long_subjunc(c):
+    return bool(c.params.do_breakpoint_detection) and (
+        c.r1.lens.max() > 160 or (c.r2 is not None and c.r2.lens.max() > 160))
+
+
+def quals_of(batch):
+    """the fixtures' FASTQ qualities (tests/golden/make_golden.py writes 'I' for every base)"""
+    from subread_amd.abi import ReadBatch
+    return ReadBatch(np.full(batch.seq.size, ord("I"), np.uint8), batch.offsets, batch.lens)
+
+
+def extras(c, windows):
+    """quals / fragile arguments of find_events for a case (None for the short-read cases)"""
+    if not long_subjunc(c):
+        return {}
+    return dict(quals=(quals_of(c.r1), quals_of(c.r2) if c.r2 is not None else None), fragile=windows)
+
+
 def check(got, flags, want, wflags):
     assert len(got) == len(want) and (got.view(np.uint8) == want.view(np.uint8)).all(), describe(got, want)
     assert (flags == wflags).all(), "%d records' flags differ" % int((flags != wflags).sum())
@@ -58,12 +76,18 @@ def check(got, flags, want, wflags):
 
 @pytest.mark.parametrize("name", EVENT_CASES)
 def test_events_match_reference(name, index_cache):
+    """The reference's records -> our event stage; for subjunc reads > 160 bp the fragile
+    junction voting windows come from the CPU restatement (the GPU's are checked against it in
+    tests/test_gpu_fragile.py)."""
     import subread_amd as sa
+    from oracle.pyoracle import OracleIndex
     c = Case(name)
     want, wflags = load_events(name)
-    g = sa.GenomeArrays(index_cache.get(c.index_key))
+    pre = index_cache.get(c.index_key)
+    g = sa.GenomeArrays(pre)
     recs = split_records(c)
-    got = sa.find_events(g, c.params, c.r1, c.r2, recs)
+    windows = OracleIndex(pre).fragile(c.params, c.r1, c.r2) if long_subjunc(c) else None
+    got = sa.find_events(g, c.params, c.r1, c.r2, recs, **extras(c, windows))
     check(got, recs[0]["result_flags"].reshape(-1).view(np.uint16), want, wflags)
     g.close()
 
@@ -91,12 +115,14 @@ def test_events_merge_of_shards_equals_one_table(index_cache):
     g.close()
 
 
-def test_events_reject_long_subjunc_reads(index_cache):
+def test_events_need_fragile_windows_for_long_subjunc_reads(index_cache):
+    """svg_events_add_batch (no fragile windows) refuses subjunc reads > 160 bp rather than
+    leaving out the fragile junction voting's events."""
     import subread_amd as sa
-    c = Case("sj_se_full_long")
+    c = Case("sj_pe_gapped_long")
     g = sa.GenomeArrays(index_cache.get(c.index_key))
-    with pytest.raises(sa.SvgError, match="not implemented"):
-        sa.find_events(g, c.params, c.r1, None, split_records(c))
+    with pytest.raises(sa.SvgError, match="fragile junction votes"):
+        sa.find_events(g, c.params, c.r1, c.r2, split_records(c))
     g.close()
 
 
@@ -110,8 +136,9 @@ def test_gpu_records_give_reference_events(name, index_cache):
     pre = index_cache.get(c.index_key)
     ix = sa.VoteIndex(pre, device=0)
     out, jout, bm = ix.vote(c.params, c.r1, c.r2)
+    windows = ix.fragile(c.params, c.r1, c.r2) if long_subjunc(c) else None
     ix.close()
     g = sa.GenomeArrays(pre)
-    got = sa.find_events(g, c.params, c.r1, c.r2, (out, jout, bm))
+    got = sa.find_events(g, c.params, c.r1, c.r2, (out, jout, bm), **extras(c, windows))
     check(got, out["result_flags"].reshape(-1).view(np.uint16), want, wflags)
     g.close()

@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ instruction/stall counters per kernel (three separate --pmc passes, no traces) of the
-# device-resident vote path (tools/prof_run.py: 1 warmup + 1 step).
+# host path bench.py times (tools/prof_run.py ... host: 1 warmup + 1 step).
 # Usage: tools/pmc_sq.sh OUTDIR [WORKLOAD]
 set -e
 out=$1; wl=${2:-c3}
@@ -12,7 +12,7 @@ C="SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_LEVEL_LDS SQ
 i=0
 for set in "$A" "$B" "$C"; do
   i=$((i+1))
-  timeout -s KILL 300 rocprofv3 --pmc $set -d $out/p$i -o run -- python3 tools/prof_run.py $wl 1 > $out/p$i.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc $set -d $out/p$i -o run -- python3 tools/prof_run.py $wl 1 host > $out/p$i.log 2>&1
 done
 python3 - "$out" <<'PY'
 import sqlite3, glob, sys, collections
