@@ -44,6 +44,7 @@ int locate_current_value_index(global_context_t *global_context, thread_context_
                                mapping_result_t *result, int rlen);
 int has_better_mapping(global_context_t *global_context, thread_context_t *thread_context,
                        subread_read_number_t current_read_number, int is_second_read, int this_aln_id);
+int find_subread_end(int len, int TOTAL_SUBREADS, int subread);   /* input-files.c:1371 */
 
 static svg_index *svg_ix;   /* one per process, one process per GPU */
 
@@ -196,6 +197,104 @@ static int vote_chunk(global_context_t *gc, int ends, const svg_chunk_reads *c)
 	return rc;
 }
 
+/*
+ * The events of one fragile-voting window that svg_fragile_batch voted on the GPU: the tail of
+ * core_fragile_junction_voting (core-junction.c:5211-5419) with the reference's own
+ * core_dynamic_align / local_add_indel_event / search_event / put_new_event.  `in` is the
+ * window's text (NUL-terminated), as core_fragile_junction_voting's InBuff.
+ */
+static void fragile_window_events(global_context_t *gc, thread_context_t *tc, const svg_fragile_window *W,
+                                  const svg_fragile_slot *slots, char *in, char *rname)
+{
+	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
+	indel_thread_context_t *itc = tc ? (indel_thread_context_t *)tc->module_thread_contexts[MODULE_INDEL_ID] : NULL;
+	HashTable *event_table = itc ? itc->event_entry_table : ic->event_entry_table;
+	const int gap = gc->current_index->index_gap, read_len = W->length;
+	unsigned q;
+	for (q = 0; q < W->n_slots; q++) {
+		const svg_fragile_slot *S = &slots[W->first_slot + q];
+		int kk, last_indel = 0, last_correct_subread = 0;
+		for (kk = 0; S->rec[kk] && kk < MAX_INDEL_SECTIONS; kk += 3) {
+			char movement_buffer[MAX_READ_LENGTH * 10 / 7];
+			int last_event_id = -1, x1, dyna_steps;
+			int indels = S->rec[kk + 2] - last_indel;
+			if (indels == 0) continue;
+			int next_correct_subread = S->rec[kk] - 1;
+			int last_correct_base = find_subread_end(read_len, gc->config.total_subreads, last_correct_subread) - 9;
+			int first_correct_base = find_subread_end(read_len, gc->config.total_subreads, next_correct_subread) - 16 + 9;
+			first_correct_base = min(first_correct_base + 10, read_len);
+			last_correct_base = max(0, last_correct_base);
+			last_correct_base = min(read_len - 1, last_correct_base);
+			dyna_steps = core_dynamic_align(gc, tc, in + last_correct_base, first_correct_base - last_correct_base,
+			                                S->position + last_correct_base + last_indel, movement_buffer, indels, rname);
+			movement_buffer[dyna_steps] = 0;
+			unsigned int cursor_on_chromosome = S->position + last_correct_base + last_indel, cursor_on_read = last_correct_base;
+			int last_mv = 0, is_in_indel = 0, current_indel_len = 0, total_mismatch = 0;
+			unsigned int indel_left_boundary = 0;
+			for (x1 = 0; x1 < dyna_steps; x1++) if (movement_buffer[x1] == 3) total_mismatch++;
+			if (total_mismatch < 2 || (gc->config.maximise_sensitivity_indel && total_mismatch <= 2))
+				for (x1 = 0; x1 < dyna_steps; x1++) {
+					int mv = movement_buffer[x1];
+					if (last_mv != mv) {
+						if ((mv == 1 || mv == 2) && !is_in_indel) {
+							indel_left_boundary = cursor_on_chromosome;
+							is_in_indel = 1;
+							current_indel_len = 0;
+						} else if (is_in_indel && (mv == 0 || mv == 3)) {
+							/* (the ambiguity count core-junction.c:5283-5292 computes is unused) */
+							if (abs(current_indel_len) <= gc->config.max_indel_length) {
+								chromosome_event_t *new_event = local_add_indel_event(gc, tc, event_table,
+								        in + cursor_on_read + min(0, current_indel_len), indel_left_boundary - 1, current_indel_len, 1, 0, 0, NULL);
+								if (last_event_id >= 0 && new_event) {
+									chromosome_event_t *event_space = itc ? itc->event_space_dynamic : ic->event_space_dynamic;
+									chromosome_event_t *last_event = event_space + last_event_id;
+									int dist = new_event->event_small_side - last_event->event_large_side + 1;
+									new_event->connected_previous_event_distance = dist;
+									last_event->connected_next_event_distance = dist;
+								}
+								last_event_id = new_event ? new_event->global_event_id : -1;
+							}
+						}
+						if (mv == 0 || mv == 3) is_in_indel = 0;
+					}
+					if (is_in_indel && mv == 1) current_indel_len += 1;
+					if (is_in_indel && mv == 2) current_indel_len -= 1;
+					if (mv == 1 || mv == 3 || mv == 0) cursor_on_chromosome++;
+					if (mv == 2 || mv == 3 || mv == 0) cursor_on_read++;
+					last_mv = mv;
+				}
+			/* indel_recorder[i + 1] with the voting loop's i (== GENE_SLIDING_STEP) */
+			last_correct_subread = S->rec[gap + 1] - 1;
+		}
+	}
+	if (W->junction) {
+		chromosome_event_t *search_return[MAX_EVENT_ENTRIES_PER_SITE], *found = NULL;
+		chromosome_event_t *event_space = itc ? itc->event_space_dynamic : ic->event_space_dynamic;
+		int kx1, found_events = search_event(gc, event_table, event_space, W->small_side, EVENT_SEARCH_BY_SMALL_SIDE,
+		                                     CHRO_EVENT_TYPE_JUNCTION | CHRO_EVENT_TYPE_FUSION, search_return);
+		for (kx1 = 0; kx1 < found_events; kx1++)
+			if (search_return[kx1]->event_large_side == W->large_side) { found = search_return[kx1]; break; }
+		if (found) found->supporting_reads++;
+		else {
+			int event_no = itc ? itc->total_events++ : ic->total_events++;
+			event_space = reallocate_event_space(gc, tc, event_no);
+			chromosome_event_t *new_event = event_space + event_no;
+			memset(new_event, 0, sizeof(chromosome_event_t));
+			new_event->event_small_side = W->small_side;
+			new_event->event_large_side = W->large_side;
+			new_event->is_negative_strand = !W->gtag;
+			new_event->event_type = CHRO_EVENT_TYPE_JUNCTION;
+			new_event->supporting_reads = 1;
+			new_event->indel_length = 0;
+			put_new_event(event_table, new_event, event_no);
+		}
+	}
+}
+
+/* svg_fragile_batch's result for the chunk being voted: made in the first block's run, used by
+ * every block's run, freed after the final one */
+static svg_fragile_result svg_frag;
+
 int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
 {
 	int ends = 1 + gc->input_reads.is_paired_end_reads, rc = 0, e, s;
@@ -213,25 +312,42 @@ int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
 	/* a multi-block index: the library votes every block (all resident in HBM) in the first
 	 * block's run of read_chunk_circles (core.c:3567-3613); the later runs re-read the chunk
 	 * for the per-block host work below */
-	if (!rc && c.n && gc->current_index_block_number == 0) rc = vote_chunk(gc, ends, &c);
+	if (!rc && c.n && gc->current_index_block_number == 0) {
+		rc = vote_chunk(gc, ends, &c);
+		/* fragile junction voting of every block, on the GPU (subjunc reads > 160 bp) */
+		svg_fragile_free(&svg_frag);
+		if (!rc && gc->config.do_breakpoint_detection) {
+			svg_params p;
+			svg_fill_params(gc, &p);
+			svg_reads a1 = {c.text[0], c.off[0], c.len[0], c.n}, a2 = {c.text[1], c.off[1], c.len[1], c.n};
+			rc = svg_fragile_batch(svg_ix, &p, &a1, ends == 2 ? &a2 : NULL, &svg_frag);
+			if (rc) SUBREADprintf("svg_fragile_batch: %s\n", svg_last_error());
+		}
+	}
+	/* this block's fragile windows, in (read, strand, end, window) order */
+	uint64_t fw = 0;
+	while (fw < svg_frag.n_windows && svg_frag.windows[fw].block < gc->current_index_block_number) fw++;
 
 	/* 3. do_voting's per-read host work, in its order */
 	char text[MAX_READ_LENGTH + 1], qual[MAX_READ_LENGTH + 1];
 	subread_read_number_t r;
 	for (r = 0; !rc && r < (subread_read_number_t)c.n; r++) {
-		/* core_fragile_junction_voting (core.c:3138-3142): strand 0 on the fetched text, strand 1
-		 * on its reverse_read, R1 then R2; the quality is never reversed inside the strand loop */
-		for (s = 0; gc->config.do_breakpoint_detection && s < 2; s++)
-			for (e = 0; e < ends; e++) {
-				int rl = c.len[e][r];
-				if (rl <= EXON_LONG_READ_LENGTH) continue;
-				memcpy(text, c.text[e] + c.off[e][r], rl);
-				memcpy(qual, c.qual[e] + c.off[e][r], rl);
-				text[rl] = qual[rl] = 0;
-				if (s) reverse_read(text, rl, gc->config.space_type);
-				core_fragile_junction_voting(gc, tc, c.name[0] + r * (MAX_READ_NAME_LEN + 1), text, qual, rl, s,
-				                             gc->config.space_type, low_border, high_border - rl, vote_fg);
-			}
+		/* core_fragile_junction_voting (core.c:3138-3142) of this read: its windows in this block,
+		 * strand 0 on the fetched text, strand 1 on its reverse_read, R1 then R2 -- voted on the
+		 * GPU (svg_fragile_batch), their events made here */
+		while (fw < svg_frag.n_windows && svg_frag.windows[fw].block == gc->current_index_block_number &&
+		       svg_frag.windows[fw].read == (uint32_t)r) {
+			const svg_fragile_window *W = &svg_frag.windows[fw++];
+			char in[MAX_READ_LENGTH + 1];
+			int rl = c.len[W->end][r];
+			memcpy(text, c.text[W->end] + c.off[W->end][r], rl);
+			text[rl] = 0;
+			if (W->strand) reverse_read(text, rl, gc->config.space_type);
+			memcpy(in, text + W->start, W->length);
+			in[W->length] = 0;
+			fragile_window_events(gc, tc, W, svg_frag.slots, in, c.name[0] + r * (MAX_READ_NAME_LEN + 1));
+		}
+		(void)vote_fg; (void)low_border; (void)high_border; (void)s;
 		if (!gc->is_final_voting_run) continue;
 		/* the final-voting-run block (core.c:3240-3290) */
 		for (e = 0; e < ends; e++) {
@@ -266,6 +382,7 @@ int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
 	}
 	chunk_free(&c);
 	free(vote_fg);
+	if (gc->is_final_voting_run) svg_fragile_free(&svg_frag);
 	return rc ? 1 : 0;
 }
 

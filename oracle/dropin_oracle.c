@@ -1,10 +1,10 @@
 /*
  * TEST INFRASTRUCTURE ONLY -- never linked into the product.
  *
- * The three svg_* entry points integration/do_voting_gpu.c calls for the vote itself
- * (svg_index_open, svg_vote_batch_packed, svg_last_error), answered by the CPU restatement
- * (svoracle.c) instead of the GPU.  oracle/Makefile compiles do_voting_gpu.c a second time
- * with those three names mapped to the svo_dropin_* functions below and links it into the
+ * The svg_* entry points integration/do_voting_gpu.c calls for the vote itself
+ * (svg_index_open, svg_vote_batch_packed, svg_fragile_batch, svg_last_error), answered by the
+ * CPU restatement (svoracle.c) instead of the GPU.  oracle/Makefile compiles do_voting_gpu.c a second time
+ * with those names mapped to the svo_dropin_* functions below and links it into the
  * reference's own subread-align / subjunc (`_ref/*-oracle-dropin`).  tests/test_dropin.py
  * runs that binary in this container (no GPU) against the stock reference: it checks the
  * binding's host logic -- chunk reading, bigtable layout, big-margin staging, text/quality
@@ -18,12 +18,22 @@
 #include "subread_vote.h"
 
 typedef struct svo_index svo_index;
+static char err[256];
 svo_index *svo_index_open(const char *prefix);
 int svo_vote_batch(const svo_index *ix, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
                    svg_mapping_result *out, svg_subjunc_result *jout, uint16_t *bm, int threads,
                    uint64_t *stats3);
+int svo_fragile_batch(const svo_index *ix, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                      svg_fragile_result *out);
 
-static char err[256];
+/* the fragile junction voting windows, from the restatement */
+int svo_dropin_fragile_batch(svg_index *idx, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
+                             svg_fragile_result *out)
+{
+	int rc = svo_fragile_batch((const svo_index *)idx, p, r1, r2, out);
+	if (rc) snprintf(err, sizeof err, "oracle fragile voting failed (%d)", rc);
+	return rc;
+}
 
 const char *svo_dropin_last_error(void) { return err; }
 

@@ -336,8 +336,9 @@ __global__ void __launch_bounds__(64) fragile_kernel(FParams fp)
 		auto slot_of = [&](int f) -> int {
 			int row = 0;
 			for (int r = 0; r < F_ROWS - 1; r++) row += f_rd(rs, r) <= f;
-			const int start = row ? __shfl(rs, row - 1) : 0;
-			return row * F_SPACE + (f - start);
+			// every lane takes part in the cross-lane read (an inactive source lane reads as nothing)
+			const int sv = __shfl(rs, row > 0 ? row - 1 : 0);
+			return row * F_SPACE + (f - (row ? sv : 0));
 		};
 		svg_fragile_window W;
 		memset(&W, 0, sizeof W);
