@@ -21,6 +21,7 @@ def cache(tmp_path_factory):
     ("pe_gapped_errmut", 1),            # PE align, test-err-mut pairs
     ("sj_pe_gapped_long", 1),           # subjunc PE > 160 bp: fragile junction voting in the binding
     ("sj_pe_mb_long_gappedM6", 1),      # subjunc PE on a 4-block index (block loop)
+    ("sj_se_mb_synth_long_fullM1", 1),  # subjunc SE > 160 bp on a 4-block index: fragile windows per block
     ("se_gapped_mixed_n14_I16", 4),     # -n 14 -I 16, N / lowercase / IUPAC, -T 4
 ])
 def test_oracle_dropin_matches_stock_reference(name, threads, cache, tmp_path):

@@ -31,12 +31,13 @@ def _need(program):
     ("pe_full_errmut", 1),              # PE align, full index
     ("sj_pe_gapped_junc", 1),           # subjunc PE, junction-reads A/B
     ("sj_se_full_junc", 1),             # subjunc SE, big-margin records, full index
-    ("sj_pe_gapped_long", 1),           # subjunc PE > 160 bp (fragile junction voting, host)
+    ("sj_pe_gapped_long", 1),           # subjunc PE > 160 bp (fragile junction voting, GPU windows)
     ("sj_se_full_long", 1),             # subjunc SE 170-400 bp
     ("se_gapped_mixed_n14_I16", 4),     # -n 14 -I 16, N / lowercase / IUPAC, -T 4
     ("se_mb_synth_fullM1", 1),          # 4-block full index
     ("pe_mb_synth_gappedM1", 1),        # 2-block gapped index
     ("sj_pe_mb_long_gappedM6", 1),      # subjunc PE, 4-block index, blocks overlapping ~2 Mbp
+    ("sj_se_mb_synth_long_fullM1", 1),  # subjunc SE > 160 bp, 4-block index: GPU fragile windows per block
 ])
 def test_gpu_dropin_matches_stock_reference(name, threads, cache, tmp_path):
     c = Case(name)
