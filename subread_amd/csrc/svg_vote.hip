@@ -2957,7 +2957,15 @@ static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads 
 	// call's work starts after the previous call's, whatever streams the two were given
 	if (h->last_pending) HIPCHK(hipStreamWaitEvent(st, h->ev_last, 0));
 	if (h->stats_on) HIPCHK(hipMemsetAsync(h->d_stats, 0, 32 * sizeof(unsigned long long), st));
-	const uint64_t n = r1->n_reads, chunk = job.chunk;
+	// chunks of <= 160 MiB of probe records (1M single-end 100-bp reads, the host pipeline's
+	// sub-batch): the records stay in the 256 MB infinity cache between the probe kernel that
+	// writes them and the lane / wave kernels that read them (SVG_CHUNK sets the chunk instead)
+	uint64_t chunk = job.chunk;
+	if (!getenv("SVG_CHUNK")) {
+		const uint64_t cc = ((uint64_t)160 << 20) / (job.per_read * 8);
+		if (cc >= 1 && cc < chunk) chunk = cc;
+	}
+	const uint64_t n = r1->n_reads;
 	const bool overlap = job.overlap_mode && chunk < n;
 	hipStream_t st2 = overlap ? h->stream2 : st;
 	if (getenv("SVG_DEBUG"))

@@ -30,3 +30,14 @@ def test_oracle_dropin_matches_stock_reference(name, threads, cache, tmp_path):
         pytest.skip("reference drop-in binaries not built (make -C oracle dropin)")
     rep = check_case(c, cache.get(c.index_key), str(tmp_path), "oracle-dropin", threads)
     assert rep["mapped"] > 0
+
+
+@pytest.mark.parametrize("name,threads", [("pe_gapped_errmut", 4), ("sj_pe_gapped_long", 1)])
+def test_votetime_harness_matches_stock_reference(name, threads, cache, tmp_path):
+    """The CPU-baseline timing harness (oracle/ref_votetime.c: reads parsed before the clock,
+    served from memory) changes nothing the aligner writes."""
+    c = Case(name)
+    if not have(c.meta["program"], "votetime"):
+        pytest.skip("reference timing binaries not built (make -C oracle votetime)")
+    rep = check_case(c, cache.get(c.index_key), str(tmp_path), "votetime", threads)
+    assert rep["mapped"] > 0
