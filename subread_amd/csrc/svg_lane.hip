@@ -145,7 +145,19 @@ struct LParams {
 	int n_chr, padding, min_pair, max_pair, mvc;
 	unsigned long long *stats;    // [3] += results; [4] += deferred reads (final pass only);
 	int stat_base, final_pass;    // diagnostics at stats[stat_base..+4]: deferrals by reason (3), candidates, deferrals
+	// count bins (fused SE path): lane_bin_kernel lists the chunk's reads by their larger strand's
+	// candidate count, bin b at bins[b * n], bin_count[b] reads; the lane kernel takes 64-read
+	// groups from the heaviest bin down (NULL: lane column k = read k or idx[k])
+	uint32_t *bins, *bin_count;
+	int bin_light_first;          // diagnostics: lightest bin first
+	int bin_single;               // diagnostics: one bin (the lane limits only)
 };
+
+// candidate-count bins: a wave's vote loop runs as many iterations as its heaviest lane has
+// candidates, so lanes of one group should carry similar counts (C3: 19 candidates per read on
+// average, but the heaviest of 64 consecutive reads typically 30-40)
+#define LBINS 4
+__host__ __device__ constexpr int lbin_of(int c) { return c <= 8 ? 0 : (c <= 16 ? 1 : (c <= 24 ? 2 : 3)); }
 
 // meta: votes [0,5) | last [5,10) | toli [10,15) | cursor [15,21) (6-bit signed) | next [21,27) |
 // end [27] | spilled [28] | x [29,31).  votes and last (a subread number + 1) are <= 31 on this
@@ -522,12 +534,37 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 	const int cutoff = lp.cutoff;
 	unsigned long long nres = 0, ndef = 0, nwhy1 = 0, nwhy2 = 0, nwhy3 = 0, ncand = 0;
 	const uint32_t m = lp.idx ? *lp.idx_count : lp.n;
-	for (uint32_t g0 = gw * 64u; g0 < m; g0 += nw * 64u) {
-		const uint32_t k = g0 + (uint32_t)L.lane;
-		const bool live = k < m;
-		const uint32_t r = !live ? 0u : lp.idx ? lp.idx[k] : k;
-		L.dfr = !live || lp.defer_all || k >= lp.cs;
-		L.why = live && k >= lp.cs ? 1 : 0;
+	uint32_t bc[LBINS] = {0u, 0u, 0u, 0u}, ngroups = (m + 63u) / 64u;
+	if (lp.bins) {
+		ngroups = 0;
+#pragma unroll
+		for (int b = 0; b < LBINS; b++) { bc[b] = lp.bin_count[b]; ngroups += (bc[b] + 63u) / 64u; }
+	}
+	for (uint32_t g = gw; g < ngroups; g += nw) {
+		uint32_t k, r;
+		bool live;
+		if (lp.bins) {
+			// group g of the bins, heaviest bin first (the long groups start early)
+			uint32_t gg = g;
+			int b = LBINS - 1;
+			for (; b > 0; b--) {
+				const int bb = lp.bin_light_first ? LBINS - 1 - b : b;
+				const uint32_t gb = (bc[bb] + 63u) / 64u;
+				if (gg < gb) break;
+				gg -= gb;
+			}
+			if (lp.bin_light_first) b = LBINS - 1 - b;
+			k = gg * 64u + (uint32_t)L.lane;
+			live = k < bc[b];
+			r = live ? lp.bins[(size_t)b * lp.n + k] : 0u;
+		} else {
+			k = g * 64u + (uint32_t)L.lane;
+			live = k < m;
+			r = !live ? 0u : lp.idx ? lp.idx[k] : k;
+		}
+		const bool nocol = !lp.bins && k >= lp.cs;
+		L.dfr = !live || lp.defer_all || nocol;
+		L.why = live && nocol ? 1 : 0;
 		int len = live ? lp.len[r] : 0;
 		if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;
 		int applied = 0, step = 0;
@@ -1406,6 +1443,86 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 }
 
 // ---------------------------------------------------------------------------------------------
+// count bins (fused SE path): thread per read, the same eligibility tests and per-strand
+// candidate counts the lane kernel starts with (its probe records, SoA); reads past the lane
+// limits go straight to the deferral list, the rest to bin lbin_of(larger strand count)
+// ---------------------------------------------------------------------------------------------
+// Block tiles of LBT consecutive reads: the tile's lists are built in LDS (local offsets), then
+// one global atomic per list and tile reserves the output range (per-wave global atomics on five
+// counters serialised the kernel), and each list goes out in the tile's read order.
+#define LBT 1024   // 4 rounds of 256 reads per tile, ~4 tiles per CU at 1M reads (latency hidden across blocks)
+template <int NPF>
+__global__ void __launch_bounds__(256) lane_bin_kernel(LParams lp)
+{
+	__shared__ uint16_t lst[LBINS + 1][LBT];   // list LBINS: deferred
+	__shared__ uint32_t lcnt[LBINS + 1], gbase[LBINS + 1];
+	const int lane = (int)__lane_id(), tid = (int)threadIdx.x;
+	unsigned long long ndef = 0;
+	for (uint32_t t0 = blockIdx.x * LBT; t0 < lp.n; t0 += gridDim.x * LBT) {
+		if (tid <= LBINS) lcnt[tid] = 0;
+		__syncthreads();
+		for (int i = 0; i < LBT / 256; i++) {
+			const uint32_t loc = (uint32_t)(i * 256 + tid), r = t0 + loc;
+			const bool live = r < lp.n;
+			int len = live ? lp.len[r] : 0;
+			if (len > SVG_READ_KEEP) len = SVG_READ_KEEP;
+			bool dfr = lp.defer_all != 0;
+			int applied = 0;
+			if (len >= 15 + lp.gap) {
+				const int cr = (len - 15 - lp.gap) << 16;
+				int step = cr / (lp.total_subreads - 1);
+				if (step < (lp.gap << 16)) step = lp.gap << 16;
+				applied = 1 + cr / step;
+			}
+			if (len < 15 + lp.gap || len > 160 || applied > 31 || applied * lp.gap > NPF || applied * lp.gap > lp.nps) dfr = true;
+			const int np = applied * lp.gap;
+			int mx = 0;
+#pragma unroll
+			for (int st = 0; st < 2; st++) {
+				int cnt = 0;
+#pragma unroll
+				for (int p = 0; p < NPF; p++) {
+					const uint32_t y = live && !dfr && p < np ? lp.precs[(size_t)(st * lp.nps + p) * lp.n + r].y : 0u;
+					cnt += (int)((y & 0xffffu) + (y >> 16));
+				}
+				mx = cnt > mx ? cnt : mx;
+			}
+			if (mx > lp.cap) dfr = true;
+			const int cl = dfr ? LBINS : (lp.bin_single ? 0 : lbin_of(mx));
+#pragma unroll
+			for (int q = 0; q <= LBINS; q++) {
+				const unsigned long long bm = __ballot(live && cl == q);
+				if (!bm) continue;
+				const int leader = __ffsll((long long)bm) - 1;
+				uint32_t base = 0;
+				if (lane == leader) base = atomicAdd(&lcnt[q], (uint32_t)__popcll(bm));
+				base = __shfl(base, leader);
+				if (live && cl == q) lst[q][base + __popcll(bm & ((1ull << lane) - 1ull))] = (uint16_t)loc;
+			}
+		}
+		__syncthreads();
+		if (tid <= LBINS) {
+			const uint32_t c = lcnt[tid];
+			gbase[tid] = c ? atomicAdd(tid == LBINS ? lp.defer_count : &lp.bin_count[tid], c) : 0u;
+		}
+		__syncthreads();
+#pragma unroll
+		for (int q = 0; q <= LBINS; q++) {
+			const uint32_t c = lcnt[q];
+			uint32_t *dst = (q == LBINS ? lp.defer_list : lp.bins + (size_t)q * lp.n) + gbase[q];
+			for (uint32_t j = (uint32_t)tid; j < c; j += 256u) dst[j] = t0 + lst[q][j];
+		}
+		ndef += lcnt[LBINS];
+		__syncthreads();   // lcnt / lst are reused by the next tile
+	}
+	if (lp.stats && tid == 0 && ndef) {
+		if (lp.final_pass) atomicAdd(&lp.stats[4], ndef);
+		atomicAdd(&lp.stats[lp.stat_base + 0], ndef);   // reason 1: candidates > CAP or length
+		atomicAdd(&lp.stats[lp.stat_base + 4], ndef);
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
 // host: two lane passes for one chunk (SE align), then the wave kernel for what is left
 //   pass 1 (light): every read, <= 40 candidates and <= 20 vote-table slots per strand
 //   pass 2 (heavy, SVG_LANE=3 only): the reads pass 1 deferred (up to n/4 of them), <= 192
@@ -1568,7 +1685,7 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 	const size_t o_c2 = (o_n1 + (size_t)4 * n + 255) & ~(size_t)255;
 	const size_t o_p2 = o_c2 + (size_t)8 * LANE_CAP2 * n2, o_n2 = o_p2 + (size_t)4 * LANE_CAP2 * n2;
 	const size_t o_l1 = (o_n2 + (size_t)4 * n2 + 255) & ~(size_t)255, o_l2 = o_l1 + (size_t)4 * n + 256;
-	const size_t o_cnt = o_l2 + (size_t)4 * n + 256, need = o_cnt + 256;
+	const size_t o_cnt = o_l2 + (size_t)4 * n + 256, o_bin = o_cnt + 256, need = o_bin + (size_t)4 * LBINS * n + 256;
 	if (need > h->lane_cap[slot]) {
 		hipFree(h->d_lane[slot]);
 		h->d_lane[slot] = NULL;
@@ -1577,9 +1694,10 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 		h->lane_cap[slot] = need;
 	}
 	uint8_t *b = (uint8_t *)h->d_lane[slot];
-	// [0] pass-1 deferrals, [1] pass-2 deferrals, [2] / [3] wave-kernel work counters after pass 1 / 2
+	// [0] pass-1 deferrals, [1] pass-2 deferrals, [2] / [3] wave-kernel work counters after pass 1 / 2,
+	// [4..7] count-bin sizes
 	uint32_t *cnt = (uint32_t *)(b + o_cnt);
-	HIPCHK(hipMemsetAsync(cnt, 0, 16, st));
+	HIPCHK(hipMemsetAsync(cnt, 0, 32, st));
 	GParams g;
 	g.precs = precs; g.len = len; g.vals = h->dix.vals; g.n = n; g.nps = nps; g.gap = h->dix.gap;
 	g.total_subreads = p->total_subreads; g.cap = LANE_CAP1;
@@ -1621,12 +1739,28 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 	lp.stat_base = 16;
 	lp.final_pass = !two || sjm;
 	lp.cs = n; lp.idx = NULL; lp.idx_count = NULL;
+	lp.bins = NULL; lp.bin_count = NULL; lp.bin_light_first = 0; lp.bin_single = 0;
 	{
-		// tuning knobs (diagnostics): SVG_LANE_K=16|20|24, SVG_LANE_CAP
+		// tuning knobs (diagnostics): SVG_LANE_K=16|20|24, SVG_LANE_CAP, SVG_LANE_BIN=0
 		const char *ek = getenv("SVG_LANE_K"), *ec = getenv("SVG_LANE_CAP");
 		const int kk = ek ? atoi(ek) : LANE_K1;
 		if (ec && atoi(ec) > 0 && atoi(ec) <= LANE_CAP1) lp.cap = atoi(ec);
 		if (ec && atoi(ec) > LANE_CAP1 && fused) lp.cap = atoi(ec) < 64 ? atoi(ec) : 64;
+		// count bins for the fused single-pass path: one thread per read sorts the chunk's reads into
+		// LBINS lists by candidate count (and defers the over-cap ones) before the lane kernel
+		const char *eb = getenv("SVG_LANE_BIN");
+		if (fused && !two && !(eb && eb[0] == '0')) {
+			lp.bins = (uint32_t *)(b + o_bin);
+			lp.bin_count = cnt + 4;
+			lp.bin_light_first = eb && eb[0] == '2';
+			lp.bin_single = eb && eb[0] == '3';
+			uint64_t bb = ((uint64_t)n + LBT - 1) / LBT, bmax = (uint64_t)h->n_cu * 8;
+			if (bb > bmax) bb = bmax;
+			if (bb < 1) bb = 1;
+			if (sjm) hipLaunchKernelGGL(lane_bin_kernel<LANE_NPF_SJ>, dim3((unsigned)bb), dim3(256), 0, st, lp);
+			else hipLaunchKernelGGL(lane_bin_kernel<LANE_NPF>, dim3((unsigned)bb), dim3(256), 0, st, lp);
+			HIPCHK(hipGetLastError());
+		}
 		if (!fused) rc = lane_launch<LANE_K1, 0>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
 		else if (sjm) rc = lane_launch<LANE_K1, LANE_NPF_SJ>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
 		else if (kk == 16) rc = lane_launch<16, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st);

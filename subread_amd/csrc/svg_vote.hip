@@ -2928,6 +2928,8 @@ int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slo
 		HIPCHK(hipStreamWaitEvent(st2, h->ev_lane[slot], 0));
 	}
 	if ((rc = timing_mark(h, 1, 0, st2))) return rc;
+	// diagnostics only (wrong records for the deferred reads): the step without the wave kernel
+	if (job->lane && getenv("SVG_DIAG_NOWAVE")) return timing_mark(h, 1, 1, st2);
 	rc = launch_vote(h, kc, st2, job->npmax, job->sj, ends);
 	if (!rc) rc = timing_mark(h, 1, 1, st2);
 	return rc;
