@@ -410,7 +410,7 @@ def main():
                         done, threads, cs),
                     "cpu_model": cpu["model"], "host_logical_cpus": cpu["logical_cpus"],
                     "usable_cpus": cpu["usable_cpus"], "cgroup_quota_cpus": cpu["cgroup_quota_cpus"]}
-        cal = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
+        cal = os.path.join(ROOT, "profiles", "r03_cpu_calibration.json")   # tools/cpu_calibration.py
         if os.path.exists(cal):
             c = json.load(open(cal))
             cpu_base["reference_over_port"] = c.get("reference_over_port")

@@ -26,19 +26,22 @@ def main():
         g = random_genome([1_000_000], 901)
     ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True)
     mode = sys.argv[3] if len(sys.argv) > 3 else "se"
-    paired = mode == "pe"
+    paired = mode in ("pe", "sjpe")
     from subread_amd.abi import PROGRAM_ALIGN, PROGRAM_SUBJUNC
     from subread_amd.sim import simulate_pairs, simulate_spliced_reads
     if mode == "pe":
         r1, r2 = simulate_pairs(g, n, 150)
         ix.set_max_read_length(150)
+    elif mode == "sjpe":   # bench.py c5pe: subjunc on 100 bp pairs
+        r1, r2 = simulate_pairs(g, n, 100, seed=4004)
+        ix.set_max_read_length(100)
     elif mode == "sj":
         r1, r2 = simulate_spliced_reads(g, n, 100), None
         ix.set_max_read_length(100)
     else:
         r1, r2 = simulate_reads(g, n, 100, seed=20261015), None
         ix.set_max_read_length(100)
-    p = default_params(PROGRAM_SUBJUNC if mode == "sj" else PROGRAM_ALIGN, paired)
+    p = default_params(PROGRAM_SUBJUNC if mode in ("sj", "sjpe") else PROGRAM_ALIGN, paired)
     ix.vote(p, r1, r2)
     ix.set_stats(True)
     t = time.time()
