@@ -75,6 +75,7 @@ struct WaveLDS {
 	uint16_t simp_votes[ENDS][MAXS];
 	uint16_t bm[SJ ? ENDS : 1][10];
 	uint8_t rnew[32];                     // batch mode: new row occupancy (0xff = unchanged)
+	alignas(16) uint32_t bkv[64];         // batch mode: the chunk's kv, for broadcast reads
 	uint8_t gwin[SJ ? 2 : 1][SJ ? 64 : 4];   // subjunc donor windows of the .array
 	char text[SJ ? ENDS : 1][2][SJ ? MAXL : 4];   // strand 0 / strand 1 (reverse_read) form, donor scoring only
 };
@@ -392,16 +393,22 @@ struct Wave {
 		}
 	}
 
-	// ---------------------------------------------------------------- batch mode (align, round 0)
-	// Lane c holds candidate c of a chunk of m <= 64, in the reference's order.  A candidate
-	// whose outcome cannot depend on the other candidates of the chunk -- no slot of the
-	// table within the tolerance in its three rows (so it finds nothing), no other chunk
-	// candidate within 2*tol (so no slot opened in the chunk can match it, nor its slot
-	// theirs), and no earlier dependent candidate opening slots in its row (so its slot
-	// index is its rank in candidate order) -- only opens a slot in row kv/5 %30
-	// (sorted-hashtable.c:1071-1106); those slots are opened together.  Returns the lanes
-	// left for the serial replay (vote_one, in order).  Exact: every table mutation of the
-	// serial order happens, in an order no candidate can observe.
+	// ---------------------------------------------------------------- batch mode (round 0)
+	// Lane c holds candidate c of a chunk of m <= 64, in the reference's order.  Two kinds of
+	// candidate have an outcome the other candidates of the chunk cannot change:
+	//  A (opens a slot): no slot of the table within the tolerance in its three rows (so it finds
+	//    nothing), no other chunk candidate within 2*tol (no slot opened in the chunk can match it,
+	//    nor its slot theirs), and no earlier serial candidate in its row (so its slot index is its
+	//    rank among the row's openers) -- it only opens a slot in row kv/5 %30
+	//    (sorted-hashtable.c:1071-1106);
+	//  B (votes): exactly one slot s within the tolerance, unspilled (toli 0: no roll-back, no
+	//    shift-indel mark), matched exactly (d == 0 == its cursor: no indel section) with
+	//    kP1 > last(s), every chunk candidate within 2*tol of it a B candidate of the same slot with a
+	//    different kP1 -- the chunk's votes on s are then s's whole fold in chunk order
+	//    (sorted-hashtable.c:1041-1047: votes += 1, last = kP1, coverage_end from the last), applied
+	//    at once by the group's last lane.
+	// A and B candidates touch slots no other candidate of the chunk reads, so they are settled
+	// together; the rest are left for the serial replay (vote_one, in order).  Returns those lanes.
 	template <int E>
 	__device__ unsigned long long batch_create(int kvv, int kov, int m, uint32_t high_b)
 	{
@@ -413,28 +420,77 @@ struct Wave {
 		// row occupancy of the candidate's three rows (every lane active for the shuffles)
 		const int n0 = __shfl(items_v, E * 32 + (int)r0), np_ = __shfl(items_v, E * 32 + (int)rp),
 		          nm = __shfl(items_v, E * 32 + (int)rm);
-		bool dep = false;
+		// the table's slots within the tolerance (up to two), the first one's index, meta and offset
+		int nmatch = 0, tslot = -1, td = 1;
+		uint32_t tM = 0u;
 		if (act) {
+			// four slots per LDS round trip
 			const int tot = n0 + np_ + nm;
-			for (int q = 0; q < tot && !dep; q++) {
-				const uint32_t row = q < n0 ? r0 : (q < n0 + np_ ? rp : rm);
-				const int idx = q < n0 ? q : (q < n0 + np_ ? q - n0 : q - n0 - np_);
-				const int d = (int)(kv - L->pm[row * SPACE + idx].x);
-				dep = d >= -tol && d <= tol;
+			for (int q0 = 0; q0 < tot && nmatch < 2; q0 += 4) {
+				int at[4];
+				uint2 e[4];
+#pragma unroll
+				for (int k = 0; k < 4; k++) {
+					const int q = q0 + k < tot ? q0 + k : tot - 1;
+					const uint32_t row = q < n0 ? r0 : (q < n0 + np_ ? rp : rm);
+					at[k] = (int)row * SPACE + (q < n0 ? q : (q < n0 + np_ ? q - n0 : q - n0 - np_));
+					e[k] = L->pm[at[k]];
+				}
+#pragma unroll
+				for (int k = 0; k < 4; k++) {
+					const int d = (int)(kv - e[k].x);
+					if (q0 + k < tot && d >= -tol && d <= tol) {
+						if (!nmatch) { tslot = at[k]; tM = e[k].y; td = d; }
+						nmatch++;
+					}
+				}
 			}
 		}
-		unsigned long long same = 0;
-		for (int j = 0; j < m; j++) {
-			const uint32_t kj = (uint32_t)rd(kvv, j), rj = ((uint32_t)rd(kov, j) >> 17) & 31u;
-			const int dd = (int)(kv - kj);
-			if (j != lane && dd >= -2 * tol && dd <= 2 * tol) dep = true;
-			if (rj == r0) same |= 1ull << j;
+		if constexpr (!SJ) STAMP(7);   // diagnostics (align variants): the slot scan
+		const bool bcand = act && nmatch == 1 && td == 0 && !m_spilled(tM) && kP1 > m_last(tM);
+		// chunk neighbours: eqm = the candidates with this kv (this lane included), nbfar = one at
+		// 0 < |d| <= 2*tol.  A B candidate's slot position is its kv, so its group (the chunk's
+		// votes on the slot) is eqm; kv broadcast from LDS, four per read
+		L->bkv[lane] = kv;
+		wsync();
+		bool nbfar = false;
+		unsigned long long eqm = 0;
+		for (int j = 0; j < m; j += 4) {
+			const uint4 q = *reinterpret_cast<const uint4 *>(&L->bkv[j]);
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				const uint32_t kj = k == 0 ? q.x : (k == 1 ? q.y : (k == 2 ? q.z : q.w));
+				if (j + k < m) {
+					const bool eq = kj == kv;
+					nbfar = nbfar || (!eq && kj - kv + (uint32_t)(2 * tol) <= (uint32_t)(4 * tol));
+					if (eq) eqm |= 1ull << (j + k);
+				}
+			}
 		}
-		dep = dep && act;
+		// same = the chunk's candidates of this lane's row, one ballot per distinct row
+		unsigned long long same = 0, rem = ballot(act);
+		while (rem) {
+			const int l = __ffsll((long long)rem) - 1;
+			const uint32_t rv = (uint32_t)rd((int)r0, l);
+			const unsigned long long mk = ballot(act && r0 == rv);
+			if (act && r0 == rv) same = mk;
+			rem &= ~mk;
+		}
+		// a B group settles when all of it are B candidates with distinct kP1 (non-decreasing in
+		// chunk order: compare with the previous member) and nothing else is within 2*tol
+		const unsigned long long below = eqm & ((1ull << lane) - 1ull);
+		const int prev = below ? 63 - __clzll((long long)below) : lane;
+		const int kprev = __shfl(kP1, prev);
+		const unsigned long long dupm = ballot(act && below != 0ull && kprev == kP1);
+		const bool isB = bcand && !nbfar && (eqm & ~ballot(bcand)) == 0ull && (eqm & dupm) == 0ull;
+		const unsigned long long grp = eqm;
+		const bool nb = nbfar || __popcll(eqm) > 1;
+		// serial: matches batch mode cannot settle, crowded openers, B groups that did not qualify
+		bool dep = act && !isB && (nmatch > 0 || nb);
 		const unsigned long long bd = ballot(dep);
 		const unsigned long long le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1ull);
-		dep = act && (same & bd & le) != 0ull;
-		const bool inr = act && !dep && kv >= kp->low && kv <= high_b;
+		dep = act && !isB && (same & bd & le) != 0ull;   // an opener after a serial candidate of its row
+		const bool inr = act && !isB && !dep && kv >= kp->low && kv <= high_b;
 		const unsigned long long cm = ballot(inr);
 		const int rank = __popcll(same & cm & (le >> 1));
 		const bool mk = inr && n0 + rank < SPACE;
@@ -444,6 +500,11 @@ struct Wave {
 			const int x = gap_x(off, kp->ix.gap);
 			L->pm[(int)r0 * SPACE + n0 + rank] = make_uint2(kv, m_pack_u(1, kP1, 0, x, kP1, x));   // no cold state
 		}
+		int nv = 0;
+		if (isB && (grp & ~le) == 0ull) {   // the group's last vote: votes += group size, last = its kP1
+			nv = m_votes(tM) + __popcll(grp);
+			L->pm[tslot].y = m_pack_u(nv, kP1, m_shift(tM), gap_x(off, kp->ix.gap), m_first(tM), m_fx(tM));
+		}
 		if (inr && (same & cm & ~le) == 0ull) L->rnew[r0] = (uint8_t)(n0 + rank + 1 < SPACE ? n0 + rank + 1 : SPACE);
 		wsync();
 		if ((lane >> 5) == E && (lane & 31) < ROWS) {
@@ -451,6 +512,8 @@ struct Wave {
 			if (v != 0xff) items_v = v;
 		}
 		if (ballot(mk) && max_vote[E] == 0) max_vote[E] = 1;
+		for (int o = 32; o; o >>= 1) { const int t = __shfl_xor(nv, o); nv = t > nv ? t : nv; }
+		if (max_vote[E] < nv) max_vote[E] = nv;
 		wsync();
 		return ballot(dep);
 	}
