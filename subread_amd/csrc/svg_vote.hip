@@ -73,6 +73,8 @@ struct WaveLDS {
 	uint32_t simp_pos[ENDS][MAXS];        // simple_mapping_t: position
 	uint16_t simp_slot[ENDS][MAXS];       // slot index, or 0x8000|stored index
 	uint16_t simp_votes[ENDS][MAXS];
+	int32_t simp_loc[ENDS == 2 ? 2 : 1][ENDS == 2 ? MAXS : 1];   // PE: locate_gene_position of each simple (position)
+	int16_t simp_chr[ENDS == 2 ? 2 : 1][ENDS == 2 ? MAXS : 1];   //     its chromosome, -1 where locate fails
 	uint16_t bm[SJ ? ENDS : 1][10];
 	uint8_t rnew[32];                     // batch mode: new row occupancy (0xff = unchanged)
 	alignas(16) uint32_t bkv[64];         // batch mode: the chunk's kv, for broadcast reads
@@ -1060,6 +1062,19 @@ struct Wave {
 			int n0 = nsimp[0], n1 = nsimp[1];
 			int npairs = n0 * n1;
 			int bs[3] = {-1, -1, -1}, bidx[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff};
+			// each simple located once (up to 64 x 64 pairs would locate both ends of every pair)
+			for (int e = 0; e < 2; e++) {
+				if (lane < nsimp[e]) {
+					int c, q;
+					const int err = locate(L->simp_pos[e][lane], &c, &q);
+					L->simp_loc[e & (ENDS - 1)][lane] = q;
+					L->simp_chr[e & (ENDS - 1)][lane] = (int16_t)(err == 0 ? c : -1);
+				}
+			}
+			wsync();
+			// each lane keeps its own first 3 pairs by (score desc, pair order asc) -- its pairs come
+			// in ascending order -- and the wave's first 3 are then taken from the lanes' heads
+			int ls0 = -1, ls1 = -1, ls2 = -1, li0 = 0x7fffffff, li1 = 0x7fffffff, li2 = 0x7fffffff;
 			for (int q0 = 0; q0 < npairs; q0 += 64) {
 				int q = q0 + lane;
 				int sc = -1;
@@ -1068,9 +1083,10 @@ struct Wave {
 					int va = L->simp_votes[0][i], vb = L->simp_votes[1][j];
 					int mx = va > vb ? va : vb, mn = va < vb ? va : vb;
 					if (mx >= p.min_votes_first) {
-						int c1, c2, q1, q2, pe = 0, same = 0;
-						int e1 = locate(L->simp_pos[0][i], &c1, &q1), e2 = locate(L->simp_pos[1][j], &c2, &q2);
-						if (e1 == 0 && e2 == 0) {
+						int pe = 0, same = 0;
+						const int c1 = L->simp_chr[0][i], c2 = L->simp_chr[ENDS - 1][j];
+						const int q1 = L->simp_loc[0][i], q2 = L->simp_loc[ENDS - 1][j];
+						if (c1 >= 0 && c2 >= 0) {
 							long long tlen = (long long)q1 - q2;
 							tlen = abs((int)tlen);
 							tlen += (q1 > q2) ? rc.rl[0] : rc.rl[1];
@@ -1083,20 +1099,19 @@ struct Wave {
 						if (pe || mn >= p.min_votes_first) sc = (va + vb) * (pe ? 1300 : (same ? 1000 : 800));
 					}
 				}
-				for (int r = 0; r < 3; r++) {
-					int m = wave_max(sc);
-					if (m < 0) break;
-					int qi = wave_min(sc == m ? q : 0x7fffffff);
-					int pos3 = 3;
-					for (int t = 0; t < 3; t++) {
-						if (bs[t] < m || (bs[t] == m && bidx[t] > qi)) { pos3 = t; break; }
-					}
-					if (pos3 < 3) {
-						for (int t = 2; t > pos3; t--) { bs[t] = bs[t - 1]; bidx[t] = bidx[t - 1]; }
-						bs[pos3] = m; bidx[pos3] = qi;
-					}
-					if (q == qi) sc = -1;
+				// (an equal score keeps the earlier pair ahead: insert after the entries >= sc)
+				if (sc > ls2) {
+					if (sc > ls0) { ls2 = ls1; li2 = li1; ls1 = ls0; li1 = li0; ls0 = sc; li0 = q; }
+					else if (sc > ls1) { ls2 = ls1; li2 = li1; ls1 = sc; li1 = q; }
+					else { ls2 = sc; li2 = q; }
 				}
+			}
+			for (int r = 0; r < 3; r++) {
+				const int m = wave_max(ls0);
+				if (m < 0) break;
+				const int qi = wave_min(ls0 == m ? li0 : 0x7fffffff);
+				bs[r] = m; bidx[r] = qi;
+				if (li0 == qi) { ls0 = ls1; li0 = li1; ls1 = ls2; li1 = li2; ls2 = -1; li2 = 0x7fffffff; }
 			}
 			for (int t = 0; t < 3 && t < p.max_vote_combinations; t++)
 				if (bs[t] >= 0) ncomb++;
