@@ -17,10 +17,15 @@
  * reads them -- that function already applies the -S reversal (core.c:1186-1198), so the
  * library is told not to reverse again (reverse_r1 = reverse_r2 = 0).  Reads are 2-bit
  * packed on the host (svg_pack_reads) and voted with svg_vote_batch_packed straight into
- * the chunk's bigtable (core-bigtable.c:84-131).  The per-read host work of do_voting that is
- * not voting then runs unchanged, in do_voting's order:
- *   - subjunc reads > 160 bp: core_fragile_junction_voting (core.c:3138-3142), per strand and
- *     end, in every index block's run (it only adds events to the event tables);
+ * the chunk's bigtable (core-bigtable.c:84-131).  Subjunc reads > 160 bp also get their
+ * fragile junction voting windows (core_fragile_junction_voting, core.c:3138-3142 ->
+ * core-junction.c:5151-5422: gehash_go_q windows, select_best_vote, the best matching halves,
+ * the donor test) from the GPU in the same block-0 run (svg_fragile_batch, every block's
+ * windows).  The per-read host work of do_voting then runs in do_voting's order with the
+ * reference's own functions:
+ *   - fragile windows -> events (fragile_window_events: core_dynamic_align,
+ *     local_add_indel_event, search_event / put_new_event, core-junction.c:5211-5419), each
+ *     index block's windows in that block's run;
  *   - the final voting run: find_new_indels / find_new_junctions per record (core.c:3240-3290).
  */
 #include <stdio.h>
