@@ -41,7 +41,86 @@ struct DevIndex {
 	const uint32_t *khash_ff;
 	uint64_t khash_lines;
 	int32_t khash_sec;        // 1: 32-byte sectors of 3 entries (8-bit run counts), 0: 64-byte lines
+	//   ksorted: bit b set when bucket b's keys are non-decreasing as shorts (built with khash), so
+	//            that its key-hash record is also prefill_votes's equal-key run (svg_probe_keys)
+	const uint32_t *ksorted;
 };
+
+// ---------------------------------------------------------------------------------------------
+// probe-image helpers shared by the vote path's probe kernels (svg_vote.hip) and the key
+// lookups (svg_keys.hip)
+
+// position (0..63) of the j-th (0-based) set bit of x; x has more than j set bits
+__device__ __forceinline__ int select64(uint64_t x, int j)
+{
+	int pos = 0, c = __popc((uint32_t)x);
+	if (j >= c) { j -= c; x >>= 32; pos = 32; }
+	uint32_t v = (uint32_t)x;
+	c = __popc(v & 0xffffu); if (j >= c) { j -= c; v >>= 16; pos += 16; }
+	c = __popc(v & 0xffu); if (j >= c) { j -= c; v >>= 8; pos += 8; }
+	c = __popc(v & 0xfu); if (j >= c) { j -= c; v >>= 4; pos += 4; }
+	c = __popc(v & 0x3u); if (j >= c) { j -= c; v >>= 2; pos += 2; }
+	return pos + (j >= (int)(v & 1u) ? 1 : 0);
+}
+
+// position of the j-th (0-based) zero bit at or above bit 40 of a 32-byte bucket code (LSB-first)
+__device__ __forceinline__ int code_zero(const uint64_t z[4], int j)
+{
+	int base = 0;
+#pragma unroll
+	for (int q = 0; q < 4; q++) {
+		const int c = __popcll(z[q]);
+		if (j < c) return base + select64(z[q], j);
+		j -= c;
+		base += 64;
+	}
+	return 256;
+}
+
+// DevIndex::khash line of a key: the key scrambled by an odd constant (a bijection), reduced to
+// [0, lines) by the high half of a 64-bit product
+__device__ __forceinline__ uint64_t khash_line(uint32_t key, uint64_t lines)
+{
+	return ((uint64_t)(key * 0x9E3779B1u) * lines) >> 32;
+}
+
+// the probe record (mid item, fwd | bwd << 16) stored under key in DevIndex::khash; rec is left
+// unchanged (and false returned) when the key has no record
+__device__ __forceinline__ bool khash_find(const DevIndex &ix, uint32_t key, uint2 &rec)
+{
+	if (key == 0xffffffffu) {
+		if (!ix.khash_ff[0]) return false;
+		rec = make_uint2(ix.khash_ff[1], ix.khash_ff[2]);
+		return true;
+	}
+	uint64_t L = khash_line(key, ix.khash_lines);
+	bool found = false;
+	if (ix.khash_sec) {
+		for (;;) {
+			const uint4 *l4 = (const uint4 *)(ix.khash + 8 * L);
+			const uint4 a = l4[0], b4 = l4[1];
+			const uint32_t ks[3] = {a.x, a.y, a.z}, mid[3] = {a.w, b4.x, b4.y};
+			const uint32_t fb[3] = {b4.z & 0xffffu, b4.z >> 16, b4.w & 0xffffu};
+#pragma unroll
+			for (int k = 0; k < 3; k++)
+				if (ks[k] == key) { rec = make_uint2(mid[k], (fb[k] & 0xffu) | ((fb[k] >> 8) << 16)); found = true; }
+			if (found || !(b4.w >> 16)) break;
+			L = L + 1 == ix.khash_lines ? 0 : L + 1;
+		}
+	} else for (;;) {
+		const uint4 *l4 = (const uint4 *)(ix.khash + 16 * L);
+		const uint4 a = l4[0], b4 = l4[1], c4 = l4[2], d4 = l4[3];
+		const uint32_t ks[5] = {a.x, a.y, a.z, a.w, b4.x};
+		const uint32_t px[5] = {b4.y, b4.w, c4.y, c4.w, d4.y};
+		const uint32_t py[5] = {b4.z, c4.x, c4.z, d4.x, d4.z};
+#pragma unroll
+		for (int k = 0; k < 5; k++)
+			if (ks[k] == key) { rec = make_uint2(px[k], py[k]); found = true; }
+		if (found || !d4.w) break;
+		L = L + 1 == ix.khash_lines ? 0 : L + 1;
+	}
+	return found;
+}
 
 #define SVG_MAX_BLOCKS 64
 
@@ -50,7 +129,7 @@ struct svg_index {
 	hipStream_t stream;
 	svg_host_index host;
 	DevIndex dix;
-	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr, *d_bgrp, *d_keys8, *d_bline, *d_bcode, *d_khash;
+	void *d_bstart, *d_keys, *d_vals, *d_values, *d_chr, *d_bgrp, *d_keys8, *d_bline, *d_bcode, *d_khash, *d_ksorted;
 	uint32_t *d_scratch;
 	size_t scratch_words;
 	unsigned long long *d_stats;

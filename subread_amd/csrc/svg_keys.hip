@@ -5,17 +5,26 @@
 // cell-counts.c:432-491), and votes over those lists itself.  That lookup is the probe half of
 // the vote path (a3-a4) with a different widening: binary search of (short)(key / buckets) in
 // the bucket's keys (sorted-hashtable.c's layout), then forward / backward steps of imax/4,
-// /3, /3 ... that only land on equal keys, then single steps to the run's ends.  One thread
-// per key runs exactly that (the literal steps matter for small indexes, whose bucket keys are
-// not sorted as shorts); every image the vote path builds for its own probes is bypassed,
-// since the plain bounds + i16 keys are always resident.
+// /3, /3 ... that only land on equal keys, then single steps to the run's ends.
+//
+// In a bucket whose keys are sorted, those steps find exactly the whole equal-key run -- the
+// run the vote path's probe images already hold:
+//   bucket code (full indexes, build_bcode): one random 32-byte sector per key gives the run's
+//     bucket-local bounds directly (count byte 255 = not coded: unsorted or > 169 items);
+//   key hash (gapped / small indexes, build_khash): one random sector gives the record
+//     (mid item, fwd, bwd) of the run, and the bucket's first item turns it bucket-local; a
+//     bucket whose keys are not sorted (DevIndex::ksorted) takes the literal search instead.
+// The literal search (one thread per key over the resident bounds + i16 keys) answers
+// everything else; SVG_KEYS_LITERAL=1 forces it (A/B and tests).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "subread_vote.h"
 #include "svg_internal.h"
 #include "svg_device.h"
 
 struct KeyParams {
+	DevIndex ix;
 	const uint32_t *bstart;
 	const int16_t *keys;
 	uint32_t nb;
@@ -24,16 +33,16 @@ struct KeyParams {
 	uint32_t *first, *count;
 };
 
-__global__ void __launch_bounds__(256) probe_keys_kernel(KeyParams kp)
+// prefill_votes's search, literally (cell-counts.c:432-491)
+__device__ __forceinline__ void keys_literal(const KeyParams &kp, uint32_t sub, uint32_t b, uint32_t &f, uint32_t &c)
 {
-	for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < kp.n; t += (uint64_t)gridDim.x * 256u) {
-		const uint32_t sub = kp.in[t];
-		const uint32_t b = sub % kp.nb;
+	{
 		const uint32_t base = kp.bstart[b];
 		const int items = (int)(kp.bstart[b + 1] - base);
 		const int16_t *ck = kp.keys + base;
 		const int16_t key = (int16_t)(sub / kp.nb);
-		uint32_t f = 0, c = 0;
+		f = 0;
+		c = 0;
 		if (items > 0) {
 			int imin = 0, imax = items - 1, last;
 			bool found = true;
@@ -70,6 +79,48 @@ __global__ void __launch_bounds__(256) probe_keys_kernel(KeyParams kp)
 				c = (uint32_t)(stoploc - last);
 			}
 		}
+	}
+}
+
+#define KEYS_LITERAL 0
+#define KEYS_CODE    1
+#define KEYS_KHASH   2
+template <int IMG>
+__global__ void __launch_bounds__(256) probe_keys_kernel(KeyParams kp)
+{
+	for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < kp.n; t += (uint64_t)gridDim.x * 256u) {
+		const uint32_t sub = kp.in[t];
+		const uint32_t q = sub / kp.nb, b = sub - q * kp.nb;
+		uint32_t f = 0, c = 0;
+		bool literal = IMG == KEYS_LITERAL;
+		if (IMG == KEYS_CODE) {
+			// the bucket's 32-byte code: the run of key_hi = q is [fe, ee) of the bucket's items
+			const uint4 *c4 = kp.ix.bcode + 2 * (size_t)b;
+			const uint4 u0 = c4[0], u1 = c4[1];
+			const uint32_t n = u0.y & 255u;
+			literal = n == 255u;
+			if (!literal && n) {
+				const uint64_t z[4] = {~(((uint64_t)u0.y << 32) | u0.x) & ~0xffffffffffull, ~(((uint64_t)u0.w << 32) | u0.z),
+				                       ~(((uint64_t)u1.y << 32) | u1.x), ~(((uint64_t)u1.w << 32) | u1.z)};
+				const int k = (int)q;
+				const int fe = k ? code_zero(z, k - 1) - 40 - (k - 1) : 0;
+				const int ee = code_zero(z, k) - 40 - k;
+				if (ee > fe) { f = (uint32_t)fe; c = (uint32_t)(ee - fe); }
+			}
+		} else if (IMG == KEYS_KHASH) {
+			// (the image keys a run by (u16)key_hi * nb + bucket: quotients past 16 bits, which only
+			// tiny indexes have, compare as wrapped shorts in the reference -- literal search)
+			literal = q > 0xffffu || !((kp.ix.ksorted[b >> 5] >> (b & 31u)) & 1u);
+			if (!literal) {
+				uint2 rec;
+				if (khash_find(kp.ix, sub, rec)) {
+					const uint32_t fwd = rec.y & 0xffffu, bwd = rec.y >> 16;
+					f = rec.x - bwd - kp.bstart[b];
+					c = fwd + bwd;
+				}
+			}
+		}
+		if (literal) keys_literal(kp, sub, b, f, c);
 		kp.first[t] = f;
 		kp.count[t] = c;
 	}
@@ -90,6 +141,7 @@ static int launch_keys(svg_index *h, svg_index *bk, const uint32_t *keys, uint64
 {
 	if (n == 0) return 0;
 	KeyParams kp;
+	kp.ix = bk->dix;
 	kp.bstart = bk->dix.bstart;
 	kp.keys = bk->dix.keys;
 	kp.nb = bk->dix.nb;
@@ -99,7 +151,12 @@ static int launch_keys(svg_index *h, svg_index *bk, const uint32_t *keys, uint64
 	kp.count = count;
 	uint64_t blocks = (n + 255) / 256, bmax = (uint64_t)h->n_cu * 16;
 	if (blocks > bmax) blocks = bmax;
-	hipLaunchKernelGGL(probe_keys_kernel, dim3((unsigned)blocks), dim3(256), 0, st, kp);
+	const char *el = getenv("SVG_KEYS_LITERAL");
+	const bool lit = el && el[0] == '1';
+	if (!lit && bk->dix.bcode) hipLaunchKernelGGL(probe_keys_kernel<KEYS_CODE>, dim3((unsigned)blocks), dim3(256), 0, st, kp);
+	else if (!lit && bk->dix.khash && bk->dix.ksorted)
+		hipLaunchKernelGGL(probe_keys_kernel<KEYS_KHASH>, dim3((unsigned)blocks), dim3(256), 0, st, kp);
+	else hipLaunchKernelGGL(probe_keys_kernel<KEYS_LITERAL>, dim3((unsigned)blocks), dim3(256), 0, st, kp);
 	HIPCHK(hipGetLastError());
 	return 0;
 }

@@ -1532,33 +1532,6 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	}
 }
 
-// position (0..63) of the j-th (0-based) set bit of x; x has more than j set bits
-__device__ __forceinline__ int select64(uint64_t x, int j)
-{
-	int pos = 0, c = __popc((uint32_t)x);
-	if (j >= c) { j -= c; x >>= 32; pos = 32; }
-	uint32_t v = (uint32_t)x;
-	c = __popc(v & 0xffffu); if (j >= c) { j -= c; v >>= 16; pos += 16; }
-	c = __popc(v & 0xffu); if (j >= c) { j -= c; v >>= 8; pos += 8; }
-	c = __popc(v & 0xfu); if (j >= c) { j -= c; v >>= 4; pos += 4; }
-	c = __popc(v & 0x3u); if (j >= c) { j -= c; v >>= 2; pos += 2; }
-	return pos + (j >= (int)(v & 1u) ? 1 : 0);
-}
-
-// position of the j-th (0-based) zero bit at or above bit 40 of a 32-byte bucket code (LSB-first)
-__device__ __forceinline__ int code_zero(const uint64_t z[4], int j)
-{
-	int base = 0;
-#pragma unroll
-	for (int q = 0; q < 4; q++) {
-		const int c = __popcll(z[q]);
-		if (j < c) return base + select64(z[q], j);
-		j -= c;
-		base += 64;
-	}
-	return 256;
-}
-
 // equal-key run of a bucket given as a bit mask over its items: gehash_go_X's binary search
 // (sorted-hashtable.c:947-981) replayed on the positions alone -- it stops at the first
 // midpoint inside the run.  False (caller falls back to the key loop) if the run is not
@@ -1856,13 +1829,6 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 //     dependent binary search plus a one-load-per-step run scan.
 // =============================================================================================
 #define PROBE_GROUP_RECS 2048
-// DevIndex::khash line of a key: the key scrambled by an odd constant (a bijection), reduced to
-// [0, lines) by the high half of a 64-bit product
-__device__ __forceinline__ uint64_t khash_line(uint32_t key, uint64_t lines)
-{
-	return ((uint64_t)(key * 0x9E3779B1u) * lines) >> 32;
-}
-
 #define IMG_LINE  0
 #define IMG_CODE  1
 #define IMG_KHASH 2
@@ -1902,37 +1868,7 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 						const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic), b = key - q * ix.nb;
 						st_i += ix.bstart[b + 1] - ix.bstart[b];
 					}
-					if (key == 0xffffffffu) {
-						if (ix.khash_ff[0]) rec = make_uint2(ix.khash_ff[1], ix.khash_ff[2]);
-					} else {
-						uint64_t L = khash_line(key, ix.khash_lines);
-						if (ix.khash_sec) {
-							for (;;) {
-								const uint4 *l4 = (const uint4 *)(ix.khash + 8 * L);
-								const uint4 a = l4[0], b4 = l4[1];
-								const uint32_t ks[3] = {a.x, a.y, a.z}, mid[3] = {a.w, b4.x, b4.y};
-								const uint32_t fb[3] = {b4.z & 0xffffu, b4.z >> 16, b4.w & 0xffffu};
-								bool found = false;
-#pragma unroll
-								for (int k = 0; k < 3; k++)
-									if (ks[k] == key) { rec = make_uint2(mid[k], (fb[k] & 0xffu) | ((fb[k] >> 8) << 16)); found = true; }
-								if (found || !(b4.w >> 16)) break;
-								L = L + 1 == ix.khash_lines ? 0 : L + 1;
-							}
-						} else for (;;) {
-							const uint4 *l4 = (const uint4 *)(ix.khash + 16 * L);
-							const uint4 a = l4[0], b4 = l4[1], c4 = l4[2], d4 = l4[3];
-							const uint32_t ks[5] = {a.x, a.y, a.z, a.w, b4.x};
-							const uint32_t px[5] = {b4.y, b4.w, c4.y, c4.w, d4.y};
-							const uint32_t py[5] = {b4.z, c4.x, c4.z, d4.x, d4.z};
-							bool found = false;
-#pragma unroll
-							for (int k = 0; k < 5; k++)
-								if (ks[k] == key) { rec = make_uint2(px[k], py[k]); found = true; }
-							if (found || !d4.w) break;
-							L = L + 1 == ix.khash_lines ? 0 : L + 1;
-						}
-					}
+					khash_find(ix, key, rec);
 					if (pp.stats) st_h += (rec.y & 0xffffu) + (rec.y >> 16);
 				} else if (CODE && probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
 					const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
@@ -2289,6 +2225,24 @@ __global__ void __launch_bounds__(256) build_khash(const uint32_t *bstart, const
 	}
 }
 
+// DevIndex::ksorted: one bit per bucket, set when the bucket's keys are non-decreasing as shorts
+__global__ void __launch_bounds__(256) build_ksorted(const uint32_t *bstart, const int16_t *keys, uint32_t nb, uint32_t *bits)
+{
+	const uint32_t nw = (nb + 31) / 32;
+	for (uint32_t w = blockIdx.x * 256u + threadIdx.x; w < nw; w += gridDim.x * 256u) {
+		uint32_t m = 0;
+		for (uint32_t k = 0; k < 32; k++) {
+			const uint32_t b = w * 32 + k;
+			if (b >= nb) break;
+			const uint32_t first = bstart[b], n = bstart[b + 1] - first;
+			bool ok = true;
+			for (uint32_t j = 1; j < n && ok; j++) ok = keys[first + j - 1] <= keys[first + j];
+			m |= (ok ? 1u : 0u) << k;
+		}
+		bits[w] = m;
+	}
+}
+
 // DevIndex::bline: one 64-byte line per bucket (first item, count, the u8 keys of <= 59 items)
 __global__ void __launch_bounds__(256) build_bline(const uint32_t *bstart, const int16_t *keys, uint32_t nb, uint4 *bline)
 {
@@ -2358,6 +2312,7 @@ int svg_index_finish_device(svg_index *h)
 	h->dix.khash_ff = NULL;
 	h->dix.khash_lines = 0;
 	h->dix.khash_sec = 0;
+	h->dix.ksorted = NULL;
 	{
 		// 32-byte bucket codes when the key_hi range is small enough for them to hold ordinary
 		// buckets (V = 47 at nb = 93,018,839, the -F -B full index): n + V <= 216 bits
@@ -2417,6 +2372,19 @@ int svg_index_finish_device(svg_index *h)
 			h->dix.khash_ff = ff;
 			h->dix.khash_lines = lines;
 			h->dix.khash_sec = sec;
+		}
+		// which buckets are sorted: there the key-hash record is cellCounts' equal-key run too
+		if (h->dix.khash && dmalloc(h, &h->d_ksorted, ((size_t)x->nb + 31) / 32 * 4 + 64) == 0) {
+			uint64_t blocks = ((uint64_t)x->nb / 32 + 256) / 256, bmax = (uint64_t)h->n_cu * 64;
+			if (blocks > bmax) blocks = bmax;
+			hipLaunchKernelGGL(build_ksorted, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
+			                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_ksorted);
+			HIPCHK(hipGetLastError());
+			HIPCHK(hipStreamSynchronize(h->stream));
+			h->dix.ksorted = (const uint32_t *)h->d_ksorted;
+		} else if (h->dix.khash) {
+			h->d_ksorted = NULL;
+			(void)hipGetLastError();
 		}
 	}
 	if (!h->dix.bcode && !h->dix.khash && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_BLINE")) {
@@ -2567,7 +2535,7 @@ extern "C" void svg_index_close(svg_index *h)
 			for (int j = 0; j < 2; j++)
 				if (h->tev[k][i][j]) hipEventDestroy(h->tev[k][i][j]);
 	hipFree(h->d_bstart); hipFree(h->d_keys); hipFree(h->d_vals); hipFree(h->d_values); hipFree(h->d_chr);
-	hipFree(h->d_bgrp); hipFree(h->d_keys8); hipFree(h->d_bline); hipFree(h->d_bcode); hipFree(h->d_khash);
+	hipFree(h->d_bgrp); hipFree(h->d_keys8); hipFree(h->d_bline); hipFree(h->d_bcode); hipFree(h->d_khash); hipFree(h->d_ksorted);
 	hipFree(h->d_scratch); hipFree(h->d_stats); hipFree(h->d_err);
 	if (h->ev_last) hipEventDestroy(h->ev_last);
 	if (h->stream) hipStreamDestroy(h->stream);
