@@ -198,6 +198,7 @@ template <int ENDS, int MAXL, int MAXP, bool SJ>
 struct Wave {
 #ifdef SVG_STAMPS
 	unsigned long long t_last, acc[8];
+	unsigned long long why[4];   // batch mode's serial candidates by reason (stats[28..31])
 #endif
 	WaveLDS<ENDS, MAXL, MAXP, SJ> *L;
 	uint32_t *cold[2];      // [ENDS] cold slot state
@@ -486,23 +487,45 @@ struct Wave {
 		const unsigned long long dupm = ballot(act && below != 0ull && kprev == kP1);
 		const bool isB = bcand && !nbfar && (eqm & ~ballot(bcand)) == 0ull && (eqm & dupm) == 0ull;
 		const unsigned long long grp = eqm;
-		const bool nb = nbfar || __popcll(eqm) > 1;
+		// A: no slot within the tolerance and nothing else within 2*tol but candidates of the same kv
+		// with distinct kP1 -- in order, the first opens a slot and the rest vote on it exactly, so
+		// the group settles as one new slot holding its whole fold (a lone candidate is the group
+		// of one)
+		const bool opener = act && nmatch == 0 && !nbfar && (eqm & dupm) == 0ull;
 		// serial: matches batch mode cannot settle, crowded openers, B groups that did not qualify
-		bool dep = act && !isB && (nmatch > 0 || nb);
-		const unsigned long long bd = ballot(dep);
+		const bool dep1 = act && !isB && !opener;
+		const unsigned long long bd = ballot(dep1);
 		const unsigned long long le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1ull);
-		dep = act && !isB && (same & bd & le) != 0ull;   // an opener after a serial candidate of its row
-		const bool inr = act && !isB && !dep && kv >= kp->low && kv <= high_b;
+		// a group's first candidate after a serial candidate of its row would open its slot out of
+		// order: it replays, and the rest of its group with it (they vote on its slot; their own
+		// place in the row does not matter -- they open nothing)
+		const bool lead = opener && below == 0ull;
+		const bool depL = lead && (same & bd & le) != 0ull;
+		const unsigned long long dlm = ballot(depL);
+		const bool dep = dep1 || depL || (opener && (eqm & dlm) != 0ull);
+#ifdef SVG_STAMPS
+		{   // ballots with every lane active; the counts are wave-uniform
+			const int w0 = __popcll(ballot(dep && nmatch >= 2)), w1 = __popcll(ballot(dep && nmatch == 1 && !bcand));
+			const int w2 = __popcll(ballot(dep && bcand)), w3 = __popcll(ballot(dep && nmatch == 0));
+			why[0] += w0; why[1] += w1; why[2] += w2; why[3] += w3;
+		}
+#endif
+		// the group's first candidate opens the slot (rank among the row's openers); the group's
+		// last one gives last and coverage end; all of its votes are in
+		const int lastl = eqm ? 63 - __clzll((long long)eqm) : lane;
+		const int kl = __shfl(kP1, lastl), ol = __shfl(off, lastl);
+		const bool inr = lead && !dep && kv >= kp->low && kv <= high_b;
 		const unsigned long long cm = ballot(inr);
 		const int rank = __popcll(same & cm & (le >> 1));
 		const bool mk = inr && n0 + rank < SPACE;
 		if (lane < 32) L->rnew[lane] = 0xff;
 		wsync();
-		if (mk) {
-			const int x = gap_x(off, kp->ix.gap);
-			L->pm[(int)r0 * SPACE + n0 + rank] = make_uint2(kv, m_pack_u(1, kP1, 0, x, kP1, x));   // no cold state
-		}
 		int nv = 0;
+		if (mk) {
+			nv = __popcll(eqm);
+			L->pm[(int)r0 * SPACE + n0 + rank] =
+				make_uint2(kv, m_pack_u(nv, kl, 0, gap_x(ol, kp->ix.gap), kP1, gap_x(off, kp->ix.gap)));   // no cold state
+		}
 		if (isB && (grp & ~le) == 0ull) {   // the group's last vote: votes += group size, last = its kP1
 			nv = m_votes(tM) + __popcll(grp);
 			L->pm[tslot].y = m_pack_u(nv, kP1, m_shift(tM), gap_x(off, kp->ix.gap), m_first(tM), m_fx(tM));
@@ -513,7 +536,6 @@ struct Wave {
 			const int v = L->rnew[lane & 31];
 			if (v != 0xff) items_v = v;
 		}
-		if (ballot(mk) && max_vote[E] == 0) max_vote[E] = 1;
 		for (int o = 32; o; o >>= 1) { const int t = __shfl_xor(nv, o); nv = t > nv ? t : nv; }
 		if (max_vote[E] < nv) max_vote[E] = nv;
 		wsync();
@@ -1483,6 +1505,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	W.ovf = base + per_end * ENDS;
 #ifdef SVG_STAMPS
 	for (int k = 0; k < 8; k++) W.acc[k] = 0;
+	for (int k = 0; k < 4; k++) W.why[k] = 0;
 	W.t_last = __builtin_amdgcn_s_memtime();
 #endif
 	W.st_probes = W.st_items = W.st_hits = W.st_results = W.st_batch = W.st_serial = 0;
@@ -1517,6 +1540,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 #ifdef SVG_STAMPS
 	if (kp.stats && lane_id() == 0)
 		for (int k = 0; k < 8; k++) atomicAdd(&kp.stats[8 + k], W.acc[k]);
+	if (kp.stats && lane_id() == 0)
+		for (int k = 0; k < 4; k++) atomicAdd(&kp.stats[28 + k], W.why[k]);
 #endif
 	if (kp.stats) {
 		unsigned long long a = W.st_items, h = W.st_hits;

@@ -59,6 +59,8 @@ def main():
             names[k], 100.0 * c[8 + k] / max(1, tot), c[8 + k] / n, c[8 + k] / nd))
     print("  lane pass: defer cap/len %d, slots %d, shift %d, candidates %d, deferrals %d" % tuple(c[16:21]))
     print("  wave kernel: batch-settled %d, serially replayed %d" % (c[26], c[27]))
+    print("  serial by reason: >= 2 slots in tolerance %d, one slot but spilled / d != 0 / kP1 <= last %d, "
+          "exact vote whose group failed %d, opener with a neighbour or after a serial one in its row %d" % tuple(c[28:32]))
 
 
 if __name__ == "__main__":
