@@ -197,7 +197,7 @@ struct ReadCtx {
 template <int ENDS, int MAXL, int MAXP, bool SJ>
 struct Wave {
 #ifdef SVG_STAMPS
-	unsigned long long t_last, acc[8];
+	unsigned long long t_last, acc[12];   // [8..11]: phase K split (top-3, simples, pairs, emission)
 	unsigned long long why[4];   // batch mode's serial candidates by reason (stats[28..31])
 #endif
 	WaveLDS<ENDS, MAXL, MAXP, SJ> *L;
@@ -1020,6 +1020,7 @@ struct Wave {
 				bound = best;
 			}
 		}
+		STAMP(8);
 		// candidate lists (simples)
 		for (int e = 0; e < ENDS; e++) {
 			int ns = 0;
@@ -1077,6 +1078,7 @@ struct Wave {
 			if constexpr (SJ) { if (lane < 12) L->jtmp[e][lane / 4][lane % 4] = 0; }
 		}
 		wsync();
+		STAMP(9);
 		int cur[2] = {0, 0};
 		int ncomb = 0;
 		if (ENDS == 2) {
@@ -1164,6 +1166,7 @@ struct Wave {
 				}
 			}
 		}
+		STAMP(10);
 		if (ncomb == 0) {
 			if (nsimp[0] == 0 && lane == 0) rec_set_noninf(L->res[0][0], 0);
 			if (ENDS == 2 && nsimp[ENDS - 1] == 0 && lane == 0) rec_set_noninf(L->res[ENDS - 1][0], 0);
@@ -1504,7 +1507,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	}
 	W.ovf = base + per_end * ENDS;
 #ifdef SVG_STAMPS
-	for (int k = 0; k < 8; k++) W.acc[k] = 0;
+	for (int k = 0; k < 12; k++) W.acc[k] = 0;
 	for (int k = 0; k < 4; k++) W.why[k] = 0;
 	W.t_last = __builtin_amdgcn_s_memtime();
 #endif
@@ -1538,10 +1541,11 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 #endif
 	}
 #ifdef SVG_STAMPS
-	if (kp.stats && lane_id() == 0)
+	if (kp.stats && lane_id() == 0) {
 		for (int k = 0; k < 8; k++) atomicAdd(&kp.stats[8 + k], W.acc[k]);
-	if (kp.stats && lane_id() == 0)
+		for (int k = 8; k < 12; k++) atomicAdd(&kp.stats[21 + k - 8], W.acc[k]);
 		for (int k = 0; k < 4; k++) atomicAdd(&kp.stats[28 + k], W.why[k]);
+	}
 #endif
 	if (kp.stats) {
 		unsigned long long a = W.st_items, h = W.st_hits;
@@ -2801,7 +2805,11 @@ static int launch_vote(svg_index *h, KParams &kp, hipStream_t st, int npmax, boo
 			if (ends == 2) return npmax <= 64 ? launch_t<2, 1216, 64, 2, 4, true>(h, kp, st) : launch_t<2, 1216, 192, 2, 4, true>(h, kp, st);
 			return npmax <= 64 ? launch_t<1, 1216, 64, 2, 4, true>(h, kp, st) : launch_t<1, 1216, 192, 2, 4, true>(h, kp, st);
 		}
-		if (ends == 2) return npmax <= 32 ? launch_t<2, 256, 32, 2, 4, true>(h, kp, st) : launch_t<2, 256, 64, 2, 4, true>(h, kp, st);
+#ifndef SVG_PESJ_OCC
+#define SVG_PESJ_OCC 4
+#endif
+		if (ends == 2)
+			return npmax <= 32 ? launch_t<2, 256, 32, 2, SVG_PESJ_OCC, true>(h, kp, st) : launch_t<2, 256, 64, 2, SVG_PESJ_OCC, true>(h, kp, st);
 		return npmax <= 32 ? launch_t<1, 256, 32, 2, 4, true>(h, kp, st) : launch_t<1, 256, 64, 2, 4, true>(h, kp, st);
 	}
 	if (h->max_read_len > 256 || npmax > 64) {
@@ -2814,7 +2822,7 @@ static int launch_vote(svg_index *h, KParams &kp, hipStream_t st, int npmax, boo
 #define SVG_WAVE_CAP 6   // C3: 317 (uncapped, 10) -> 328 Mreads/s; 4 and 3 starve the wave kernel
 #endif
 #ifndef SVG_SE_OCC
-#define SVG_SE_OCC 5
+#define SVG_SE_OCC 6   // 80 VGPRs: the wave kernel shares the CUs with the next chunk's probe / lane kernels (C3: OCC 4 139, 5 116, 6 108, 8 134 ms/step)
 #endif
 	return npmax <= 32 ? launch_t<1, 256, 32, 2, SVG_SE_OCC, false>(h, kp, st) : launch_t<1, 256, 64, 2, SVG_SE_OCC, false>(h, kp, st);
 }
