@@ -1,0 +1,6 @@
+# GPU box: the round-end tiers on the current tree -- every -m gpu test, smoke(), one default bench.py
+# run; logs and the JSON line under gpurun_out/
+mkdir -p gpurun_out
+timeout -k 10 780 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
+timeout -k 10 400 python -u bench.py "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err
