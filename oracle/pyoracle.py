@@ -48,6 +48,9 @@ def lib():
         L.svo_fragile_batch.restype = ctypes.c_int
         L.svo_fragile_batch.argtypes = [ctypes.c_void_p] * 5
         L.svo_fragile_free.argtypes = [ctypes.c_void_p]
+        L.svo_long_vote_batch.restype = ctypes.c_int
+        L.svo_long_vote_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        L.svo_long_free.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -128,3 +131,17 @@ class OracleIndex:
             return res.arrays()
         finally:
             lib().svo_fragile_free(ctypes.byref(res))
+
+    def long_vote(self, reads, threads=None):
+        """svo_long_vote_batch: sublong's voting step restated (svg_long_vote_batch's form)
+        -> (vstart, votes, order)."""
+        from subread_amd.abi import SvgLongResult
+        s = reads.struct()
+        res = SvgLongResult()
+        rc = lib().svo_long_vote_batch(self.h, ctypes.byref(s), int(threads or os.cpu_count() or 1), ctypes.byref(res))
+        if rc != 0:
+            raise RuntimeError("svo_long_vote_batch failed: %d" % rc)
+        try:
+            return res.arrays()
+        finally:
+            lib().svo_long_free(ctypes.byref(res))

@@ -29,6 +29,7 @@
  *                     match_chro / gvindex_get      gene-value-index.c:856-959, 96-107
  *   index files       gehash_load                   sorted-hashtable.c:1390-1625
  *   cellCounts lists  prefill_votes                 cell-counts.c:432-491
+ *   sublong voting    LRMdo_one_voting_read / go_QQ  longread-one/longread-mapping.c:552, LRMsorted-hashtable.c:443
  *                     gvindex_load                  gene-value-index.c:190-228
  *                     load_offsets                  gene-algorithms.c:1293-1370
  */
@@ -1361,4 +1362,219 @@ void svo_fragile_free(svg_fragile_result *r)
 	if (!r) return;
 	free(r->windows); free(r->slots);
 	r->windows = NULL; r->slots = NULL; r->n_windows = r->n_slots = 0;
+}
+
+/* ------------------------------------------------------------------ sublong's voting step
+ * Restated from the reference's long-read aligner (src/longread-one):
+ *   LRMdo_one_voting_read      longread-mapping.c:552-560 (strand 0, then LRMreverse_read)
+ *   subread offsets            LRMcalc_total_subreads / LRMcalc_subread_start, :516-538
+ *   16-mer key                 LRMgenekey2int, LRMfile-io.c:22-31; LRMbase2int, LRMconfig.h:279
+ *   probe + tally              LRMgehash_go_QQ, LRMsorted-hashtable.c:443-518
+ *   copy                       LRMcopy_longvotes_to_itr, longread-mapping.c:668-682
+ *   location sort              LRMmerge_sort (LRMhelper.c:6-43) with the location compare /
+ *                              exchange / merge of longread-mapping.c:562-622
+ * Block 0 of the index only (LRMload_index, longread-mapping.c:377-388). */
+#include "subread_long.h"
+#define LR_ROWS 64973
+#define LR_SPACE 51
+
+typedef struct {
+	uint16_t items[LR_ROWS];
+	uint32_t pos[LR_ROWS][LR_SPACE];
+	uint16_t votes[LR_ROWS][LR_SPACE];
+	uint8_t neg[LR_ROWS][LR_SPACE];
+	uint32_t cs[LR_ROWS][LR_SPACE], ce[LR_ROWS][LR_SPACE];
+} lvtab_t;
+
+static inline char lr_conv(char c)
+{
+	return c == 'A' ? 'T' : c == 'C' ? 'G' : c == 'G' ? 'C' : (c == 'T' || c == 'U') ? 'A' : 'N';
+}
+
+/* one subread: the bucket search, then every item of the equal-key run votes */
+static void lr_probe(const svo_index *ix, uint32_t key, int offset, int neg, lvtab_t *v)
+{
+	const uint32_t b = key % ix->nb, base = ix->bstart[b];
+	const int items = (int)(ix->bstart[b + 1] - base);
+	const int16_t *ck = ix->keys + base, k = (int16_t)(key / ix->nb);
+	if (!items) return;
+	int lo = 0, hi = items, at = 0;
+	while (lo < items) {
+		at = (lo + hi) / 2;
+		if (ck[at] > k) hi = at - 1;
+		else if (ck[at] < k) lo = at + 1;
+		else break;
+		if (hi < lo) return;
+	}
+	while (at > 0 && ck[at - 1] == k) at--;
+	for (; at < items && ck[at] == k; at++) {
+		const uint32_t kv = ix->vals[base + (uint32_t)at] - (uint32_t)offset;
+		const uint32_t row = kv % LR_ROWS;
+		const int used = v->items[row];
+		int s;
+		for (s = 0; s < used; s++)
+			if (v->pos[row][s] == kv && v->neg[row][s] == neg && (uint32_t)offset < v->ce[row][s] + 14u) break;
+		if (s < used) {
+			v->votes[row][s]++;
+			if ((uint32_t)(offset + 16) > v->ce[row][s]) v->ce[row][s] = (uint32_t)(offset + 16);
+		} else if (used < LR_SPACE) {
+			v->items[row] = (uint16_t)(used + 1);
+			v->pos[row][used] = kv;
+			v->neg[row][used] = (uint8_t)neg;
+			v->votes[row][used] = 1;
+			v->cs[row][used] = (uint32_t)offset;
+			v->ce[row][used] = (uint32_t)(offset + 16);
+		}
+	}
+}
+
+static void lr_vote_read(const svo_index *ix, const char *seq, uint32_t L, lvtab_t *v, char *rev)
+{
+	memset(v->items, 0, sizeof v->items);
+	if (L < 16) return;
+	int S = (int)((L - 16 + 1) / 3);
+	if (S > 1200000) S = 1200000;
+	const double gap = S > 1 ? (double)(L - 16) * 1.0 / (double)(S - 1) + 0.000001 : 0.0;
+	for (uint32_t j = 0; j < L; j++) rev[j] = lr_conv(seq[L - 1 - j]);
+	for (int neg = 0; neg < 2; neg++) {
+		const char *t = neg ? rev : seq;
+		for (int i = 0; i < S; i++) {
+			const int off = i < S - 1 ? (int)(gap * i) : (int)L - 16;
+			uint32_t key = 0;
+			for (int q = 0; q < 16; q++) key |= b2i(t[off + q]) << (30 - 2 * q);
+			lr_probe(ix, key, off, neg, v);
+		}
+	}
+}
+
+/* LRMmerge_sort's recursion over (key, idx) pairs */
+static void lr_sort(uint32_t *key, uint32_t *idx, uint32_t *tk, uint32_t *ti, int start, int items)
+{
+	if (items > 6) {
+		const int h = items / 2;
+		lr_sort(key, idx, tk, ti, start, h);
+		lr_sort(key, idx, tk, ti, start + h, items - h);
+		int a = start, b = start + h, w = 0;
+		while (w < items) {
+			const int left = a < start + h && (b >= start + items || key[a] < key[b]);
+			const int from = left ? a++ : b++;
+			tk[w] = key[from]; ti[w] = idx[from]; w++;
+		}
+		memcpy(key + start, tk, sizeof(uint32_t) * (size_t)items);
+		memcpy(idx + start, ti, sizeof(uint32_t) * (size_t)items);
+		return;
+	}
+	for (int i = start; i < start + items - 1; i++) {
+		int m = i;
+		for (int j = i + 1; j < start + items; j++)
+			if (key[m] > key[j]) m = j;
+		if (m != i) {
+			uint32_t t = key[i]; key[i] = key[m]; key[m] = t;
+			t = idx[i]; idx[i] = idx[m]; idx[m] = t;
+		}
+	}
+}
+
+typedef struct {
+	const svo_index *ix;
+	const svg_long_reads *R;
+	uint64_t r0, r1;
+	svg_long_vote *votes;     /* per worker, grown */
+	uint32_t *order;
+	uint64_t n, cap;
+	uint64_t *count;          /* per read (global array) */
+	int rc;
+} lr_job;
+
+static void *lr_worker(void *arg)
+{
+	lr_job *J = arg;
+	lvtab_t *v = malloc(sizeof *v);
+	char *rev = malloc(SVG_LONG_MAX_READ_LENGTH);
+	uint32_t *key = NULL, *idx = NULL, *tk = NULL, *ti = NULL;
+	size_t kcap = 0;
+	if (!v || !rev) { J->rc = SVG_E_NOMEM; free(v); free(rev); return NULL; }
+	for (uint64_t r = J->r0; r < J->r1; r++) {
+		const uint32_t L = J->R->lens[r];
+		lr_vote_read(J->ix, J->R->seq + J->R->offsets[r], L, v, rev);
+		uint64_t n = 0;
+		for (int row = 0; row < LR_ROWS; row++) n += v->items[row];
+		if (J->n + n > J->cap) {
+			J->cap = (J->n + n) * 2 + 1024;
+			J->votes = realloc(J->votes, sizeof(svg_long_vote) * J->cap);
+			J->order = realloc(J->order, sizeof(uint32_t) * J->cap);
+		}
+		if (n > kcap) {
+			kcap = n * 2;
+			key = realloc(key, 4 * kcap); idx = realloc(idx, 4 * kcap);
+			tk = realloc(tk, 4 * kcap); ti = realloc(ti, 4 * kcap);
+		}
+		svg_long_vote *o = J->votes + J->n;
+		uint64_t k = 0;
+		for (int row = 0; row < LR_ROWS; row++)
+			for (int s = 0; s < v->items[row]; s++, k++) {
+				o[k].pos = v->pos[row][s];
+				o[k].coverage_start = v->cs[row][s];
+				o[k].coverage_end = v->ce[row][s];
+				o[k].votes = v->votes[row][s];
+				o[k].negative = v->neg[row][s];
+				o[k]._pad = 0;
+				o[k].slot = (uint32_t)row << 16 | (uint32_t)s;
+				key[k] = o[k].pos + o[k].coverage_start;
+				idx[k] = (uint32_t)k;
+			}
+		lr_sort(key, idx, tk, ti, 0, (int)n);
+		memcpy(J->order + J->n, idx, 4 * n);
+		J->n += n;
+		J->count[r] = n;
+	}
+	free(v); free(rev); free(key); free(idx); free(tk); free(ti);
+	return NULL;
+}
+
+/* svg_long_vote_batch's result (malloc'ed: free with svo_long_free) */
+int svo_long_vote_batch(const svo_index *ix, const svg_long_reads *R, int threads, svg_long_result *out)
+{
+	memset(out, 0, sizeof *out);
+	if (!ix || !R) return SVG_E_ARG;
+	for (uint64_t r = 0; r < R->n_reads; r++)
+		if (R->lens[r] > SVG_LONG_READ_KEEP) return SVG_E_ARG;
+	if (threads < 1) threads = 1;
+	if ((uint64_t)threads > R->n_reads) threads = R->n_reads ? (int)R->n_reads : 1;
+	lr_job *J = calloc((size_t)threads, sizeof *J);
+	pthread_t *tid = calloc((size_t)threads, sizeof *tid);
+	uint64_t *count = calloc(R->n_reads + 1, 8);
+	for (int t = 0; t < threads; t++) {
+		J[t].ix = ix; J[t].R = R; J[t].count = count;
+		J[t].r0 = R->n_reads * (uint64_t)t / (uint64_t)threads;
+		J[t].r1 = R->n_reads * (uint64_t)(t + 1) / (uint64_t)threads;
+		pthread_create(&tid[t], NULL, lr_worker, &J[t]);
+	}
+	uint64_t total = 0;
+	int rc = 0;
+	for (int t = 0; t < threads; t++) { pthread_join(tid[t], NULL); total += J[t].n; if (J[t].rc) rc = J[t].rc; }
+	out->n_reads = R->n_reads;
+	out->vstart = malloc(8 * (R->n_reads + 1));
+	out->votes = malloc(sizeof(svg_long_vote) * (total + 1));
+	out->order = malloc(4 * (total + 1));
+	out->vstart[0] = 0;
+	for (uint64_t r = 0; r < R->n_reads; r++) out->vstart[r + 1] = out->vstart[r] + count[r];
+	uint64_t w = 0;
+	for (int t = 0; t < threads; t++) {
+		if (J[t].n) {
+			memcpy(out->votes + w, J[t].votes, sizeof(svg_long_vote) * J[t].n);
+			memcpy(out->order + w, J[t].order, 4 * J[t].n);
+		}
+		w += J[t].n;
+		free(J[t].votes); free(J[t].order);
+	}
+	free(J); free(tid); free(count);
+	return rc;
+}
+
+void svo_long_free(svg_long_result *r)
+{
+	if (!r) return;
+	free(r->vstart); free(r->votes); free(r->order);
+	memset(r, 0, sizeof *r);
 }

@@ -33,6 +33,8 @@ EXPORTS = [
     "svg_get_kernel_timing", "svg_device_status", "svg_pack_reads", "svg_vote_batch_packed",
     "svg_vote_batch_packed_device", "svg_probe_keys", "svg_probe_keys_device", "svg_host_threads",
     "svg_fragile_batch", "svg_fragile_free",
+    # sublong's voting step (include/subread_long.h)
+    "svg_long_vote_batch", "svg_long_free",
     # host post-vote events (include/subread_events.h)
     "svg_event_params_default", "svg_genome_arrays_open", "svg_genome_arrays_close", "svg_events_create",
     "svg_events_destroy", "svg_events_add_batch", "svg_events_merge", "svg_events_count", "svg_events_get",
@@ -104,6 +106,9 @@ def lib():
         L.svg_fragile_batch.argtypes = [vp] * 5
         L.svg_fragile_batch.restype = i32
         L.svg_fragile_free.argtypes = [vp]
+        L.svg_long_vote_batch.argtypes = [vp] * 3
+        L.svg_long_vote_batch.restype = i32
+        L.svg_long_free.argtypes = [vp]
         L.svg_events_add_batch2.argtypes = [vp] * 8 + [u64] + [vp] * 4
         L.svg_events_add_batch2.restype = i32
         L.svg_index_build.argtypes = [ctypes.c_char_p, i32, i32, i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
@@ -382,6 +387,19 @@ class VoteIndex:
             return res.arrays()
         finally:
             lib().svg_fragile_free(ctypes.byref(res))
+
+    def long_vote(self, reads):
+        """svg_long_vote_batch: sublong's voting step (LRMdo_one_voting_read + the copy and location
+        sort, longread-mapping.c:552,668,1317) for a LongReads batch -> (vstart, votes, order)."""
+        from .abi import SvgLongResult
+        s = reads.struct()
+        res = SvgLongResult()
+        rc = lib().svg_long_vote_batch(self.h, ctypes.byref(s), ctypes.byref(res))
+        _check(rc, "svg_long_vote_batch")
+        try:
+            return res.arrays()
+        finally:
+            lib().svg_long_free(ctypes.byref(res))
 
     def set_max_read_length(self, n):
         _check(lib().svg_set_max_read_length(self.h, int(n)), "svg_set_max_read_length")

@@ -160,6 +160,75 @@ class SvgFragileResult(ctypes.Structure):
         return r
 
 
+# svg_long_vote (include/subread_long.h): one used slot of sublong's LRMgene_vote_t
+LONG_VOTE_DTYPE = np.dtype([("pos", "<u4"), ("coverage_start", "<u4"), ("coverage_end", "<u4"),
+                            ("votes", "<u2"), ("negative", "u1"), ("_pad", "u1"), ("slot", "<u4")])
+assert LONG_VOTE_DTYPE.itemsize == 20
+
+
+class LongReads:
+    """sublong's reads (svg_long_reads): concatenated ASCII, u64 offsets, u32 lengths."""
+
+    def __init__(self, seq, offsets, lens):
+        self.seq = np.ascontiguousarray(seq, dtype=np.uint8)
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        assert self.offsets.shape == self.lens.shape
+
+    @classmethod
+    def from_list(cls, reads):
+        reads = [r.encode() if isinstance(r, str) else bytes(r) for r in reads]
+        lens = np.array([len(r) for r in reads], dtype=np.uint32)
+        offs = np.zeros(len(reads), dtype=np.uint64)
+        if len(reads) > 1:
+            offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        seq = np.frombuffer(b"".join(reads), dtype=np.uint8) if reads else np.zeros(0, np.uint8)
+        return cls(seq, offs, lens)
+
+    def __len__(self):
+        return int(self.lens.shape[0])
+
+    def read(self, i):
+        o = int(self.offsets[i])
+        return bytes(self.seq[o:o + int(self.lens[i])])
+
+    def slice(self, a, b):
+        return LongReads(self.seq, self.offsets[a:b], self.lens[a:b])
+
+    def struct(self):
+        s = SvgLongReads()
+        s.seq = self.seq.ctypes.data if self.seq.size else None
+        s.offsets = self.offsets.ctypes.data if len(self) else None
+        s.lens = self.lens.ctypes.data if len(self) else None
+        s.n_reads = len(self)
+        s._keep = self
+        return s
+
+
+class SvgLongReads(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("lens", ctypes.c_void_p),
+                ("n_reads", ctypes.c_uint64)]
+
+
+class SvgLongResult(ctypes.Structure):
+    _fields_ = [("n_reads", ctypes.c_uint64), ("vstart", ctypes.c_void_p), ("votes", ctypes.c_void_p),
+                ("order", ctypes.c_void_p)]
+
+    def arrays(self):
+        """Copies: (vstart[n+1] u64, votes LONG_VOTE_DTYPE, order u32)."""
+        n = int(self.n_reads)
+        vs = np.zeros(n + 1, np.uint64)
+        if self.vstart:
+            ctypes.memmove(vs.ctypes.data, self.vstart, vs.nbytes)
+        k = int(vs[-1])
+        v = np.zeros(k, LONG_VOTE_DTYPE)
+        o = np.zeros(k, np.uint32)
+        if k:
+            ctypes.memmove(v.ctypes.data, self.votes, v.nbytes)
+            ctypes.memmove(o.ctypes.data, self.order, o.nbytes)
+        return vs, v, o
+
+
 class SvgBatchStats(ctypes.Structure):
     _fields_ = [
         ("probes", ctypes.c_uint64),

@@ -191,6 +191,43 @@ def simulate_pairs(genome, n, length=150, seed=4004, first=0, insert_mean=300.0,
     return ReadBatch.fixed(s1), ReadBatch.fixed(s2)
 
 
+def simulate_long_reads(genome, n, mean_len=3000, seed=71, sub=0.03, ins=0.02, dele=0.02, min_len=200,
+                        max_len=200_000, lengths=None):
+    """Long reads (sublong): lengths log-normal around mean_len (or the given `lengths`), uniform
+    start on a contig long enough, per-base substitutions / insertions / deletions at the given
+    rates (ONT-like), strand 50/50.  Deterministic in (seed, n).  -> LongReads."""
+    from .abi import LongReads
+    rng = np.random.default_rng(seed)
+    if lengths is None:
+        sd = 0.6
+        lengths = np.exp(rng.normal(np.log(mean_len) - sd * sd / 2, sd, n)).astype(np.int64)
+        lengths = np.clip(lengths, min_len, max_len)
+    lengths = np.asarray(lengths, dtype=np.int64)
+    comp = np.full(256, ord("N"), dtype=np.uint8)
+    for a_, b_ in (("A", "T"), ("C", "G"), ("G", "C"), ("T", "A")):
+        comp[ord(a_)] = ord(b_)
+    alphabet = np.frombuffer(b"ACGT", dtype=np.uint8)
+    out = []
+    for i in range(len(lengths)):
+        L = int(lengths[i])
+        span = int(L * (1 + dele - ins)) + 8
+        ok = np.flatnonzero(genome.lens.astype(np.int64) > span + 1)
+        c = int(ok[rng.integers(0, len(ok))])
+        st = int(genome.starts[c]) + int(rng.integers(0, int(genome.lens[c]) - span))
+        seg = genome.flat[st:st + span]
+        u = rng.random(span)
+        op = np.where(u < sub, 1, np.where(u < sub + ins, 2, np.where(u < sub + ins + dele, 3, 0)))
+        base = np.where(op == 1, alphabet[rng.integers(0, 4, span)], seg)
+        keep = op != 3
+        pieces = base[keep]
+        ins_at = np.flatnonzero(op[keep] == 2) + 1
+        r = np.insert(pieces, ins_at, alphabet[rng.integers(0, 4, len(ins_at))])[:L]
+        if rng.random() < 0.5:
+            r = comp[r[::-1]]
+        out.append(r.tobytes())
+    return LongReads.from_list(out)
+
+
 def write_fastq(path, batch, names=None):
     with open(path, "wb") as f:
         for i in range(len(batch)):

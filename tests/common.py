@@ -53,7 +53,27 @@ SYNTH_GENOMES = {
 }
 
 
+# sublong's vote table has 64973 rows of 51 slots: 54 copies of one element exactly 64973 bases
+# apart put 54 positions of every subread of it in the same row (LRMsorted-hashtable.c:503-514)
+LR_ROWS = 64973
+
+
+def lrrow54_genome():
+    from subread_amd.sim import Genome, random_genome
+    g = random_genome([54 * LR_ROWS + 5000, 200000], 5454)
+    a = g.seqs[0].copy()
+    elem = random_genome([2000], 5455).seqs[0]
+    for j in range(54):
+        a[j * LR_ROWS + 1000:j * LR_ROWS + 3000] = elem
+    return Genome(g.names, [a, g.seqs[1]])
+
+
+CUSTOM_GENOMES = {"lrrow54": lrrow54_genome}
+
+
 def synth_genome(gname):
+    if gname in CUSTOM_GENOMES:
+        return CUSTOM_GENOMES[gname]()
     from subread_amd.sim import random_genome
     lengths, seed = SYNTH_GENOMES[gname]
     return random_genome(lengths, seed, repeats=(2500, 300, 16, 0.04))
@@ -92,7 +112,7 @@ class IndexCache:
                 with gzip.open(os.path.join(GOLD, "chr901.fa.gz"), "rb") as f, open(path, "wb") as o:
                     o.write(f.read())
             return path
-        if gname in SYNTH_GENOMES:
+        if gname in SYNTH_GENOMES or gname in CUSTOM_GENOMES:
             path = os.path.join(self.root, gname + ".fa")
             if not os.path.exists(path):
                 synth_genome(gname).write_fasta(path)

@@ -1,5 +1,5 @@
 """CPU: the C-ABI library loads, exports every symbol include/subread_vote.h and
-include/subread_events.h declare, and its host-side pieces behave (no GPU compute here)."""
+include/subread_events.h and include/subread_long.h declare, and its host-side pieces behave (no GPU compute here)."""
 import ctypes
 import re
 import os
@@ -15,7 +15,7 @@ ensure_built()
 
 def header_symbols():
     syms = set()
-    for h in ("subread_vote.h", "subread_events.h"):
+    for h in ("subread_vote.h", "subread_events.h", "subread_long.h"):
         txt = open(os.path.join(ROOT, "include", h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         syms |= set(re.findall(r"\b(svg_[a-z0-9_]+)\s*\(", txt))
