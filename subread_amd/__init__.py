@@ -396,10 +396,8 @@ class VoteIndex:
         res = SvgLongResult()
         rc = lib().svg_long_vote_batch(self.h, ctypes.byref(s), ctypes.byref(res))
         _check(rc, "svg_long_vote_batch")
-        try:
-            return res.arrays()
-        finally:
-            lib().svg_long_free(ctypes.byref(res))
+        # views over the library's arrays (no copy of the ~24 B per slot); freed with the last view
+        return res.views(lambda r: lib().svg_long_free(ctypes.byref(r)))
 
     def set_max_read_length(self, n):
         _check(lib().svg_set_max_read_length(self.h, int(n)), "svg_set_max_read_length")

@@ -210,9 +210,40 @@ class SvgLongReads(ctypes.Structure):
                 ("n_reads", ctypes.c_uint64)]
 
 
+class _Owner:
+    """Frees a library-owned result once every numpy view of it is gone."""
+
+    def __init__(self, res, free):
+        self.res, self.free, self.n = res, free, 3
+
+    def drop(self):
+        self.n -= 1
+        if self.n == 0:
+            self.free(self.res)
+
+
 class SvgLongResult(ctypes.Structure):
     _fields_ = [("n_reads", ctypes.c_uint64), ("vstart", ctypes.c_void_p), ("votes", ctypes.c_void_p),
                 ("order", ctypes.c_void_p)]
+
+    def views(self, free):
+        """(vstart, votes, order) numpy arrays over the library's buffers, no copy; `free(result)`
+        runs when the last of them is garbage-collected."""
+        import weakref
+        n = int(self.n_reads)
+        vs = np.ctypeslib.as_array(ctypes.cast(self.vstart, ctypes.POINTER(ctypes.c_uint64)), (n + 1,))
+        k = int(vs[-1])
+        if k == 0:
+            out = (vs.copy(), np.zeros(0, LONG_VOTE_DTYPE), np.zeros(0, np.uint32))
+            free(self)
+            return out
+        raw = np.ctypeslib.as_array(ctypes.cast(self.votes, ctypes.POINTER(ctypes.c_uint8)), (k * 20,))
+        v = raw.view(LONG_VOTE_DTYPE)
+        o = np.ctypeslib.as_array(ctypes.cast(self.order, ctypes.POINTER(ctypes.c_uint32)), (k,))
+        owner = _Owner(self, free)
+        for a in (vs, raw, o):
+            weakref.finalize(a, owner.drop)
+        return vs, v, o
 
     def arrays(self):
         """Copies: (vstart[n+1] u64, votes LONG_VOTE_DTYPE, order u32)."""

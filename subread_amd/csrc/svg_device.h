@@ -173,6 +173,8 @@ struct svg_index {
 	int nblocks;
 	struct svg_index *blk[SVG_MAX_BLOCKS];
 	int stored;
+	// svg_long_vote_batch's grow-only device arenas and pinned staging (svg_long.hip)
+	struct svg_longws *lws;
 };
 
 #define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) { svg_set_error("HIP error %s at %s:%d", hipGetErrorString(_e), __FILE__, __LINE__); return SVG_E_DEVICE; } } while (0)
@@ -201,6 +203,8 @@ static inline int svg_ensure(svg_index *h, void **p, size_t *cap, size_t need)
 
 // svg_io.hip
 void svg_io_free(svg_index *h);
+// svg_long.hip
+void svg_long_ws_free(svg_index *h);
 
 // ---------------------------------------------------------------------------------------------
 // kernel parameters (passed by value)

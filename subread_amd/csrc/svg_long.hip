@@ -34,8 +34,11 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
+#include <thread>
 #include <vector>
 #include "subread_vote.h"
 #include "subread_long.h"
@@ -281,7 +284,6 @@ struct LEmit {
 	const uint4 *sdata;
 	uint64_t n_seg;
 	svg_long_vote *out;
-	uint32_t *rcount;         // per read of the chunk
 };
 
 __global__ void __launch_bounds__(256) long_emit_kernel(LEmit le)
@@ -299,7 +301,6 @@ __global__ void __launch_bounds__(256) long_emit_kernel(LEmit le)
 	v._pad = 0;
 	v.slot = (uint32_t)(((k >> 32) & 0xffffu) << 16) | (uint32_t)l_rank(le.skey, t);
 	le.out[le.kpos[t]] = v;
-	atomicAdd(&le.rcount[k >> 48], 1u);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -384,32 +385,69 @@ __global__ void __launch_bounds__(256) long_order_kernel(const svg_long_vote *vo
 	for (uint32_t k = threadIdx.x; k < n; k += 256) order[base + k] = AI[k];
 }
 
+// read r's slots start at vstart[r]: the first segment of read r in the sorted order, counted in
+// kept segments before it
+__global__ void __launch_bounds__(256) long_vstart_kernel(const uint64_t *skey, const uint32_t *kpos, uint64_t G, uint64_t K,
+                                                           uint32_t n, uint64_t *vstart)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r > n) return;
+	const uint64_t key = (uint64_t)r << 48;
+	uint64_t lo = 0, hi = G;
+	while (lo < hi) { const uint64_t m = (lo + hi) >> 1; if (skey[m] < key) lo = m + 1; else hi = m; }
+	vstart[r] = lo < G ? (uint64_t)kpos[lo] : K;
+}
+
 // ---------------------------------------------------------------------------------------------
 // host
 
-namespace {
-struct DBuf {
-	svg_index *h;
-	std::vector<void *> ptrs;
-	std::vector<size_t> sizes;
-	explicit DBuf(svg_index *hh) : h(hh) {}
-	~DBuf() { release(); }
-	void release()
-	{
-		for (size_t i = 0; i < ptrs.size(); i++) { hipFree(ptrs[i]); h->device_bytes -= sizes[i]; }
-		ptrs.clear();
-		sizes.clear();
+// grow-only device arenas and pinned staging of the handle (svg_index::lws)
+struct svg_longws {
+	void *dA; size_t capA;     // probe phase: text, read table, probe arrays, scan temp
+	void *dB; size_t capB;     // candidate phase: keys / payloads / segments / slots, sort and scan temps
+	void *hs[2]; size_t hcap;  // pinned staging (uploads and downloads in pieces)
+	hipEvent_t ev[2];
+};
+
+void svg_long_ws_free(svg_index *h)
+{
+	svg_longws *w = h->lws;
+	if (!w) return;
+	hipFree(w->dA); hipFree(w->dB);
+	for (int i = 0; i < 2; i++) {
+		if (w->hs[i]) hipHostFree(w->hs[i]);
+		if (w->ev[i]) hipEventDestroy(w->ev[i]);
 	}
-	template <class T> int get(T **p, size_t n)
+	h->device_bytes -= w->capA + w->capB;
+	free(w);
+	h->lws = NULL;
+}
+
+namespace {
+// bump allocation inside an arena (a dry run with base NULL measures it)
+struct Carve {
+	char *base;
+	size_t off;
+	template <class T> T *take(size_t n)
 	{
-		void *q = NULL;
-		if (dmalloc(h, &q, n * sizeof(T) + 64)) return SVG_E_NOMEM;
-		ptrs.push_back(q);
-		sizes.push_back(n * sizeof(T) + 64);
-		*p = (T *)q;
-		return 0;
+		off = (off + 255) & ~(size_t)255;
+		T *p = (T *)(base ? base + off : NULL);
+		off += n * sizeof(T) + 64;
+		return p;
 	}
 };
+
+int arena(svg_index *h, void **p, size_t *cap, size_t need)
+{
+	if (need <= *cap) return 0;
+	if (*p) { HIPCHK(hipStreamSynchronize(h->stream)); hipFree(*p); h->device_bytes -= *cap; }
+	*p = NULL;
+	*cap = 0;
+	need += need / 4;
+	if (dmalloc(h, p, need)) return SVG_E_NOMEM;
+	*cap = need;
+	return 0;
+}
 
 inline uint32_t lr_subreads(uint32_t L)   // LRMcalc_total_subreads, longread-mapping.c:516-524
 {
@@ -422,14 +460,77 @@ inline unsigned blocks_of(uint64_t n, unsigned per) { return (unsigned)((n + per
 
 #define LCHK(x) do { if ((x) != hipSuccess) { svg_set_error("svg_long_vote_batch: HIP error %s at %s:%d", hipGetErrorString(hipGetLastError()), __FILE__, __LINE__); return SVG_E_DEVICE; } } while (0)
 
-// one chunk of reads [r0, r1): appends its slots and orders to the vectors
-int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, const uint64_t cand_cap,
-               std::vector<svg_long_vote> &votes, std::vector<uint32_t> &order, std::vector<uint64_t> &counts, bool *too_big)
+const size_t PIECE = 64ull << 20;   // bytes per staged transfer
+
+// memcpy split over the host pool's thread count
+void par_copy(void *dst, const void *src, size_t n, int T)
+{
+	if (n < (4u << 20) || T < 2) { memcpy(dst, src, n); return; }
+	std::vector<std::thread> th;
+	const size_t part = (n / (size_t)T + 4095) & ~(size_t)4095;
+	for (int t = 0; t < T; t++) {
+		const size_t a = (size_t)t * part;
+		if (a >= n) break;
+		const size_t b = a + part < n ? a + part : n;
+		th.emplace_back([=] { memcpy((char *)dst + a, (const char *)src + a, b - a); });
+	}
+	for (auto &x : th) x.join();
+}
+
+struct Span { void *dst; const void *src; size_t n; };
+
+// device -> host in pieces through the two pinned buffers: piece i+1 is in flight while the host
+// threads copy piece i to its destination
+int staged_download(svg_index *h, const std::vector<Span> &spans, int T)
+{
+	svg_longws *w = h->lws;
+	hipStream_t st = h->stream;
+	struct Piece { char *dst; const char *src; size_t n; };
+	std::vector<Piece> pcs;
+	for (const Span &s : spans)
+		for (size_t o = 0; o < s.n; o += PIECE)
+			pcs.push_back({(char *)s.dst + o, (const char *)s.src + o, s.n - o < PIECE ? s.n - o : PIECE});
+	for (size_t i = 0; i <= pcs.size(); i++) {
+		if (i < pcs.size()) {
+			LCHK(hipMemcpyAsync(w->hs[i & 1], pcs[i].src, pcs[i].n, hipMemcpyDeviceToHost, st));
+			LCHK(hipEventRecord(w->ev[i & 1], st));
+		}
+		if (i > 0) {
+			const size_t j = i - 1;
+			LCHK(hipEventSynchronize(w->ev[j & 1]));
+			par_copy(pcs[j].dst, w->hs[j & 1], pcs[j].n, T);
+		}
+	}
+	return 0;
+}
+
+struct LOut {
+	svg_long_vote *votes;
+	uint32_t *order;
+	uint64_t n, cap;
+	int reserve(uint64_t add)
+	{
+		if (n + add <= cap) return 0;
+		const uint64_t nc = (n + add) + (n + add) / 2 + 4096;
+		svg_long_vote *v = (svg_long_vote *)realloc(votes, sizeof(svg_long_vote) * nc);
+		if (v) votes = v;
+		uint32_t *o = (uint32_t *)realloc(order, 4 * nc);
+		if (o) order = o;
+		if (!v || !o) { svg_set_error("svg_long_vote_batch: out of host memory"); return SVG_E_NOMEM; }
+		cap = nc;
+		return 0;
+	}
+};
+
+// one chunk of reads [r0, r1): appends its slots, orders and per-read counts
+int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, const uint64_t cand_cap, LOut &res,
+               std::vector<uint64_t> &counts, bool *too_big, int T)
 {
 	hipStream_t st = h->stream;
+	svg_longws *w = h->lws;
 	const uint32_t n = (uint32_t)(r1 - r0);
 	*too_big = false;
-	std::vector<uint64_t> toff(n);
+	std::vector<uint64_t> toff(n + 1);
 	std::vector<uint32_t> len(n), pbase(n + 1);
 	uint64_t tb = 0, P = 0;
 	for (uint32_t i = 0; i < n; i++) {
@@ -440,17 +541,40 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 		pbase[i] = (uint32_t)P;
 		P += 2ull * lr_subreads(L);
 	}
+	toff[n] = tb;
 	pbase[n] = (uint32_t)P;
 	if (P == 0) { for (uint32_t i = 0; i < n; i++) counts.push_back(0); return 0; }
-	std::vector<char> text(tb + 16);
-	for (uint32_t i = 0; i < n; i++) memcpy(&text[toff[i]], R->seq + R->offsets[r0 + i], len[i]);
-	DBuf B(h);
-	char *d_text; uint64_t *d_toff; uint32_t *d_len, *d_pbase;
-	uint64_t *d_pcnt, *d_pcb, *d_pmeta; uint32_t *d_pfirst;
-	if (B.get(&d_text, tb + 16) || B.get(&d_toff, n) || B.get(&d_len, n) || B.get(&d_pbase, n + 1) || B.get(&d_pcnt, P) ||
-	    B.get(&d_pcb, P) || B.get(&d_pmeta, P) || B.get(&d_pfirst, P))
-		return SVG_E_NOMEM;
-	LCHK(hipMemcpyAsync(d_text, text.data(), tb + 16, hipMemcpyHostToDevice, st));
+	// ---- probe phase
+	size_t scan1 = 0;
+	LCHK(hipcub::DeviceScan::ExclusiveSum(NULL, scan1, (uint64_t *)NULL, (uint64_t *)NULL, (int)P, st));
+	Carve ca = {NULL, 0};
+	for (int pass = 0; pass < 2; pass++) {
+		if (pass) { if (int e = arena(h, &w->dA, &w->capA, ca.off)) return e; ca.base = (char *)w->dA; ca.off = 0; }
+		ca.take<char>(tb + 16); ca.take<uint64_t>(n); ca.take<uint32_t>(n); ca.take<uint32_t>(n + 1);
+		ca.take<uint64_t>(P); ca.take<uint64_t>(P); ca.take<uint64_t>(P); ca.take<uint32_t>(P); ca.take<char>(scan1);
+	}
+	ca.off = 0;
+	char *d_text = ca.take<char>(tb + 16);
+	uint64_t *d_toff = ca.take<uint64_t>(n);
+	uint32_t *d_len = ca.take<uint32_t>(n), *d_pbase = ca.take<uint32_t>(n + 1);
+	uint64_t *d_pcnt = ca.take<uint64_t>(P), *d_pcb = ca.take<uint64_t>(P), *d_pmeta = ca.take<uint64_t>(P);
+	uint32_t *d_pfirst = ca.take<uint32_t>(P);
+	void *d_tmp1 = ca.take<char>(scan1);
+	// the chunk's text, read after read, through the pinned staging
+	for (uint64_t a = 0; a < tb; a += PIECE) {
+		const uint64_t b = a + PIECE < tb ? a + PIECE : tb;
+		const int k = (int)((a / PIECE) & 1);
+		LCHK(hipEventSynchronize(w->ev[k]));   // the buffer's previous transfer is done
+		char *stg = (char *)w->hs[k];
+		uint32_t i = (uint32_t)(std::upper_bound(toff.begin(), toff.end(), a) - toff.begin()) - 1;
+		for (uint64_t o = a; o < b; i++) {
+			const uint64_t e = toff[i + 1] < b ? toff[i + 1] : b;
+			par_copy(stg + (o - a), R->seq + R->offsets[r0 + i] + (o - toff[i]), e - o, e - o >= (16u << 20) ? T : 1);
+			o = e;
+		}
+		LCHK(hipMemcpyAsync(d_text + a, stg, b - a, hipMemcpyHostToDevice, st));
+		LCHK(hipEventRecord(w->ev[k], st));
+	}
 	LCHK(hipMemcpyAsync(d_toff, toff.data(), 8ull * n, hipMemcpyHostToDevice, st));
 	LCHK(hipMemcpyAsync(d_len, len.data(), 4ull * n, hipMemcpyHostToDevice, st));
 	LCHK(hipMemcpyAsync(d_pbase, pbase.data(), 4ull * (n + 1), hipMemcpyHostToDevice, st));
@@ -464,12 +588,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 		hipLaunchKernelGGL(long_probe_kernel<LIMG_KHASH>, dim3(blocks_of(P, 256)), dim3(256), 0, st, lp);
 	else hipLaunchKernelGGL(long_probe_kernel<LIMG_LITERAL>, dim3(blocks_of(P, 256)), dim3(256), 0, st, lp);
 	LCHK(hipGetLastError());
-	// candidate bases
-	size_t tmp_bytes = 0;
-	void *d_tmp = NULL;
-	LCHK(hipcub::DeviceScan::ExclusiveSum(NULL, tmp_bytes, d_pcnt, d_pcb, (int)P, st));
-	if (B.get((char **)&d_tmp, tmp_bytes)) return SVG_E_NOMEM;
-	LCHK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, d_pcnt, d_pcb, (int)P, st));
+	LCHK(hipcub::DeviceScan::ExclusiveSum(d_tmp1, scan1, d_pcnt, d_pcb, (int)P, st));
 	uint64_t last[2];
 	LCHK(hipMemcpyAsync(&last[0], d_pcb + P - 1, 8, hipMemcpyDeviceToHost, st));
 	LCHK(hipMemcpyAsync(&last[1], d_pcnt + P - 1, 8, hipMemcpyDeviceToHost, st));
@@ -478,90 +597,89 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	if (C > cand_cap && n > 1) { *too_big = true; return 0; }
 	if (C >= 0x7fffffffull) { svg_set_error("svg_long_vote_batch: read %llu has %llu candidates", (unsigned long long)r0, (unsigned long long)C); return SVG_E_UNSUPPORTED; }
 	if (C == 0) { for (uint32_t i = 0; i < n; i++) counts.push_back(0); return 0; }
-	uint64_t *d_ck, *d_ck2; uint32_t *d_cv, *d_cv2, *d_coff, *d_head, *d_sid;
-	if (B.get(&d_ck, C) || B.get(&d_ck2, C) || B.get(&d_cv, C) || B.get(&d_cv2, C) || B.get(&d_coff, C) ||
-	    B.get(&d_head, C) || B.get(&d_sid, C))
-		return SVG_E_NOMEM;
+	// ---- candidate phase (segments and slots are bounded by the candidates)
+	int rbits = 1;
+	while ((1u << rbits) < n) rbits++;
+	size_t t_sort1 = 0, t_scan = 0, t_sort2 = 0;
+	LCHK(hipcub::DeviceRadixSort::SortPairs(NULL, t_sort1, (uint64_t *)NULL, (uint64_t *)NULL, (uint32_t *)NULL, (uint32_t *)NULL,
+	                                        (int)C, 0, 33 + rbits, st));
+	LCHK(hipcub::DeviceScan::ExclusiveSum(NULL, t_scan, (uint32_t *)NULL, (uint32_t *)NULL, (int)C, st));
+	LCHK(hipcub::DeviceRadixSort::SortPairs(NULL, t_sort2, (uint64_t *)NULL, (uint64_t *)NULL, (uint32_t *)NULL, (uint32_t *)NULL,
+	                                        (int)C, 0, 48 + rbits, st));
+	size_t t_max = t_sort1 > t_scan ? t_sort1 : t_scan;
+	t_max = t_max > t_sort2 ? t_max : t_sort2;
+	Carve cb = {NULL, 0};
+	uint64_t *d_ck = NULL, *d_ck2 = NULL, *d_sk = NULL, *d_sk2 = NULL, *d_vs = NULL;
+	uint32_t *d_cv = NULL, *d_cv2 = NULL, *d_coff = NULL, *d_head = NULL, *d_sid = NULL, *d_si = NULL, *d_si2 = NULL, *d_ord = NULL;
+	uint4 *d_sd = NULL;
+	svg_long_vote *d_out = NULL;
+	void *d_tmp = NULL;
+	for (int pass = 0; pass < 2; pass++) {
+		if (pass) { if (int e = arena(h, &w->dB, &w->capB, cb.off)) return e; cb.base = (char *)w->dB; cb.off = 0; }
+		d_ck = cb.take<uint64_t>(C); d_ck2 = cb.take<uint64_t>(C); d_cv = cb.take<uint32_t>(C); d_cv2 = cb.take<uint32_t>(C);
+		d_coff = cb.take<uint32_t>(C); d_head = cb.take<uint32_t>(C); d_sid = cb.take<uint32_t>(C);
+		d_sk = cb.take<uint64_t>(C); d_sk2 = cb.take<uint64_t>(C); d_si = cb.take<uint32_t>(C); d_si2 = cb.take<uint32_t>(C);
+		d_sd = cb.take<uint4>(C); d_out = cb.take<svg_long_vote>(C); d_ord = cb.take<uint32_t>(C); d_vs = cb.take<uint64_t>(n + 1);
+		d_tmp = cb.take<char>(t_max);
+	}
 	LExpand le;
 	le.vals = h->dix.vals; le.pcnt = d_pcnt; le.pbase_c = d_pcb; le.pfirst = d_pfirst; le.pmeta = d_pmeta; le.n_probes = P;
 	le.ckey = d_ck; le.cval = d_cv; le.coff = d_coff;
 	hipLaunchKernelGGL(long_expand_kernel, dim3(blocks_of(P, 256)), dim3(256), 0, st, le);
 	LCHK(hipGetLastError());
-	int rbits = 1;
-	while ((1u << rbits) < n) rbits++;
 	// sort 1: (read, strand, kv), stable
-	size_t sb = 0;
-	LCHK(hipcub::DeviceRadixSort::SortPairs(NULL, sb, d_ck, d_ck2, d_cv, d_cv2, (int)C, 0, 33 + rbits, st));
-	void *d_tmp2 = NULL;
-	if (B.get((char **)&d_tmp2, sb)) return SVG_E_NOMEM;
-	LCHK(hipcub::DeviceRadixSort::SortPairs(d_tmp2, sb, d_ck, d_ck2, d_cv, d_cv2, (int)C, 0, 33 + rbits, st));
+	size_t tb1 = t_max;
+	LCHK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb1, d_ck, d_ck2, d_cv, d_cv2, (int)C, 0, 33 + rbits, st));
 	hipLaunchKernelGGL(long_head_kernel, dim3(blocks_of(C, 256)), dim3(256), 0, st, d_ck2, d_cv2, d_coff, C, d_head);
 	LCHK(hipGetLastError());
-	size_t sb2 = 0;
-	LCHK(hipcub::DeviceScan::ExclusiveSum(NULL, sb2, d_head, d_sid, (int)C, st));
-	void *d_tmp3 = NULL;
-	if (B.get((char **)&d_tmp3, sb2)) return SVG_E_NOMEM;
-	LCHK(hipcub::DeviceScan::ExclusiveSum(d_tmp3, sb2, d_head, d_sid, (int)C, st));
+	size_t tb2 = t_max;
+	LCHK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb2, d_head, d_sid, (int)C, st));
 	uint32_t lh[2];
 	LCHK(hipMemcpyAsync(&lh[0], d_sid + C - 1, 4, hipMemcpyDeviceToHost, st));
 	LCHK(hipMemcpyAsync(&lh[1], d_head + C - 1, 4, hipMemcpyDeviceToHost, st));
 	LCHK(hipStreamSynchronize(st));
 	const uint64_t G = (uint64_t)lh[0] + lh[1];
-	// segments (reusing the first sort's input buffers: d_ck -> second keys, d_cv -> first index)
-	uint32_t *d_sfirst = d_cv;
+	uint32_t *d_sfirst = d_cv;   // the first sort's input payloads are free now
 	hipLaunchKernelGGL(long_segstart_kernel, dim3(blocks_of(C, 256)), dim3(256), 0, st, d_head, d_sid, C, d_sfirst);
 	LCHK(hipGetLastError());
-	uint64_t *d_sk, *d_sk2; uint32_t *d_si, *d_si2; uint4 *d_sd;
-	if (B.get(&d_sk, G) || B.get(&d_sk2, G) || B.get(&d_si, G) || B.get(&d_si2, G) || B.get(&d_sd, G)) return SVG_E_NOMEM;
 	LSeg ls;
 	ls.key = d_ck2; ls.val = d_cv2; ls.coff = d_coff; ls.sfirst = d_sfirst; ls.n_cand = C; ls.n_seg = G;
 	ls.skey = d_sk; ls.sidx = d_si; ls.sdata = d_sd;
 	hipLaunchKernelGGL(long_seg_kernel, dim3(blocks_of(G, 256)), dim3(256), 0, st, ls);
 	LCHK(hipGetLastError());
 	// sort 2: (read, row, first candidate)
-	size_t sb3 = 0;
-	LCHK(hipcub::DeviceRadixSort::SortPairs(NULL, sb3, d_sk, d_sk2, d_si, d_si2, (int)G, 0, 48 + rbits, st));
-	void *d_tmp4 = NULL;
-	if (B.get((char **)&d_tmp4, sb3)) return SVG_E_NOMEM;
-	LCHK(hipcub::DeviceRadixSort::SortPairs(d_tmp4, sb3, d_sk, d_sk2, d_si, d_si2, (int)G, 0, 48 + rbits, st));
+	size_t tb3 = t_max;
+	LCHK(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb3, d_sk, d_sk2, d_si, d_si2, (int)G, 0, 48 + rbits, st));
 	uint32_t *d_keep = d_head, *d_kpos = d_sid;   // G <= C
 	hipLaunchKernelGGL(long_keep_kernel, dim3(blocks_of(G, 256)), dim3(256), 0, st, d_sk2, G, d_keep);
 	LCHK(hipGetLastError());
-	size_t sb4 = 0;
-	LCHK(hipcub::DeviceScan::ExclusiveSum(NULL, sb4, d_keep, d_kpos, (int)G, st));
-	void *d_tmp5 = NULL;
-	if (B.get((char **)&d_tmp5, sb4)) return SVG_E_NOMEM;
-	LCHK(hipcub::DeviceScan::ExclusiveSum(d_tmp5, sb4, d_keep, d_kpos, (int)G, st));
+	size_t tb4 = t_max;
+	LCHK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb4, d_keep, d_kpos, (int)G, st));
 	uint32_t lk[2];
 	LCHK(hipMemcpyAsync(&lk[0], d_kpos + G - 1, 4, hipMemcpyDeviceToHost, st));
 	LCHK(hipMemcpyAsync(&lk[1], d_keep + G - 1, 4, hipMemcpyDeviceToHost, st));
 	LCHK(hipStreamSynchronize(st));
 	const uint64_t K = (uint64_t)lk[0] + lk[1];
-	svg_long_vote *d_out; uint32_t *d_rc, *d_ord; uint64_t *d_vs;
-	if (B.get(&d_out, K) || B.get(&d_rc, n) || B.get(&d_ord, K) || B.get(&d_vs, n + 1)) return SVG_E_NOMEM;
-	LCHK(hipMemsetAsync(d_rc, 0, 4ull * n, st));
 	LEmit em;
-	em.skey = d_sk2; em.sidx = d_si2; em.keep = d_keep; em.kpos = d_kpos; em.sdata = d_sd; em.n_seg = G; em.out = d_out; em.rcount = d_rc;
+	em.skey = d_sk2; em.sidx = d_si2; em.keep = d_keep; em.kpos = d_kpos; em.sdata = d_sd; em.n_seg = G; em.out = d_out;
 	hipLaunchKernelGGL(long_emit_kernel, dim3(blocks_of(G, 256)), dim3(256), 0, st, em);
 	LCHK(hipGetLastError());
-	std::vector<uint32_t> rc(n);
-	LCHK(hipMemcpyAsync(rc.data(), d_rc, 4ull * n, hipMemcpyDeviceToHost, st));
-	LCHK(hipStreamSynchronize(st));
-	std::vector<uint64_t> vs(n + 1);
-	vs[0] = 0;
-	for (uint32_t i = 0; i < n; i++) vs[i + 1] = vs[i] + rc[i];
-	LCHK(hipMemcpyAsync(d_vs, vs.data(), 8ull * (n + 1), hipMemcpyHostToDevice, st));
+	hipLaunchKernelGGL(long_vstart_kernel, dim3(blocks_of(n + 1, 256)), dim3(256), 0, st, d_sk2, d_kpos, G, K, n, d_vs);
+	LCHK(hipGetLastError());
 	// the order kernel's ping-pong arrays reuse the candidate buffers (K <= C)
 	hipLaunchKernelGGL(long_order_kernel, dim3(n), dim3(256), 0, st, d_out, d_vs, (uint32_t *)d_ck, d_coff,
 	                   (uint32_t *)d_ck2, d_cv2, d_ord);
 	LCHK(hipGetLastError());
-	const size_t v0 = votes.size();
-	votes.resize(v0 + K);
-	order.resize(v0 + K);
-	LCHK(hipMemcpyAsync(votes.data() + v0, d_out, sizeof(svg_long_vote) * K, hipMemcpyDeviceToHost, st));
-	LCHK(hipMemcpyAsync(order.data() + v0, d_ord, 4ull * K, hipMemcpyDeviceToHost, st));
-	LCHK(hipStreamSynchronize(st));
-	for (uint32_t i = 0; i < n; i++) counts.push_back(rc[i]);
+	if (int e = res.reserve(K)) return e;
+	std::vector<uint64_t> vs(n + 1);
+	std::vector<Span> spans = {{vs.data(), d_vs, 8ull * (n + 1)}, {res.votes + res.n, d_out, sizeof(svg_long_vote) * K},
+	                           {res.order + res.n, d_ord, 4ull * K}};
+	if (int e = staged_download(h, spans, T)) return e;
+	res.n += K;
+	for (uint32_t i = 0; i < n; i++) counts.push_back(vs[i + 1] - vs[i]);
+	if (getenv("SVG_LONG_DEBUG"))
+		fprintf(stderr, "[svg_long] reads %u probes %llu candidates %llu segments %llu slots %llu\n", n,
+		        (unsigned long long)P, (unsigned long long)C, (unsigned long long)G, (unsigned long long)K);
 	return 0;
 }
 }  // namespace
@@ -586,13 +704,24 @@ extern "C" int svg_long_vote_batch(svg_index *h, const svg_long_reads *R, svg_lo
 		}
 	HIPCHK(hipSetDevice(h->device));
 	if (h->last_pending) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_last, 0));
+	if (!h->lws) {
+		svg_longws *w = (svg_longws *)calloc(1, sizeof(svg_longws));
+		if (!w) { svg_set_error("out of host memory"); return SVG_E_NOMEM; }
+		h->lws = w;
+		for (int i = 0; i < 2; i++) {
+			HIPCHK(hipHostMalloc(&w->hs[i], PIECE, hipHostMallocDefault));
+			HIPCHK(hipEventCreateWithFlags(&w->ev[i], hipEventDisableTiming));
+		}
+		w->hcap = PIECE;
+	}
+	const int T = svg_host_threads();
 	// chunks: <= 65535 reads (16-bit read field of the segment key), <= 32M probes
 	const char *ec = getenv("SVG_LONG_PROBES");
 	const uint64_t pcap = ec && atoll(ec) > 0 ? (uint64_t)atoll(ec) : (32ull << 20);
 	const uint64_t ccap = 256ull << 20;
-	std::vector<svg_long_vote> votes;
-	std::vector<uint32_t> order;
+	LOut res = {NULL, NULL, 0, 0};
 	std::vector<uint64_t> counts;
+	counts.reserve(R->n_reads);
 	uint64_t r0 = 0;
 	while (r0 < R->n_reads) {
 		uint64_t r1 = r0, P = 0;
@@ -604,23 +733,21 @@ extern "C" int svg_long_vote_batch(svg_index *h, const svg_long_reads *R, svg_lo
 		}
 		for (;;) {
 			bool big = false;
-			const int rc = long_chunk(h, R, r0, r1, ccap, votes, order, counts, &big);
-			if (rc) return rc;
+			const int rc = long_chunk(h, R, r0, r1, ccap, res, counts, &big, T);
+			if (rc) { free(res.votes); free(res.order); return rc; }
 			if (!big) break;
+			if (getenv("SVG_LONG_DEBUG")) fprintf(stderr, "[svg_long] split %llu reads\n", (unsigned long long)(r1 - r0));
 			r1 = r0 + (r1 - r0) / 2;   // too many candidates: half the reads
 		}
 		r0 = r1;
 	}
+	if (res.reserve(1)) { free(res.votes); free(res.order); return SVG_E_NOMEM; }
 	out->n_reads = R->n_reads;
+	out->votes = res.votes;
+	out->order = res.order;
 	out->vstart = (uint64_t *)malloc(8 * (R->n_reads + 1));
-	out->votes = (svg_long_vote *)malloc(sizeof(svg_long_vote) * (votes.size() + 1));
-	out->order = (uint32_t *)malloc(4 * (order.size() + 1));
-	if (!out->vstart || !out->votes || !out->order) { svg_long_free(out); svg_set_error("out of host memory"); return SVG_E_NOMEM; }
+	if (!out->vstart) { svg_long_free(out); svg_set_error("out of host memory"); return SVG_E_NOMEM; }
 	out->vstart[0] = 0;
 	for (uint64_t r = 0; r < R->n_reads; r++) out->vstart[r + 1] = out->vstart[r] + counts[r];
-	if (!votes.empty()) {
-		memcpy(out->votes, votes.data(), sizeof(svg_long_vote) * votes.size());
-		memcpy(out->order, order.data(), 4 * order.size());
-	}
 	return 0;
 }

@@ -2541,6 +2541,7 @@ extern "C" void svg_index_close(svg_index *h)
 	if (h->up_stream) hipStreamSynchronize(h->up_stream);
 	if (h->down_stream) hipStreamSynchronize(h->down_stream);
 	svg_io_free(h);
+	svg_long_ws_free(h);
 	for (int s = 0; s < 2; s++) {
 		hipFree(h->d_prec[s]);
 		hipFree(h->d_lane[s]);

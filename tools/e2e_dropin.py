@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""End to end ("report end-to-end, including the host realignment and SAM,
+separately"): the reference's own subread-align run twice on the same FASTQ and index files --
+stock (its CPU voting step) and the drop-in (oracle/_ref/subread-align-dropin: the same binary
+with integration/do_voting_gpu.c voting on the GPU through libsubread_amd.so) -- wall time of
+each whole program (index load, FASTQ parse, voting, iteration two, SAM / VCF writing), and the
+outputs compared byte for byte.
+
+Workload: a --mbp Mbp genome (contigs of GRCh38-like relative lengths, repeat families), full
+one-block index files written by our builder (md5-identical to subread-buildindex -F -B),
+--reads x 100 bp SE reads (1% substitutions, 0.1% indels), -T --threads.
+-> one JSON line on stdout."""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mbp", type=int, default=200)
+    ap.add_argument("--reads", type=int, default=2_000_000)
+    ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--workdir", default="")
+    args = ap.parse_args()
+    import subread_amd as sa
+    from subread_amd.sim import c3_lengths, random_genome, simulate_reads
+    from tests import dropin
+    from bench import cpu_info
+    cpu = cpu_info()
+    T = args.threads or cpu["usable_cpus"]
+    wd = args.workdir or tempfile.mkdtemp(prefix="svg_e2e_")
+    t0 = time.time()
+    g = random_genome(c3_lengths(args.mbp * 1_000_000), 3000, repeats=(args.mbp * 300, 300, 200, 0.12))
+    fa, pre = os.path.join(wd, "g.fa"), os.path.join(wd, "g_full")
+    g.write_fasta(fa)
+    sa.build_index(fa, pre, gap=1, force_one_block=True)
+    log("[e2e] genome %.0f Mbp + index files in %.1fs" % (g.length / 1e6, time.time() - t0))
+    rb = simulate_reads(g, args.reads, 100, seed=20261015, sub=0.01, indel=0.001)
+    fq, fq1 = os.path.join(wd, "r.fq"), os.path.join(wd, "r1.fq")
+    dropin.write_fastq(fq, rb)
+    dropin.write_fastq(fq1, rb.slice(0, 1))
+    import threading
+    stop = threading.Event()
+
+    def heartbeat():   # the programs' own output is captured: keep the GPU runner's log moving
+        t = time.time()
+        while not stop.wait(30):
+            log("[e2e] ... %.0f s" % (time.time() - t))
+    threading.Thread(target=heartbeat, daemon=True).start()
+    res, start = {}, {}
+    for kind in ("dump", "dropin"):
+        # the fixed cost first (index load(s), voting space, output files): the same program on one read
+        out = os.path.join(wd, "one_" + kind)
+        ts = time.perf_counter()
+        dropin.run(0, kind, pre, fq1, None, out, threads=T, timeout=1500)
+        start[kind] = time.perf_counter() - ts
+        out = os.path.join(wd, "out_" + kind)
+        ts = time.perf_counter()
+        dropin.run(0, kind, pre, fq, None, out, threads=T, timeout=1500)
+        res[kind] = time.perf_counter() - ts
+        log("[e2e] %s: %.1f s (%.1f s on one read)" % (kind, res[kind], start[kind]))
+    stop.set()
+    dropin.compare(os.path.join(wd, "out_dump"), os.path.join(wd, "out_dropin"))
+    log("[e2e] SAM / VCF byte-identical")
+    line = {"metric": "end-to-end subread-align (index load + parse + vote + iteration two + SAM), Mreads/s",
+            "stock_value": round(args.reads / res["dump"] / 1e6, 4), "dropin_value": round(args.reads / res["dropin"] / 1e6, 4),
+            "unit": "Mreads/s", "stock_s": round(res["dump"], 2), "dropin_s": round(res["dropin"], 2),
+            "speedup": round(res["dump"] / res["dropin"], 2),
+            "startup_s": {"stock": round(start["dump"], 2), "dropin": round(start["dropin"], 2)},
+            "mapping_only": {"stock_value": round(args.reads / max(1e-9, res["dump"] - start["dump"]) / 1e6, 4),
+                             "dropin_value": round(args.reads / max(1e-9, res["dropin"] - start["dropin"]) / 1e6, 4),
+                             "note": "whole-program time minus the same program's time on one read"},
+            "outputs_identical": True, "threads": T,
+            "cpu_model": cpu["model"],
+            "config": {"genome_mbp": round(g.length / 1e6, 1), "reads": args.reads, "read_len": 100, "mode": "SE, -t 1 (DNA)",
+                       "index": "full one-block files (our builder, md5-identical to subread-buildindex -F -B)"}}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
