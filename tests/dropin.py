@@ -118,3 +118,39 @@ def check_case(case, index, tmp, kind, threads=1, env=None):
     assert votes.size == case.expected.size and (votes.reshape(case.expected.shape) == case.expected).all(), \
         "drop-in vote records differ from the golden records"
     return rep
+
+
+# ---- sublong (src/longread-one): stock _ref/sublong vs _ref/sublong-dropin (GPU voting through
+# integration/lrm_voting_gpu.c) or _ref/sublong-oracle-dropin (the restatement), same FASTQ
+
+def sublong_binary(kind):
+    return os.path.join(REFBIN, "sublong" if kind == "stock" else "sublong-" + kind)
+
+
+def run_sublong(kind, index, fq, out, threads=1, timeout=900):
+    args = [sublong_binary(kind), "-i", index, "-r", fq, "-o", out, "--SAMoutput", "-T", str(threads)]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, "%s failed (%d):\n%s\n%s" % (kind, r.returncode, r.stdout[-3000:], r.stderr[-3000:])
+    return r
+
+
+def write_long_fastq(path, reads):
+    """FASTQ of a LongReads batch (empty reads skipped: sublong's reader stops at one)."""
+    with open(path, "wb") as f:
+        for i in range(len(reads)):
+            s = reads.read(i)
+            if s:
+                f.write(b"@r%d\n%s\n+\n%s\n" % (i, s, bytes(33 + (i * 7 + k * 13) % 41 for k in range(len(s)))))
+
+
+def compare_sam(a_path, b_path, any_order=False):
+    """Byte comparison of two SAM files without their @PG lines; any_order: as sorted line sets
+    (sublong -T > 1 writes each thread's records in the order its reads were fetched)."""
+    a = [l for l in open(a_path, "rb") if not l.startswith(b"@PG")]
+    b = [l for l in open(b_path, "rb") if not l.startswith(b"@PG")]
+    if any_order:
+        a, b = sorted(a), sorted(b)
+    bad = [i for i in range(min(len(a), len(b))) if a[i] != b[i]][:3]
+    assert len(a) == len(b) and not bad, "SAM differs (%d vs %d lines): %s" % (
+        len(a), len(b), "; ".join("line %d: %r / %r" % (i, a[i][:200], b[i][:200]) for i in bad))
+    return len(a)

@@ -6,6 +6,8 @@ big-margin staging, the post-vote tail's text/quality orientation, fragile junct
 long subjunc reads, the multi-block run loop, -T > 1 -- apart from the kernels;
 tests/test_gpu_dropin.py runs the same binding with the GPU library.  Needs the binaries
 built from /root/reference (this container; skipped where they are absent)."""
+import os
+
 import pytest
 
 from tests.common import Case, IndexCache
@@ -41,3 +43,19 @@ def test_votetime_harness_matches_stock_reference(name, threads, cache, tmp_path
         pytest.skip("reference timing binaries not built (make -C oracle votetime)")
     rep = check_case(c, cache.get(c.index_key), str(tmp_path), "votetime", threads)
     assert rep["mapped"] > 0
+
+
+def test_sublong_oracle_dropin_matches_stock(cache, tmp_path):
+    """sublong with integration/lrm_voting_gpu.c as its per-read loop, votes from the restatement:
+    the stock sublong's SAM byte for byte (batched fetch, vote-table rebuild, text orientation)."""
+    from tests import dropin
+    from tests.test_sublong import fixture
+    if not os.path.exists(dropin.sublong_binary("oracle-dropin")):
+        pytest.skip("oracle/_ref not built (no /root/reference)")
+    reads = fixture("chr901_full")[0]
+    fq = str(tmp_path / "r.fq")
+    dropin.write_long_fastq(fq, reads)
+    pre = cache.get("chr901_full")
+    dropin.run_sublong("stock", pre, fq, str(tmp_path / "stock.sam"))
+    dropin.run_sublong("oracle-dropin", pre, fq, str(tmp_path / "dropin.sam"))
+    assert dropin.compare_sam(str(tmp_path / "stock.sam"), str(tmp_path / "dropin.sam")) > 30

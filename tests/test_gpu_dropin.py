@@ -68,3 +68,31 @@ def test_gpu_dropin_c2_200k(tmp_path):
     assert votes.size == 200_000 * 3 * 68
     assert rep["sam_records"] >= 200_000 and rep["mapped"] > 190_000, rep
     print("c2", rep)
+
+
+@pytest.mark.parametrize("key,n_sim,threads", [
+    ("chr901_full", 150, 1),     # the sublong fixture's reads (edges, N / lowercase / IUPAC) + simulated ONT-like reads
+    ("lrrow54_full", 60, 1),     # reads over 54 element copies (a full vote-table row) and a 200 kb read
+    ("chr901_full", 150, 4),     # -T 4: threads share the GPU handle
+])
+def test_gpu_sublong_dropin_matches_stock(key, n_sim, threads, cache, tmp_path):
+    """The reference's own sublong with integration/lrm_voting_gpu.c as its per-read loop (votes
+    by svg_long_vote_batch on the GPU): the stock sublong's SAM byte for byte -- the reference's
+    LRMdo_dynamic_programming_read (copy, location sort, windows, chains, gap filling, SAM)
+    consumes the GPU vote tables."""
+    from subread_amd.abi import LongReads
+    from subread_amd.sim import Genome, simulate_long_reads
+    from tests import dropin
+    from tests.test_sublong import fixture
+    if not os.path.exists(dropin.sublong_binary("dropin")):
+        pytest.fail("oracle/_ref sublong binaries missing: build them in the survey container (make -C oracle)")
+    fx = fixture(key)[0]
+    g = Genome.read_fasta(cache.genome_fasta(key.rsplit("_", 1)[0]))
+    sim = simulate_long_reads(g, n_sim, mean_len=4000, seed=77)
+    reads = LongReads.from_list([fx.read(i) for i in range(len(fx))] + [sim.read(i) for i in range(len(sim))])
+    fq = str(tmp_path / "r.fq")
+    dropin.write_long_fastq(fq, reads)
+    pre = cache.get(key)
+    dropin.run_sublong("stock", pre, fq, str(tmp_path / "stock.sam"), threads=threads)
+    dropin.run_sublong("dropin", pre, fq, str(tmp_path / "dropin.sam"), threads=threads)
+    assert dropin.compare_sam(str(tmp_path / "stock.sam"), str(tmp_path / "dropin.sam"), any_order=threads > 1) > n_sim
