@@ -2303,8 +2303,19 @@ int svg_index_finish_device(svg_index *h)
 	HIPCHK(hipSetDevice(h->device));
 	if ((rc = dmalloc(h, &h->d_values, (size_t)x->values_bytes + 64)) || (rc = dmalloc(h, &h->d_chr, 4 * (size_t)x->n_chr + 64)))
 		return rc;
-	HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-	HIPCHK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+	{
+		// SVG_STREAM_PRIO=1: the probe + lane kernels' stream (the step's critical path) at the highest
+		// priority, the overlapped wave kernel's at the lowest, so the CUs go to the critical path first
+		const char *ep = getenv("SVG_STREAM_PRIO");
+		int lo = 0, hi = 0;
+		if (ep && ep[0] == '1' && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && lo != hi) {
+			HIPCHK(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi));
+			HIPCHK(hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, lo));
+		} else {
+			HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+			HIPCHK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+		}
+	}
 	HIPCHK(hipEventCreateWithFlags(&h->ev_up[2], hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&h->ev_done[2], hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&h->ev_down[2], hipEventDisableTiming));
