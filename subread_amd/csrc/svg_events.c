@@ -10,6 +10,7 @@
 #define _GNU_SOURCE
 #include <stdio.h>
 #include <stdlib.h>
+#include <pthread.h>
 #include <string.h>
 #include <stdint.h>
 #include "subread_vote.h"
@@ -1179,42 +1180,35 @@ static int64_t side_search(const side_t *v, int64_t n, uint32_t pos)
  * each event whose small or large side lies strictly inside its covered range shrunk by 5 bases
  * at both ends (an event once per record; at most 100 small-side events per record).
  */
-int svg_events_anti_support(svg_events *t, const svg_params *p, const svg_event_params *ep_in, uint64_t n_reads, int ends,
-                            const svg_mapping_result *out)
-{
-	const int mb = p ? p->multi_best : 0;
-	svg_event_params epd;
-	const svg_event_params *ep = ep_in;
-	side_t *sm, *lg;
+typedef struct {
+	const side_t *sm, *lg;
+	int64_t ne;
+	const svg_params *p;
+	const svg_event_params *ep;
+	const svg_mapping_result *out;
+	uint64_t r0, r1;
+	int ends, mb;
 	uint32_t *cnt;
-	int64_t ne, i;
-	uint64_t r;
-	if (!t || !p || !out || ends < 1 || ends > 2 || mb < 1 || mb > 3) { svg_set_error("svg_events_anti_support: bad argument"); return SVG_E_ARG; }
-	if (!ep) { svg_event_params_default(&epd); ep = &epd; }
-	ne = (int64_t)t->n;
-	if (ne < 1) return 0;
-	sm = malloc(sizeof(side_t) * (size_t)ne);
-	lg = malloc(sizeof(side_t) * (size_t)ne);
-	cnt = calloc((size_t)ne, sizeof(uint32_t));
-	if (!sm || !lg || !cnt) { free(sm); free(lg); free(cnt); svg_set_error("out of memory"); return SVG_E_NOMEM; }
-	for (i = 0; i < ne; i++) {
-		sm[i].pos = t->ev[i].small_side; sm[i].id = (uint32_t)i;
-		lg[i].pos = t->ev[i].large_side; lg[i].id = (uint32_t)i;
-	}
-	qsort(sm, (size_t)ne, sizeof(side_t), side_cmp);
-	qsort(lg, (size_t)ne, sizeof(side_t), side_cmp);
-	for (r = 0; r < n_reads; r++) {
+} anti_job;
+
+/* anti_supporting_read_scan's per-record body over reads [r0, r1) into the job's counters */
+static void *anti_worker(void *arg)
+{
+	anti_job *J = arg;
+	const side_t *sm = J->sm, *lg = J->lg;
+	const int64_t ne = J->ne;
+	for (uint64_t r = J->r0; r < J->r1; r++) {
 		int e, b;
-		for (e = 0; e < ends; e++)
-			for (b = 0; b < mb; b++) {
-				const svg_mapping_result *m = &out[(r * (uint64_t)ends + (uint64_t)e) * (uint64_t)mb + (uint64_t)b];
+		for (e = 0; e < J->ends; e++)
+			for (b = 0; b < J->mb; b++) {
+				const svg_mapping_result *m = &J->out[(r * (uint64_t)J->ends + (uint64_t)e) * (uint64_t)J->mb + (uint64_t)b];
 				uint32_t cancelled[ANTI_LIMIT];
 				int nc = 0;
 				int64_t x, l0, l1, r0, r1;
 				uint32_t cs, ce;
 				if (m->selected_votes < 1) break;
-				if (!ep->report_multi_mapping_reads && (m->result_flags & 32)) continue;   /* CORE_IS_BREAKEVEN */
-				if (m->selected_votes < p->min_votes_first) continue;
+				if (!J->ep->report_multi_mapping_reads && (m->result_flags & 32)) continue;   /* CORE_IS_BREAKEVEN */
+				if (m->selected_votes < J->p->min_votes_first) continue;
 				cs = m->selected_position + m->confident_coverage_start;
 				ce = m->selected_position + m->confident_coverage_end;
 				l0 = side_search(sm, ne, cs - 1) + 1;
@@ -1224,7 +1218,7 @@ int svg_events_anti_support(svg_events *t, const svg_params *p, const svg_event_
 				for (x = l0; x <= r0 && x < ne && nc < ANTI_LIMIT; x++) {
 					const uint32_t pos = sm[x].pos;
 					if (pos <= cs + 5 || pos >= ce - 5) continue;
-					cnt[sm[x].id]++;
+					J->cnt[sm[x].id]++;
 					cancelled[nc++] = sm[x].id;
 				}
 				for (x = l1; x <= r1 && x < ne; x++) {
@@ -1232,11 +1226,55 @@ int svg_events_anti_support(svg_events *t, const svg_params *p, const svg_event_
 					int k, dup = 0;
 					if (pos <= cs + 5 || pos >= ce - 5) continue;
 					for (k = 0; k < nc; k++) if (cancelled[k] == lg[x].id) { dup = 1; break; }
-					if (!dup) cnt[lg[x].id]++;
+					if (!dup) J->cnt[lg[x].id]++;
 				}
 			}
 	}
+	return NULL;
+}
+
+int svg_events_anti_support(svg_events *t, const svg_params *p, const svg_event_params *ep_in, uint64_t n_reads, int ends,
+                            const svg_mapping_result *out)
+{
+	const int mb = p ? p->multi_best : 0;
+	svg_event_params epd;
+	const svg_event_params *ep = ep_in;
+	side_t *sm, *lg;
+	uint32_t *cnt;
+	int64_t ne, i;
+	if (!t || !p || !out || ends < 1 || ends > 2 || mb < 1 || mb > 3) { svg_set_error("svg_events_anti_support: bad argument"); return SVG_E_ARG; }
+	if (!ep) { svg_event_params_default(&epd); ep = &epd; }
+	ne = (int64_t)t->n;
+	if (ne < 1) return 0;
+	/* the reads split over host threads, each with its own counters (sums: order-independent) */
+	int T = svg_host_threads();
+	if ((uint64_t)T > n_reads / 4096 + 1) T = (int)(n_reads / 4096 + 1);
+	if (T < 1) T = 1;
+	sm = malloc(sizeof(side_t) * (size_t)ne);
+	lg = malloc(sizeof(side_t) * (size_t)ne);
+	cnt = calloc((size_t)ne * (size_t)T, sizeof(uint32_t));
+	anti_job *jobs = calloc((size_t)T, sizeof(anti_job));
+	pthread_t *tid = calloc((size_t)T, sizeof(pthread_t));
+	if (!sm || !lg || !cnt || !jobs || !tid) { free(sm); free(lg); free(cnt); free(jobs); free(tid); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	for (i = 0; i < ne; i++) {
+		sm[i].pos = t->ev[i].small_side; sm[i].id = (uint32_t)i;
+		lg[i].pos = t->ev[i].large_side; lg[i].id = (uint32_t)i;
+	}
+	qsort(sm, (size_t)ne, sizeof(side_t), side_cmp);
+	qsort(lg, (size_t)ne, sizeof(side_t), side_cmp);
+	for (int k = 0; k < T; k++) {
+		anti_job *J = &jobs[k];
+		J->sm = sm; J->lg = lg; J->ne = ne; J->p = p; J->ep = ep; J->out = out; J->ends = ends; J->mb = mb;
+		J->r0 = n_reads * (uint64_t)k / (uint64_t)T;
+		J->r1 = n_reads * (uint64_t)(k + 1) / (uint64_t)T;
+		J->cnt = cnt + (size_t)ne * (size_t)k;
+		if (k) pthread_create(&tid[k], NULL, anti_worker, J);
+	}
+	anti_worker(&jobs[0]);
+	for (int k = 1; k < T; k++) pthread_join(tid[k], NULL);
+	for (int k = 1; k < T; k++)
+		for (i = 0; i < ne; i++) cnt[i] += cnt[(size_t)ne * (size_t)k + (size_t)i];
 	for (i = 0; i < ne; i++) t->ev[i].anti_supporting_reads = (uint16_t)(t->ev[i].anti_supporting_reads + cnt[i]);
-	free(sm); free(lg); free(cnt);
+	free(sm); free(lg); free(cnt); free(jobs); free(tid);
 	return 0;
 }
