@@ -36,8 +36,11 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <time.h>
 #include <string.h>
 #include <algorithm>
+#include <malloc.h>
+#include <mutex>
 #include <thread>
 #include <vector>
 #include "subread_vote.h"
@@ -504,10 +507,26 @@ int staged_download(svg_index *h, const std::vector<Span> &spans, int T)
 	return 0;
 }
 
+// One freed result's arrays are kept for the next call (process-wide): a batch's slots are
+// ~24 B each (GBs for long-read batches), and handing the same pages back avoids unmapping them
+// in svg_long_free and faulting fresh ones in during the next download.
+std::mutex g_cache_mu;
+void *g_cache_v = NULL, *g_cache_o = NULL;
+
 struct LOut {
 	svg_long_vote *votes;
 	uint32_t *order;
 	uint64_t n, cap;
+	void adopt_cache()
+	{
+		std::lock_guard<std::mutex> lk(g_cache_mu);
+		if (!g_cache_v || !g_cache_o) return;
+		votes = (svg_long_vote *)g_cache_v;
+		order = (uint32_t *)g_cache_o;
+		const uint64_t cv = malloc_usable_size(votes) / sizeof(svg_long_vote), co = malloc_usable_size(order) / 4;
+		cap = cv < co ? cv : co;
+		g_cache_v = g_cache_o = NULL;
+	}
 	int reserve(uint64_t add)
 	{
 		if (n + add <= cap) return 0;
@@ -530,6 +549,10 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	svg_longws *w = h->lws;
 	const uint32_t n = (uint32_t)(r1 - r0);
 	*too_big = false;
+	const bool dbg = getenv("SVG_LONG_DEBUG") != NULL;
+	auto now = [] { struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6; };
+	const double t0 = dbg ? now() : 0;
+	double t_up = 0, t_probe = 0, t_seg = 0, t_keep = 0, t_dev = 0;
 	std::vector<uint64_t> toff(n + 1);
 	std::vector<uint32_t> len(n), pbase(n + 1);
 	uint64_t tb = 0, P = 0;
@@ -578,6 +601,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	LCHK(hipMemcpyAsync(d_toff, toff.data(), 8ull * n, hipMemcpyHostToDevice, st));
 	LCHK(hipMemcpyAsync(d_len, len.data(), 4ull * n, hipMemcpyHostToDevice, st));
 	LCHK(hipMemcpyAsync(d_pbase, pbase.data(), 4ull * (n + 1), hipMemcpyHostToDevice, st));
+	if (dbg) { LCHK(hipStreamSynchronize(st)); t_up = now(); }
 	LProbe lp;
 	lp.ix = h->dix; lp.text = d_text; lp.toff = d_toff; lp.len = d_len; lp.pbase = d_pbase; lp.n_reads = n;
 	lp.n_probes = P; lp.pcnt = d_pcnt; lp.pfirst = d_pfirst; lp.pmeta = d_pmeta;
@@ -594,6 +618,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	LCHK(hipMemcpyAsync(&last[1], d_pcnt + P - 1, 8, hipMemcpyDeviceToHost, st));
 	LCHK(hipStreamSynchronize(st));
 	const uint64_t C = last[0] + last[1];
+	if (dbg) t_probe = now();
 	if (C > cand_cap && n > 1) { *too_big = true; return 0; }
 	if (C >= 0x7fffffffull) { svg_set_error("svg_long_vote_batch: read %llu has %llu candidates", (unsigned long long)r0, (unsigned long long)C); return SVG_E_UNSUPPORTED; }
 	if (C == 0) { for (uint32_t i = 0; i < n; i++) counts.push_back(0); return 0; }
@@ -639,6 +664,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	LCHK(hipMemcpyAsync(&lh[1], d_head + C - 1, 4, hipMemcpyDeviceToHost, st));
 	LCHK(hipStreamSynchronize(st));
 	const uint64_t G = (uint64_t)lh[0] + lh[1];
+	if (dbg) t_seg = now();
 	uint32_t *d_sfirst = d_cv;   // the first sort's input payloads are free now
 	hipLaunchKernelGGL(long_segstart_kernel, dim3(blocks_of(C, 256)), dim3(256), 0, st, d_head, d_sid, C, d_sfirst);
 	LCHK(hipGetLastError());
@@ -660,6 +686,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	LCHK(hipMemcpyAsync(&lk[1], d_keep + G - 1, 4, hipMemcpyDeviceToHost, st));
 	LCHK(hipStreamSynchronize(st));
 	const uint64_t K = (uint64_t)lk[0] + lk[1];
+	if (dbg) t_keep = now();
 	LEmit em;
 	em.skey = d_sk2; em.sidx = d_si2; em.keep = d_keep; em.kpos = d_kpos; em.sdata = d_sd; em.n_seg = G; em.out = d_out;
 	hipLaunchKernelGGL(long_emit_kernel, dim3(blocks_of(G, 256)), dim3(256), 0, st, em);
@@ -670,6 +697,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	hipLaunchKernelGGL(long_order_kernel, dim3(n), dim3(256), 0, st, d_out, d_vs, (uint32_t *)d_ck, d_coff,
 	                   (uint32_t *)d_ck2, d_cv2, d_ord);
 	LCHK(hipGetLastError());
+	if (dbg) { LCHK(hipStreamSynchronize(st)); t_dev = now(); }
 	if (int e = res.reserve(K)) return e;
 	std::vector<uint64_t> vs(n + 1);
 	std::vector<Span> spans = {{vs.data(), d_vs, 8ull * (n + 1)}, {res.votes + res.n, d_out, sizeof(svg_long_vote) * K},
@@ -677,9 +705,11 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	if (int e = staged_download(h, spans, T)) return e;
 	res.n += K;
 	for (uint32_t i = 0; i < n; i++) counts.push_back(vs[i + 1] - vs[i]);
-	if (getenv("SVG_LONG_DEBUG"))
-		fprintf(stderr, "[svg_long] reads %u probes %llu candidates %llu segments %llu slots %llu\n", n,
-		        (unsigned long long)P, (unsigned long long)C, (unsigned long long)G, (unsigned long long)K);
+	if (dbg)
+		fprintf(stderr, "[svg_long] reads %u probes %llu candidates %llu segments %llu slots %llu | ms: upload %.1f probe %.1f "
+		        "sort1+segments %.1f sort2+keep %.1f emit+order %.1f download %.1f\n", n, (unsigned long long)P,
+		        (unsigned long long)C, (unsigned long long)G, (unsigned long long)K, t_up - t0, t_probe - t_up, t_seg - t_probe,
+		        t_keep - t_seg, t_dev - t_keep, now() - t_dev);
 	return 0;
 }
 }  // namespace
@@ -687,7 +717,18 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 extern "C" void svg_long_free(svg_long_result *r)
 {
 	if (!r) return;
-	free(r->vstart); free(r->votes); free(r->order);
+	free(r->vstart);
+	{
+		// keep the larger arrays for the next call, free the others
+		std::lock_guard<std::mutex> lk(g_cache_mu);
+		void *v = r->votes, *o = r->order;
+		if (v && o && (!g_cache_v || malloc_usable_size(v) > malloc_usable_size(g_cache_v))) {
+			std::swap(v, g_cache_v);
+			std::swap(o, g_cache_o);
+		}
+		free(v);
+		free(o);
+	}
 	memset(r, 0, sizeof *r);
 }
 
@@ -720,6 +761,7 @@ extern "C" int svg_long_vote_batch(svg_index *h, const svg_long_reads *R, svg_lo
 	const uint64_t pcap = ec && atoll(ec) > 0 ? (uint64_t)atoll(ec) : (32ull << 20);
 	const uint64_t ccap = 256ull << 20;
 	LOut res = {NULL, NULL, 0, 0};
+	res.adopt_cache();
 	std::vector<uint64_t> counts;
 	counts.reserve(R->n_reads);
 	uint64_t r0 = 0;
