@@ -407,20 +407,34 @@ __global__ void __launch_bounds__(256) long_vstart_kernel(const uint64_t *skey, 
 // grow-only device arenas and pinned staging of the handle (svg_index::lws)
 struct svg_longws {
 	void *dA; size_t capA;     // probe phase: text, read table, probe arrays, scan temp
-	void *dB; size_t capB;     // candidate phase: keys / payloads / segments / slots, sort and scan temps
-	void *hs[2]; size_t hcap;  // pinned staging (uploads and downloads in pieces)
+	void *dB; size_t capB;     // candidate phase: keys / payloads / segments, sort and scan temps
+	void *hs[2]; size_t hcap;  // pinned staging of the uploads (in pieces)
 	hipEvent_t ev[2];
+	// the chunk's results by chunk parity: device slots / orders / read starts, their pinned copy,
+	// the download stream and its events -- chunk c's download and host copy run while chunk c+1
+	// is on the device
+	void *dO[2]; size_t capO[2];
+	void *hO[2]; size_t hcapO[2];
+	hipStream_t down;
+	hipEvent_t ev_res[2], ev_down[2];
 };
 
 void svg_long_ws_free(svg_index *h)
 {
 	svg_longws *w = h->lws;
 	if (!w) return;
+	if (w->down) hipStreamSynchronize(w->down);
 	hipFree(w->dA); hipFree(w->dB);
 	for (int i = 0; i < 2; i++) {
 		if (w->hs[i]) hipHostFree(w->hs[i]);
 		if (w->ev[i]) hipEventDestroy(w->ev[i]);
+		hipFree(w->dO[i]);
+		if (w->hO[i]) hipHostFree(w->hO[i]);
+		if (w->ev_res[i]) hipEventDestroy(w->ev_res[i]);
+		if (w->ev_down[i]) hipEventDestroy(w->ev_down[i]);
+		h->device_bytes -= w->capO[i];
 	}
+	if (w->down) hipStreamDestroy(w->down);
 	h->device_bytes -= w->capA + w->capB;
 	free(w);
 	h->lws = NULL;
@@ -480,33 +494,6 @@ void par_copy(void *dst, const void *src, size_t n, int T)
 	for (auto &x : th) x.join();
 }
 
-struct Span { void *dst; const void *src; size_t n; };
-
-// device -> host in pieces through the two pinned buffers: piece i+1 is in flight while the host
-// threads copy piece i to its destination
-int staged_download(svg_index *h, const std::vector<Span> &spans, int T)
-{
-	svg_longws *w = h->lws;
-	hipStream_t st = h->stream;
-	struct Piece { char *dst; const char *src; size_t n; };
-	std::vector<Piece> pcs;
-	for (const Span &s : spans)
-		for (size_t o = 0; o < s.n; o += PIECE)
-			pcs.push_back({(char *)s.dst + o, (const char *)s.src + o, s.n - o < PIECE ? s.n - o : PIECE});
-	for (size_t i = 0; i <= pcs.size(); i++) {
-		if (i < pcs.size()) {
-			LCHK(hipMemcpyAsync(w->hs[i & 1], pcs[i].src, pcs[i].n, hipMemcpyDeviceToHost, st));
-			LCHK(hipEventRecord(w->ev[i & 1], st));
-		}
-		if (i > 0) {
-			const size_t j = i - 1;
-			LCHK(hipEventSynchronize(w->ev[j & 1]));
-			par_copy(pcs[j].dst, w->hs[j & 1], pcs[j].n, T);
-		}
-	}
-	return 0;
-}
-
 // One freed result's arrays are kept for the next call (process-wide): a batch's slots are
 // ~24 B each (GBs for long-read batches), and handing the same pages back avoids unmapping them
 // in svg_long_free and faulting fresh ones in during the next download.
@@ -542,8 +529,15 @@ struct LOut {
 };
 
 // one chunk of reads [r0, r1): appends its slots, orders and per-read counts
+// the host side of a chunk's download: wait for its pinned copy, then copy it into the result
+struct Pending {
+	std::thread th;
+	bool active = false;
+	void join() { if (active) { th.join(); active = false; } }
+};
+
 int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, const uint64_t cand_cap, LOut &res,
-               std::vector<uint64_t> &counts, bool *too_big, int T)
+               std::vector<uint64_t> &counts, bool *too_big, int T, int par, Pending &prev)
 {
 	hipStream_t st = h->stream;
 	svg_longws *w = h->lws;
@@ -566,7 +560,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	}
 	toff[n] = tb;
 	pbase[n] = (uint32_t)P;
-	if (P == 0) { for (uint32_t i = 0; i < n; i++) counts.push_back(0); return 0; }
+	if (P == 0) { for (uint32_t i = 0; i < n; i++) counts[r0 + i] = 0; return 0; }
 	// ---- probe phase
 	size_t scan1 = 0;
 	LCHK(hipcub::DeviceScan::ExclusiveSum(NULL, scan1, (uint64_t *)NULL, (uint64_t *)NULL, (int)P, st));
@@ -621,7 +615,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	if (dbg) t_probe = now();
 	if (C > cand_cap && n > 1) { *too_big = true; return 0; }
 	if (C >= 0x7fffffffull) { svg_set_error("svg_long_vote_batch: read %llu has %llu candidates", (unsigned long long)r0, (unsigned long long)C); return SVG_E_UNSUPPORTED; }
-	if (C == 0) { for (uint32_t i = 0; i < n; i++) counts.push_back(0); return 0; }
+	if (C == 0) { for (uint32_t i = 0; i < n; i++) counts[r0 + i] = 0; return 0; }
 	// ---- candidate phase (segments and slots are bounded by the candidates)
 	int rbits = 1;
 	while ((1u << rbits) < n) rbits++;
@@ -644,7 +638,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 		d_ck = cb.take<uint64_t>(C); d_ck2 = cb.take<uint64_t>(C); d_cv = cb.take<uint32_t>(C); d_cv2 = cb.take<uint32_t>(C);
 		d_coff = cb.take<uint32_t>(C); d_head = cb.take<uint32_t>(C); d_sid = cb.take<uint32_t>(C);
 		d_sk = cb.take<uint64_t>(C); d_sk2 = cb.take<uint64_t>(C); d_si = cb.take<uint32_t>(C); d_si2 = cb.take<uint32_t>(C);
-		d_sd = cb.take<uint4>(C); d_out = cb.take<svg_long_vote>(C); d_ord = cb.take<uint32_t>(C); d_vs = cb.take<uint64_t>(n + 1);
+		d_sd = cb.take<uint4>(C);
 		d_tmp = cb.take<char>(t_max);
 	}
 	LExpand le;
@@ -687,6 +681,13 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	LCHK(hipStreamSynchronize(st));
 	const uint64_t K = (uint64_t)lk[0] + lk[1];
 	if (dbg) t_keep = now();
+	// this chunk's results go to the parity's output buffers (the previous chunk's may still be on
+	// their way to the host)
+	Carve co = {NULL, 0};
+	for (int pass = 0; pass < 2; pass++) {
+		if (pass) { if (int e = arena(h, &w->dO[par], &w->capO[par], co.off)) return e; co.base = (char *)w->dO[par]; co.off = 0; }
+		d_vs = co.take<uint64_t>(n + 1); d_out = co.take<svg_long_vote>(K); d_ord = co.take<uint32_t>(K);
+	}
 	LEmit em;
 	em.skey = d_sk2; em.sidx = d_si2; em.keep = d_keep; em.kpos = d_kpos; em.sdata = d_sd; em.n_seg = G; em.out = d_out;
 	hipLaunchKernelGGL(long_emit_kernel, dim3(blocks_of(G, 256)), dim3(256), 0, st, em);
@@ -697,19 +698,45 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	hipLaunchKernelGGL(long_order_kernel, dim3(n), dim3(256), 0, st, d_out, d_vs, (uint32_t *)d_ck, d_coff,
 	                   (uint32_t *)d_ck2, d_cv2, d_ord);
 	LCHK(hipGetLastError());
+	LCHK(hipEventRecord(w->ev_res[par], st));
 	if (dbg) { LCHK(hipStreamSynchronize(st)); t_dev = now(); }
+	// the previous chunk's host copy is done before the result grows (realloc) or its staging is reused
+	prev.join();
 	if (int e = res.reserve(K)) return e;
-	std::vector<uint64_t> vs(n + 1);
-	std::vector<Span> spans = {{vs.data(), d_vs, 8ull * (n + 1)}, {res.votes + res.n, d_out, sizeof(svg_long_vote) * K},
-	                           {res.order + res.n, d_ord, 4ull * K}};
-	if (int e = staged_download(h, spans, T)) return e;
+	const size_t bytes = 8ull * (n + 1) + (sizeof(svg_long_vote) + 4) * K;
+	if (w->hcapO[par] < bytes) {
+		if (w->hO[par]) hipHostFree(w->hO[par]);
+		w->hO[par] = NULL;
+		w->hcapO[par] = 0;
+		const size_t cap = bytes + bytes / 4;
+		if (hipHostMalloc(&w->hO[par], cap, hipHostMallocDefault) != hipSuccess) { svg_set_error("svg_long_vote_batch: pinned staging of %zu bytes", cap); return SVG_E_NOMEM; }
+		w->hcapO[par] = cap;
+	}
+	char *hv = (char *)w->hO[par];
+	LCHK(hipStreamWaitEvent(w->down, w->ev_res[par], 0));
+	LCHK(hipMemcpyAsync(hv, d_vs, 8ull * (n + 1), hipMemcpyDeviceToHost, w->down));
+	LCHK(hipMemcpyAsync(hv + 8ull * (n + 1), d_out, sizeof(svg_long_vote) * K, hipMemcpyDeviceToHost, w->down));
+	LCHK(hipMemcpyAsync(hv + 8ull * (n + 1) + sizeof(svg_long_vote) * K, d_ord, 4ull * K, hipMemcpyDeviceToHost, w->down));
+	LCHK(hipEventRecord(w->ev_down[par], w->down));
+	svg_long_vote *dst_v = res.votes + res.n;
+	uint32_t *dst_o = res.order + res.n;
 	res.n += K;
-	for (uint32_t i = 0; i < n; i++) counts.push_back(vs[i + 1] - vs[i]);
+	hipEvent_t ev = w->ev_down[par];
+	uint64_t *cnt = counts.data() + r0;
+	const double t_issue = dbg ? now() : 0;
+	prev.th = std::thread([=] {
+		hipEventSynchronize(ev);
+		const uint64_t *vs = (const uint64_t *)hv;
+		for (uint32_t i = 0; i < n; i++) cnt[i] = vs[i + 1] - vs[i];
+		par_copy(dst_v, hv + 8ull * (n + 1), sizeof(svg_long_vote) * K, T);
+		par_copy(dst_o, hv + 8ull * (n + 1) + sizeof(svg_long_vote) * K, 4ull * K, T);
+	});
+	prev.active = true;
 	if (dbg)
 		fprintf(stderr, "[svg_long] reads %u probes %llu candidates %llu segments %llu slots %llu | ms: upload %.1f probe %.1f "
-		        "sort1+segments %.1f sort2+keep %.1f emit+order %.1f download %.1f\n", n, (unsigned long long)P,
+		        "sort1+segments %.1f sort2+keep %.1f emit+order %.1f prev-copy-wait+issue %.1f\n", n, (unsigned long long)P,
 		        (unsigned long long)C, (unsigned long long)G, (unsigned long long)K, t_up - t0, t_probe - t_up, t_seg - t_probe,
-		        t_keep - t_seg, t_dev - t_keep, now() - t_dev);
+		        t_keep - t_seg, t_dev - t_keep, t_issue - t_dev);
 	return 0;
 }
 }  // namespace
@@ -754,6 +781,11 @@ extern "C" int svg_long_vote_batch(svg_index *h, const svg_long_reads *R, svg_lo
 			HIPCHK(hipEventCreateWithFlags(&w->ev[i], hipEventDisableTiming));
 		}
 		w->hcap = PIECE;
+		HIPCHK(hipStreamCreateWithFlags(&w->down, hipStreamNonBlocking));
+		for (int i = 0; i < 2; i++) {
+			HIPCHK(hipEventCreateWithFlags(&w->ev_res[i], hipEventDisableTiming));
+			HIPCHK(hipEventCreateWithFlags(&w->ev_down[i], hipEventDisableTiming));
+		}
 	}
 	const int T = svg_host_threads();
 	// chunks: <= 65535 reads (16-bit read field of the segment key), <= 32M probes
@@ -762,8 +794,9 @@ extern "C" int svg_long_vote_batch(svg_index *h, const svg_long_reads *R, svg_lo
 	const uint64_t ccap = 256ull << 20;
 	LOut res = {NULL, NULL, 0, 0};
 	res.adopt_cache();
-	std::vector<uint64_t> counts;
-	counts.reserve(R->n_reads);
+	std::vector<uint64_t> counts(R->n_reads + 1, 0);
+	Pending pend;
+	int par = 0;
 	uint64_t r0 = 0;
 	while (r0 < R->n_reads) {
 		uint64_t r1 = r0, P = 0;
@@ -775,14 +808,16 @@ extern "C" int svg_long_vote_batch(svg_index *h, const svg_long_reads *R, svg_lo
 		}
 		for (;;) {
 			bool big = false;
-			const int rc = long_chunk(h, R, r0, r1, ccap, res, counts, &big, T);
-			if (rc) { free(res.votes); free(res.order); return rc; }
+			const int rc = long_chunk(h, R, r0, r1, ccap, res, counts, &big, T, par, pend);
+			if (rc) { pend.join(); free(res.votes); free(res.order); return rc; }
 			if (!big) break;
 			if (getenv("SVG_LONG_DEBUG")) fprintf(stderr, "[svg_long] split %llu reads\n", (unsigned long long)(r1 - r0));
 			r1 = r0 + (r1 - r0) / 2;   // too many candidates: half the reads
 		}
 		r0 = r1;
+		par ^= 1;
 	}
+	pend.join();
 	if (res.reserve(1)) { free(res.votes); free(res.order); return SVG_E_NOMEM; }
 	out->n_reads = R->n_reads;
 	out->votes = res.votes;
