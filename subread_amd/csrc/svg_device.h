@@ -142,11 +142,13 @@ struct svg_index {
 	// chunk pipeline: probe + lane kernels of chunk c run on the caller's stream while the wave
 	// kernel of chunk c-1 runs on stream2, so the per-chunk buffers come in two slots (c & 1)
 	hipStream_t stream2;
-	hipEvent_t ev_lane[2], ev_wave[2];   // slot's records + deferral list ready / wave kernel done
-	void *d_prec[2]; size_t prec_cap[2];   // probe records of one chunk
-	void *d_big[2]; size_t big_cap[2];     // probe_line_kernel's big-bucket list (count, slot indexes)
+	// (three slots: the host pipeline's probe-ahead mode runs the probe kernels of sub-batch i+1
+	// beside the lane kernel of i and the wave kernel of i-1)
+	hipEvent_t ev_lane[3], ev_wave[3], ev_probe[3];   // slot's records + deferral list ready / wave kernel done / probe records ready
+	void *d_prec[3]; size_t prec_cap[3];   // probe records of one chunk
+	void *d_big[3]; size_t big_cap[3];     // probe_line_kernel's big-bucket list (count, slot indexes)
 	// lane-per-read SE path (svg_lane.hip): candidate lists + deferral list, per-wave cold scratch
-	void *d_lane[2]; size_t lane_cap[2];
+	void *d_lane[3]; size_t lane_cap[3];
 	uint32_t *d_lscratch; size_t lscratch_words;     // light pass
 	uint32_t *d_lscratch2; size_t lscratch2_words;   // heavy pass
 	// svg_set_timing: event pairs per launch (kinds: 0 probe_kernel, 1 vote_kernel, 2 gather_kernel,
@@ -158,7 +160,7 @@ struct svg_index {
 	// staging for svg_vote_batch (host buffers): two sub-batch slots, uploads and downloads on
 	// their own streams so PCIe traffic of sub-batches i+1 / i-1 overlaps the vote of i
 	void *d_in[3]; size_t d_in_cap[3];     // uploads run one sub-batch ahead: three input slots
-	void *d_out[2]; size_t d_out_cap[2];
+	void *d_out[3]; size_t d_out_cap[3];
 	hipStream_t up_stream, down_stream;
 	hipEvent_t ev_up[3], ev_done[3], ev_down[3];
 	// sticky device error word (KParams::err) and the handle's last queued work: every call
@@ -273,6 +275,10 @@ struct VoteJob {
 int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2, svg_mapping_result *out,
                      svg_subjunc_result *jout, uint16_t *big_margin, VoteJob *job);
 int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slot, hipStream_t st, hipStream_t st2);
+// the two halves of svg_vote_chunk: the probe kernels (into the slot's probe records), then the
+// lane kernels on st and the wave kernel on st2
+int svg_vote_chunk_probe(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slot, hipStream_t st);
+int svg_vote_chunk_vote(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slot, hipStream_t st, hipStream_t st2);
 int svg_vote_batch_device_packed(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
                                  const svg_packed_reads *pk, svg_mapping_result *out, svg_subjunc_result *jout,
                                  uint16_t *big_margin, hipStream_t stream);

@@ -501,7 +501,14 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	const size_t rec_b = (size_t)R * 68, j_b = jo ? (size_t)R * 16 : 0, bm_b = bmo ? (size_t)ends * SVG_BIG_MARGIN_WORDS * 2 : 0;
 	const CompLayout CL = comp_layout(sub, R, ends, jo, bmo);
 	const size_t o_j = (sub * rec_b + 255) & ~(size_t)255, o_bm = (o_j + sub * j_b + 255) & ~(size_t)255;
-	for (int s = 0; s < 2; s++)
+	// probe-ahead (SVG_PROBE_AHEAD=1; single-end align from packed reads, one index block): the probe
+	// kernels of sub-batch i+1 run on the upload stream right behind its upload, beside the lane
+	// kernels of i (stream) and the wave kernel of i-1 (stream2), in three device slots.  Measured
+	// slower at C3 (118.2 vs 112.8 ms/step, profiles/r03/sweeps/c3_probe_ahead_*.json): three
+	// kernels sharing the CUs slow the latency-bound probe chain more than the overlap saves
+	const char *ea = getenv("SVG_PROBE_AHEAD");
+	const bool ahead = packed && !sjm && !pe && h->nblocks < 2 && n > sub && ea && ea[0] == '1';
+	for (int s = 0; s < (ahead ? 3 : 2); s++)
 		if ((rc = svg_ensure(h, &h->d_out[s], &h->d_out_cap[s], o_bm + sub * bm_b + 64))) return rc;
 	for (int s = 0; s < 3; s++) {
 		if ((rc = svg_ensure(h, &io->d_comp[s], &io->d_comp_cap[s], CL.bytes))) return rc;
@@ -663,8 +670,37 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		return 0;
 	};
 
+	// probe-ahead: the job of sub-batch j (packed reads, no unpack) in jobs[j % 3], its probes on
+	// the upload stream after its upload, ev_probe[j % 3] when its probe records are ready
+	VoteJob jobs[3];
+	auto probe_ahead = [&](uint64_t j) -> int {
+		const int s3 = (int)(j % 3);
+		const uint64_t b = j * sub, m = j + 1 < nsub ? sub : n - b;
+		const Up &U = up[s3];
+		uint8_t *din = (uint8_t *)h->d_in[s3];
+		svg_reads dr0;
+		svg_packed_reads pk0;
+		pk0.bases = (const uint32_t *)(din + U.o_bases[0]) - U.wlo[0];
+		pk0.xmask = q1->xmask ? (const uint32_t *)(din + U.o_x[0]) - U.xlo[0] : NULL;
+		pk0.starts = q1->starts ? (const uint64_t *)(din + U.o_st[0]) : NULL;
+		pk0.stride = q1->stride;
+		pk0.lens = (const uint16_t *)(din + U.o_len[0]);
+		pk0.n_reads = m;
+		dr0 = svg_reads{NULL, NULL, pk0.lens, m};
+		h->max_read_len = U.maxlen;
+		uint8_t *dout = (uint8_t *)h->d_out[s3];
+		int rc2 = svg_vote_prepare(h, p, &dr0, NULL, (svg_mapping_result *)dout, NULL, NULL, &jobs[s3]);
+		if (rc2) return rc2;
+		set_packed(jobs[s3], &pk0, 1, b);
+		if (m > jobs[s3].chunk) { svg_set_error("probe-ahead: sub-batch of %llu reads over one chunk", (unsigned long long)m); return SVG_E_UNSUPPORTED; }
+		if ((rc2 = svg_vote_chunk_probe(h, &jobs[s3], 0, m, s3, h->up_stream))) return rc2;
+		HIPCHK(hipEventRecord(h->ev_probe[s3], h->up_stream));
+		return 0;
+	};
+
 	bool overlap_any = false;
 	rc = upload(0);
+	if (!rc && ahead) rc = probe_ahead(0);
 	// iteration i: upload i+1, vote i, download i-2, expand i-3 -- the host blocks on sub-batch
 	// i-2 only, with i-1 and i already queued behind it on the GPU
 	for (uint64_t i = 0; i < nsub + 3 && !rc; i++) {
@@ -674,7 +710,21 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		const uint64_t b = i * sub, m = i + 1 < nsub ? sub : n - b;
 		double tu = dbg ? now() : 0;
 		if (i + 1 < nsub && (rc = upload(i + 1))) break;
+		if (i + 1 < nsub && ahead && (rc = probe_ahead(i + 1))) break;
 		if (dbg) { w_up += now() - tu; tu = now(); }
+		uint8_t *dout;
+		hipStream_t st2 = st;
+		if (ahead) {
+			// lane kernels of sub-batch i once its probe records are ready, the wave kernel beside
+			VoteJob &job = jobs[s3];
+			HIPCHK(hipStreamWaitEvent(st, h->ev_probe[s3], 0));
+			const bool overlap = job.overlap_mode;
+			overlap_any = overlap_any || overlap;
+			st2 = overlap ? h->stream2 : st;
+			if ((rc = svg_vote_chunk_vote(h, &job, 0, m, s3, st, st2))) break;
+			dout = (uint8_t *)h->d_out[s3];
+			if (dbg) w_vote += now() - tu;
+		} else {
 		const Up &U = up[s3];
 		uint8_t *din = (uint8_t *)h->d_in[s3];
 		// ---- vote on stream (probe, lane) / stream2 (wave); slot s free once sub-batch i-2 is done
@@ -706,7 +756,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 			}
 		}
 		if (rc) break;
-		uint8_t *dout = (uint8_t *)h->d_out[s];
+		dout = (uint8_t *)h->d_out[s];
 		VoteJob job;
 		if ((rc = svg_vote_prepare(h, p, &dr[0], pe ? &dr[1] : NULL, (svg_mapping_result *)dout,
 		                           jo ? (svg_subjunc_result *)(dout + o_j) : NULL, bmo ? (uint16_t *)(dout + o_bm) : NULL, &job)))
@@ -716,7 +766,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		// the records the earlier ones left)
 		const bool overlap = job.overlap_mode && nsub > 1 && m <= job.chunk && h->nblocks < 2;
 		overlap_any = overlap_any || overlap;
-		hipStream_t st2 = overlap ? h->stream2 : st;
+		st2 = overlap ? h->stream2 : st;
 		for (uint64_t c0 = 0; c0 < m && !rc; c0 += job.chunk)   // one chunk unless reads are long
 			rc = svg_vote_chunk(h, &job, c0, m - c0 < job.chunk ? m - c0 : job.chunk, s, st, st2);
 		for (int k = 1; k < h->nblocks && !rc; k++) {
@@ -732,6 +782,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		}
 		if (rc) break;
 		if (dbg) w_vote += now() - tu;
+		}
 		// ---- compaction into compact slot s3 (free once sub-batch i-3's download is done)
 		if (i >= 3) HIPCHK(hipStreamWaitEvent(st2, h->ev_down[s3], 0));
 		{

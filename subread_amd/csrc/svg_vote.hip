@@ -2319,9 +2319,12 @@ int svg_index_finish_device(svg_index *h)
 	HIPCHK(hipEventCreateWithFlags(&h->ev_up[2], hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&h->ev_done[2], hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&h->ev_down[2], hipEventDisableTiming));
-	for (int s = 0; s < 2; s++) {
+	for (int s = 0; s < 3; s++) {
 		HIPCHK(hipEventCreateWithFlags(&h->ev_lane[s], hipEventDisableTiming));
 		HIPCHK(hipEventCreateWithFlags(&h->ev_wave[s], hipEventDisableTiming));
+		HIPCHK(hipEventCreateWithFlags(&h->ev_probe[s], hipEventDisableTiming));
+	}
+	for (int s = 0; s < 2; s++) {
 		HIPCHK(hipEventCreateWithFlags(&h->ev_up[s], hipEventDisableTiming));
 		HIPCHK(hipEventCreateWithFlags(&h->ev_done[s], hipEventDisableTiming));
 		HIPCHK(hipEventCreateWithFlags(&h->ev_down[s], hipEventDisableTiming));
@@ -2553,20 +2556,14 @@ extern "C" void svg_index_close(svg_index *h)
 	if (h->down_stream) hipStreamSynchronize(h->down_stream);
 	svg_io_free(h);
 	svg_long_ws_free(h);
-	for (int s = 0; s < 2; s++) {
+	for (int s = 0; s < 3; s++) {
 		hipFree(h->d_prec[s]);
 		hipFree(h->d_lane[s]);
 		hipFree(h->d_big[s]);
 		hipFree(h->d_in[s]);
-		if (s == 1) hipFree(h->d_in[2]);
 		hipFree(h->d_out[s]);
-		if (s == 1) {
-			hipEvent_t e3[3] = {h->ev_up[2], h->ev_done[2], h->ev_down[2]};
-			for (int k = 0; k < 3; k++)
-				if (e3[k]) hipEventDestroy(e3[k]);
-		}
-		hipEvent_t *evs[5] = {h->ev_lane, h->ev_wave, h->ev_up, h->ev_done, h->ev_down};
-		for (int k = 0; k < 5; k++)
+		hipEvent_t *evs[6] = {h->ev_lane, h->ev_wave, h->ev_probe, h->ev_up, h->ev_done, h->ev_down};
+		for (int k = 0; k < 6; k++)
 			if (evs[k][s]) hipEventDestroy(evs[k][s]);
 	}
 	hipFree(h->d_lscratch);
@@ -2918,18 +2915,15 @@ int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, con
 // reads [c0, c0+cn) of the prepared batch; slot's probe records / lane buffers must be free
 int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slot, hipStream_t st, hipStream_t st2)
 {
+	int rc = svg_vote_chunk_probe(h, job, c0, cn, slot, st);
+	return rc ? rc : svg_vote_chunk_vote(h, job, c0, cn, slot, st, st2);
+}
+
+int svg_vote_chunk_probe(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slot, hipStream_t st)
+{
 	const KParams &kp = job->kp;
-	const svg_params *p = &kp.p;
-	const int ends = job->ends, nps = job->nps;
 	int rc;
 	if ((rc = svg_ensure(h, &h->d_prec[slot], &h->prec_cap[slot], cn * job->per_read * 8))) return rc;
-	// overlapped, the wave kernel leaves CU slots to the next chunk's probe kernel, whose
-	// latency-bound chain needs the occupancy (the wave kernel has slack on its stream)
-	h->wave_cap = 0;
-	if (st2 != st) {
-		const char *ew = getenv("SVG_WAVE_CAP");
-		h->wave_cap = ew ? atoi(ew) : SVG_WAVE_CAP;
-	}
 	PParams pp = job->pp;
 	pp.out = (uint2 *)h->d_prec[slot];
 	pp.off1 = kp.off1 + c0; pp.len1 = kp.len1 + c0;
@@ -2990,7 +2984,23 @@ int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slo
 	}
 #undef PROBE_LAUNCH
 	HIPCHK(hipGetLastError());
-	if ((rc = timing_mark(h, 0, 1, st))) return rc;
+	return timing_mark(h, 0, 1, st);
+}
+
+int svg_vote_chunk_vote(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slot, hipStream_t st, hipStream_t st2)
+{
+	const KParams &kp = job->kp;
+	const svg_params *p = &kp.p;
+	const int ends = job->ends, nps = job->nps;
+	const bool pe = kp.len2 != NULL;
+	int rc;
+	// overlapped, the wave kernel leaves CU slots to the next chunk's probe kernel, whose
+	// latency-bound chain needs the occupancy (the wave kernel has slack on its stream)
+	h->wave_cap = 0;
+	if (st2 != st) {
+		const char *ew = getenv("SVG_WAVE_CAP");
+		h->wave_cap = ew ? atoi(ew) : SVG_WAVE_CAP;
+	}
 	KParams kc = kp;
 	kc.off1 = kp.off1 + c0; kc.len1 = kp.len1 + c0;
 	if (pe) { kc.off2 = kp.off2 + c0; kc.len2 = kp.len2 + c0; }
