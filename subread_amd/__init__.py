@@ -106,9 +106,10 @@ def lib():
         L.svg_fragile_batch.argtypes = [vp] * 5
         L.svg_fragile_batch.restype = i32
         L.svg_fragile_free.argtypes = [vp]
-        L.svg_long_vote_batch.argtypes = [vp] * 3
-        L.svg_long_vote_batch.restype = i32
-        L.svg_long_free.argtypes = [vp]
+        if hasattr(L, "svg_long_vote_batch"):   # (older builds loaded side by side for A/B runs lack it)
+            L.svg_long_vote_batch.argtypes = [vp] * 3
+            L.svg_long_vote_batch.restype = i32
+            L.svg_long_free.argtypes = [vp]
         L.svg_events_add_batch2.argtypes = [vp] * 8 + [u64] + [vp] * 4
         L.svg_events_add_batch2.restype = i32
         L.svg_index_build.argtypes = [ctypes.c_char_p, i32, i32, i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(vp)]
