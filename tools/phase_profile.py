@@ -57,6 +57,9 @@ def main():
     for k in range(8):
         print("  %-12s %6.2f%%  %8.0f cycles/read  %8.0f cycles per wave-kernel read" % (
             names[k], 100.0 * c[8 + k] / max(1, tot), c[8 + k] / n, c[8 + k] / nd))
+    kt = [c[21], c[22], c[23]]   # phase K split: top-3 (acc[8]), simples after big-margin (acc[9]), pairs (acc[10])
+    print("  phase K split (not in the shares above): top-3 %.0f, simples %.0f, pairs %.0f cycles per wave-kernel read"
+          % tuple(x / nd for x in kt))
     print("  lane pass: defer cap/len %d, slots %d, shift %d, candidates %d, deferrals %d" % tuple(c[16:21]))
     print("  wave kernel: batch-settled %d, serially replayed %d" % (c[26], c[27]))
     print("  serial by reason: >= 2 slots in tolerance %d, one slot but spilled / d != 0 / kP1 <= last %d, "
