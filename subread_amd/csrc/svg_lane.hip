@@ -143,6 +143,7 @@ struct LParams {
 	const uint16_t *len2;
 	const uint32_t *chr_end;
 	int n_chr, padding, min_pair, max_pair, mvc;
+	int max_pairs;                // a pair's simples products past this go to the wave kernel (per-lane pair loop bound)
 	unsigned long long *stats;    // [3] += results; [4] += deferred reads (final pass only);
 	int stat_base, final_pass;    // diagnostics at stats[stat_base..+4]: deferrals by reason (3), candidates, deferrals
 	// count bins (fused SE path): lane_bin_kernel lists the chunk's reads by their larger strand's
@@ -1167,7 +1168,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 			};
 			simples(std::integral_constant<int, 0>());
 			simples(std::integral_constant<int, 1>());
-			if (ns[0] * ns[1] > 96) { L.dfr = true; L.why = 2; continue; }   // bounded per-lane pair loop
+			if (ns[0] * ns[1] > lp.max_pairs) { L.dfr = true; L.why = 2; continue; }   // bounded per-lane pair loop
 			// value / position / record of a simple
 			auto sv = [&](int E, uint32_t id, uint32_t &pos) __attribute__((always_inline)) -> int {
 				if (id < 32u) { const uint2 x = L.pm[id * 64 + L.lane]; pos = x.x; return lm_votes(x.y); }
@@ -1615,6 +1616,10 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	LParams lp;
 	memset(&lp, 0, sizeof lp);
 	lp.len = len1; lp.len2 = len2; lp.n = n; lp.cap = LANE_PE_CAP;
+	{
+		const char *ec = getenv("SVG_LANE_PE_CAP");   // tuning knob: candidates per end and strand
+		if (ec && atoi(ec) > 0) lp.cap = atoi(ec);
+	}
 	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps;
 	lp.gap = h->dix.gap; lp.total_subreads = p->total_subreads;
 	lp.tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
@@ -1624,6 +1629,11 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	lp.min_votes_first = p->min_votes_first; lp.min_votes_second = p->min_votes_second;
 	lp.chr_end = h->dix.chr_end; lp.n_chr = (int)h->dix.n_chr; lp.padding = h->dix.padding;
 	lp.min_pair = p->min_pair_distance; lp.max_pair = p->max_pair_distance; lp.mvc = p->max_vote_combinations;
+	{
+		const char *ep = getenv("SVG_LANE_PAIRS");
+		// 96 -> 256: C5pe deferrals 34% -> 21% of the pairs, 942 -> 779 ms/step (profiles/r03/sweeps/c5pe_pairs_*.json)
+		lp.max_pairs = ep && atoi(ep) > 0 ? atoi(ep) : 256;
+	}
 	lp.out = out;
 	lp.jout = jout;
 	lp.bm_out = jout ? bm_out : NULL;
