@@ -960,9 +960,12 @@ __device__ __forceinline__ int llocate(const uint32_t *ce, int ntot, int padding
 	return -1;
 }
 
-// simples (simple_mapping_t) of one end as a packed list of 6-bit ids: slot (< 32) or 32 + stored
-// index; PLW words hold 5 * PLW >= 31 slots + 3 stored records
-#define PLW 7
+#ifndef LANE_PE_K
+#define LANE_PE_K 31   // shared by both ends' tables (<= 47: 6-bit ids, stored results at LPE_RID + i)
+#endif
+// simples (simple_mapping_t) of one end as a packed list of 6-bit ids: slot (< LPE_RID) or
+// LPE_RID + stored index; PLW words hold 5 * PLW >= LANE_PE_K slots + 3 stored records
+#define PLW ((LANE_PE_K + 3 + 4) / 5)
 __device__ __forceinline__ uint32_t pl_get(const uint32_t (&w)[PLW], int i)
 {
 	const int q = i / 5, sh = (i - q * 5) * 6;
@@ -991,6 +994,8 @@ __device__ __forceinline__ void pl_put(uint32_t (&w)[PLW], int i, uint32_t id)
 // records per end and the junction search / donor scoring of every record taken from a table, as
 // in lane_kernel
 // (waves_per_eu 3: the subjunc variant needs 179 VGPRs unconstrained, 168 without spills at 3 waves)
+// simples of a pair: slot ids < LPE_RID, the end's stored results (multi-block) at LPE_RID + i (6-bit ids)
+#define LPE_RID 48u
 template <int K, int NPF, bool SJ>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) lane_pe_kernel(LParams lp)
 {
@@ -1162,7 +1167,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 #pragma unroll
 					for (int i = 0; i < 3; i++) {
 						const uint32_t m = E ? rm1[i] : rm0[i];
-						if (i < mb && ns[E] < mvs && RM_V(m) == N) { pl_put(pl[E], ns[E], 32u + (uint32_t)i); ns[E]++; }
+						if (i < mb && ns[E] < mvs && RM_V(m) == N) { pl_put(pl[E], ns[E], LPE_RID + (uint32_t)i); ns[E]++; }
 					}
 				}
 			};
@@ -1171,8 +1176,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 			if (ns[0] * ns[1] > lp.max_pairs) { L.dfr = true; L.why = 2; continue; }   // bounded per-lane pair loop
 			// value / position / record of a simple
 			auto sv = [&](int E, uint32_t id, uint32_t &pos) __attribute__((always_inline)) -> int {
-				if (id < 32u) { const uint2 x = L.pm[id * 64 + L.lane]; pos = x.x; return lm_votes(x.y); }
-				const int i = (int)id - 32;
+				if (id < LPE_RID) { const uint2 x = L.pm[id * 64 + L.lane]; pos = x.x; return lm_votes(x.y); }
+				const int i = (int)id - (int)LPE_RID;
 				const uint32_t m = E ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]);
 				pos = E ? sel3(i, rp1[0], rp1[1], rp1[2]) : sel3(i, rp0[0], rp0[1], rp0[2]);
 				return RM_V(m);
@@ -1227,8 +1232,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 				uint32_t pos;
 				const int v = sv(E, id, pos);
 				uint32_t m;
-				if (id < 32u) m = RM((st << 6) | (int)id, v, applied[E]) | (lm_ext(L.pm[id * 64 + L.lane].y) << 22);
-				else { const int i = (int)id - 32; m = E ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]); }
+				if (id < LPE_RID) m = RM((st << 6) | (int)id, v, applied[E]) | (lm_ext(L.pm[id * 64 + L.lane].y) << 22);
+				else { const int i = (int)id - (int)LPE_RID; m = E ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]); }
 				const int c = cur[E];
 				const uint32_t q0 = E ? tp1[0] : tp0[0], q1 = E ? tp1[1] : tp0[1];
 				if ((c > 0 && q0 == pos) || (c > 1 && q1 == pos)) return;
@@ -1240,7 +1245,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 					// core-junction.c:2413-2425)
 					const int b = (E * 3 + c) * 4;
 					uint32_t nib = 0;
-					if (id >= 32u) nib = (jm >> ((E * 3 + (int)id - 32) * 4)) & 15u;
+					if (id >= LPE_RID) nib = (jm >> ((E * 3 + (int)id - (int)LPE_RID) * 4)) & 15u;
 					else needj |= 1u << (E * 3 + c);
 					tjm = (tjm & ~(15u << b)) | (nib << b);
 				}
@@ -1303,7 +1308,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 								const int ov = csM > cs2 ? ce2 - csM : ceM - cs2;
 								if (ov > 14 || abs((int)dist) < 6) continue;
 								if (nl == LJLIST) { L.dfr = true; L.why = 2; break; }
-								lst[nl * 64] = ((uint32_t)E << 7) | ((uint32_t)c << 5) | qs;
+								lst[nl * 64] = ((uint32_t)E << 8) | ((uint32_t)c << 6) | qs;
 								nl++;
 								ends_used |= 1u << E;
 							}
@@ -1327,7 +1332,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 				};
 				for (int k = 0; k < nl; k++) {
 					const uint32_t ent = lst[k * 64];
-					const int key = (int)(ent >> 5), qs = (int)(ent & 31u);
+					const int key = (int)(ent >> 6), qs = (int)(ent & 63u);
 					if (key != Jk) {
 						flush();
 						Jk = key; JE = key >> 2; Jc = key & 3;
@@ -1591,7 +1596,7 @@ int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int s
 	return 1;
 }
 
-#define LANE_PE_K 31   // shared by both ends' tables; 5-bit slot ids (NIL = 31)
+
 #define LANE_PE_CAP 40
 
 // paired-end: lane_pe_kernel over every pair of the chunk; deferred pairs listed for vote_kernel
