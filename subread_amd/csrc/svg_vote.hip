@@ -3074,12 +3074,32 @@ static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads 
 	if (getenv("SVG_DEBUG"))
 		fprintf(stderr, "[svg] batch of %llu reads: chunks of %llu, chunk pipeline %s\n", (unsigned long long)n,
 		        (unsigned long long)chunk, overlap ? "on" : "off");
+	// mapping records only (no subjunc / big-margin records, one index block): a chunk's records are
+	// written to a chunk-sized staging slot -- the lane kernel's scattered per-read stores then land
+	// in the infinity cache, as in the host pipeline -- and copied into `out` in one D2D copy after
+	// the chunk's wave kernel (SVG_DEV_STAGE=1).  Measured no faster at C3 (device path 406 vs 409
+	// Mreads/s, profiles/r03/sweeps/c3_devstage_*.json; parity green), so off by default
+	const size_t rec = (size_t)job.ends * (size_t)p->multi_best * 68;
+	const char *esg = getenv("SVG_DEV_STAGE");
+	const bool stage = overlap && !jout && !big_margin && h->nblocks < 2 && esg && esg[0] == '1';
+	if (stage)
+		for (int s = 0; s < 2; s++)
+			if ((rc = svg_ensure(h, &h->d_out[s], &h->d_out_cap[s], chunk * rec + 64))) return rc;
 	bool slot_busy[2] = {false, false};
 	for (uint64_t c0 = 0; c0 < n && !rc; c0 += chunk) {
 		const uint64_t cn = n - c0 < chunk ? n - c0 : chunk;
 		const int slot = overlap ? (int)((c0 / chunk) & 1) : 0;
 		if (slot_busy[slot]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[slot], 0));
-		rc = svg_vote_chunk(h, &job, c0, cn, slot, st, st2);
+		if (stage) {
+			// the chunk's records at d_out[slot]: the kernels index out + (c0 + i) * rec
+			VoteJob jc = job;
+			jc.kp.out = (uint8_t *)h->d_out[slot] - c0 * rec;
+			rc = svg_vote_chunk(h, &jc, c0, cn, slot, st, st2);
+			if (!rc && hipMemcpyAsync((uint8_t *)out + c0 * rec, h->d_out[slot], cn * rec, hipMemcpyDeviceToDevice, st2) != hipSuccess) {
+				svg_set_error("record copy failed: %s", hipGetErrorString(hipGetLastError()));
+				rc = SVG_E_DEVICE;
+			}
+		} else rc = svg_vote_chunk(h, &job, c0, cn, slot, st, st2);
 		if (!rc && overlap) {
 			HIPCHK(hipEventRecord(h->ev_wave[slot], st2));
 			slot_busy[slot] = true;
