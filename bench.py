@@ -95,6 +95,27 @@ def cpu_info():
     return {"model": model, "logical_cpus": ncpu, "usable_cpus": usable, "cgroup_quota_cpus": quota}
 
 
+def committed_fracs(wl, kernel, bytes_per_launch):
+    """The dominant kernel's roofline fraction recomputed from the committed evidence: the newest
+    profiles/r*_<wl>_kernel_record.json (HIP events of a GPU run, per launch) and the newest
+    profiles/r*_<wl>_serial_trace.json (rocprofv3 kernel trace of the single-stream pipeline)."""
+    import glob
+    out = {}
+    for kind, pat in (("kernel_record", "r*_%s_kernel_record.json"), ("serial_trace", "r*_%s_serial_trace.json")):
+        fs = sorted(glob.glob(os.path.join(ROOT, "profiles", pat % wl)))
+        if not fs:
+            continue
+        d = json.load(open(fs[-1]))
+        k = d.get("kernel_record", d.get("kernels", {})).get(kernel)
+        if not k:
+            continue
+        ms = k["ms"] / k["launches"] if "launches" in k else k["avg_ms"]
+        out[kind] = {"file": os.path.relpath(fs[-1], ROOT), "launch_ms": round(ms, 4),
+                     "achieved": round(bytes_per_launch / (ms / 1e3) / 1e9, 2),
+                     "frac": round(bytes_per_launch / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -111,6 +132,10 @@ def main():
     ap.add_argument("--ascii-reads", type=int, default=8_000_000, help="reads of the ASCII host-entry figure (0: skip)")
     ap.add_argument("--long-reads", type=int, default=20_000,
                     help="ONT-like long reads of the sublong secondary figure on the same index (0: skip)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="library option name=value (svg_set_option; A/B runs -- none changes a record)")
+    ap.add_argument("--kernel-record", default="",
+                    help="also write the timing step's per-kernel HIP-event table and the step times here (JSON)")
     args = ap.parse_args()
 
     import torch
@@ -137,6 +162,9 @@ def main():
         BIG_MARGIN_WORDS
     from subread_amd.sim import random_genome, simulate_reads, simulate_pairs, simulate_spliced_reads
 
+    for o in args.opt:
+        k, v = o.split("=", 1)
+        sa.set_option(k, int(v))
     cpu = cpu_info()
     threads = args.cpu_threads or cpu["usable_cpus"]
     W = workload(args.workload)
@@ -359,6 +387,20 @@ def main():
         else:
             kd["regime"] = "latency/issue-bound (%.0f GB/s of HBM traffic, %.1f%% of peak)" % (bw, 100 * bw / HBM_PEAK_GBS)
 
+    # the roof the dominant kernel is actually against, from its own numbers: HBM bandwidth or the
+    # HBM random-access rate (both "hbm"), else latency / issue (a serial state machine per read)
+    reg = kernels[dom]["regime"]
+    bound = "hbm" if reg in ("hbm-bandwidth", "hbm-random-access-rate") else "latency"
+    # the same kernel's frac from the committed evidence under profiles/: the HIP-event kernel record
+    # of a GPU run of this workload (tools/prof_run.py / --kernel-record) and the serialised
+    # single-stream rocprofv3 trace summary (tools/profile_serial.sh)
+    committed = committed_fracs(args.workload, dom, vote_bytes / launches_per_step)
+    if args.kernel_record:
+        json.dump({"workload": args.workload, "reads_per_step": n * ends, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+                   "host_step_ms": [round((b - a) * 1e3, 1) for a, b in zip([t_start] + step_ends[:-1], step_ends)],
+                   "kernel_record": {k: {"ms": round(ms, 4), "launches": nl} for k, (ms, nl) in kt.items() if nl},
+                   "algorithmic_bytes_per_launch": {k: kbytes[k] / kernels[k]["launches_per_step"] for k in kernels}},
+                  open(args.kernel_record, "w"), indent=1)
     check = None
     oi = None
     if rank == 0 and not (args.no_check and args.no_cpu):
@@ -450,12 +492,18 @@ def main():
                         done, threads, cs),
                     "cpu_model": cpu["model"], "host_logical_cpus": cpu["logical_cpus"],
                     "usable_cpus": cpu["usable_cpus"], "cgroup_quota_cpus": cpu["cgroup_quota_cpus"]}
-        cal = os.path.join(ROOT, "profiles", "r03_cpu_calibration.json")   # tools/cpu_calibration.py
-        if os.path.exists(cal):
+        # tools/cpu_calibration.py: the reference's voting step over this restatement, same reads and
+        # index; the newest calibration taken on this CPU model, else the newest
+        import glob
+        cals = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_cpu_calibration.json")))
+        same = [c for c in cals if json.load(open(c)).get("cpu_model") == cpu["model"]]
+        cal = (same or cals or [None])[-1]
+        if cal:
             c = json.load(open(cal))
             cpu_base["reference_over_port"] = c.get("reference_over_port")
             cpu_base["reference_equiv_value"] = round(cpu_base["value"] * c["reference_over_port"], 4)
             cpu_base["calibration"] = "%s: %s" % (os.path.relpath(cal, ROOT), c.get("summary", ""))
+            cpu_base["calibration_same_cpu_model"] = bool(same)
 
     total_reads = n * ends * world * args.steps
     value = total_reads / elapsed / 1e6
@@ -475,13 +523,14 @@ def main():
                            "reference-format files via svg_index_open" if prefix else "built in HBM by svg_index_build_mem"),
                        "parallelism": "reads sharded across %d GPU(s), index replicated, no collective" % world,
                        "host_threads_per_rank": int(sa.lib().svg_host_threads())},
-            "roofline": {"bound": "hbm", "regime": kernels[dom]["regime"], "kernel": dom, "achieved": round(vote_achieved, 2),
+            "roofline": {"bound": bound, "regime": kernels[dom]["regime"], "kernel": dom, "achieved": round(vote_achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(vote_achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_unit": "GB per launch",
                          "traffic_source": traffic_src,
                          "launch_ms": round(vote_launch_s * 1e3, 3), "launches_per_step": launches_per_step,
                          "algorithmic_bytes_per_read": round(vote_bytes / n, 1),
                          "kernels": kernels,
+                         "committed": committed,
                          "deferred_reads": st.get("deferred", 0),
                          "path": {"achieved": round(achieved, 2), "algorithmic_bytes_per_read": round(algo_bytes / n, 1),
                                   "step_ms": round(step_s * 1e3, 3), "frac": round(achieved / HBM_PEAK_GBS, 5)}},

@@ -222,8 +222,7 @@ int svg_vote_batch(svg_index *idx, const svg_params *p,
 /* The same from 2-bit packed reads (host buffers).  Both host entry points run a sub-batch
  * pipeline: upload of sub-batch i+1, vote of i (probe + lane kernels) beside the wave kernel and
  * compaction of i-1, download of i-2 (only the non-zero records, compacted on the GPU) and
- * expansion of i-3 into `out` by worker threads overlap.  Workers: SVG_HOST_THREADS, else
- * svg_host_threads().  Pinned caller buffers copy fastest. */
+ * expansion of i-3 into `out` by worker threads overlap.  Workers: svg_host_threads().  Pinned caller buffers copy fastest. */
 int svg_vote_batch_packed(svg_index *idx, const svg_params *p,
                           const svg_packed_reads *r1, const svg_packed_reads *r2,
                           svg_mapping_result *out, svg_subjunc_result *jout,
@@ -309,8 +308,7 @@ int  svg_fragile_batch(svg_index *idx, const svg_params *p, const svg_reads *r1,
 void svg_fragile_free(svg_fragile_result *r);
 
 /* Per-batch statistics of the last svg_vote_batch* call on this handle
- * (filled only when the handle was opened with SVG_STATS=1 in the environment
- * or after svg_set_stats(idx,1)); used for the algorithmic-byte roofline. */
+ * (filled only after svg_set_stats(idx,1)); used for the algorithmic-byte roofline. */
 typedef struct svg_batch_stats {
 	uint64_t probes;             /* gehash_go_X calls                         */
 	uint64_t bucket_items;       /* sum of items in the probed buckets        */
@@ -348,10 +346,32 @@ int svg_get_kernel_timing(svg_index *idx, double ms[4], int launches[4]);
 
 const char *svg_last_error(void);
 int svg_abi_version(void);
-/* Expansion worker threads the host entry points use: SVG_HOST_THREADS if set, else the CPUs
- * this process may run on (affinity mask capped by the cgroup CPU quota) divided by
+/* Expansion worker threads the host entry points use: the "host_threads" option if set, else
+ * the CPUs this process may run on (affinity mask capped by the cgroup CPU quota) divided by
  * LOCAL_WORLD_SIZE (one rank per GPU on the node), clamped to 2..12. */
 int svg_host_threads(void);
+
+/*
+ * Process-wide implementation options.  The library reads no environment variable of its own
+ * (only torchrun's LOCAL_WORLD_SIZE, to size host thread pools): tests and tuning set these
+ * explicitly.  No option changes a record -- every setting selects among exact implementations
+ * of the same reference behaviour (probe images, kernel paths, chunk and sub-batch sizes, pool
+ * sizes) or turns on diagnostics printed to stderr.  Names (value 0 / -1 = the default):
+ *   host_threads, host_sub      expansion workers; reads per host sub-batch
+ *   chunk, overlap              reads per probe-record chunk; 1/0 force the two-stream chunk pipeline
+ *   lane                        1 lane kernels + deferral (default), 2 defer every read to the
+ *                               wave kernel, 3 no lane kernels (wave kernel only)
+ *   lane_unfused, lane_bin      separate gather kernel; 2 = no count bins
+ *   lane_cap, lane_pe_cap, lane_pairs, lane_mid   lane-path capacities (candidates, pairs)
+ *   no_bcode, no_khash, khash64, no_bline, no_compact, probe_v1, no_window, probe_colmajor
+ *                               probe images / probe kernel variants picked at index load
+ *   wave_cap                    resident wave-kernel blocks per CU beside the next chunk
+ *   keys_literal, long_probes   svg_probe_keys / svg_long_vote_batch variants
+ *   debug, pipe_debug, long_debug  diagnostics on stderr
+ * svg_set_option returns SVG_E_ARG for an unknown name; svg_get_option returns the current value
+ * (0 for an unknown name). */
+int     svg_set_option(const char *name, int64_t value);
+int64_t svg_get_option(const char *name);
 
 /*
  * Index builder (replaces subread-buildindex for a single-block index,

@@ -112,6 +112,26 @@ static void dump_events(global_context_t *gc, const char *fn)
 }
 
 int __real_anti_supporting_read_scan(global_context_t *global_context);
+int __real_write_indel_final_results(global_context_t *global_context);
+
+/* SVG_REF_TIMING=1: the reference's own phase clocks, accumulated over every chunk by
+ * read_chunk_circles (core.c:3552-3641) -- index loading, the voting step, the stage between
+ * voting and realignment (anti_supporting_read_scan + remove_neighbour + rewind, core.c:3613-3634)
+ * and iteration two (realignment + SAM writing, core.c:3636-3641).  The reference's own print
+ * of them is commented out (core.c:480-485).  write_final_results calls
+ * write_indel_final_results (core.c:1220) once, after the last chunk, so the clocks are final
+ * here; the wall clock of the whole run so far (start_time, core.c:4013) is printed beside them. */
+int __wrap_write_indel_final_results(global_context_t *gc)
+{
+	double t0 = miltime();
+	int rc = __real_write_indel_final_results(gc);
+	if (getenv("SVG_REF_TIMING"))
+		fprintf(stderr, "SVG_REF_PHASES load_index=%.6f voting=%.6f before_realign=%.6f realign=%.6f "
+		        "write_vcf=%.6f wall=%.6f reads=%lld\n", gc->timecost_load_index, gc->timecost_voting,
+		        gc->timecost_before_realign, gc->timecost_for_realign, miltime() - t0,
+		        miltime() - gc->start_time, (long long)gc->all_processed_reads);
+	return rc;
+}
 
 int __wrap_anti_supporting_read_scan(global_context_t *gc)
 {

@@ -32,7 +32,7 @@ EXPORTS = [
     "svg_set_max_read_length", "svg_sim_pairs", "svg_set_timing", "svg_get_timing",
     "svg_get_kernel_timing", "svg_device_status", "svg_pack_reads", "svg_vote_batch_packed",
     "svg_vote_batch_packed_device", "svg_probe_keys", "svg_probe_keys_device", "svg_host_threads",
-    "svg_fragile_batch", "svg_fragile_free",
+    "svg_fragile_batch", "svg_fragile_free", "svg_set_option", "svg_get_option",
     # sublong's voting step (include/subread_long.h)
     "svg_long_vote_batch", "svg_long_free",
     # host post-vote events (include/subread_events.h)
@@ -103,6 +103,10 @@ def lib():
         L.svg_probe_keys_device.restype = i32
         L.svg_last_error.restype = ctypes.c_char_p
         L.svg_host_threads.restype = i32
+        L.svg_set_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+        L.svg_set_option.restype = i32
+        L.svg_get_option.argtypes = [ctypes.c_char_p]
+        L.svg_get_option.restype = ctypes.c_int64
         L.svg_fragile_batch.argtypes = [vp] * 5
         L.svg_fragile_batch.restype = i32
         L.svg_fragile_free.argtypes = [vp]
@@ -154,6 +158,35 @@ def _check(rc, what):
     if rc != 0:
         msg = lib().svg_last_error().decode(errors="replace")
         raise SvgError("%s failed: %s (%s)" % (what, ERRORS.get(rc, rc), msg))
+
+
+def set_option(name, value):
+    """svg_set_option: a process-wide implementation option (include/subread_vote.h); none
+    changes a record."""
+    _check(lib().svg_set_option(str(name).encode(), int(value)), "svg_set_option(%s)" % name)
+
+
+def get_option(name):
+    return int(lib().svg_get_option(str(name).encode()))
+
+
+class options:
+    """Context manager: set options for a block, restore the previous values after it."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.old[k] = get_option(k)
+            set_option(k, v)
+        return self
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            set_option(k, v)
+        return False
 
 
 def params_default(program=PROGRAM_ALIGN, paired=False):

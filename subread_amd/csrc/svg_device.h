@@ -142,15 +142,12 @@ struct svg_index {
 	// chunk pipeline: probe + lane kernels of chunk c run on the caller's stream while the wave
 	// kernel of chunk c-1 runs on stream2, so the per-chunk buffers come in two slots (c & 1)
 	hipStream_t stream2;
-	// (three slots: the host pipeline's probe-ahead mode runs the probe kernels of sub-batch i+1
-	// beside the lane kernel of i and the wave kernel of i-1)
 	hipEvent_t ev_lane[3], ev_wave[3], ev_probe[3];   // slot's records + deferral list ready / wave kernel done / probe records ready
 	void *d_prec[3]; size_t prec_cap[3];   // probe records of one chunk
 	void *d_big[3]; size_t big_cap[3];     // probe_line_kernel's big-bucket list (count, slot indexes)
 	// lane-per-read SE path (svg_lane.hip): candidate lists + deferral list, per-wave cold scratch
 	void *d_lane[3]; size_t lane_cap[3];
 	uint32_t *d_lscratch; size_t lscratch_words;     // light pass
-	uint32_t *d_lscratch2; size_t lscratch2_words;   // heavy pass
 	// svg_set_timing: event pairs per launch (kinds: 0 probe_kernel, 1 vote_kernel, 2 gather_kernel,
 	// 3 lane_kernel), folded into the sums when the ring fills
 	int timing;

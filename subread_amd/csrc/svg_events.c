@@ -1255,7 +1255,12 @@ int svg_events_anti_support(svg_events *t, const svg_params *p, const svg_event_
 	cnt = calloc((size_t)ne * (size_t)T, sizeof(uint32_t));
 	anti_job *jobs = calloc((size_t)T, sizeof(anti_job));
 	pthread_t *tid = calloc((size_t)T, sizeof(pthread_t));
-	if (!sm || !lg || !cnt || !jobs || !tid) { free(sm); free(lg); free(cnt); free(jobs); free(tid); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	char *started = calloc((size_t)T, 1);
+	if (!sm || !lg || !cnt || !jobs || !tid || !started) {
+		free(sm); free(lg); free(cnt); free(jobs); free(tid); free(started);
+		svg_set_error("out of memory");
+		return SVG_E_NOMEM;
+	}
 	for (i = 0; i < ne; i++) {
 		sm[i].pos = t->ev[i].small_side; sm[i].id = (uint32_t)i;
 		lg[i].pos = t->ev[i].large_side; lg[i].id = (uint32_t)i;
@@ -1268,13 +1273,17 @@ int svg_events_anti_support(svg_events *t, const svg_params *p, const svg_event_
 		J->r0 = n_reads * (uint64_t)k / (uint64_t)T;
 		J->r1 = n_reads * (uint64_t)(k + 1) / (uint64_t)T;
 		J->cnt = cnt + (size_t)ne * (size_t)k;
-		if (k) pthread_create(&tid[k], NULL, anti_worker, J);
+		/* a thread that cannot be created (thread or memory limits) scans its range inline */
+		if (k) started[k] = pthread_create(&tid[k], NULL, anti_worker, J) == 0;
 	}
 	anti_worker(&jobs[0]);
-	for (int k = 1; k < T; k++) pthread_join(tid[k], NULL);
+	for (int k = 1; k < T; k++) {
+		if (started[k]) pthread_join(tid[k], NULL);
+		else anti_worker(&jobs[k]);
+	}
 	for (int k = 1; k < T; k++)
 		for (i = 0; i < ne; i++) cnt[i] += cnt[(size_t)ne * (size_t)k + (size_t)i];
 	for (i = 0; i < ne; i++) t->ev[i].anti_supporting_reads = (uint16_t)(t->ev[i].anti_supporting_reads + cnt[i]);
-	free(sm); free(lg); free(cnt); free(jobs); free(tid);
+	free(sm); free(lg); free(cnt); free(jobs); free(tid); free(started);
 	return 0;
 }

@@ -595,7 +595,8 @@ extern "C" int svg_fragile_batch(svg_index *h, const svg_params *p, const svg_re
 	}
 	for (int b = 0; b < h->nblocks && !rc; b++) {
 		const svg_index *bk = b ? h->blk[b] : h;
-		for (int attempt = 0; attempt < 2; attempt++) {
+		bool stored = false;
+		for (int attempt = 0; attempt < 2 && !rc; attempt++) {
 			if (!d_s && (rc = dmalloc(h, (void **)&d_s, sizeof(svg_fragile_slot) * (size_t)scap))) break;
 			FParams fp;
 			memset(&fp, 0, sizeof fp);
@@ -630,7 +631,14 @@ extern "C" int svg_fragile_batch(svg_index *h, const svg_params *p, const svg_re
 				W->first_slot = (uint32_t)slots.size();
 				for (uint32_t q = 0; q < W->n_slots; q++) slots.push_back(s[f + q]);
 			}
+			stored = true;
 			break;
+		}
+		// the second attempt has room for every slot the first one counted; a block that still was
+		// not stored is an error, never a silently unwritten window range
+		if (!rc && !stored) {
+			svg_set_error("svg_fragile_batch: block %d: reported slots exceed the retried capacity", b);
+			rc = SVG_E_DEVICE;
 		}
 	}
 done:

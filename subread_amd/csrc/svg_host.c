@@ -37,6 +37,34 @@ void svg_set_error(const char *fmt, ...)
 const char *svg_last_error(void) { return g_err; }
 int svg_abi_version(void) { return SVG_ABI_VERSION; }
 
+/* Implementation options (include/subread_vote.h): explicit, process-wide, never read from the
+ * environment, and none of them changes a record. */
+static struct { const char *name; volatile int64_t value; } g_opts[] = {
+	{"host_threads", 0}, {"host_sub", 0}, {"chunk", 0}, {"overlap", -1},
+	{"lane", 0}, {"lane_unfused", 0}, {"lane_bin", 0}, {"lane_cap", 0}, {"lane_pe_cap", 0},
+	{"lane_pairs", 0}, {"lane_mid", 0},
+	{"no_bcode", 0}, {"no_khash", 0}, {"khash64", 0}, {"no_bline", 0}, {"no_compact", 0},
+	{"probe_v1", 0}, {"no_window", 0}, {"probe_colmajor", 0},
+	{"wave_cap", -1}, {"keys_literal", 0}, {"long_probes", 0},
+	{"debug", 0}, {"pipe_debug", 0}, {"long_debug", 0},
+};
+#define N_OPTS ((int)(sizeof g_opts / sizeof g_opts[0]))
+
+int svg_set_option(const char *name, int64_t value)
+{
+	for (int i = 0; name && i < N_OPTS; i++)
+		if (!strcmp(g_opts[i].name, name)) { g_opts[i].value = value; return 0; }
+	svg_set_error("unknown option '%s'", name ? name : "(null)");
+	return SVG_E_ARG;
+}
+
+int64_t svg_get_option(const char *name)
+{
+	for (int i = 0; name && i < N_OPTS; i++)
+		if (!strcmp(g_opts[i].name, name)) return g_opts[i].value;
+	return 0;
+}
+
 /* init_global_context (core-indel.c:4399-4538) -> parse_opts_* -> load_global_context (core.c:4075-4094) */
 void svg_params_default(svg_params *p, int program, int paired_end)
 {
@@ -158,9 +186,10 @@ static int load_tab(const char *fn, svg_host_index *ix, int threads)
 			jb[t].base = m; jb[t].hdr_off = hdr; jb[t].ix = ix;
 			jb[t].b0 = (uint32_t)((uint64_t)ix->nb * t / nt);
 			jb[t].b1 = (uint32_t)((uint64_t)ix->nb * (t + 1) / nt);
-			pthread_create(&th[t], NULL, copy_worker, &jb[t]);
+			if (pthread_create(&th[t], NULL, copy_worker, &jb[t])) { copy_worker(&jb[t]); th[t] = 0; }
 		}
-		for (t = 0; t < nt; t++) pthread_join(th[t], NULL);
+		for (t = 0; t < nt; t++)
+			if (th[t]) pthread_join(th[t], NULL);   /* 0: that range ran inline */
 	}
 	free(hdr);
 	munmap(ix->map, ix->map_len);

@@ -234,8 +234,8 @@ static int usable_cpus()
 // 264.8, 12 threads 399.1 / 402.2, 16 threads 399.8 / 383.7 Mreads/s -- and at least 2
 static int host_threads()
 {
-	const char *e = getenv("SVG_HOST_THREADS");
-	if (e && atoi(e) > 0) return atoi(e);
+	const int64_t o = svg_get_option("host_threads");
+	if (o > 0) return (int)o;
 	int n = usable_cpus();
 	const char *lw = getenv("LOCAL_WORLD_SIZE");
 	int ranks = lw ? atoi(lw) : 1;
@@ -296,9 +296,7 @@ static int host_ensure(void **p, size_t *cap, size_t need)
 	hipHostFree(*p);
 	*p = NULL;
 	*cap = 0;
-	// SVG_STAGE_NC=1: coarse-grained (non-coherent) staging memory
-	const unsigned fl = getenv("SVG_STAGE_NC") ? hipHostMallocNonCoherent : hipHostMallocDefault;
-	if (hipHostMalloc(p, need, fl) != hipSuccess) {
+	if (hipHostMalloc(p, need, hipHostMallocDefault) != hipSuccess) {
 		(void)hipGetLastError();
 		svg_set_error("hipHostMalloc(%zu) failed", need);
 		return SVG_E_NOMEM;
@@ -495,20 +493,13 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		if (!io->pool) io->pool = new SvgPool(nt);
 	}
 	uint64_t sub = pe ? (1ull << 19) : (1ull << 20);
-	{ const char *es = getenv("SVG_HOST_SUB"); if (es && atoll(es) > 0) sub = (uint64_t)atoll(es); }
+	if (svg_get_option("host_sub") > 0) sub = (uint64_t)svg_get_option("host_sub");
 	if (sub > n) sub = n;
 	const uint16_t *L1 = packed ? q1->lens : a1->lens, *L2 = pe ? (packed ? q2->lens : a2->lens) : NULL;
 	const size_t rec_b = (size_t)R * 68, j_b = jo ? (size_t)R * 16 : 0, bm_b = bmo ? (size_t)ends * SVG_BIG_MARGIN_WORDS * 2 : 0;
 	const CompLayout CL = comp_layout(sub, R, ends, jo, bmo);
 	const size_t o_j = (sub * rec_b + 255) & ~(size_t)255, o_bm = (o_j + sub * j_b + 255) & ~(size_t)255;
-	// probe-ahead (SVG_PROBE_AHEAD=1; single-end align from packed reads, one index block): the probe
-	// kernels of sub-batch i+1 run on the upload stream right behind its upload, beside the lane
-	// kernels of i (stream) and the wave kernel of i-1 (stream2), in three device slots.  Measured
-	// slower at C3 (118.2 vs 112.8 ms/step, profiles/r03/sweeps/c3_probe_ahead_*.json): three
-	// kernels sharing the CUs slow the latency-bound probe chain more than the overlap saves
-	const char *ea = getenv("SVG_PROBE_AHEAD");
-	const bool ahead = packed && !sjm && !pe && h->nblocks < 2 && n > sub && ea && ea[0] == '1';
-	for (int s = 0; s < (ahead ? 3 : 2); s++)
+	for (int s = 0; s < 2; s++)
 		if ((rc = svg_ensure(h, &h->d_out[s], &h->d_out_cap[s], o_bm + sub * bm_b + 64))) return rc;
 	for (int s = 0; s < 3; s++) {
 		if ((rc = svg_ensure(h, &io->d_comp[s], &io->d_comp_cap[s], CL.bytes))) return rc;
@@ -526,7 +517,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	}
 
 	// SVG_PIPE_DEBUG=1: where the host thread waits (seconds per batch)
-	const bool dbg = getenv("SVG_PIPE_DEBUG") != NULL;
+	const bool dbg = svg_get_option("pipe_debug") != 0;
 	double w_done = 0, w_pool = 0, w_up = 0, w_vote = 0;
 	auto now = []() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
 	// D2H of the compacted sub-batch j (compact slot j % 3) into staging slot j % 3
@@ -670,37 +661,8 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		return 0;
 	};
 
-	// probe-ahead: the job of sub-batch j (packed reads, no unpack) in jobs[j % 3], its probes on
-	// the upload stream after its upload, ev_probe[j % 3] when its probe records are ready
-	VoteJob jobs[3];
-	auto probe_ahead = [&](uint64_t j) -> int {
-		const int s3 = (int)(j % 3);
-		const uint64_t b = j * sub, m = j + 1 < nsub ? sub : n - b;
-		const Up &U = up[s3];
-		uint8_t *din = (uint8_t *)h->d_in[s3];
-		svg_reads dr0;
-		svg_packed_reads pk0;
-		pk0.bases = (const uint32_t *)(din + U.o_bases[0]) - U.wlo[0];
-		pk0.xmask = q1->xmask ? (const uint32_t *)(din + U.o_x[0]) - U.xlo[0] : NULL;
-		pk0.starts = q1->starts ? (const uint64_t *)(din + U.o_st[0]) : NULL;
-		pk0.stride = q1->stride;
-		pk0.lens = (const uint16_t *)(din + U.o_len[0]);
-		pk0.n_reads = m;
-		dr0 = svg_reads{NULL, NULL, pk0.lens, m};
-		h->max_read_len = U.maxlen;
-		uint8_t *dout = (uint8_t *)h->d_out[s3];
-		int rc2 = svg_vote_prepare(h, p, &dr0, NULL, (svg_mapping_result *)dout, NULL, NULL, &jobs[s3]);
-		if (rc2) return rc2;
-		set_packed(jobs[s3], &pk0, 1, b);
-		if (m > jobs[s3].chunk) { svg_set_error("probe-ahead: sub-batch of %llu reads over one chunk", (unsigned long long)m); return SVG_E_UNSUPPORTED; }
-		if ((rc2 = svg_vote_chunk_probe(h, &jobs[s3], 0, m, s3, h->up_stream))) return rc2;
-		HIPCHK(hipEventRecord(h->ev_probe[s3], h->up_stream));
-		return 0;
-	};
-
 	bool overlap_any = false;
 	rc = upload(0);
-	if (!rc && ahead) rc = probe_ahead(0);
 	// iteration i: upload i+1, vote i, download i-2, expand i-3 -- the host blocks on sub-batch
 	// i-2 only, with i-1 and i already queued behind it on the GPU
 	for (uint64_t i = 0; i < nsub + 3 && !rc; i++) {
@@ -710,21 +672,10 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		const uint64_t b = i * sub, m = i + 1 < nsub ? sub : n - b;
 		double tu = dbg ? now() : 0;
 		if (i + 1 < nsub && (rc = upload(i + 1))) break;
-		if (i + 1 < nsub && ahead && (rc = probe_ahead(i + 1))) break;
 		if (dbg) { w_up += now() - tu; tu = now(); }
 		uint8_t *dout;
 		hipStream_t st2 = st;
-		if (ahead) {
-			// lane kernels of sub-batch i once its probe records are ready, the wave kernel beside
-			VoteJob &job = jobs[s3];
-			HIPCHK(hipStreamWaitEvent(st, h->ev_probe[s3], 0));
-			const bool overlap = job.overlap_mode;
-			overlap_any = overlap_any || overlap;
-			st2 = overlap ? h->stream2 : st;
-			if ((rc = svg_vote_chunk_vote(h, &job, 0, m, s3, st, st2))) break;
-			dout = (uint8_t *)h->d_out[s3];
-			if (dbg) w_vote += now() - tu;
-		} else {
+		{
 		const Up &U = up[s3];
 		uint8_t *din = (uint8_t *)h->d_in[s3];
 		// ---- vote on stream (probe, lane) / stream2 (wave); slot s free once sub-batch i-2 is done

@@ -151,8 +151,7 @@ static int launch_keys(svg_index *h, svg_index *bk, const uint32_t *keys, uint64
 	kp.count = count;
 	uint64_t blocks = (n + 255) / 256, bmax = (uint64_t)h->n_cu * 16;
 	if (blocks > bmax) blocks = bmax;
-	const char *el = getenv("SVG_KEYS_LITERAL");
-	const bool lit = el && el[0] == '1';
+	const bool lit = svg_get_option("keys_literal") != 0;
 	if (!lit && bk->dix.bcode) hipLaunchKernelGGL(probe_keys_kernel<KEYS_CODE>, dim3((unsigned)blocks), dim3(256), 0, st, kp);
 	else if (!lit && bk->dix.khash && bk->dix.ksorted)
 		hipLaunchKernelGGL(probe_keys_kernel<KEYS_KHASH>, dim3((unsigned)blocks), dim3(256), 0, st, kp);

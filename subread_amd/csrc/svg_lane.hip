@@ -150,8 +150,6 @@ struct LParams {
 	// candidate count, bin b at bins[b * n], bin_count[b] reads; the lane kernel takes 64-read
 	// groups from the heaviest bin down (NULL: lane column k = read k or idx[k])
 	uint32_t *bins, *bin_count;
-	int bin_light_first;          // diagnostics: lightest bin first
-	int bin_single;               // diagnostics: one bin (the lane limits only)
 };
 
 // candidate-count bins: a wave's vote loop runs as many iterations as its heaviest lane has
@@ -549,12 +547,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 			uint32_t gg = g;
 			int b = LBINS - 1;
 			for (; b > 0; b--) {
-				const int bb = lp.bin_light_first ? LBINS - 1 - b : b;
+				const int bb = b;
 				const uint32_t gb = (bc[bb] + 63u) / 64u;
 				if (gg < gb) break;
 				gg -= gb;
 			}
-			if (lp.bin_light_first) b = LBINS - 1 - b;
 			k = gg * 64u + (uint32_t)L.lane;
 			live = k < bc[b];
 			r = live ? lp.bins[(size_t)b * lp.n + k] : 0u;
@@ -1494,7 +1491,7 @@ __global__ void __launch_bounds__(256) lane_bin_kernel(LParams lp)
 				mx = cnt > mx ? cnt : mx;
 			}
 			if (mx > lp.cap) dfr = true;
-			const int cl = dfr ? LBINS : (lp.bin_single ? 0 : lbin_of(mx));
+			const int cl = dfr ? LBINS : lbin_of(mx);
 #pragma unroll
 			for (int q = 0; q <= LBINS; q++) {
 				const unsigned long long bm = __ballot(live && cl == q);
@@ -1540,8 +1537,6 @@ __global__ void __launch_bounds__(256) lane_bin_kernel(LParams lp)
 #define LANE_NPF 10   // probe records per strand held in registers by the fused light pass
 #define LANE_NPF_SJ 14   // subjunc: -n 14
 #define LANE_CAP1 40
-#define LANE_K2 64
-#define LANE_CAP2 192
 
 template <int K, int NPF>
 static int lane_launch(svg_index *h, LParams &lp, uint32_t **cold, size_t *cold_words, hipStream_t st)
@@ -1583,8 +1578,7 @@ static int gather_launch(svg_index *h, const GParams &g, hipStream_t st)
 
 int svg_lane_eligible(const svg_index *h, const svg_params *p, int paired, int sj)
 {
-	const char *e = getenv("SVG_LANE");
-	if (e && e[0] == '0') return 0;
+	if (svg_get_option("lane") == 3) return 0;   // wave kernel only (testing)
 	if (h->max_read_len > 160) return 0;
 	// subjunc: junction search on (the lane paths carry big-margin records and defer every read
 	// or pair that needs donor scoring)
@@ -1605,7 +1599,6 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
                       const uint64_t *off1, const char *seq2, const uint64_t *off2, unsigned long long *stats,
                       uint32_t **defer_list, uint32_t **defer_count, hipStream_t st)
 {
-	const char *e = getenv("SVG_LANE");
 	const size_t o_l1 = 0, o_cnt = (o_l1 + (size_t)4 * n + 255) & ~(size_t)255, need = o_cnt + 256;
 	if (need > h->lane_cap[slot]) {
 		hipFree(h->d_lane[slot]);
@@ -1621,10 +1614,7 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	LParams lp;
 	memset(&lp, 0, sizeof lp);
 	lp.len = len1; lp.len2 = len2; lp.n = n; lp.cap = LANE_PE_CAP;
-	{
-		const char *ec = getenv("SVG_LANE_PE_CAP");   // tuning knob: candidates per end and strand
-		if (ec && atoi(ec) > 0) lp.cap = atoi(ec);
-	}
+	if (svg_get_option("lane_pe_cap") > 0) lp.cap = (int)svg_get_option("lane_pe_cap");   // candidates per end and strand
 	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps;
 	lp.gap = h->dix.gap; lp.total_subreads = p->total_subreads;
 	lp.tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
@@ -1634,11 +1624,8 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	lp.min_votes_first = p->min_votes_first; lp.min_votes_second = p->min_votes_second;
 	lp.chr_end = h->dix.chr_end; lp.n_chr = (int)h->dix.n_chr; lp.padding = h->dix.padding;
 	lp.min_pair = p->min_pair_distance; lp.max_pair = p->max_pair_distance; lp.mvc = p->max_vote_combinations;
-	{
-		const char *ep = getenv("SVG_LANE_PAIRS");
-		// 96 -> 256: C5pe deferrals 34% -> 21% of the pairs, 942 -> 779 ms/step (profiles/r03/sweeps/c5pe_pairs_*.json)
-		lp.max_pairs = ep && atoi(ep) > 0 ? atoi(ep) : 256;
-	}
+	// 96 -> 256: C5pe deferrals 34% -> 21% of the pairs, 942 -> 779 ms/step (profiles/r03/sweeps/c5pe_pairs_*.json)
+	lp.max_pairs = svg_get_option("lane_pairs") > 0 ? (int)svg_get_option("lane_pairs") : 256;
 	lp.out = out;
 	lp.jout = jout;
 	lp.bm_out = jout ? bm_out : NULL;
@@ -1656,7 +1643,7 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	lp.rev2 = p->reverse_r2 != 0;
 	lp.defer_list = (uint32_t *)(b + o_l1);
 	lp.defer_count = cnt;
-	lp.defer_all = e && e[0] == '2';
+	lp.defer_all = svg_get_option("lane") == 2;
 	lp.stats = stats;
 	lp.stat_base = 16;
 	lp.final_pass = 1;
@@ -1692,15 +1679,10 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
                    uint8_t *out, uint8_t *jout, uint16_t *bm, const char *seq, const uint64_t *off,
                    unsigned long long *stats, uint32_t **defer_list, uint32_t **defer_count, hipStream_t st)
 {
-	const uint32_t n2 = n / 4 + 64;   // heavy-pass columns
-	const char *e = getenv("SVG_LANE");
-	const bool two = e && e[0] == '3';   // heavy pass on request
-	// buffers: light cand/cpk/cnt over n columns, heavy over n2 columns, deferral lists 1 and 2
+	// buffers: cand/cpk/cnt over n columns (unfused gather), deferral list, counters, count bins
 	const size_t o_c1 = 0, o_p1 = o_c1 + (size_t)8 * LANE_CAP1 * n, o_n1 = o_p1 + (size_t)4 * LANE_CAP1 * n;
-	const size_t o_c2 = (o_n1 + (size_t)4 * n + 255) & ~(size_t)255;
-	const size_t o_p2 = o_c2 + (size_t)8 * LANE_CAP2 * n2, o_n2 = o_p2 + (size_t)4 * LANE_CAP2 * n2;
-	const size_t o_l1 = (o_n2 + (size_t)4 * n2 + 255) & ~(size_t)255, o_l2 = o_l1 + (size_t)4 * n + 256;
-	const size_t o_cnt = o_l2 + (size_t)4 * n + 256, o_bin = o_cnt + 256, need = o_bin + (size_t)4 * LBINS * n + 256;
+	const size_t o_l1 = (o_n1 + (size_t)4 * n + 255) & ~(size_t)255;
+	const size_t o_cnt = o_l1 + (size_t)4 * n + 256, o_bin = o_cnt + 256, need = o_bin + (size_t)4 * LBINS * n + 256;
 	if (need > h->lane_cap[slot]) {
 		hipFree(h->d_lane[slot]);
 		h->d_lane[slot] = NULL;
@@ -1709,8 +1691,7 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 		h->lane_cap[slot] = need;
 	}
 	uint8_t *b = (uint8_t *)h->d_lane[slot];
-	// [0] pass-1 deferrals, [1] pass-2 deferrals, [2] / [3] wave-kernel work counters after pass 1 / 2,
-	// [4..7] count-bin sizes
+	// [0] deferrals, [2] wave-kernel work counter, [4..7] count-bin sizes
 	uint32_t *cnt = (uint32_t *)(b + o_cnt);
 	HIPCHK(hipMemsetAsync(cnt, 0, 32, st));
 	GParams g;
@@ -1721,7 +1702,7 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 	// reads of <= LANE_NPF probes per strand (the full index at the default -n): the gather is
 	// fused into the lane kernel; otherwise the gather kernel writes candidate lists first
 	const bool sjm = jout != NULL;   // subjunc (lane_kernel<..., true>)
-	const bool fused = nps <= (sjm ? LANE_NPF_SJ : LANE_NPF) && !(e && e[0] == '1' && e[1] == 'g');   // "1g": unfused (testing)
+	const bool fused = nps <= (sjm ? LANE_NPF_SJ : LANE_NPF) && !svg_get_option("lane_unfused");
 	int rc = 0;
 	if (!fused && (rc = gather_launch(h, g, st))) return rc;
 	LParams lp;
@@ -1749,26 +1730,22 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 	lp.rev = p->reverse_r1 != 0;
 	lp.defer_list = (uint32_t *)(b + o_l1);
 	lp.defer_count = cnt;
-	lp.defer_all = e && e[0] == '2';
+	lp.defer_all = svg_get_option("lane") == 2;
 	lp.stats = stats;
 	lp.stat_base = 16;
-	lp.final_pass = !two || sjm;
+	lp.final_pass = 1;
 	lp.cs = n; lp.idx = NULL; lp.idx_count = NULL;
-	lp.bins = NULL; lp.bin_count = NULL; lp.bin_light_first = 0; lp.bin_single = 0;
+	lp.bins = NULL; lp.bin_count = NULL;
 	{
-		// tuning knobs (diagnostics): SVG_LANE_K=16|20|24, SVG_LANE_CAP, SVG_LANE_BIN=0
-		const char *ek = getenv("SVG_LANE_K"), *ec = getenv("SVG_LANE_CAP");
-		const int kk = ek ? atoi(ek) : LANE_K1;
-		if (ec && atoi(ec) > 0 && atoi(ec) <= LANE_CAP1) lp.cap = atoi(ec);
-		if (ec && atoi(ec) > LANE_CAP1 && fused) lp.cap = atoi(ec) < 64 ? atoi(ec) : 64;
+		// option lane_cap: candidates per strand (<= 64 fused); lane_bin 2: no count bins
+		const int oc = (int)svg_get_option("lane_cap");
+		if (oc > 0 && oc <= LANE_CAP1) lp.cap = oc;
+		if (oc > LANE_CAP1 && fused) lp.cap = oc < 64 ? oc : 64;
 		// count bins for the fused single-pass path: one thread per read sorts the chunk's reads into
 		// LBINS lists by candidate count (and defers the over-cap ones) before the lane kernel
-		const char *eb = getenv("SVG_LANE_BIN");
-		if (fused && !two && !(eb && eb[0] == '0')) {
+		if (fused && svg_get_option("lane_bin") != 2) {
 			lp.bins = (uint32_t *)(b + o_bin);
 			lp.bin_count = cnt + 4;
-			lp.bin_light_first = eb && eb[0] == '2';
-			lp.bin_single = eb && eb[0] == '3';
 			uint64_t bb = ((uint64_t)n + LBT - 1) / LBT, bmax = (uint64_t)h->n_cu * 8;
 			if (bb > bmax) bb = bmax;
 			if (bb < 1) bb = 1;
@@ -1778,27 +1755,10 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 		}
 		if (!fused) rc = lane_launch<LANE_K1, 0>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
 		else if (sjm) rc = lane_launch<LANE_K1, LANE_NPF_SJ>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
-		else if (kk == 16) rc = lane_launch<16, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
-		else if (kk == 24) rc = lane_launch<24, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
 		else rc = lane_launch<LANE_K1, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
 	}
 	if (rc) return rc;
 	*defer_list = lp.defer_list;
 	*defer_count = cnt;
-	if (!two || sjm) return 0;
-	// heavy pass over pass 1's deferral list
-	g.cap = LANE_CAP2;
-	g.cand = (uint32_t *)(b + o_c2); g.cpk = (uint16_t *)(b + o_p2); g.ccnt = (uint16_t *)(b + o_n2);
-	g.cs = n2; g.idx = lp.defer_list; g.idx_count = cnt;
-	if ((rc = gather_launch(h, g, st))) return rc;
-	lp.cand = g.cand; lp.cpk = g.cpk; lp.ccnt = g.ccnt; lp.cap = LANE_CAP2;
-	lp.cs = n2; lp.idx = g.idx; lp.idx_count = cnt;
-	lp.defer_list = (uint32_t *)(b + o_l2);
-	lp.defer_count = cnt + 1;
-	lp.stat_base = 21;
-	lp.final_pass = 1;
-	if ((rc = lane_launch<LANE_K2, 0>(h, lp, &h->d_lscratch2, &h->lscratch2_words, st))) return rc;
-	*defer_list = lp.defer_list;
-	*defer_count = cnt + 1;
 	return 0;
 }

@@ -419,8 +419,13 @@ struct svg_longws {
 	hipEvent_t ev_res[2], ev_down[2];
 };
 
+namespace { void long_cache_release(); }
+
 void svg_long_ws_free(svg_index *h)
 {
+	// the result-page cache (below) goes with the handle that filled it: a process that closes its
+	// index does not keep GBs of freed long-read results
+	long_cache_release();
 	svg_longws *w = h->lws;
 	if (!w) return;
 	if (w->down) hipStreamSynchronize(w->down);
@@ -500,6 +505,14 @@ void par_copy(void *dst, const void *src, size_t n, int T)
 std::mutex g_cache_mu;
 void *g_cache_v = NULL, *g_cache_o = NULL;
 
+void long_cache_release()
+{
+	std::lock_guard<std::mutex> lk(g_cache_mu);
+	free(g_cache_v);
+	free(g_cache_o);
+	g_cache_v = g_cache_o = NULL;
+}
+
 struct LOut {
 	svg_long_vote *votes;
 	uint32_t *order;
@@ -543,7 +556,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	svg_longws *w = h->lws;
 	const uint32_t n = (uint32_t)(r1 - r0);
 	*too_big = false;
-	const bool dbg = getenv("SVG_LONG_DEBUG") != NULL;
+	const bool dbg = svg_get_option("long_debug") != 0;
 	auto now = [] { struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6; };
 	const double t0 = dbg ? now() : 0;
 	double t_up = 0, t_probe = 0, t_seg = 0, t_keep = 0, t_dev = 0;
@@ -599,8 +612,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	LProbe lp;
 	lp.ix = h->dix; lp.text = d_text; lp.toff = d_toff; lp.len = d_len; lp.pbase = d_pbase; lp.n_reads = n;
 	lp.n_probes = P; lp.pcnt = d_pcnt; lp.pfirst = d_pfirst; lp.pmeta = d_pmeta;
-	const char *el = getenv("SVG_KEYS_LITERAL");
-	const bool lit = el && el[0] == '1';
+	const bool lit = svg_get_option("keys_literal") != 0;
 	if (!lit && h->dix.bcode) hipLaunchKernelGGL(long_probe_kernel<LIMG_CODE>, dim3(blocks_of(P, 256)), dim3(256), 0, st, lp);
 	else if (!lit && h->dix.khash && h->dix.ksorted)
 		hipLaunchKernelGGL(long_probe_kernel<LIMG_KHASH>, dim3(blocks_of(P, 256)), dim3(256), 0, st, lp);
@@ -789,8 +801,7 @@ extern "C" int svg_long_vote_batch(svg_index *h, const svg_long_reads *R, svg_lo
 	}
 	const int T = svg_host_threads();
 	// chunks: <= 65535 reads (16-bit read field of the segment key), <= 32M probes
-	const char *ec = getenv("SVG_LONG_PROBES");
-	const uint64_t pcap = ec && atoll(ec) > 0 ? (uint64_t)atoll(ec) : (32ull << 20);
+	const uint64_t pcap = svg_get_option("long_probes") > 0 ? (uint64_t)svg_get_option("long_probes") : (32ull << 20);
 	const uint64_t ccap = 256ull << 20;
 	LOut res = {NULL, NULL, 0, 0};
 	res.adopt_cache();
@@ -811,7 +822,7 @@ extern "C" int svg_long_vote_batch(svg_index *h, const svg_long_reads *R, svg_lo
 			const int rc = long_chunk(h, R, r0, r1, ccap, res, counts, &big, T, par, pend);
 			if (rc) { pend.join(); free(res.votes); free(res.order); return rc; }
 			if (!big) break;
-			if (getenv("SVG_LONG_DEBUG")) fprintf(stderr, "[svg_long] split %llu reads\n", (unsigned long long)(r1 - r0));
+			if (svg_get_option("long_debug")) fprintf(stderr, "[svg_long] split %llu reads\n", (unsigned long long)(r1 - r0));
 			r1 = r0 + (r1 - r0) / 2;   // too many candidates: half the reads
 		}
 		r0 = r1;

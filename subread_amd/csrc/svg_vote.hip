@@ -2303,19 +2303,8 @@ int svg_index_finish_device(svg_index *h)
 	HIPCHK(hipSetDevice(h->device));
 	if ((rc = dmalloc(h, &h->d_values, (size_t)x->values_bytes + 64)) || (rc = dmalloc(h, &h->d_chr, 4 * (size_t)x->n_chr + 64)))
 		return rc;
-	{
-		// SVG_STREAM_PRIO=1: the probe + lane kernels' stream (the step's critical path) at the highest
-		// priority, the overlapped wave kernel's at the lowest, so the CUs go to the critical path first
-		const char *ep = getenv("SVG_STREAM_PRIO");
-		int lo = 0, hi = 0;
-		if (ep && ep[0] == '1' && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && lo != hi) {
-			HIPCHK(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi));
-			HIPCHK(hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, lo));
-		} else {
-			HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-			HIPCHK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
-		}
-	}
+	HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+	HIPCHK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
 	HIPCHK(hipEventCreateWithFlags(&h->ev_up[2], hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&h->ev_done[2], hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&h->ev_down[2], hipEventDisableTiming));
@@ -2360,7 +2349,7 @@ int svg_index_finish_device(svg_index *h)
 		// 32-byte bucket codes when the key_hi range is small enough for them to hold ordinary
 		// buckets (V = 47 at nb = 93,018,839, the -F -B full index): n + V <= 216 bits
 		const uint32_t V = 0xffffffffu / x->nb + 1u;
-		if (V <= 80u && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_BCODE")) {
+		if (V <= 80u && !svg_get_option("no_compact") && !svg_get_option("no_bcode")) {
 			if (dmalloc(h, &h->d_bcode, (size_t)x->nb * 32 + 64) == 0) {
 				uint64_t blocks = ((uint64_t)x->nb + 255) / 256, bmax = (uint64_t)h->n_cu * 64;
 				if (blocks > bmax) blocks = bmax;
@@ -2375,10 +2364,10 @@ int svg_index_finish_device(svg_index *h)
 			}
 		}
 	}
-	if (!h->dix.bcode && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_KHASH")) {
+	if (!h->dix.bcode && !svg_get_option("no_compact") && !svg_get_option("no_khash")) {
 		// key-hash image of the probe records: 32-byte sectors of 3 entries (lines ~ items / 1.8),
 		// or 64-byte lines of 5 entries (~ items / 3) when a run count needs more than 8 bits
-		for (int sec = getenv("SVG_KHASH64") ? 0 : 1; sec >= 0 && !h->dix.khash; sec--) {
+		for (int sec = svg_get_option("khash64") ? 0 : 1; sec >= 0 && !h->dix.khash; sec--) {
 			const uint64_t lines = (sec ? x->items * 5 / 9 : x->items / 3) + 1024, lb = sec ? 32 : 64;
 			if (dmalloc(h, &h->d_khash, lines * lb + 64) != 0) {
 				h->d_khash = NULL;
@@ -2430,7 +2419,7 @@ int svg_index_finish_device(svg_index *h)
 			(void)hipGetLastError();
 		}
 	}
-	if (!h->dix.bcode && !h->dix.khash && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT") && !getenv("SVG_NO_BLINE")) {
+	if (!h->dix.bcode && !h->dix.khash && x->nb >= 16843009u && !svg_get_option("no_compact") && !svg_get_option("no_bline")) {
 		// (2^32-1)/nb <= 255: every key_hi fits a byte; 64 B per bucket (5.95 GB at nb = 93M)
 		// optional image: without the HBM for it the index still opens with the group/key images
 		if (dmalloc(h, &h->d_bline, (size_t)x->nb * 64 + 64) == 0) {
@@ -2446,7 +2435,7 @@ int svg_index_finish_device(svg_index *h)
 			(void)hipGetLastError();
 		}
 	}
-	if (!h->dix.bline && !h->dix.bcode && !h->dix.khash && x->nb >= 16843009u && !getenv("SVG_NO_COMPACT")) {
+	if (!h->dix.bline && !h->dix.bcode && !h->dix.khash && x->nb >= 16843009u && !svg_get_option("no_compact")) {
 		// (2^32-1)/nb <= 255: every key_hi fits a byte
 		const size_t ng = ((size_t)x->nb + 15) / 16;
 		if ((rc = dmalloc(h, &h->d_bgrp, ng * 32 + 64)) || (rc = dmalloc(h, &h->d_keys8, x->items + 128))) return rc;
@@ -2470,8 +2459,7 @@ int svg_index_finish_device(svg_index *h)
 	if ((rc = dmalloc(h, (void **)&h->d_err, 64))) return rc;
 	HIPCHK(hipMemset(h->d_err, 0, 64));
 	HIPCHK(hipEventCreateWithFlags(&h->ev_last, hipEventDisableTiming));
-	const char *se = getenv("SVG_STATS");
-	h->stats_on = se && se[0] == '1';
+	h->stats_on = 0;
 	h->max_read_len = 256;
 	return 0;
 }
@@ -2567,7 +2555,6 @@ extern "C" void svg_index_close(svg_index *h)
 			if (evs[k][s]) hipEventDestroy(evs[k][s]);
 	}
 	hipFree(h->d_lscratch);
-	hipFree(h->d_lscratch2);
 	for (int k = 0; k < 4; k++)
 		for (int i = 0; i < 64; i++)
 			for (int j = 0; j < 2; j++)
@@ -2780,7 +2767,7 @@ static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 	if (per_cu < 1) { svg_set_error("kernel LDS too large"); return SVG_E_DEVICE; }
 	if (per_cu > 4 * OCC / WPB) per_cu = 4 * OCC / WPB;   // 4 SIMDs x OCC waves
 	if (h->wave_cap > 0 && per_cu > h->wave_cap) per_cu = h->wave_cap;
-	if (getenv("SVG_DEBUG"))
+	if (svg_get_option("debug"))
 		fprintf(stderr, "[svg] vote_kernel<%d,%d,%d,%d,%d,%d>: LDS %zu B/wave, %d blocks/CU\n", ENDS, MAXL,
 		        MAXP, WPB, OCC, (int)SJ, sizeof(LT), per_cu);
 	uint64_t blocks = (uint64_t)h->n_cu * per_cu;
@@ -2883,16 +2870,16 @@ int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, con
 	job->per_read = (uint64_t)job->ends * 2 * nps;
 	uint64_t chunk = ((uint64_t)1 << 30) / (job->per_read * 8);
 	if (chunk > (uint64_t)0x7fffffff / job->per_read) chunk = (uint64_t)0x7fffffff / job->per_read;
-	{ const char *ec = getenv("SVG_CHUNK"); if (ec && atoll(ec) > 0 && (uint64_t)atoll(ec) < chunk) chunk = (uint64_t)atoll(ec); }   // testing
+	{ const int64_t oc = svg_get_option("chunk"); if (oc > 0 && (uint64_t)oc < chunk) chunk = (uint64_t)oc; }   // testing
 	if (chunk < 1) chunk = 1;
 	job->chunk = chunk;
 	// chunk pipeline: the wave kernel of chunk c runs on stream2 while the probe and lane kernels
 	// of chunk c+1 run on st; slot c & 1 holds a chunk's probe records and lane buffers until its
 	// wave kernel is done.  On by default for single-end align only (C3: 289 -> 304 Mreads/s; PE
 	// and subjunc, whose wave kernels are 2-3x longer, lost 1-2%: the kernels time-share the CUs
-	// there).  SVG_OVERLAP=0/1 forces it off/on.
-	const char *eo = getenv("SVG_OVERLAP");
-	job->overlap_mode = eo ? eo[0] == '1' : (!job->sj && !r2);
+	// there).  Option "overlap" 0/1 forces it off/on.
+	const int64_t oo = svg_get_option("overlap");
+	job->overlap_mode = oo >= 0 ? oo == 1 : (!job->sj && !r2);
 	PParams &pp = job->pp;
 	memset(&pp, 0, sizeof pp);
 	pp.ix = h->dix;
@@ -2907,8 +2894,8 @@ int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, con
 	            !h->stored;   // later blocks of a multi-block index merge with stored records: wave kernel
 	kp.stored = h->stored;
 	pp.soa = job->lane ? 1 : 0;
-	pp.window = h->dix.nb >= 131073u && !getenv("SVG_NO_WINDOW");   // key_hi <= 32767: int16 order == key order
-	{ const char *e = getenv("SVG_PROBE_MAP"); pp.readmajor = !(e && e[0] == '0'); }
+	pp.window = h->dix.nb >= 131073u && !svg_get_option("no_window");   // key_hi <= 32767: int16 order == key order
+	pp.readmajor = !svg_get_option("probe_colmajor");
 	return 0;
 }
 
@@ -2944,7 +2931,7 @@ int svg_vote_chunk_probe(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, i
 		}
 	}
 #define PROBE_LAUNCH(E, L, P) hipLaunchKernelGGL((probe_kernel<E, 8, L, P>), dim3((unsigned)pb), dim3(256), 0, st, pp)
-	if ((h->dix.bline || h->dix.bcode || h->dix.khash) && !getenv("SVG_PROBE_V1")) {
+	if ((h->dix.bline || h->dix.bcode || h->dix.khash) && !svg_get_option("probe_v1")) {
 		// bucket lines: grouped probe kernel + the big-bucket kernel on its list
 		pp.group = (uint32_t)(PROBE_GROUP_RECS / job->per_read);
 		if (pp.group > 64) pp.group = 64;
@@ -2998,8 +2985,8 @@ int svg_vote_chunk_vote(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, in
 	// latency-bound chain needs the occupancy (the wave kernel has slack on its stream)
 	h->wave_cap = 0;
 	if (st2 != st) {
-		const char *ew = getenv("SVG_WAVE_CAP");
-		h->wave_cap = ew ? atoi(ew) : SVG_WAVE_CAP;
+		const int64_t ow = svg_get_option("wave_cap");
+		h->wave_cap = ow >= 0 ? (int)ow : SVG_WAVE_CAP;
 	}
 	KParams kc = kp;
 	kc.off1 = kp.off1 + c0; kc.len1 = kp.len1 + c0;
@@ -3029,8 +3016,6 @@ int svg_vote_chunk_vote(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, in
 		HIPCHK(hipStreamWaitEvent(st2, h->ev_lane[slot], 0));
 	}
 	if ((rc = timing_mark(h, 1, 0, st2))) return rc;
-	// diagnostics only (wrong records for the deferred reads): the step without the wave kernel
-	if (job->lane && getenv("SVG_DIAG_NOWAVE")) return timing_mark(h, 1, 1, st2);
 	rc = launch_vote(h, kc, st2, job->npmax, job->sj, ends);
 	if (!rc) rc = timing_mark(h, 1, 1, st2);
 	return rc;
@@ -3062,44 +3047,24 @@ static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads 
 	if (h->stats_on) HIPCHK(hipMemsetAsync(h->d_stats, 0, 32 * sizeof(unsigned long long), st));
 	// chunks of <= 160 MiB of probe records (1M single-end 100-bp reads, the host pipeline's
 	// sub-batch): the records stay in the 256 MB infinity cache between the probe kernel that
-	// writes them and the lane / wave kernels that read them (SVG_CHUNK sets the chunk instead)
+	// writes them and the lane / wave kernels that read them (option "chunk" sets the chunk instead)
 	uint64_t chunk = job.chunk;
-	if (!getenv("SVG_CHUNK")) {
+	if (svg_get_option("chunk") <= 0) {
 		const uint64_t cc = ((uint64_t)160 << 20) / (job.per_read * 8);
 		if (cc >= 1 && cc < chunk) chunk = cc;
 	}
 	const uint64_t n = r1->n_reads;
 	const bool overlap = job.overlap_mode && chunk < n;
 	hipStream_t st2 = overlap ? h->stream2 : st;
-	if (getenv("SVG_DEBUG"))
+	if (svg_get_option("debug"))
 		fprintf(stderr, "[svg] batch of %llu reads: chunks of %llu, chunk pipeline %s\n", (unsigned long long)n,
 		        (unsigned long long)chunk, overlap ? "on" : "off");
-	// mapping records only (no subjunc / big-margin records, one index block): a chunk's records are
-	// written to a chunk-sized staging slot -- the lane kernel's scattered per-read stores then land
-	// in the infinity cache, as in the host pipeline -- and copied into `out` in one D2D copy after
-	// the chunk's wave kernel (SVG_DEV_STAGE=1).  Measured no faster at C3 (device path 406 vs 409
-	// Mreads/s, profiles/r03/sweeps/c3_devstage_*.json; parity green), so off by default
-	const size_t rec = (size_t)job.ends * (size_t)p->multi_best * 68;
-	const char *esg = getenv("SVG_DEV_STAGE");
-	const bool stage = overlap && !jout && !big_margin && h->nblocks < 2 && esg && esg[0] == '1';
-	if (stage)
-		for (int s = 0; s < 2; s++)
-			if ((rc = svg_ensure(h, &h->d_out[s], &h->d_out_cap[s], chunk * rec + 64))) return rc;
 	bool slot_busy[2] = {false, false};
 	for (uint64_t c0 = 0; c0 < n && !rc; c0 += chunk) {
 		const uint64_t cn = n - c0 < chunk ? n - c0 : chunk;
 		const int slot = overlap ? (int)((c0 / chunk) & 1) : 0;
 		if (slot_busy[slot]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[slot], 0));
-		if (stage) {
-			// the chunk's records at d_out[slot]: the kernels index out + (c0 + i) * rec
-			VoteJob jc = job;
-			jc.kp.out = (uint8_t *)h->d_out[slot] - c0 * rec;
-			rc = svg_vote_chunk(h, &jc, c0, cn, slot, st, st2);
-			if (!rc && hipMemcpyAsync((uint8_t *)out + c0 * rec, h->d_out[slot], cn * rec, hipMemcpyDeviceToDevice, st2) != hipSuccess) {
-				svg_set_error("record copy failed: %s", hipGetErrorString(hipGetLastError()));
-				rc = SVG_E_DEVICE;
-			}
-		} else rc = svg_vote_chunk(h, &job, c0, cn, slot, st, st2);
+		rc = svg_vote_chunk(h, &job, c0, cn, slot, st, st2);
 		if (!rc && overlap) {
 			HIPCHK(hipEventRecord(h->ev_wave[slot], st2));
 			slot_busy[slot] = true;

@@ -77,11 +77,10 @@ def _usable_cpus():
     return n
 
 
-def test_host_threads_follow_affinity_quota_and_ranks(monkeypatch):
-    """svg_host_threads: SVG_HOST_THREADS wins; else this process's usable CPUs (affinity capped by
+def test_host_threads_follow_affinity_quota_and_ranks(monkeypatch, svgopt):
+    """svg_host_threads: the host_threads option wins; else this process's usable CPUs (affinity capped by
     the cgroup quota) shared among LOCAL_WORLD_SIZE ranks, clamped to 2..12 (svg_io.hip)."""
     L = sa.lib()
-    monkeypatch.delenv("SVG_HOST_THREADS", raising=False)
     monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
     u = _usable_cpus()
     assert L.svg_host_threads() == max(2, min(12, u))
@@ -89,5 +88,7 @@ def test_host_threads_follow_affinity_quota_and_ranks(monkeypatch):
     assert L.svg_host_threads() == max(2, min(12, u // 2))
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "64")
     assert L.svg_host_threads() == 2
-    monkeypatch.setenv("SVG_HOST_THREADS", "5")
+    svgopt.set("host_threads", 5)
     assert L.svg_host_threads() == 5
+    svgopt.reset("host_threads")
+    assert L.svg_host_threads() == 2

@@ -53,7 +53,7 @@ def test_packed_mask_is_exercised():
 
 @pytest.mark.parametrize("mode", ["se", "pe", "sj"])
 @pytest.mark.parametrize("entry", ["ascii", "packed"])
-def test_compacted_pipeline_small_subbatches(mode, entry, gpu_indexes, index_cache, monkeypatch):
+def test_compacted_pipeline_small_subbatches(mode, entry, gpu_indexes, index_cache, svgopt):
     import subread_amd as sa
     from oracle.pyoracle import OracleIndex
     from subread_amd.abi import default_params, PROGRAM_ALIGN, PROGRAM_SUBJUNC
@@ -72,8 +72,8 @@ def test_compacted_pipeline_small_subbatches(mode, entry, gpu_indexes, index_cac
     want = pack_records(ref, rj if mode == "sj" else None, rbm if mode == "sj" else None)
     ix = gpu_indexes(key)
     for sub, th in (("3001", "1"), ("7777", "3"), ("64", "8")):
-        monkeypatch.setenv("SVG_HOST_SUB", sub)
-        monkeypatch.setenv("SVG_HOST_THREADS", th)
+        svgopt.set("host_sub", int(sub))
+        svgopt.set("host_threads", int(th))
         if entry == "ascii":
             out, jout, bm = ix.vote(p, r1, r2)
         else:
@@ -84,7 +84,7 @@ def test_compacted_pipeline_small_subbatches(mode, entry, gpu_indexes, index_cac
 
 @pytest.mark.parametrize("name", ["se_mb_long_gappedM6", "sj_pe_mb_long_gappedM6", "pe_mb_long_fullM17"])
 @pytest.mark.parametrize("entry", ["ascii", "packed"])
-def test_compacted_pipeline_multi_block(name, entry, gpu_indexes, index_cache, monkeypatch):
+def test_compacted_pipeline_multi_block(name, entry, gpu_indexes, index_cache, svgopt):
     """Multi-block indexes through the host pipeline with many sub-batches: later blocks run on
     the first block's stream from the stored records of each sub-batch, device and staging slots
     are reused; golden records (4-6 blocks) and the oracle on 15k simulated reads of the genome."""
@@ -95,8 +95,8 @@ def test_compacted_pipeline_multi_block(name, entry, gpu_indexes, index_cache, m
     ix = gpu_indexes(c.index_key)
     assert ix.n_blocks > 1
     for sub, th in (("97", "2"), ("1000", "5")):
-        monkeypatch.setenv("SVG_HOST_SUB", sub)
-        monkeypatch.setenv("SVG_HOST_THREADS", th)
+        svgopt.set("host_sub", int(sub))
+        svgopt.set("host_threads", int(th))
         if entry == "ascii":
             out, jout, bm = ix.vote(c.params, c.r1, c.r2)
         else:
@@ -117,8 +117,8 @@ def test_compacted_pipeline_multi_block(name, entry, gpu_indexes, index_cache, m
     ref, rj, rbm, _ = OracleIndex(index_cache.get(c.index_key)).vote(c.params, r1, r2, threads=16)
     sj = bool(c.params.do_breakpoint_detection)
     want = pack_records(ref, rj if sj else None, rbm if sj else None)
-    monkeypatch.setenv("SVG_HOST_SUB", "3001")
-    monkeypatch.setenv("SVG_HOST_THREADS", "3")
+    svgopt.set("host_sub", 3001)
+    svgopt.set("host_threads", 3)
     if entry == "ascii":
         out, jout, bm = ix.vote(c.params, r1, r2)
     else:

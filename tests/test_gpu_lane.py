@@ -1,8 +1,8 @@
 """GPU parity of the single-end lane-per-read path (svg_lane.hip) and of its hand-off
 to the wave-per-read kernel: every SE align case is voted four ways -- lane path with
-deferral (default), wave kernel only (SVG_LANE=0), every read deferred through the
-indirect wave-kernel launch (SVG_LANE=2), and lane path plus the 64-slot heavy pass
-(SVG_LANE=3) -- and each must be byte-identical to the reference's records / the oracle."""
+deferral (default; "1g": with the separate gather kernel), wave kernel only ("0": option lane=3),
+every read deferred through the indirect wave-kernel launch ("2": option lane=2) -- and each must
+be byte-identical to the reference's records / the oracle."""
 import numpy as np
 import pytest
 
@@ -13,10 +13,17 @@ pytestmark = pytest.mark.gpu
 
 # lane path (default: gather fused into the lane kernel), lane path with the separate gather
 # kernel, wave kernel only, every read deferred, lane + heavy pass
-MODES = ["1", "1g", "0", "2", "3"]
+MODES = ["1", "1g", "0", "2"]
 SE_ALIGN = [n for n in golden_names() if n.startswith("se_")]
 PE_ALIGN = [n for n in golden_names() if n.startswith("pe_")]
 PE_MODES = ["1", "0", "2"]
+
+
+def set_lane(svgopt, mode):
+    """the lane-path mode of a test: "1" lane kernels (default), "1g" unfused gather, "0" wave kernel
+    only, "2" every read deferred to the wave kernel"""
+    svgopt.set("lane", {"1": 1, "1g": 1, "0": 3, "2": 2}[mode])
+    svgopt.set("lane_unfused", 1 if mode == "1g" else 0)
 
 
 @pytest.fixture(scope="module")
@@ -35,8 +42,8 @@ def gpu_indexes(index_cache):
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("name", SE_ALIGN)
-def test_lane_modes_match_reference_golden(name, mode, gpu_indexes, monkeypatch):
-    monkeypatch.setenv("SVG_LANE", mode)
+def test_lane_modes_match_reference_golden(name, mode, gpu_indexes, svgopt):
+    set_lane(svgopt, mode)
     c = Case(name)
     ix = gpu_indexes(c.index_key)
     out, jout, bm = ix.vote(c.params, c.r1, c.r2)
@@ -47,11 +54,11 @@ def test_lane_modes_match_reference_golden(name, mode, gpu_indexes, monkeypatch)
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("key,n,sub,indel", [("chr901_full", 150000, 0.02, 0.02), ("chr901_gapped", 60000, 0.03, 0.05),
                                              ("synth4242_full", 60000, 0.01, 0.01)])
-def test_lane_modes_match_oracle(key, n, sub, indel, mode, gpu_indexes, index_cache, monkeypatch):
+def test_lane_modes_match_oracle(key, n, sub, indel, mode, gpu_indexes, index_cache, svgopt):
     from oracle.pyoracle import OracleIndex
     from subread_amd.abi import default_params, PROGRAM_ALIGN
     from subread_amd.sim import Genome, simulate_reads
-    monkeypatch.setenv("SVG_LANE", mode)
+    set_lane(svgopt, mode)
     pre = index_cache.get(key)
     g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
     r1 = simulate_reads(g, n, 100, seed=321, sub=sub, indel=indel, nrate=0.002)
@@ -68,7 +75,7 @@ def test_lane_modes_match_oracle(key, n, sub, indel, mode, gpu_indexes, index_ca
     assert (got == want).all(), describe_mismatch(got, want, 1, 3)
     if mode == "2":
         assert st["deferred"] == n
-    elif mode in ("1", "1g", "3") and key.startswith("chr901"):
+    elif mode in ("1", "1g") and key.startswith("chr901"):
         assert st["deferred"] < n // 4, str(st["why"])    # most reads stay on the lane path (synth4242 is repeat-heavy)
     assert st["results"] == int((out["selected_votes"] > 0).sum())
 
@@ -76,14 +83,14 @@ def test_lane_modes_match_oracle(key, n, sub, indel, mode, gpu_indexes, index_ca
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("lengths", [(0, 1, 15, 16, 17, 18, 19, 40, 150, 159, 160),
                                      (16, 18, 100, 159, 160, 161, 170)])
-def test_lane_edge_lengths(mode, lengths, gpu_indexes, index_cache, monkeypatch):
+def test_lane_edge_lengths(mode, lengths, gpu_indexes, index_cache, svgopt):
     """Reads shorter than 15+gap, at the 160 bp limit of the lane path and (second
     batch, which makes the whole batch ineligible) above it, on both index kinds;
     reads with N bases and lowercase letters included."""
     from oracle.pyoracle import OracleIndex
     from subread_amd.abi import ReadBatch, default_params, PROGRAM_ALIGN
     from subread_amd.sim import Genome
-    monkeypatch.setenv("SVG_LANE", mode)
+    set_lane(svgopt, mode)
     rng = np.random.default_rng(5)
     g = Genome.read_fasta(index_cache.genome_fasta("chr901"))
     seqs = []
@@ -108,9 +115,9 @@ def test_lane_edge_lengths(mode, lengths, gpu_indexes, index_cache, monkeypatch)
 
 @pytest.mark.parametrize("mode", PE_MODES)
 @pytest.mark.parametrize("name", PE_ALIGN)
-def test_lane_pe_modes_match_reference_golden(name, mode, gpu_indexes, monkeypatch):
+def test_lane_pe_modes_match_reference_golden(name, mode, gpu_indexes, svgopt):
     """Paired-end lane path (lane_pe_kernel, one lane per pair) on the reference's PE records."""
-    monkeypatch.setenv("SVG_LANE", mode)
+    set_lane(svgopt, mode)
     c = Case(name)
     ix = gpu_indexes(c.index_key)
     out, jout, bm = ix.vote(c.params, c.r1, c.r2)
@@ -125,13 +132,13 @@ def test_lane_pe_modes_match_reference_golden(name, mode, gpu_indexes, monkeypat
                                                                                "max_vote_combinations": 2, "multi_best": 2,
                                                                                "min_pair_distance": 100,
                                                                                "max_pair_distance": 400})])
-def test_lane_pe_modes_match_oracle(key, n, length, params, mode, gpu_indexes, index_cache, monkeypatch):
+def test_lane_pe_modes_match_oracle(key, n, length, params, mode, gpu_indexes, index_cache, svgopt):
     """Simulated pairs (fragments N(300,50) clipped, R2 reverse complement) and pairs of
     unrelated reads; the last case changes -m, -B-like limits, multi_best and -d/-D."""
     from oracle.pyoracle import OracleIndex
     from subread_amd.abi import default_params, PROGRAM_ALIGN
     from subread_amd.sim import Genome, simulate_pairs, simulate_reads
-    monkeypatch.setenv("SVG_LANE", mode)
+    set_lane(svgopt, mode)
     pre = index_cache.get(key)
     g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
     r1, r2 = simulate_pairs(g, n, length, seed=91, insert_max=700)
@@ -161,10 +168,10 @@ SJ_SE = [n for n in golden_names() if n.startswith("sj_se_")]
 
 @pytest.mark.parametrize("mode", PE_MODES)
 @pytest.mark.parametrize("name", SJ_SE)
-def test_lane_sj_modes_match_reference_golden(name, mode, gpu_indexes, monkeypatch):
+def test_lane_sj_modes_match_reference_golden(name, mode, gpu_indexes, svgopt):
     """Subjunc SE on the lane path (big-margin records, junction search and donor scoring in
     the lane kernel) on the reference's subjunc records."""
-    monkeypatch.setenv("SVG_LANE", mode)
+    set_lane(svgopt, mode)
     c = Case(name)
     ix = gpu_indexes(c.index_key)
     out, jout, bm = ix.vote(c.params, c.r1, c.r2)
@@ -177,11 +184,11 @@ def test_lane_sj_modes_match_reference_golden(name, mode, gpu_indexes, monkeypat
                                                  ("chr901_full", 20000, 150, {"big_margin_record_size": 6}),
                                                  ("chr901_full", 20000, 100, {"maximum_intron_length": 2000,
                                                                               "big_margin_record_size": 3})])
-def test_lane_sj_modes_match_oracle(key, n, length, params, mode, gpu_indexes, index_cache, monkeypatch):
+def test_lane_sj_modes_match_oracle(key, n, length, params, mode, gpu_indexes, index_cache, svgopt):
     from oracle.pyoracle import OracleIndex
     from subread_amd.abi import default_params, PROGRAM_SUBJUNC
     from subread_amd.sim import Genome, simulate_spliced_reads
-    monkeypatch.setenv("SVG_LANE", mode)
+    set_lane(svgopt, mode)
     pre = index_cache.get(key)
     g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
     r1 = simulate_spliced_reads(g, n, length, seed=61)
@@ -205,10 +212,10 @@ SJ_PE = [n for n in golden_names() if n.startswith("sj_pe_")]
 
 @pytest.mark.parametrize("mode", PE_MODES)
 @pytest.mark.parametrize("name", SJ_PE)
-def test_lane_sj_pe_modes_match_reference_golden(name, mode, gpu_indexes, monkeypatch):
+def test_lane_sj_pe_modes_match_reference_golden(name, mode, gpu_indexes, svgopt):
     """Subjunc PE on the paired lane path (lane_pe_kernel<SJ>: big-margin records, junction
     search and donor scoring per end) on the reference's records."""
-    monkeypatch.setenv("SVG_LANE", mode)
+    set_lane(svgopt, mode)
     c = Case(name)
     ix = gpu_indexes(c.index_key)
     out, jout, bm = ix.vote(c.params, c.r1, c.r2)
@@ -220,13 +227,13 @@ def test_lane_sj_pe_modes_match_reference_golden(name, mode, gpu_indexes, monkey
 @pytest.mark.parametrize("key,n,length,params", [("chr901_full", 40000, 100, {}), ("synth4242_gapped", 20000, 120, {}),
                                                  ("chr901_full", 20000, 150, {"big_margin_record_size": 6,
                                                                               "maximum_intron_length": 3000})])
-def test_lane_sj_pe_modes_match_oracle(key, n, length, params, mode, gpu_indexes, index_cache, monkeypatch):
+def test_lane_sj_pe_modes_match_oracle(key, n, length, params, mode, gpu_indexes, index_cache, svgopt):
     """Subjunc pairs: simulated fragments (no splicing) for half of the pairs, spliced reads for
     the other half (R2 unrelated), vs the oracle."""
     from oracle.pyoracle import OracleIndex
     from subread_amd.abi import default_params, PROGRAM_SUBJUNC, ReadBatch
     from subread_amd.sim import Genome, simulate_pairs, simulate_spliced_reads
-    monkeypatch.setenv("SVG_LANE", mode)
+    set_lane(svgopt, mode)
     pre = index_cache.get(key)
     g = Genome.read_fasta(index_cache.genome_fasta(key.rsplit("_", 1)[0]))
     a1, a2 = simulate_pairs(g, n, length, seed=71, insert_max=700)

@@ -138,9 +138,9 @@ def test_gpu_empty_batch(gpu_indexes):
 
 
 @pytest.mark.parametrize("mode", ["se", "pe", "sj"])
-def test_gpu_pipelines_match_oracle(mode, gpu_indexes, index_cache, monkeypatch):
-    """The two pipelines: host sub-batches (SVG_HOST_SUB: upload / vote / download of
-    neighbouring sub-batches overlap) and probe-record chunks (SVG_CHUNK, SVG_OVERLAP=1:
+def test_gpu_pipelines_match_oracle(mode, gpu_indexes, index_cache, svgopt):
+    """The two pipelines: host sub-batches (option host_sub: upload / vote / download of
+    neighbouring sub-batches overlap) and probe-record chunks (options chunk, overlap=1:
     the wave kernel of chunk c on a second stream beside chunk c+1's probe and lane
     kernels, double-buffered records) -- many small sub-batches and chunks, ragged tails."""
     from oracle.pyoracle import OracleIndex
@@ -159,24 +159,24 @@ def test_gpu_pipelines_match_oracle(mode, gpu_indexes, index_cache, monkeypatch)
     ref, rj, rbm, _ = OracleIndex(pre).vote(p, r1, r2, threads=16)
     want = pack_records(ref, rj if mode == "sj" else None, rbm if mode == "sj" else None)
     ix = gpu_indexes(key)
-    for env in ({"SVG_HOST_SUB": "7001"}, {"SVG_CHUNK": "2999", "SVG_OVERLAP": "1"},
-                {"SVG_HOST_SUB": "10007", "SVG_CHUNK": "3001", "SVG_OVERLAP": "1"}):
+    for env in ({"host_sub": 7001}, {"chunk": 2999, "overlap": 1},
+                {"host_sub": 10007, "chunk": 3001, "overlap": 1}):
         for k, v in env.items():
-            monkeypatch.setenv(k, v)
+            svgopt.set(k, v)
         out, jout, bm = ix.vote(p, r1, r2)
         for k in env:
-            monkeypatch.delenv(k)
+            svgopt.reset(k)
         got = pack_records(out, jout if mode == "sj" else None, bm if mode == "sj" else None)
         assert (got == want).all(), "%s: %s" % (env, describe_mismatch(got, want, 2 if mode == "pe" else 1, 3))
 
 
-def test_gpu_probe_images_match_oracle(monkeypatch):
+def test_gpu_probe_images_match_oracle(svgopt):
     """The probe images picked at index load: 32-byte unary bucket codes (default for -F -B
-    indexes), the key-hash of probe records in 32-byte sectors (SVG_NO_BCODE=1; the default of
-    every index the code does not fit, e.g. gapped ones) or 64-byte lines (+ SVG_KHASH64=1),
-    64-byte bucket lines (+ SVG_NO_KHASH=1), 16-bucket
-    groups + u8 keys (+ SVG_NO_BLINE=1), plain bounds + i16 keys (SVG_NO_COMPACT=1), and the
-    one-kernel probe of the previous build (SVG_PROBE_V1=1).  The genome carries repeat families, so
+    indexes), the key-hash of probe records in 32-byte sectors (no_bcode; the default of
+    every index the code does not fit, e.g. gapped ones) or 64-byte lines (+ khash64),
+    64-byte bucket lines (+ no_khash), 16-bucket
+    groups + u8 keys (+ no_bline), plain bounds + i16 keys (no_compact), and the
+    one-kernel probe of the previous build (probe_v1).  The genome carries repeat families, so
     that buckets past a code's 169 keys / a line's 59 keys take the big-bucket search."""
     import subread_amd as sa
     from oracle.pyoracle import OracleIndex
@@ -186,17 +186,17 @@ def test_gpu_probe_images_match_oracle(monkeypatch):
     r1 = simulate_reads(g, 40000, 100, seed=5, sub=0.01, indel=0.001)
     p = default_params(PROGRAM_ALIGN, False)
     want = None
-    for env in ({}, {"SVG_NO_BCODE": "1"}, {"SVG_NO_BCODE": "1", "SVG_KHASH64": "1"}, {"SVG_NO_BCODE": "1", "SVG_NO_KHASH": "1"},
-                {"SVG_NO_BCODE": "1", "SVG_NO_KHASH": "1", "SVG_NO_BLINE": "1"}, {"SVG_NO_COMPACT": "1"},
-                {"SVG_PROBE_V1": "1"}, {"SVG_PROBE_V1": "1", "SVG_NO_BCODE": "1"}):
+    for env in ({}, {"no_bcode": 1}, {"no_bcode": 1, "khash64": 1}, {"no_bcode": 1, "no_khash": 1},
+                {"no_bcode": 1, "no_khash": 1, "no_bline": 1}, {"no_compact": 1},
+                {"probe_v1": 1}, {"probe_v1": 1, "no_bcode": 1}):
         for k, v in env.items():
-            monkeypatch.setenv(k, v)
+            svgopt.set(k, v)
         # repeat threshold 400 (-f 400): keys with up to 400 occurrences stay, so some buckets
         # exceed a code's 169 items too
         ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True, repeat_threshold=400, device=0)
-        if "SVG_PROBE_V1" not in env:
+        if "probe_v1" not in env:
             for k in env:
-                monkeypatch.delenv(k)
+                svgopt.reset(k)
         if want is None:
             a = ix.export()
             sizes = np.diff(a["bstart"].astype(np.int64))
@@ -208,14 +208,14 @@ def test_gpu_probe_images_match_oracle(monkeypatch):
         out, _, _ = ix.vote(p, r1)
         ix.close()
         for k in env:
-            monkeypatch.delenv(k, raising=False)
+            svgopt.reset(k)
         got = pack_records(out, None, None)
         assert (got == want).all(), "%s: %s" % (env, describe_mismatch(got, want, 1, 3))
 
 
 @pytest.mark.parametrize("key,mode,n", [("long777_fullM17", "se", 40000), ("long777_fullM17", "pe", 15000),
                                         ("long777_gappedM6", "sj", 20000), ("synth4242_fullM1", "pe", 15000)])
-def test_gpu_multi_block_matches_oracle(key, mode, n, gpu_indexes, index_cache, monkeypatch):
+def test_gpu_multi_block_matches_oracle(key, mode, n, gpu_indexes, index_cache, svgopt):
     """Multi-block indexes: every block resident in HBM, voted in order, later blocks merging
     into the records the earlier ones left (core.c:3567-3613).  long777's blocks overlap by
     ~2 Mbp, so most reads are found again in several blocks.  Host pipeline with small
@@ -238,12 +238,12 @@ def test_gpu_multi_block_matches_oracle(key, mode, n, gpu_indexes, index_cache, 
     sj = mode == "sj"
     want = pack_records(ref, rj if sj else None, rbm if sj else None)
     ends = 2 if mode == "pe" else 1
-    for env in ({}, {"SVG_HOST_SUB": "7001"}):
+    for env in ({}, {"host_sub": 7001}):
         for k, v in env.items():
-            monkeypatch.setenv(k, v)
+            svgopt.set(k, v)
         out, jout, bm = ix.vote(p, r1, r2)
         for k in env:
-            monkeypatch.delenv(k)
+            svgopt.reset(k)
         got = pack_records(out, jout if sj else None, bm if sj else None)
         assert (got == want).all(), "%s: %s" % (env, describe_mismatch(got, want, ends, 3))
     if not sj:

@@ -9,7 +9,7 @@ oracle restatement on the same index arrays:
   * C5 shape: subjunc on spliced RNA-seq-like reads.
   * C3g: the same genome with the reference's DEFAULT index type (gapped, subread-buildindex
     defaults, index-builder.c:1173; ~87 items per bucket), probed through the key-hash image --
-    32-byte sectors with overflow chains, and the 64-byte-line form (SVG_KHASH64) that indexes
+    32-byte sectors with overflow chains, and the 64-byte-line form (option khash64) that indexes
     with run counts over 255 use.
 Reference semantics: sorted-hashtable.c:937-1123 (probe + tally), core-junction.c:2199-2530
 (top-K), core-junction.c:1073-1334,3675-3834 (junction voting)."""
@@ -98,15 +98,15 @@ def test_c5_subjunc_spliced(c3):
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("image", ["khash32", "khash64"])
-def test_c3g_gapped_index_se_100bp(c3_genome, image, monkeypatch):
+def test_c3g_gapped_index_se_100bp(c3_genome, image, svgopt):
     import subread_amd as sa
     from oracle.pyoracle import OracleIndex
     from subread_amd.abi import default_params, ReadBatch
     from subread_amd.sim import simulate_reads
     if image == "khash64":
-        monkeypatch.setenv("SVG_KHASH64", "1")
+        svgopt.set("khash64", 1)
     ix = sa.VoteIndex.build_genome(c3_genome, gap=3, memory_mb=8000, force_one_block=False, device=0)
-    monkeypatch.delenv("SVG_KHASH64", raising=False)
+    svgopt.reset("khash64")
     try:
         assert ix.info.index_gap == 3 and ix.n_blocks == 1 and ix.info.items > 900_000_000
         oi = OracleIndex(arrays=ix.export())

@@ -3,8 +3,8 @@ C ABI: bit-exact against the reference's own outputs (tests/golden/sublong/sublo
 oracle/_ref/ref-sublong: LRMdo_one_voting_read + LRMcopy_longvotes_to_itr + LRMmerge_sort,
 longread-mapping.c:552-560,668-682,1317) on full and gapped indexes -- a full vote-table row,
 wrapped vote counts, N / lowercase / IUPAC text, 16..64-base edge lengths -- through the image
-probes, the literal go_QQ search (SVG_KEYS_LITERAL=1) and many small chunks
-(SVG_LONG_PROBES); against the oracle restatement on larger simulated sets."""
+probes, the literal go_QQ search (option keys_literal) and many small chunks
+(option long_probes); against the oracle restatement on larger simulated sets."""
 import os
 
 import numpy as np
@@ -20,12 +20,12 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("mode", ["image", "literal", "chunks"])
 @pytest.mark.parametrize("key", INDEXES)
-def test_gpu_sublong_matches_reference(key, mode, index_cache, monkeypatch):
+def test_gpu_sublong_matches_reference(key, mode, index_cache, svgopt):
     import subread_amd as sa
     if mode == "literal":
-        monkeypatch.setenv("SVG_KEYS_LITERAL", "1")
+        svgopt.set("keys_literal", 1)
     if mode == "chunks":
-        monkeypatch.setenv("SVG_LONG_PROBES", "20000")
+        svgopt.set("long_probes", 20000)
     reads, vs, v, o = fixture(key)
     ix = sa.VoteIndex(index_cache.get(key), device=0)
     try:

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """svg_probe_keys throughput (GPU box): cellCounts' prefill_votes lookups on the C3 genome's
 full index (bucket-code image) and gapped index (key-hash image), keys already in HBM
-(svg_probe_keys_device), image path vs the literal search (SVG_KEYS_LITERAL=1), and the two
+(svg_probe_keys_device), image path vs the literal search (option keys_literal), and the two
 paths' answers compared key for key (the literal search is the reference's procedure; the
 small-index parity vs the reference itself is tests/test_gpu_prefill.py).
 
@@ -38,7 +38,7 @@ def run(ix, dk, n, literal, reps=5):
     dev = dk.device
     first = torch.empty(n, dtype=torch.int32, device=dev)
     count = torch.empty(n, dtype=torch.int32, device=dev)
-    os.environ["SVG_KEYS_LITERAL"] = "1" if literal else "0"
+    sa.set_option("keys_literal", 1 if literal else 0)
     L = sa.lib()
 
     def call():

@@ -1,5 +1,5 @@
 """GPU box: host pipeline (packed reads, pinned buffers) at C3 over sub-batch sizes and
-worker-thread counts, with SVG_PIPE_DEBUG wait accounting."""
+worker-thread counts, with the pipe_debug option's wait accounting."""
 import os
 import sys
 import time
@@ -29,11 +29,11 @@ pk = sa.pack_reads(rb, 100, threads=16, alloc=pinned)
 pk.lens = pinned(n, np.uint16)
 pk.lens[:] = rb.lens
 o = pinned(n * 3, sa.MAPPING_DTYPE).reshape(n, 1, 3)
-os.environ["SVG_PIPE_DEBUG"] = "1"
+sa.set_option("pipe_debug", 1)
 for sub in os.environ.get("SUBS", "262144 524288 1048576 2097152").split():
     for th in os.environ.get("THREADS", "8 16").split():
-        os.environ["SVG_HOST_SUB"] = sub
-        os.environ["SVG_HOST_THREADS"] = th
+        sa.set_option("host_sub", int(sub))
+        sa.set_option("host_threads", int(th))
         ix.vote_packed(p, pk, None, bufs=(o, None, None))
         best = 0
         for k in range(3):

@@ -7,14 +7,14 @@ import os
 import sys
 import time
 
-os.environ.setdefault("SVG_HOST_SUB", "1000000000")   # one device call: the counters cover the batch
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import subread_amd as sa  # noqa: E402
 from subread_amd.abi import default_params  # noqa: E402
 from subread_amd.sim import random_genome, simulate_reads, c3_lengths  # noqa: E402
+
+sa.set_option("host_sub", 1000000000)   # one device call: the counters cover the batch
 
 
 def main():

@@ -7,7 +7,11 @@ steps and nothing else on the GPU, so that a rocprofv3 trace or PMC pass holds
               (1M-read sub-batches: 48 launches per kernel per 50M-read step)
   MODE device: svg_vote_batch_packed_device, reads and records resident in HBM (bench.py's
               device_path figure; 6.25M-read chunks)
-Usage: prof_run.py WORKLOAD [STEPS] [MODE]   (WORKLOAD c3 | c3g | c4 | c5; reads per step as bench.py)"""
+  name=value   library options (svg_set_option) set before the run, e.g. overlap=0 for the
+              single-stream (serialised) pipeline whose kernel durations sum to at most its step
+After the timed steps, host mode runs one more step with per-launch HIP events on each launch's
+stream (svg_set_timing) and prints them as one JSON line ("kernel_record").
+Usage: prof_run.py WORKLOAD [STEPS] [MODE] [name=value ...]   (WORKLOAD c3 | c3g | c4 | c5)"""
 import os
 import sys
 import time
@@ -25,6 +29,9 @@ def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     mode = sys.argv[3] if len(sys.argv) > 3 else "host"
+    opts = dict(a.split("=", 1) for a in sys.argv[4:])
+    for k, v in opts.items():
+        sa.set_option(k, int(v))
     g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))
     gap = 3 if wl == "c3g" else 1
     ix = sa.VoteIndex.build_genome(g, gap=gap, memory_mb=8000, force_one_block=gap == 1, device=0)
@@ -71,6 +78,16 @@ def main():
         t = time.perf_counter() - t
         print("%s host: %d reads x %d ends, %.1f ms/step, %.1f Mreads/s" % (wl, n, ends, t / steps * 1e3,
                                                                           n * ends * steps / t / 1e6))
+        ix.set_timing(True)
+        t1 = time.perf_counter()
+        step()
+        t1 = time.perf_counter() - t1
+        kt = ix.kernel_timing()
+        ix.set_timing(False)
+        import json
+        print(json.dumps({"kernel_record": {k: {"ms": round(ms, 4), "launches": nl} for k, (ms, nl) in kt.items() if nl},
+                          "timed_step_ms": round(t / steps * 1e3, 3), "record_step_ms": round(t1 * 1e3, 3),
+                          "workload": wl, "reads": n * ends, "options": opts}), flush=True)
         return
 
     def dq(rb):

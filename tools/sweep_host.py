@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
-"""Knob sweep on the host path (GPU box): one index build, then for each configuration (env
-settings the library reads at call time) 1 warmup + STEPS timed steps of bench.py's host step.
-Usage: sweep_host.py WORKLOAD STEPS 'NAME:K=V,K=V' ...   (an empty config list = baseline only)
-Diagnostic knobs (SVG_DIAG_*) give wrong records; this prints timings only."""
+"""Option sweep on the host path (GPU box): one index build, then for each configuration (library
+options, svg_set_option) 1 warmup + STEPS timed steps of bench.py's host step.
+Usage: sweep_host.py WORKLOAD STEPS 'NAME:opt=V,opt=V' ...   (an empty config list = baseline only)"""
 import os
 import sys
 import time
@@ -61,8 +60,9 @@ def main():
             pinned(n * ends * 3, SUBJUNC_DTYPE).reshape(n, ends, 3) if sj else None,
             pinned(n * ends * BIG_MARGIN_WORDS, np.uint16).reshape(n, ends, BIG_MARGIN_WORDS) if sj else None)
     for name, env in confs:
-        old = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
+        old = {k: sa.get_option(k) for k in env}
+        for k, v in env.items():
+            sa.set_option(k, int(v))
         ix.vote_packed(p, pk1, pk2, bufs=bufs)
         t = time.perf_counter()
         for _ in range(steps):
@@ -71,10 +71,7 @@ def main():
         print("%-12s %-40s %7.1f ms/step %7.1f Mreads/s" % (name, ",".join("%s=%s" % kv for kv in env.items()),
                                                              t / steps * 1e3, n * ends * steps / t / 1e6), flush=True)
         for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+            sa.set_option(k, v)
 
 
 if __name__ == "__main__":
