@@ -31,6 +31,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 #include "subread.h"
 #include "core.h"
 #include "core-indel.h"
@@ -390,6 +391,108 @@ int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
 	if (gc->is_final_voting_run) svg_fragile_free(&svg_frag);
 	return rc ? 1 : 0;
 }
+
+/*
+ * SAM emission of iteration two (include/subread_sam.h).  write_single_fragment (core.c:1888-2178)
+ * hands each fragment's finished fields to add_buffered_fragment (core.c:1835-1884), which with
+ * SAM output spins every -T thread on the output lock until the fragments before its own are out.
+ * add_buffered_fragment_svg formats the same line(s) (svg_sam_format) and puts them in the
+ * library's ordered sink, which writes them in the same order without any thread waiting.  BAM
+ * output keeps the reference's own writer calls (SamBam_writer_add_read), which order themselves.
+ */
+#include "sambam-file.h"
+#include "subread_sam.h"
+
+static svg_sam_writer *svg_sam;
+static pthread_mutex_t svg_sam_mu = PTHREAD_MUTEX_INITIALIZER;
+
+void add_buffered_fragment_svg(global_context_t *gc, thread_context_t *tc, subread_read_number_t pair_number,
+	char *read_name1, unsigned int flags1, char *chro_name1, unsigned int chro_position1, int mapping_quality1, char *cigar1,
+	char *next_chro_name1, unsigned int next_chro_pos1, int temp_len1, int read_len1,
+	char *read_text1, char *qual_text1, char *additional_columns1,
+	char *read_name2, unsigned int flags2, char *chro_name2, unsigned int chro_position2, int mapping_quality2, char *cigar2,
+	char *next_chro_name2, unsigned int next_chro_pos2, int temp_len2, int read_len2,
+	char *read_text2, char *qual_text2, char *additional_columns2,
+	int all_locations, int this_location)
+{
+	const int pe = gc->input_reads.is_paired_end_reads;
+	if (gc->config.is_BAM_output) {
+		/* the reference's unordered per-thread BAM path (core.c:1847-1852); ordered BAM output
+		 * (--keepReadOrder) is not taken by this binding */
+		SamBam_writer_add_read(gc->output_bam_writer, tc->thread_id, read_name1, flags1, chro_name1, chro_position1,
+		                       mapping_quality1, cigar1, next_chro_name1, next_chro_pos1, temp_len1, read_len1, read_text1,
+		                       qual_text1, additional_columns1, !pe);
+		if (pe)
+			SamBam_writer_add_read(gc->output_bam_writer, tc->thread_id, read_name2, flags2, chro_name2, chro_position2,
+			                       mapping_quality2, cigar2, next_chro_name2, next_chro_pos2, temp_len2, read_len2,
+			                       read_text2, qual_text2, additional_columns2, 1);
+		return;
+	}
+	pthread_mutex_lock(&svg_sam_mu);
+	if (!svg_sam && svg_sam_writer_open(gc->output_sam_fp, &svg_sam))
+		SUBREADprintf("svg_sam_writer_open: %s\n", svg_last_error());
+	/* run_maybe_threads sets last_written_fragment_number = -1 before every iteration two
+	 * (core.c:3384-3386), which this function otherwise leaves alone: a new chunk */
+	if (svg_sam && gc->last_written_fragment_number == -1) {
+		if (svg_sam_writer_begin_chunk(svg_sam, gc->processed_reads_in_chunk))
+			SUBREADprintf("svg_sam_writer_begin_chunk: %s\n", svg_last_error());
+		gc->last_written_fragment_number = -2;
+	}
+	pthread_mutex_unlock(&svg_sam_mu);
+	if (!svg_sam) { gc->output_sam_is_full = 1; return; }
+	svg_sam_record r1 = {read_name1, (int32_t)flags1, chro_name1, chro_position1, mapping_quality1, cigar1, next_chro_name1,
+	                     next_chro_pos1, temp_len1, read_text1, qual_text1, additional_columns1};
+	svg_sam_record r2 = {read_name2, (int32_t)flags2, chro_name2, chro_position2, mapping_quality2, cigar2, next_chro_name2,
+	                     next_chro_pos2, temp_len2, read_text2, qual_text2, additional_columns2};
+	size_t cap = 4096 + 2 * (size_t)(read_len1 + read_len2) + strlen(additional_columns1) +
+	             (pe ? strlen(additional_columns2) : 0) + strlen(read_name1) + (pe ? strlen(read_name2) : 0) +
+	             strlen(cigar1) + (pe ? strlen(cigar2) : 0) + strlen(qual_text1) + (pe ? strlen(qual_text2) : 0);
+	char stackbuf[8192], *buf = cap <= sizeof stackbuf ? stackbuf : malloc(cap);
+	int64_t n1 = buf ? svg_sam_format(&r1, buf, cap) : -1, n2 = 0;
+	if (n1 >= 0 && pe) n2 = svg_sam_format(&r2, buf + n1, cap - (size_t)n1);
+	if (n1 < 0 || n2 < 0) {
+		SUBREADprintf("svg_sam_format: record of fragment %lld does not fit\n", (long long)pair_number);
+		gc->output_sam_is_full = 1;
+	} else {
+		/* the reference's fragment is complete once all_locations <= this_location + 1
+		 * (core.c:1875): an unmapped fragment comes with all_locations = 0 */
+		const int all = all_locations > this_location + 1 ? all_locations : this_location + 1;
+		int rc = svg_sam_writer_put(svg_sam, pair_number, this_location, all, buf, (size_t)(n1 + n2));
+		if (rc || svg_sam_writer_failed(svg_sam)) {
+			SUBREADprintf("svg_sam_writer_put (fragment %lld, location %d of %d): error %d, write %s\n", (long long)pair_number,
+			              this_location, all_locations, rc, svg_sam_writer_failed(svg_sam) ? "failed" : "ok");
+			gc->output_sam_is_full = 1;
+		}
+	}
+	if (buf != stackbuf) free(buf);
+}
+
+/* the sink is flushed at each chunk's last fragment; closed (and its FILE* flushed) once the
+ * run is over -- the harness calls this from its end-of-run hook */
+void svg_sam_finish(void)
+{
+	if (svg_sam && svg_sam_writer_close(svg_sam)) SUBREADprintf("svg_sam_writer_close: %s\n", svg_last_error());
+	svg_sam = NULL;
+}
+
+#ifdef SVG_DROPIN_DO_VOTING
+/* harness build: the reference's core.o is compiled with add_buffered_fragment weak (below) */
+void add_buffered_fragment(global_context_t *gc, thread_context_t *tc, subread_read_number_t pair_number,
+	char *read_name1, unsigned int flags1, char *chro_name1, unsigned int chro_position1, int mapping_quality1, char *cigar1,
+	char *next_chro_name1, unsigned int next_chro_pos1, int temp_len1, int read_len1,
+	char *read_text1, char *qual_text1, char *additional_columns1,
+	char *read_name2, unsigned int flags2, char *chro_name2, unsigned int chro_position2, int mapping_quality2, char *cigar2,
+	char *next_chro_name2, unsigned int next_chro_pos2, int temp_len2, int read_len2,
+	char *read_text2, char *qual_text2, char *additional_columns2,
+	int all_locations, int this_location)
+{
+	add_buffered_fragment_svg(gc, tc, pair_number, read_name1, flags1, chro_name1, chro_position1, mapping_quality1, cigar1,
+	                          next_chro_name1, next_chro_pos1, temp_len1, read_len1, read_text1, qual_text1,
+	                          additional_columns1, read_name2, flags2, chro_name2, chro_position2, mapping_quality2, cigar2,
+	                          next_chro_name2, next_chro_pos2, temp_len2, read_len2, read_text2, qual_text2,
+	                          additional_columns2, all_locations, this_location);
+}
+#endif
 
 #ifdef SVG_DROPIN_DO_VOTING
 /*

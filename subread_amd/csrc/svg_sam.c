@@ -1,0 +1,255 @@
+/*
+ * svg_sam.c -- ordered SAM emission (include/subread_sam.h).
+ *
+ * Replaces the ordered write of add_buffered_fragment (reference core.c:1835-1884): there every
+ * iteration-two thread spins on the output lock (lock, compare last_written_fragment_number
+ * with its fragment - 1, unlock, usleep(2)) until the fragments before its own are out.  Here a
+ * producer never waits: its text goes into a reorder ring slot keyed by fragment number, and the
+ * producer that completes the oldest unwritten fragment drains every complete fragment from
+ * there on into a staging buffer that leaves in large fwrite()s.  The bytes and their order are
+ * the reference's: fragments in number order, each fragment's locations in put order (one
+ * thread writes all locations of its fragment, in order, core.c:2707-2782,2905-2948).
+ */
+#define _GNU_SOURCE
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+#include "svg_internal.h"
+#include "subread_sam.h"
+
+typedef struct {
+	char *buf;
+	size_t len, cap;
+	int got;          /* locations put so far */
+	int all;          /* all_locations of the fragment (0: nothing put yet) */
+} sam_slot;
+
+struct svg_sam_writer {
+	FILE *fp;
+	pthread_mutex_t mu;
+	sam_slot *ring;
+	uint64_t size;          /* power of two */
+	int64_t next;           /* oldest fragment not written yet */
+	int64_t pending;        /* fragments with text held in the ring */
+	int64_t chunk_end;      /* fragments in the chunk: flush once `next` reaches it */
+	char *out;              /* staging of drained fragments */
+	size_t out_len, out_cap;
+	int failed;
+};
+
+#define OUT_FLUSH (4u << 20)
+
+static int out_flush(svg_sam_writer *w)
+{
+	if (w->out_len && fwrite(w->out, 1, w->out_len, w->fp) != w->out_len) w->failed = 1;
+	w->out_len = 0;
+	return w->failed;
+}
+
+static int out_append(svg_sam_writer *w, const char *s, size_t n)
+{
+	if (w->out_len + n > w->out_cap) {
+		if (out_flush(w)) return SVG_E_IO;
+		if (n > w->out_cap) {     /* one fragment larger than the staging buffer: straight out */
+			if (fwrite(s, 1, n, w->fp) != n) w->failed = 1;
+			return w->failed ? SVG_E_IO : 0;
+		}
+	}
+	memcpy(w->out + w->out_len, s, n);
+	w->out_len += n;
+	return 0;
+}
+
+int svg_sam_writer_open(void *file, svg_sam_writer **out)
+{
+	if (!file || !out) { svg_set_error("svg_sam_writer_open: NULL argument"); return SVG_E_ARG; }
+	svg_sam_writer *w = calloc(1, sizeof *w);
+	if (!w) { svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	w->fp = (FILE *)file;
+	w->size = 1024;
+	w->ring = calloc(w->size, sizeof(sam_slot));
+	w->chunk_end = -1;
+	w->out_cap = OUT_FLUSH;
+	w->out = malloc(w->out_cap);
+	if (!w->ring || !w->out) { free(w->ring); free(w->out); free(w); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	pthread_mutex_init(&w->mu, NULL);
+	*out = w;
+	return 0;
+}
+
+/* the ring must hold fragment f: grow (re-slot by f mod size) while f - next >= size */
+static int ring_reserve(svg_sam_writer *w, int64_t f)
+{
+	if ((uint64_t)(f - w->next) < w->size) return 0;
+	uint64_t ns = w->size;
+	while ((uint64_t)(f - w->next) >= ns) ns *= 2;
+	sam_slot *nr = calloc(ns, sizeof(sam_slot));
+	if (!nr) { svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	for (uint64_t i = 0; i < w->size; i++) {
+		const int64_t g = w->next + (int64_t)i;     /* slots hold fragments next .. next+size-1 */
+		nr[(uint64_t)g & (ns - 1)] = w->ring[(uint64_t)g & (w->size - 1)];
+	}
+	free(w->ring);
+	w->ring = nr;
+	w->size = ns;
+	return 0;
+}
+
+/* write every complete fragment from `next` on (lock held) */
+static int drain(svg_sam_writer *w)
+{
+	int rc = 0;
+	for (;;) {
+		sam_slot *s = &w->ring[(uint64_t)w->next & (w->size - 1)];
+		if (!s->all || s->got < s->all) break;
+		if (!rc) rc = out_append(w, s->buf, s->len);
+		s->len = 0;
+		s->got = s->all = 0;
+		w->next++;
+		w->pending--;
+	}
+	if ((w->out_len >= OUT_FLUSH / 2 || w->next == w->chunk_end) && out_flush(w)) rc = SVG_E_IO;
+	if (w->next == w->chunk_end && fflush(w->fp)) { w->failed = 1; rc = SVG_E_IO; }
+	return rc;
+}
+
+int svg_sam_writer_put(svg_sam_writer *w, int64_t fragment, int location, int all_locations, const char *text, size_t len)
+{
+	if (!w || fragment < 0 || all_locations < 1 || location < 0 || location >= all_locations || (len && !text)) {
+		svg_set_error("svg_sam_writer_put: bad argument");
+		return SVG_E_ARG;
+	}
+	int rc = 0;
+	pthread_mutex_lock(&w->mu);
+	if (fragment < w->next) {
+		pthread_mutex_unlock(&w->mu);
+		svg_set_error("svg_sam_writer_put: fragment %lld was already written", (long long)fragment);
+		return SVG_E_ARG;
+	}
+	if ((rc = ring_reserve(w, fragment))) { pthread_mutex_unlock(&w->mu); return rc; }
+	sam_slot *s = &w->ring[(uint64_t)fragment & (w->size - 1)];
+	if (!s->all) { s->all = all_locations; w->pending++; }
+	if (fragment == w->next && s->got == 0 && location + 1 == all_locations) {
+		/* the oldest missing fragment arriving whole: no copy through the slot */
+		rc = out_append(w, text, len);
+		s->got = s->all = 0;
+		w->next++;
+		w->pending--;
+		if (!rc) rc = drain(w);
+	} else {
+		if (s->len + len > s->cap) {
+			size_t nc = (s->len + len) * 2 + 256;
+			char *nb = realloc(s->buf, nc);
+			if (!nb) { pthread_mutex_unlock(&w->mu); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+			s->buf = nb;
+			s->cap = nc;
+		}
+		memcpy(s->buf + s->len, text, len);
+		s->len += len;
+		s->got++;
+		if (fragment == w->next) rc = drain(w);
+	}
+	pthread_mutex_unlock(&w->mu);
+	return rc;
+}
+
+int svg_sam_writer_begin_chunk(svg_sam_writer *w, int64_t n_fragments)
+{
+	if (!w) return SVG_E_ARG;
+	pthread_mutex_lock(&w->mu);
+	const int64_t p = w->pending;
+	if (!p) { w->next = 0; w->chunk_end = n_fragments; }
+	pthread_mutex_unlock(&w->mu);
+	if (p) { svg_set_error("svg_sam_writer_begin_chunk: %lld fragments of the last chunk incomplete", (long long)p); return SVG_E_ARG; }
+	return 0;
+}
+
+int64_t svg_sam_writer_pending(svg_sam_writer *w)
+{
+	if (!w) return 0;
+	pthread_mutex_lock(&w->mu);
+	const int64_t p = w->pending;
+	pthread_mutex_unlock(&w->mu);
+	return p;
+}
+
+int svg_sam_writer_failed(svg_sam_writer *w)
+{
+	return w ? w->failed : 0;
+}
+
+int svg_sam_writer_close(svg_sam_writer *w)
+{
+	if (!w) return 0;
+	pthread_mutex_lock(&w->mu);
+	int rc = out_flush(w) ? SVG_E_IO : 0;
+	if (fflush(w->fp)) rc = SVG_E_IO;
+	const int64_t p = w->pending;
+	pthread_mutex_unlock(&w->mu);
+	for (uint64_t i = 0; i < w->size; i++) free(w->ring[i].buf);
+	free(w->ring);
+	free(w->out);
+	pthread_mutex_destroy(&w->mu);
+	free(w);
+	if (p) { svg_set_error("svg_sam_writer_close: %lld fragments never completed", (long long)p); return SVG_E_ARG; }
+	if (rc) svg_set_error("svg_sam_writer_close: write failed");
+	return rc;
+}
+
+/* ---- one SAM line, byte-identical to "%s\t%d\t%s\t%u\t%d\t%s\t%s\t%u\t%d\t%s\t%s%s%s\n" */
+static char *put_str(char *p, const char *s, const char *end)
+{
+	while (*s && p < end) *p++ = *s++;
+	return *s ? NULL : p;
+}
+
+static char *put_u32(char *p, uint32_t v, const char *end)
+{
+	char t[10];
+	int n = 0;
+	do { t[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+	if (p + n > end) return NULL;
+	while (n) *p++ = t[--n];
+	return p;
+}
+
+static char *put_i32(char *p, int32_t v, const char *end)
+{
+	if (v < 0) {
+		if (p >= end) return NULL;
+		*p++ = '-';
+		return put_u32(p, (uint32_t)(-(int64_t)v), end);
+	}
+	return put_u32(p, (uint32_t)v, end);
+}
+
+#define PUT(e) do { if (!(p = (e))) goto full; } while (0)
+#define TAB() do { if (p >= end) goto full; *p++ = '\t'; } while (0)
+
+int64_t svg_sam_format(const svg_sam_record *r, char *buf, size_t cap)
+{
+	if (!r || !buf) return SVG_E_ARG;
+	char *p = buf;
+	const char *end = buf + cap;
+	PUT(put_str(p, r->qname, end)); TAB();
+	PUT(put_i32(p, r->flag, end)); TAB();
+	PUT(put_str(p, r->rname, end)); TAB();
+	PUT(put_u32(p, r->pos, end)); TAB();
+	PUT(put_i32(p, r->mapq, end)); TAB();
+	PUT(put_str(p, r->cigar, end)); TAB();
+	PUT(put_str(p, r->rnext, end)); TAB();
+	PUT(put_u32(p, r->pnext, end)); TAB();
+	PUT(put_i32(p, r->tlen, end)); TAB();
+	PUT(put_str(p, r->seq, end)); TAB();
+	PUT(put_str(p, r->qual, end));
+	if (r->tags && r->tags[0]) {
+		TAB();
+		PUT(put_str(p, r->tags, end));
+	}
+	if (p >= end) goto full;
+	*p++ = '\n';
+	return (int64_t)(p - buf);
+full:
+	return SVG_E_ARG;
+}
