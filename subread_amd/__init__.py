@@ -39,6 +39,9 @@ EXPORTS = [
     "svg_event_params_default", "svg_genome_arrays_open", "svg_genome_arrays_close", "svg_events_create",
     "svg_events_destroy", "svg_events_add_batch", "svg_events_merge", "svg_events_count", "svg_events_get",
     "svg_events_anti_support", "svg_events_add_batch2",
+    # SAM emission (include/subread_sam.h)
+    "svg_sam_writer_open", "svg_sam_writer_close", "svg_sam_writer_begin_chunk", "svg_sam_writer_put",
+    "svg_sam_writer_pending", "svg_sam_writer_failed", "svg_sam_format",
 ]
 
 _lib = None
@@ -103,6 +106,20 @@ def lib():
         L.svg_probe_keys_device.restype = i32
         L.svg_last_error.restype = ctypes.c_char_p
         L.svg_host_threads.restype = i32
+        L.svg_sam_writer_open.argtypes = [vp, ctypes.POINTER(vp)]
+        L.svg_sam_writer_open.restype = i32
+        L.svg_sam_writer_close.argtypes = [vp]
+        L.svg_sam_writer_close.restype = i32
+        L.svg_sam_writer_begin_chunk.argtypes = [vp, ctypes.c_int64]
+        L.svg_sam_writer_begin_chunk.restype = i32
+        L.svg_sam_writer_put.argtypes = [vp, ctypes.c_int64, i32, i32, vp, ctypes.c_size_t]
+        L.svg_sam_writer_put.restype = i32
+        L.svg_sam_writer_pending.argtypes = [vp]
+        L.svg_sam_writer_pending.restype = ctypes.c_int64
+        L.svg_sam_writer_failed.argtypes = [vp]
+        L.svg_sam_writer_failed.restype = i32
+        L.svg_sam_format.argtypes = [vp, vp, ctypes.c_size_t]
+        L.svg_sam_format.restype = ctypes.c_int64
         L.svg_set_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
         L.svg_set_option.restype = i32
         L.svg_get_option.argtypes = [ctypes.c_char_p]

@@ -230,7 +230,8 @@ struct Lane {
 	static constexpr int HPW = 32 / HB, NHW = (LROWS + HPW - 1) / HPW;
 	int tol;               // min(16, -I) (<= 5 on this path)
 	uint32_t low;          // first valid array position
-	uint2 *pm;             // LDS: pm[slot * 64 + lane]
+	uint2 *pm;             // LDS: pm[slot * 64 + lane] = (position, meta), halves swapped for lanes 16-31 / 48-63
+	bool swp;              // this lane stores (meta, position): lane & 16
 	uint32_t *cold;        // this lane's scratch: word w of slot s of strand st at cold[((st*K+s)*CW+w)*64]
 	int lane;
 	uint32_t h[ENDS][NHW];
@@ -254,6 +255,32 @@ struct Lane {
 		const uint32_t clr = ~(NIL << sh), v = s << sh;
 #pragma unroll
 		for (int k = 0; k < NHW; k++) h[E][k] = pick(q == (uint32_t)k, (h[E][k] & clr) | v, h[E][k]);
+	}
+	// The slot pool is read whole (ds_read_b64: 32-lane groups, bank (a/4) mod 64, conflict-free
+	// for [slot][lane]) but its meta word is also read and written alone (ds_read_b32 /
+	// ds_write_b32: bank (a/4) mod 32, so lanes l and l+16 of a group would share a bank).  Lanes
+	// with bit 4 set keep the two words in the other order, which puts those 32-bit accesses of a
+	// 32-lane group on 32 different banks.
+	__device__ __forceinline__ uint2 slot(uint32_t s) const
+	{
+		const uint2 e = pm[s * 64 + lane];
+		return swp ? make_uint2(e.y, e.x) : e;
+	}
+	__device__ __forceinline__ uint32_t meta(uint32_t s) const
+	{
+		return reinterpret_cast<const uint32_t *>(pm)[(s * 64 + lane) * 2 + (swp ? 0 : 1)];
+	}
+	__device__ __forceinline__ uint32_t spos(uint32_t s) const
+	{
+		return reinterpret_cast<const uint32_t *>(pm)[(s * 64 + lane) * 2 + (swp ? 1 : 0)];
+	}
+	__device__ __forceinline__ void set_meta(uint32_t s, uint32_t M) const
+	{
+		reinterpret_cast<uint32_t *>(pm)[(s * 64 + lane) * 2 + (swp ? 0 : 1)] = M;
+	}
+	__device__ __forceinline__ void set_slot(uint32_t s, uint32_t pos, uint32_t M) const
+	{
+		pm[s * 64 + lane] = swp ? make_uint2(M, pos) : make_uint2(pos, M);
 	}
 	__device__ __forceinline__ uint32_t *cw(int st, int s, int w) const { return cold + ((st * K + s) * CW + w) * 64; }
 	// subjunc scratch after the slot words: the junction record of result slot (st, s), read codes
@@ -292,7 +319,7 @@ struct Lane {
 		for (;;) {
 			while (s == NIL && ri < 2) { ri++; s = head<E>(ri == 1 ? rp : rm); }
 			if (s == NIL) break;
-			const uint2 e = pm[s * 64 + lane];
+			const uint2 e = slot(s);
 			uint32_t M = e.y;
 			const int d = (int)(kv - e.x);
 			if (d >= -tol && d <= tol) {
@@ -331,12 +358,12 @@ struct Lane {
 						cur = d;
 					}
 					M = lm_pack(votes, kP1, tl, cur, lm_next(M)) | lm_endbit(M) | spill | ((uint32_t)lgap_x(off, gap) << 29);
-					pm[s * 64 + lane].y = M;
+					set_meta(s, M);
 					if (max_vote[E] < votes) max_vote[E] = votes;
 					found = true;
 					break;
 				}
-				if (chg) { M = lm_pack(votes, last, tl, lm_cursor(M), lm_next(M)) | (M & (LM_END | LM_SPILL | (3u << 29))); pm[s * 64 + lane].y = M; }
+				if (chg) { M = lm_pack(votes, last, tl, lm_cursor(M), lm_next(M)) | (M & (LM_END | LM_SPILL | (3u << 29))); set_meta(s, M); }
 			}
 			if (ri == 0) { tail = s; tailM = M; n0++; }
 			s = lm_next(M);
@@ -345,10 +372,10 @@ struct Lane {
 		if (!found && kv >= low && kv <= high_b && (K <= 24 || n0 < 24)) {
 			if (nslots == K) { dfr = true; why = 2; return; }
 			const uint32_t ns = (uint32_t)nslots++;
-			pm[ns * 64 + lane] = make_uint2(kv, lm_pack(1, kP1, 0, 0, NIL) | (E ? LM_END : 0u) | ((uint32_t)lgap_x(off, gap) << 29));
+			set_slot(ns, kv, lm_pack(1, kP1, 0, 0, NIL) | (E ? LM_END : 0u) | ((uint32_t)lgap_x(off, gap) << 29));
 			*cw(st, (int)ns, 0) = (uint32_t)off | ((uint32_t)kP1 << 8);   // coverage_start, rec[0] (first kP1)
 			if (tail == NIL) set_head<E>(r0, ns);
-			else pm[tail * 64 + lane].y = lm_set_next(tailM, ns);
+			else set_meta(tail, lm_set_next(tailM, ns));
 			if (max_vote[E] < 1) max_vote[E] = 1;
 		}
 	}
@@ -528,6 +555,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 	L.low = lp.low;
 	L.lane = (int)__lane_id();
 	L.pm = reinterpret_cast<uint2 *>(lds_raw);
+	L.swp = (L.lane & 16) != 0;
 	L.cold = lp.cold + (size_t)gw * (lane_cold_words(K, SJ) * 64) + L.lane;
 	const int mb = lp.multi_best, mvs = lp.max_vote_simples, mvf = lp.min_votes_first, mvsec = lp.min_votes_second;
 	const int cutoff = lp.cutoff;
@@ -667,7 +695,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 			// ---- SE gate (core.c:3215-3233) and top-K (core-junction.c:2199-2530, ends = 1)
 			if (L.max_vote[0] >= mvf) {
 				int t0 = 0, t1 = 0, t2 = 0;
-				for (int s = 0; s < L.nslots; s++) ltop3(t0, t1, t2, lm_votes(L.pm[s * 64 + L.lane].y));
+				for (int s = 0; s < L.nslots; s++) ltop3(t0, t1, t2, lm_votes(L.meta(s)));
 				if (rv0 > 0) ltop3(t0, t1, t2, rv0);
 				if (mb > 1 && rv1 > 0) ltop3(t0, t1, t2, rv1);
 				if (mb > 2 && rv2 > 0) ltop3(t0, t1, t2, rv2);
@@ -680,7 +708,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 						for (uint32_t row = 0; row < LROWS && taken < mvs; row++) {
 							uint32_t q = L.template head<0>(row);
 							while (q != Lane<K>::NIL && taken < mvs) {
-								const uint32_t M = L.pm[q * 64 + L.lane].y;
+								const uint32_t M = L.meta(q);
 								const int v = lm_votes(M);
 								if (v >= t2) {
 									const int rs = (int)(*L.cw(st, (int)q, 0) & 0xffu);
@@ -705,7 +733,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 				// table slots of each value in row-major order (row, then slot order = pool order)
 				uint32_t a0 = ~0u, b0 = ~0u, c0 = ~0u, a1 = ~0u, b1 = ~0u, c1 = ~0u, a2 = ~0u, b2 = ~0u, c2 = ~0u;
 				for (int s = 0; s < L.nslots; s++) {
-					const uint2 e = L.pm[s * 64 + L.lane];
+					const uint2 e = L.slot(s);
 					const int v = lm_votes(e.y);
 					if (v < mvsec) continue;
 					const uint32_t key = (lrow(e.x) << 6) | (uint32_t)s;
@@ -724,9 +752,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 					ns++;
 				};
 				auto add_val = [&](int N, uint32_t ka, uint32_t kb, uint32_t kc) __attribute__((always_inline)) {
-					if (ka != ~0u && ns < mvs) add(128 | (int)(ka & 63u), L.pm[(ka & 63u) * 64 + L.lane].x, N);
-					if (kb != ~0u && ns < mvs) add(128 | (int)(kb & 63u), L.pm[(kb & 63u) * 64 + L.lane].x, N);
-					if (kc != ~0u && ns < mvs) add(128 | (int)(kc & 63u), L.pm[(kc & 63u) * 64 + L.lane].x, N);
+					if (ka != ~0u && ns < mvs) add(128 | (int)(ka & 63u), L.spos((ka & 63u)), N);
+					if (kb != ~0u && ns < mvs) add(128 | (int)(kb & 63u), L.spos((kb & 63u)), N);
+					if (kc != ~0u && ns < mvs) add(128 | (int)(kc & 63u), L.spos((kc & 63u)), N);
 					if (ns < mvs && rv0 == N) add(0, rpos0, N);
 					if (mb > 1 && ns < mvs && rv1 == N) add(1, rpos1, N);
 					if (mb > 2 && ns < mvs && rv2 == N) add(2, rpos2, N);
@@ -743,7 +771,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 					if ((cur > 0 && tp0 == pos) || (cur > 1 && tp1 == pos)) return;
 					int src, u, vv = v;
 					uint32_t x;
-					if (kind & 128) { src = (st << 6) | (kind & 63); u = applied; x = lm_ext(L.pm[(kind & 63) * 64 + L.lane].y); }
+					if (kind & 128) { src = (st << 6) | (kind & 63); u = applied; x = lm_ext(L.meta((kind & 63))); }
 					else {
 						src = sel3(kind, rsrc0, rsrc1, rsrc2);
 						u = sel3(kind, ru0, ru1, ru2);
@@ -776,13 +804,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 						const int src = sel3(c, ts0, ts1, ts2);
 						if (src < 0 || (src >> 6) != st) continue;
 						const int sM = src & 63;
-						const uint2 eM = L.pm[sM * 64 + L.lane];
+						const uint2 eM = L.slot(sM);
 						const int vM = lm_votes(eM.y);
 						const int csM = (int)(*L.cw(st, sM, 0) & 0xffu), ceM = lcov_end(lm_last(eM.y), lm_x(eM.y), step, lp.gap);
 						for (uint32_t row = 0; row < LROWS && !L.dfr; row++) {
 							uint32_t q = L.template head<0>(row);
 							while (q != Lane<K>::NIL) {
-								const uint2 e2 = L.pm[q * 64 + L.lane];
+								const uint2 e2 = L.slot(q);
 								const uint32_t qs = q;
 								q = lm_next(e2.y);
 								if ((int)qs == sM || vM < lm_votes(e2.y)) continue;
@@ -823,12 +851,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 							flush();
 							Jc = c; Jv = 0; Jcs = 0; Jce = 0; Jsplit = 0; Jnormal = 0; Jf = -1; Jpos = 0;
 							sM = sel3(c, ts0, ts1, ts2) & 63;
-							const uint2 eM = L.pm[sM * 64 + L.lane];
+							const uint2 eM = L.slot(sM);
 							Mpos = eM.x;
 							Mcs = (int)(*L.cw(st, sM, 0) & 0xffu);
 							Mce = lcov_end(lm_last(eM.y), lm_x(eM.y), step, lp.gap);
 						}
-						const uint2 e2 = L.pm[qs * 64 + L.lane];
+						const uint2 e2 = L.slot(qs);
 						const int V = lm_votes(e2.y);
 						const int cs2 = (int)(*L.cw(st, qs, 0) & 0xffu), ce2 = lcov_end(lm_last(e2.y), lm_x(e2.y), step, lp.gap);
 						// is_better_inner (core-junction.c:961)
@@ -1003,6 +1031,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 	L.low = lp.low;
 	L.lane = (int)__lane_id();
 	L.pm = reinterpret_cast<uint2 *>(lds_raw);
+	L.swp = (L.lane & 16) != 0;
 	L.cold = lp.cold + (size_t)gw * (lane_cold_words(K, SJ, 2) * 64) + L.lane;
 	const int mb = lp.multi_best, mvs = lp.max_vote_simples, mvf = lp.min_votes_first, mvsec = lp.min_votes_second;
 	const int cutoff = lp.cutoff, mvc = lp.mvc;
@@ -1101,7 +1130,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 #pragma unroll
 			for (int e = 0; e < 2; e++) { ta[e][0] = 0; ta[e][1] = 0; ta[e][2] = 0; }
 			for (int s = 0; s < L.nslots; s++) {
-				const uint32_t M = L.pm[s * 64 + L.lane].y;
+				const uint32_t M = L.meta(s);
 				const int v = lm_votes(M);
 				if (lm_endbit(M)) ltop3(ta[1][0], ta[1][1], ta[1][2], v);
 				else ltop3(ta[0][0], ta[0][1], ta[0][2], v);
@@ -1131,7 +1160,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 						for (uint32_t row = 0; row < LROWS && ns[E] < mvs; row++) {
 							uint32_t s = L.template head<E>(row);
 							while (s != Lane<K, 2>::NIL && ns[E] < mvs) {
-								const uint32_t M = L.pm[s * 64 + L.lane].y;
+								const uint32_t M = L.meta(s);
 								const int v = lm_votes(M);
 								if (v >= ta[E][2]) {
 									const int rs = (int)(*L.cw(st, (int)s, 0) & 0xffu);
@@ -1155,7 +1184,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 						for (uint32_t row = 0; row < LROWS; row++) {
 							uint32_t s = L.template head<E>(row);
 							while (s != Lane<K, 2>::NIL) {
-								const uint32_t M = L.pm[s * 64 + L.lane].y;
+								const uint32_t M = L.meta(s);
 								if (lm_votes(M) == N && ns[E] < mvs) { pl_put(pl[E], ns[E], s); ns[E]++; }
 								s = lm_next(M);
 							}
@@ -1173,7 +1202,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 			if (ns[0] * ns[1] > lp.max_pairs) { L.dfr = true; L.why = 2; continue; }   // bounded per-lane pair loop
 			// value / position / record of a simple
 			auto sv = [&](int E, uint32_t id, uint32_t &pos) __attribute__((always_inline)) -> int {
-				if (id < LPE_RID) { const uint2 x = L.pm[id * 64 + L.lane]; pos = x.x; return lm_votes(x.y); }
+				if (id < LPE_RID) { const uint2 x = L.slot(id); pos = x.x; return lm_votes(x.y); }
 				const int i = (int)id - (int)LPE_RID;
 				const uint32_t m = E ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]);
 				pos = E ? sel3(i, rp1[0], rp1[1], rp1[2]) : sel3(i, rp0[0], rp0[1], rp0[2]);
@@ -1229,7 +1258,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 				uint32_t pos;
 				const int v = sv(E, id, pos);
 				uint32_t m;
-				if (id < LPE_RID) m = RM((st << 6) | (int)id, v, applied[E]) | (lm_ext(L.pm[id * 64 + L.lane].y) << 22);
+				if (id < LPE_RID) m = RM((st << 6) | (int)id, v, applied[E]) | (lm_ext(L.meta(id)) << 22);
 				else { const int i = (int)id - (int)LPE_RID; m = E ? sel3(i, rm1[0], rm1[1], rm1[2]) : sel3(i, rm0[0], rm0[1], rm0[2]); }
 				const int c = cur[E];
 				const uint32_t q0 = E ? tp1[0] : tp0[0], q1 = E ? tp1[1] : tp0[1];
@@ -1287,13 +1316,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 					for (int c = 0; c < cur[E] && !L.dfr; c++) {
 						if (!((needj >> (E * 3 + c)) & 1u)) continue;
 						const int sM = RM_SRC(E ? sel3(c, tm1[0], tm1[1], tm1[2]) : sel3(c, tm0[0], tm0[1], tm0[2])) & 63;
-						const uint2 eM = L.pm[sM * 64 + L.lane];
+						const uint2 eM = L.slot(sM);
 						const int vM = lm_votes(eM.y), stE = E ? step[1] : step[0];
 						const int csM = (int)(*L.cw(st, sM, 0) & 0xffu), ceM = lcov_end(lm_last(eM.y), lm_x(eM.y), stE, lp.gap);
 						for (uint32_t row = 0; row < LROWS && !L.dfr; row++) {
 							uint32_t q = E ? L.template head<1>(row) : L.template head<0>(row);
 							while (q != Lane<K, 2>::NIL) {
-								const uint2 e2 = L.pm[q * 64 + L.lane];
+								const uint2 e2 = L.slot(q);
 								const uint32_t qs = q;
 								q = lm_next(e2.y);
 								if ((int)qs == sM || vM < lm_votes(e2.y)) continue;
@@ -1337,12 +1366,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 						sM = RM_SRC(JE ? sel3(Jc, tm1[0], tm1[1], tm1[2]) : sel3(Jc, tm0[0], tm0[1], tm0[2])) & 63;
 						stE = JE ? step[1] : step[0];
 						rl = JE ? len[1] : len[0];
-						const uint2 eM = L.pm[sM * 64 + L.lane];
+						const uint2 eM = L.slot(sM);
 						Mpos = eM.x;
 						Mcs = (int)(*L.cw(st, sM, 0) & 0xffu);
 						Mce = lcov_end(lm_last(eM.y), lm_x(eM.y), stE, lp.gap);
 					}
-					const uint2 e2 = L.pm[qs * 64 + L.lane];
+					const uint2 e2 = L.slot(qs);
 					const int V = lm_votes(e2.y);
 					const int cs2 = (int)(*L.cw(st, qs, 0) & 0xffu), ce2 = lcov_end(lm_last(e2.y), lm_x(e2.y), stE, lp.gap);
 					// is_better_inner (core-junction.c:961)
