@@ -351,6 +351,18 @@ int svg_abi_version(void);
  * LOCAL_WORLD_SIZE (one rank per GPU on the node), clamped to 2..12. */
 int svg_host_threads(void);
 
+/* NUMA placement of the host side.  svg_host_placement: the NUMA node of `device`'s
+ * PCIe function (-1 unknown) and how many CPUs of that node this process may run on; the host
+ * entry points pin their expansion workers to those CPUs (when there are any) and take their
+ * pinned staging pages from that node.  svg_host_alloc: pinned host memory whose pages come from
+ * the node of idx's GPU -- for the caller's reads and records, which the workers and the copy
+ * engines touch at ~100 GB/s per rank; release with svg_host_free.  svg_cpulist_parse parses a
+ * sysfs cpulist ("0-15,64-79") into a byte mask of `max` entries and returns the CPUs it set. */
+int  svg_host_placement(int device, int *node, int *cpus_on_node);
+int  svg_host_alloc(svg_index *idx, size_t bytes, void **out);
+void svg_host_free(void *p);
+int  svg_cpulist_parse(const char *list, uint8_t *mask, int max);
+
 /*
  * Process-wide implementation options.  The library reads no environment variable of its own
  * (only torchrun's LOCAL_WORLD_SIZE, to size host thread pools): tests and tuning set these

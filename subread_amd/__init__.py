@@ -33,6 +33,7 @@ EXPORTS = [
     "svg_get_kernel_timing", "svg_device_status", "svg_pack_reads", "svg_vote_batch_packed",
     "svg_vote_batch_packed_device", "svg_probe_keys", "svg_probe_keys_device", "svg_host_threads",
     "svg_fragile_batch", "svg_fragile_free", "svg_set_option", "svg_get_option",
+    "svg_host_placement", "svg_host_alloc", "svg_host_free", "svg_cpulist_parse",
     # sublong's voting step (include/subread_long.h)
     "svg_long_vote_batch", "svg_long_free",
     # host post-vote events (include/subread_events.h)
@@ -120,6 +121,13 @@ def lib():
         L.svg_sam_writer_failed.restype = i32
         L.svg_sam_format.argtypes = [vp, vp, ctypes.c_size_t]
         L.svg_sam_format.restype = ctypes.c_int64
+        L.svg_host_placement.argtypes = [i32, vp, vp]
+        L.svg_host_placement.restype = i32
+        L.svg_host_alloc.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
+        L.svg_host_alloc.restype = i32
+        L.svg_host_free.argtypes = [vp]
+        L.svg_cpulist_parse.argtypes = [ctypes.c_char_p, vp, i32]
+        L.svg_cpulist_parse.restype = i32
         L.svg_set_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
         L.svg_set_option.restype = i32
         L.svg_get_option.argtypes = [ctypes.c_char_p]
@@ -350,6 +358,17 @@ def pack_reads(batch, stride=None, threads=8, alloc=None):
                        stride or 0, batch.lens)
 
 
+class _HostMem:
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __del__(self):
+        try:
+            lib().svg_host_free(ctypes.c_void_p(self.ptr))
+        except Exception:
+            pass
+
+
 class VoteIndex:
     """An index resident in HBM of one GPU (svg_index_open / svg_index_build*)."""
 
@@ -391,6 +410,24 @@ class VoteIndex:
     @property
     def n_blocks(self):
         return self.info.n_blocks
+
+    def host_alloc(self, count, dtype=np.uint8):
+        """svg_host_alloc: a pinned host numpy array whose pages sit on the NUMA node of this
+        index's GPU; freed (svg_host_free) when the array is no longer referenced."""
+        dt = np.dtype(dtype)
+        nbytes = max(1, int(count) * dt.itemsize)
+        p = ctypes.c_void_p()
+        _check(lib().svg_host_alloc(self.h, nbytes, ctypes.byref(p)), "svg_host_alloc")
+        buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
+        buf._owner = _HostMem(p.value)
+        return np.ctypeslib.as_array(buf)[:int(count) * dt.itemsize].view(dt)
+
+    def host_placement(self):
+        """(NUMA node of the GPU, usable CPUs on it) -- where svg_host_alloc's pages and the
+        expansion workers go."""
+        node, ncpu = ctypes.c_int(), ctypes.c_int()
+        lib().svg_host_placement(self.info.device, ctypes.byref(node), ctypes.byref(ncpu))
+        return node.value, ncpu.value
 
     def export(self):
         """Host copy of the index arrays of block 00 (dict usable by the oracle's from_arrays)."""

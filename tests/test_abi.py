@@ -4,6 +4,7 @@ import ctypes
 import re
 import os
 
+import pytest
 import numpy as np
 
 import subread_amd as sa
@@ -15,7 +16,7 @@ ensure_built()
 
 def header_symbols():
     syms = set()
-    for h in ("subread_vote.h", "subread_events.h", "subread_long.h"):
+    for h in ("subread_vote.h", "subread_events.h", "subread_long.h", "subread_sam.h"):
         txt = open(os.path.join(ROOT, "include", h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         syms |= set(re.findall(r"\b(svg_[a-z0-9_]+)\s*\(", txt))
@@ -92,3 +93,38 @@ def test_host_threads_follow_affinity_quota_and_ranks(monkeypatch, svgopt):
     assert L.svg_host_threads() == 5
     svgopt.reset("host_threads")
     assert L.svg_host_threads() == 2
+
+
+def test_cpulist_parse():
+    """svg_cpulist_parse: the sysfs node cpulist format the NUMA placement reads
+    (/sys/devices/system/node/nodeN/cpulist)."""
+    import numpy as np
+    L = sa.lib()
+    for text, want in ((b"0-15,64-79\n", list(range(16)) + list(range(64, 80))), (b"3", [3]), (b"", []),
+                       (b"0,2,4-6", [0, 2, 4, 5, 6]), (b"120-130", list(range(120, 128)))):
+        m = np.zeros(128, np.uint8)
+        n = L.svg_cpulist_parse(text, m.ctypes.data, 128)
+        assert n == len(want) and list(np.nonzero(m)[0]) == want, (text, n)
+
+
+@pytest.mark.gpu
+def test_host_placement_reports_node_and_cpus():
+    """svg_host_placement (GPU box): the NUMA node of device 0's PCIe function as sysfs gives it,
+    and the CPUs of that node this process may use (the expansion workers' affinity); the node's
+    pinned allocation (svg_host_alloc) comes back usable."""
+    import ctypes
+    import os
+    import torch
+    assert torch.cuda.is_available()
+    node, ncpu = ctypes.c_int(-7), ctypes.c_int(-7)
+    assert sa.lib().svg_host_placement(0, ctypes.byref(node), ctypes.byref(ncpu)) == 0
+    assert node.value >= -1 and ncpu.value >= 0
+    if node.value >= 0:
+        cl = open("/sys/devices/system/node/node%d/cpulist" % node.value).read()
+        import numpy as np
+        m = np.zeros(4096, np.uint8)
+        sa.lib().svg_cpulist_parse(cl.encode(), m.ctypes.data, 4096)
+        want = len(set(np.nonzero(m)[0]) & os.sched_getaffinity(0))
+        assert ncpu.value == want
+    else:
+        assert ncpu.value == 0
