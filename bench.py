@@ -196,6 +196,7 @@ def main():
     log("[bench] index in HBM (%.1f GB, %d items) in %.1fs" % (ix.info.device_bytes / 1e9, ix.info.items,
                                                             time.time() - t1))
 
+    placement = ix.host_placement()
     # this rank's shard of the read stream: reads (pairs) rank*n .. rank*n+n-1
     t1 = time.time()
     kind = W["kind"]
@@ -217,10 +218,11 @@ def main():
     keep = []
 
     def pinned(count, dt):
-        dt = np.dtype(dt)
-        t = torch.empty(max(1, count * dt.itemsize), dtype=torch.uint8, pin_memory=True)
-        keep.append(t)
-        return t.numpy()[:count * dt.itemsize].view(dt)
+        # pinned pages on the NUMA node of this rank's GPU (svg_host_alloc), where the expansion
+        # workers and the copy engines touch them
+        a = ix.host_alloc(count, dt)
+        keep.append(a)
+        return a
     t1 = time.time()
     pk1 = sa.pack_reads(rb, L, threads=threads, alloc=pinned)
     pk2 = sa.pack_reads(rb2, L, threads=threads, alloc=pinned) if rb2 is not None else None
@@ -522,7 +524,12 @@ def main():
                            "full" if ix.info.index_gap == 1 else "gapped", ix.info.index_gap, ix.info.buckets, ix.info.items,
                            "reference-format files via svg_index_open" if prefix else "built in HBM by svg_index_build_mem"),
                        "parallelism": "reads sharded across %d GPU(s), index replicated, no collective" % world,
-                       "host_threads_per_rank": int(sa.lib().svg_host_threads())},
+                       "host_threads_per_rank": int(sa.lib().svg_host_threads()),
+                       "host_placement": {"gpu_numa_node": placement[0], "usable_cpus_on_node": placement[1],
+                                          "pinned_pages": "svg_host_alloc: preferred node %d" % placement[0]
+                                          if placement[0] >= 0 else "svg_host_alloc: node unknown (default policy)",
+                                          "expansion_workers": "pinned to the node's CPUs" if placement[1] > 0
+                                          else "unpinned (no usable CPU on the node)"}},
             "roofline": {"bound": bound, "regime": kernels[dom]["regime"], "kernel": dom, "achieved": round(vote_achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(vote_achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_unit": "GB per launch",
