@@ -12,6 +12,8 @@
  *   svg_attach           once, after load_global_context (core.c:4013) has the index prefix
  *   do_voting_gpu        per chunk and index block, from ONE host thread per GPU
  *                        (run_in_thread, core.c:3366)
+ *   do_voting_gpu_mt     the same from each of the run's -T threads: thread 0 reads and votes
+ *                        the chunk, every thread does the per-read host work of its slice
  *
  * The chunk's reads come from fetch_next_read_pair (core.c:1121) exactly as do_voting
  * reads them -- that function already applies the -S reversal (core.c:1186-1198), so the
@@ -53,6 +55,7 @@ int has_better_mapping(global_context_t *global_context, thread_context_t *threa
 int find_subread_end(int len, int TOTAL_SUBREADS, int subread);   /* input-files.c:1371 */
 
 static svg_index *svg_ix;   /* one per process, one process per GPU */
+static pthread_mutex_t svg_sam_mu_init = PTHREAD_MUTEX_INITIALIZER;   /* one-time setup of the shared state */
 
 int svg_attach(global_context_t *gc, int device)
 {
@@ -301,59 +304,77 @@ static void fragile_window_events(global_context_t *gc, thread_context_t *tc, co
  * every block's run, freed after the final one */
 static svg_fragile_result svg_frag;
 
-int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
-{
-	int ends = 1 + gc->input_reads.is_paired_end_reads, rc = 0, e, s;
-	svg_chunk_reads c;
-	memset(&c, 0, sizeof c);
-	/* do_voting's per-run state (core.c:3081-3089) */
-	unsigned int low_border = gc->current_value_index->start_base_offset;
-	unsigned int high_border = gc->current_value_index->start_base_offset + gc->current_value_index->length;
-	if (tc) tc->current_value_index = gc->current_value_index;
-	int need_junction_step = gc->config.do_breakpoint_detection || gc->config.do_fusion_detection || gc->config.do_long_del_detection;
-	gene_vote_t *vote_fg = gc->config.do_breakpoint_detection ? malloc(sizeof(gene_vote_t)) : NULL;
-	if (gc->config.do_breakpoint_detection && !vote_fg) return 1;
+/* the chunk of the current run, shared by the run's threads (read and voted by thread 0) */
+static svg_chunk_reads svg_chunk;
+static uint64_t *svg_win;       /* svg_win[r] .. svg_win[r+1]: read r's fragile windows in this block */
 
-	rc = read_chunk(gc, tc, ends, &c);
+/* thread 0 (or the only thread): the chunk's reads, the GPU vote (first block's run: every block),
+ * the fragile windows, and the per-read index of this block's windows */
+static int vote_stage(global_context_t *gc, thread_context_t *tc)
+{
+	int ends = 1 + gc->input_reads.is_paired_end_reads, rc;
+	memset(&svg_chunk, 0, sizeof svg_chunk);
+	svg_chunk_reads *c = &svg_chunk;
+	rc = read_chunk(gc, tc, ends, c);
 	/* a multi-block index: the library votes every block (all resident in HBM) in the first
 	 * block's run of read_chunk_circles (core.c:3567-3613); the later runs re-read the chunk
-	 * for the per-block host work below */
-	if (!rc && c.n && gc->current_index_block_number == 0) {
-		rc = vote_chunk(gc, ends, &c);
+	 * for the per-block host work */
+	if (!rc && c->n && gc->current_index_block_number == 0) {
+		rc = vote_chunk(gc, ends, c);
 		/* fragile junction voting of every block, on the GPU (subjunc reads > 160 bp) */
 		svg_fragile_free(&svg_frag);
 		if (!rc && gc->config.do_breakpoint_detection) {
 			svg_params p;
 			svg_fill_params(gc, &p);
-			svg_reads a1 = {c.text[0], c.off[0], c.len[0], c.n}, a2 = {c.text[1], c.off[1], c.len[1], c.n};
+			svg_reads a1 = {c->text[0], c->off[0], c->len[0], c->n}, a2 = {c->text[1], c->off[1], c->len[1], c->n};
 			rc = svg_fragile_batch(svg_ix, &p, &a1, ends == 2 ? &a2 : NULL, &svg_frag);
 			if (rc) SUBREADprintf("svg_fragile_batch: %s\n", svg_last_error());
 		}
 	}
-	/* this block's fragile windows, in (read, strand, end, window) order */
+	/* this block's fragile windows are in (read, strand, end, window) order: read r's are
+	 * svg_win[r] .. svg_win[r+1]-1 */
+	free(svg_win);
+	svg_win = calloc(c->n + 2, sizeof(uint64_t));
+	if (!svg_win) return 1;
 	uint64_t fw = 0;
 	while (fw < svg_frag.n_windows && svg_frag.windows[fw].block < gc->current_index_block_number) fw++;
+	for (uint64_t r = 0; r <= c->n; r++) {
+		svg_win[r] = fw;
+		while (fw < svg_frag.n_windows && svg_frag.windows[fw].block == gc->current_index_block_number &&
+		       svg_frag.windows[fw].read == (uint32_t)r)
+			fw++;
+	}
+	return rc;
+}
 
-	/* 3. do_voting's per-read host work, in its order */
+/* do_voting's per-read host work for reads [r0, r1) of the chunk, in its order, into tc's event
+ * tables (the reference's threads each fill their own, merged by
+ * finalise_indel_and_junction_thread, core.c:3452) */
+static void tail_stage(global_context_t *gc, thread_context_t *tc, uint64_t r0, uint64_t r1)
+{
+	const svg_chunk_reads *c = &svg_chunk;
+	int ends = 1 + gc->input_reads.is_paired_end_reads, e;
+	/* do_voting's per-run state (core.c:3081-3089) */
+	if (tc) tc->current_value_index = gc->current_value_index;
+	int need_junction_step = gc->config.do_breakpoint_detection || gc->config.do_fusion_detection || gc->config.do_long_del_detection;
 	char text[MAX_READ_LENGTH + 1], qual[MAX_READ_LENGTH + 1];
 	subread_read_number_t r;
-	for (r = 0; !rc && r < (subread_read_number_t)c.n; r++) {
+	for (r = (subread_read_number_t)r0; r < (subread_read_number_t)r1; r++) {
 		/* core_fragile_junction_voting (core.c:3138-3142) of this read: its windows in this block,
 		 * strand 0 on the fetched text, strand 1 on its reverse_read, R1 then R2 -- voted on the
 		 * GPU (svg_fragile_batch), their events made here */
-		while (fw < svg_frag.n_windows && svg_frag.windows[fw].block == gc->current_index_block_number &&
-		       svg_frag.windows[fw].read == (uint32_t)r) {
-			const svg_fragile_window *W = &svg_frag.windows[fw++];
+		uint64_t fw;
+		for (fw = svg_win[r]; fw < svg_win[r + 1]; fw++) {
+			const svg_fragile_window *W = &svg_frag.windows[fw];
 			char in[MAX_READ_LENGTH + 1];
-			int rl = c.len[W->end][r];
-			memcpy(text, c.text[W->end] + c.off[W->end][r], rl);
+			int rl = c->len[W->end][r];
+			memcpy(text, c->text[W->end] + c->off[W->end][r], rl);
 			text[rl] = 0;
 			if (W->strand) reverse_read(text, rl, gc->config.space_type);
 			memcpy(in, text + W->start, W->length);
 			in[W->length] = 0;
-			fragile_window_events(gc, tc, W, svg_frag.slots, in, c.name[0] + r * (MAX_READ_NAME_LEN + 1));
+			fragile_window_events(gc, tc, W, svg_frag.slots, in, c->name[0] + r * (MAX_READ_NAME_LEN + 1));
 		}
-		(void)vote_fg; (void)low_border; (void)high_border; (void)s;
 		if (!gc->is_final_voting_run) continue;
 		/* the final-voting-run block (core.c:3240-3290) */
 		for (e = 0; e < ends; e++) {
@@ -361,12 +382,12 @@ int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
 			 * the tail starts from that state (read_1_reversed = 1) and reverses both together when a
 			 * record's strand needs it, so text and quality stay in opposite orientations, as there */
 			int has_reversed = 1;
-			int rl = c.len[e][r];
-			memcpy(text, c.text[e] + c.off[e][r], rl);
-			memcpy(qual, c.qual[e] + c.off[e][r], rl);
+			int rl = c->len[e][r];
+			memcpy(text, c->text[e] + c->off[e][r], rl);
+			memcpy(qual, c->qual[e] + c->off[e][r], rl);
 			text[rl] = qual[rl] = 0;
 			reverse_read(text, rl, gc->config.space_type);
-			char *rn = c.name[e] + r * (MAX_READ_NAME_LEN + 1);
+			char *rn = c->name[e] + r * (MAX_READ_NAME_LEN + 1);
 			int b;
 			for (b = 0; b < gc->config.multi_best_reads; b++) {
 				mapping_result_t *cur = _global_retrieve_alignment_ptr(gc, r, e, b);
@@ -386,9 +407,52 @@ int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
 			}
 		}
 	}
-	chunk_free(&c);
-	free(vote_fg);
+}
+
+static void run_end(global_context_t *gc)
+{
+	chunk_free(&svg_chunk);
+	memset(&svg_chunk, 0, sizeof svg_chunk);
+	free(svg_win);
+	svg_win = NULL;
 	if (gc->is_final_voting_run) svg_fragile_free(&svg_frag);
+}
+
+/* one thread: the whole run */
+int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
+{
+	int rc = vote_stage(gc, tc);
+	if (!rc) tail_stage(gc, tc, 0, svg_chunk.n);
+	run_end(gc);
+	return rc ? 1 : 0;
+}
+
+/* every one of the run's `nthreads` threads (run_in_thread, one do_voting each): thread 0 reads
+ * and votes the chunk, then each thread does the per-read host work of a contiguous slice of it
+ * into its own event tables, as the reference's threads do for the reads they fetch */
+static pthread_barrier_t svg_bar;
+static int svg_bar_n;
+static volatile int svg_run_rc;
+
+int do_voting_gpu_mt(global_context_t *gc, thread_context_t *tc, int nthreads)
+{
+	pthread_mutex_lock(&svg_sam_mu_init);
+	if (svg_bar_n != nthreads) {
+		if (svg_bar_n) pthread_barrier_destroy(&svg_bar);
+		pthread_barrier_init(&svg_bar, NULL, (unsigned)nthreads);
+		svg_bar_n = nthreads;
+	}
+	pthread_mutex_unlock(&svg_sam_mu_init);
+	const int tid = tc->thread_id;
+	if (tid == 0) svg_run_rc = vote_stage(gc, tc);
+	pthread_barrier_wait(&svg_bar);
+	if (!svg_run_rc) {
+		const uint64_t n = svg_chunk.n;
+		tail_stage(gc, tc, n * (uint64_t)tid / (uint64_t)nthreads, n * (uint64_t)(tid + 1) / (uint64_t)nthreads);
+	}
+	pthread_barrier_wait(&svg_bar);
+	const int rc = svg_run_rc;
+	if (tid == 0) run_end(gc);
 	return rc ? 1 : 0;
 }
 
@@ -498,16 +562,21 @@ void add_buffered_fragment(global_context_t *gc, thread_context_t *tc, subread_r
 /*
  * Harness build only (oracle/Makefile `dropin`): the reference's core.o is compiled with
  * do_voting weak, so this definition takes run_in_thread's call (core.c:3366-3368).  Thread 0
- * (or the single -T 1 caller) feeds the whole chunk to the GPU; the other voting threads
- * fetch nothing, so read numbers stay sequential.  The device is SVG_DEVICE (default 0).
+ * (or the single -T 1 caller) reads the whole chunk and feeds it to the GPU, so read numbers
+ * stay sequential; then every voting thread does the per-read host work of its slice of the
+ * chunk (do_voting_gpu_mt).  The device is SVG_DEVICE (default 0).
  */
 int do_voting(global_context_t *gc, thread_context_t *tc)
 {
-	if (tc && tc->thread_id != 0) return 0;
+	pthread_mutex_lock(&svg_sam_mu_init);
+	int rc = 0;
 	if (!svg_ix) {
 		const char *d = getenv("SVG_DEVICE");
-		if (svg_attach(gc, d ? atoi(d) : 0)) return 1;
+		rc = svg_attach(gc, d ? atoi(d) : 0);
 	}
-	return do_voting_gpu(gc, tc);
+	pthread_mutex_unlock(&svg_sam_mu_init);
+	if (rc) return 1;
+	if (!tc || gc->config.all_threads < 2) return do_voting_gpu(gc, tc);
+	return do_voting_gpu_mt(gc, tc, gc->config.all_threads);
 }
 #endif
