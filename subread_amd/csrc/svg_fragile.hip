@@ -54,6 +54,7 @@ struct FParams {
 	svg_fragile_slot *sout;
 	uint32_t *scount;     // slots written (may exceed scap: the host retries with room)
 	uint32_t scap;
+	int literal;          // option keys_literal: the literal bucket search for every probe (A/B, tests)
 };
 
 struct FLDS {
@@ -236,6 +237,66 @@ __device__ void f_vote(FLDS *L, int &items, int &maxv, uint32_t kv, int kP1, int
 	f_sync();
 }
 
+// the equal-key run [f, f + c) (absolute item indices) of `key` in bucket b, as gehash_go_q's
+// search leaves it (sorted-hashtable.c:760-812): from the 32-byte bucket code (full indexes:
+// two selects on its zero bits), from the key-hash record (gapped / small indexes: mid - bwd,
+// fwd + bwd), or -- for a bucket the image does not hold (code count byte 255, or keys not sorted)
+// -- the literal binary search, back to the first equal key and forward to the last
+__device__ __forceinline__ void go_run(const DevIndex &x, uint32_t key, uint32_t b, uint32_t &f, uint32_t &c, bool literal)
+{
+	const uint32_t q = key / x.nb;
+	f = 0;
+	c = 0;
+	if (literal) {
+	} else if (x.bcode) {
+		const uint4 *c4 = x.bcode + 2 * (size_t)b;
+		const uint4 u0 = c4[0], u1 = c4[1];
+		const uint32_t n = u0.y & 255u;
+		if (n != 255u) {
+			if (n) {
+				const uint64_t z[4] = {~(((uint64_t)u0.y << 32) | u0.x) & ~0xffffffffffull, ~(((uint64_t)u0.w << 32) | u0.z),
+				                       ~(((uint64_t)u1.y << 32) | u1.x), ~(((uint64_t)u1.w << 32) | u1.z)};
+				const int k = (int)q;
+				const int fe = k ? code_zero(z, k - 1) - 40 - (k - 1) : 0;
+				const int ee = code_zero(z, k) - 40 - k;
+				if (ee > fe) { f = u0.x + (uint32_t)fe; c = (uint32_t)(ee - fe); }
+			}
+			return;
+		}
+	} else if (x.khash && x.ksorted && q <= 0xffffu && ((x.ksorted[b >> 5] >> (b & 31u)) & 1u)) {
+		uint2 rec;
+		if (khash_find(x, key, rec)) {
+			const uint32_t fwd = rec.y & 0xffffu, bwd = rec.y >> 16;
+			f = rec.x - bwd;
+			c = fwd + bwd;
+		}
+		return;
+	}
+	const int16_t k16 = (int16_t)q;
+	const uint32_t first = x.bstart[b];
+	const int n = (int)(x.bstart[b + 1] - first);
+	const int16_t *KK = x.keys + first;
+	if (n) {
+		int lo = 0, hi = n - 1, idx;
+		bool hit = false;
+		for (;;) {
+			idx = (lo + hi) / 2;
+			const int16_t kk = KK[idx];
+			if (kk > k16) hi = idx - 1;
+			else if (kk < k16) lo = idx + 1;
+			else { hit = true; break; }
+			if (hi < lo) break;
+		}
+		if (hit) {
+			while (idx && KK[idx - 1] == k16) idx--;
+			int e = idx;
+			while (e < n && KK[e] == k16) e++;
+			f = first + (uint32_t)idx;
+			c = (uint32_t)(e - idx);
+		}
+	}
+}
+
 __global__ void __launch_bounds__(64) fragile_kernel(FParams fp)
 {
 	__shared__ FLDS L_;
@@ -273,31 +334,11 @@ __global__ void __launch_bounds__(64) fragile_kernel(FParams fp)
 			uint32_t key = 0;
 			for (int q = 0; q < 16; q++) key |= f_b2i(L->text[off + q]) << (30 - 2 * q);
 			// gehash_go_q (sorted-hashtable.c:760-795): binary search, then back to the first equal key
+			// and forward over the run -- in a bucket whose keys are sorted, exactly the bucket's whole
+			// equal-key run, which the vote path's probe images hold (go_run)
 			const uint32_t b = key % x.nb;
-			const int16_t k16 = (int16_t)(key / x.nb);
-			const uint32_t first = x.bstart[b];
-			const int n = (int)(x.bstart[b + 1] - first);
-			const int16_t *KK = x.keys + first;
 			uint32_t f0 = 0;
-			if (n) {
-				int lo = 0, hi = n - 1, idx;
-				bool hit = false;
-				for (;;) {
-					idx = (lo + hi) / 2;
-					const int16_t kk = KK[idx];
-					if (kk > k16) hi = idx - 1;
-					else if (kk < k16) lo = idx + 1;
-					else { hit = true; break; }
-					if (hi < lo) break;
-				}
-				if (hit) {
-					while (idx && KK[idx - 1] == k16) idx--;
-					int e = idx;
-					while (e < n && KK[e] == k16) e++;
-					f0 = first + (uint32_t)idx;
-					cnt = (uint32_t)(e - idx);
-				}
-			}
+			go_run(x, key, b, f0, cnt, fp.literal != 0);
 			L->pfirst[lane] = f0;
 			L->pcnt[lane] = cnt;
 			L->ppk[lane] = (uint16_t)((k + 1) | (off << 6));
@@ -603,6 +644,7 @@ extern "C" int svg_fragile_batch(svg_index *h, const svg_params *p, const svg_re
 			fp.ix = bk->dix; fp.text = d_text; fp.jobs = d_jobs; fp.n_jobs = (uint32_t)nj; fp.block = b; fp.f3 = d_f3;
 			fp.low = bk->dix.start_base_offset; fp.high = bk->dix.start_base_offset + bk->dix.length;
 			fp.wout = d_w; fp.sout = d_s; fp.scount = d_cnt; fp.scap = scap;
+			fp.literal = svg_get_option("keys_literal") != 0;
 			uint64_t grid = (uint64_t)h->n_cu * 5;
 			if (grid > nj) grid = nj;
 			if (hipMemsetAsync(d_cnt, 0, 4, st) != hipSuccess) { rc = SVG_E_DEVICE; break; }

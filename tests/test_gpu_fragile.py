@@ -62,9 +62,12 @@ def _spliced(g, n, lens, seed):
     return ReadBatch.from_list(out)
 
 
+@pytest.mark.parametrize("probe", ["image", "literal"])
 @pytest.mark.parametrize("key,paired", [("chr901_full", False), ("chr901_gapped", True), ("long777_gappedM6", False),
                                         ("synth4242_fullM1", True)])
-def test_fragile_windows_simulated(key, paired, index_cache):
+def test_fragile_windows_simulated(key, paired, probe, index_cache, svgopt):
+    """probe: the equal-key runs from the probe images (bucket code / key-hash, go_run) or the literal
+    gehash_go_q search (option keys_literal) -- identical windows either way"""
     import subread_amd as sa
     from oracle.pyoracle import OracleIndex
     from subread_amd.abi import default_params, PROGRAM_SUBJUNC
@@ -75,6 +78,7 @@ def test_fragile_windows_simulated(key, paired, index_cache):
     r1 = _spliced(g, 150, lens, 71)
     r2 = _spliced(g, 150, lens, 83) if paired else None
     p = default_params(PROGRAM_SUBJUNC, paired)
+    svgopt.set("keys_literal", 1 if probe == "literal" else 0)
     ix = sa.VoteIndex(pre, device=0)
     got = ix.fragile(p, r1, r2)
     ix.close()
