@@ -265,12 +265,14 @@ __device__ __forceinline__ void go_run(const DevIndex &x, uint32_t key, uint32_t
 		}
 	} else if (x.khash && x.ksorted && q <= 0xffffu && ((x.ksorted[b >> 5] >> (b & 31u)) & 1u)) {
 		uint2 rec;
-		if (khash_find(x, key, rec)) {
+		const bool hit = khash_find(x, key, rec);
+		if (!hit) return;
+		if (!svg_rec_inline(x.kinline, rec.y)) {   // (an inline record holds a position: literal search)
 			const uint32_t fwd = rec.y & 0xffffu, bwd = rec.y >> 16;
 			f = rec.x - bwd;
 			c = fwd + bwd;
+			return;
 		}
-		return;
 	}
 	const int16_t k16 = (int16_t)q;
 	const uint32_t first = x.bstart[b];

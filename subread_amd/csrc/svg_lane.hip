@@ -62,6 +62,7 @@ struct GParams {
 	uint32_t cs;             // column stride of cand/cpk/ccnt
 	const uint32_t *idx;     // NULL: column r = read r; else column k = read idx[k], k < min(*idx_count, cs)
 	const uint32_t *idx_count;
+	int kinline;             // DevIndex::kinline: one-hit records carry the position itself
 };
 
 __global__ void __launch_bounds__(256) gather_kernel(GParams g)
@@ -129,6 +130,7 @@ struct LParams {
 	const uint2 *precs;           // fused gather (NPF > 0): probe records, SoA [(end * 2 + strand) * nps + p][n]
 	const uint32_t *vals;
 	int nps;
+	int kinline;                  // DevIndex::kinline: one-hit probe records carry the position itself
 	// subjunc (lane_kernel<..., SJ = true>)
 	uint8_t *jout;                // subjunc_result_t records of the chunk
 	uint16_t *bm_out;             // big-margin records of the chunk
@@ -661,7 +663,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 			for (int o = 32; o; o >>= 1) { int t = __shfl_xor(mc, o); mc = t > mc ? t : mc; }
 			int pb = 0;
 			uint32_t jb = 0;
-			auto next = [&](uint32_t &item, uint32_t &pk) __attribute__((always_inline)) {
+			auto next = [&](uint32_t &item, uint32_t &pk) __attribute__((always_inline)) -> bool {
 				while (jb >= (ry[0] & 0xffffu) + (ry[0] >> 16)) {
 #pragma unroll
 					for (int p = 0; p + 1 < NPF; p++) { rx[p] = rx[p + 1]; ry[p] = ry[p + 1]; }
@@ -677,17 +679,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 				int off = (int)(((int64_t)step * sk) >> 16);
 				if (lp.gap > 1) off -= off % lp.gap - x;
 				pk = (uint32_t)(sk + 1) | ((uint32_t)off << 6);
+				return svg_rec_inline(lp.kinline, ry[0]);   // item is the position itself
 			};
 			uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0, it = 0, pkn = 0;
-			if (0 < mycnt) { next(it, pkn); q0 = lp.vals[it]; k0 = pkn; }
-			if (1 < mycnt) { next(it, pkn); q1 = lp.vals[it]; k1 = pkn; }
-			if (2 < mycnt) { next(it, pkn); q2 = lp.vals[it]; k2 = pkn; }
-			if (3 < mycnt) { next(it, pkn); q3 = lp.vals[it]; k3 = pkn; }
+			if (0 < mycnt) { q0 = next(it, pkn) ? it : lp.vals[it]; k0 = pkn; }
+			if (1 < mycnt) { q1 = next(it, pkn) ? it : lp.vals[it]; k1 = pkn; }
+			if (2 < mycnt) { q2 = next(it, pkn) ? it : lp.vals[it]; k2 = pkn; }
+			if (3 < mycnt) { q3 = next(it, pkn) ? it : lp.vals[it]; k3 = pkn; }
 			for (int j = 0; j < mc; j++) {
 				const uint32_t val = q0, pk = k0;
 				q0 = q1; q1 = q2; q2 = q3;
 				k0 = k1; k1 = k2; k2 = k3;
-				if (j + 4 < mycnt) { next(it, pkn); q3 = lp.vals[it]; k3 = pkn; }
+				if (j + 4 < mycnt) { q3 = next(it, pkn) ? it : lp.vals[it]; k3 = pkn; }
 				if (j < mycnt && !L.dfr) L.template vote<0>(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b, lp.gap);
 			}
 			}
@@ -1091,7 +1094,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 				for (int o = 32; o; o >>= 1) { int t = __shfl_xor(mc, o); mc = t > mc ? t : mc; }
 				int pb = 0;
 				uint32_t jb = 0;
-				auto next = [&](uint32_t &item, uint32_t &pk) __attribute__((always_inline)) {
+				auto next = [&](uint32_t &item, uint32_t &pk) __attribute__((always_inline)) -> bool {
 					while (jb >= (ry[0] & 0xffffu) + (ry[0] >> 16)) {
 #pragma unroll
 						for (int p = 0; p + 1 < NPF; p++) { rx[p] = rx[p + 1]; ry[p] = ry[p + 1]; }
@@ -1107,17 +1110,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 					int off = (int)(((int64_t)step[E] * sk) >> 16);
 					if (lp.gap > 1) off -= off % lp.gap - x;
 					pk = (uint32_t)(sk + 1) | ((uint32_t)off << 6);
+					return svg_rec_inline(lp.kinline, ry[0]);   // item is the position itself
 				};
 				uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0, it = 0, pkn = 0;
-				if (0 < mycnt) { next(it, pkn); q0 = lp.vals[it]; k0 = pkn; }
-				if (1 < mycnt) { next(it, pkn); q1 = lp.vals[it]; k1 = pkn; }
-				if (2 < mycnt) { next(it, pkn); q2 = lp.vals[it]; k2 = pkn; }
-				if (3 < mycnt) { next(it, pkn); q3 = lp.vals[it]; k3 = pkn; }
+				if (0 < mycnt) { q0 = next(it, pkn) ? it : lp.vals[it]; k0 = pkn; }
+				if (1 < mycnt) { q1 = next(it, pkn) ? it : lp.vals[it]; k1 = pkn; }
+				if (2 < mycnt) { q2 = next(it, pkn) ? it : lp.vals[it]; k2 = pkn; }
+				if (3 < mycnt) { q3 = next(it, pkn) ? it : lp.vals[it]; k3 = pkn; }
 				for (int j = 0; j < mc; j++) {
 					const uint32_t val = q0, pk = k0;
 					q0 = q1; q1 = q2; q2 = q3;
 					k0 = k1; k1 = k2; k2 = k3;
-					if (j + 4 < mycnt) { next(it, pkn); q3 = lp.vals[it]; k3 = pkn; }
+					if (j + 4 < mycnt) { q3 = next(it, pkn) ? it : lp.vals[it]; k3 = pkn; }
 					if (j < mycnt && !L.dfr) L.template vote<E>(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b[E], lp.gap);
 				}
 			};
@@ -1644,7 +1648,7 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	memset(&lp, 0, sizeof lp);
 	lp.len = len1; lp.len2 = len2; lp.n = n; lp.cap = LANE_PE_CAP;
 	if (svg_get_option("lane_pe_cap") > 0) lp.cap = (int)svg_get_option("lane_pe_cap");   // candidates per end and strand
-	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps;
+	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps; lp.kinline = svg_probe_inline(h);
 	lp.gap = h->dix.gap; lp.total_subreads = p->total_subreads;
 	lp.tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
 	lp.low = h->dix.start_base_offset;
@@ -1724,7 +1728,7 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 	uint32_t *cnt = (uint32_t *)(b + o_cnt);
 	HIPCHK(hipMemsetAsync(cnt, 0, 32, st));
 	GParams g;
-	g.precs = precs; g.len = len; g.vals = h->dix.vals; g.n = n; g.nps = nps; g.gap = h->dix.gap;
+	g.precs = precs; g.len = len; g.vals = h->dix.vals; g.n = n; g.nps = nps; g.gap = h->dix.gap; g.kinline = svg_probe_inline(h);
 	g.total_subreads = p->total_subreads; g.cap = LANE_CAP1;
 	g.cand = (uint32_t *)(b + o_c1); g.cpk = (uint16_t *)(b + o_p1); g.ccnt = (uint16_t *)(b + o_n1);
 	g.cs = n; g.idx = NULL; g.idx_count = NULL;
@@ -1736,7 +1740,7 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 	if (!fused && (rc = gather_launch(h, g, st))) return rc;
 	LParams lp;
 	lp.cand = g.cand; lp.cpk = g.cpk; lp.ccnt = g.ccnt; lp.len = len; lp.n = n; lp.cap = LANE_CAP1;
-	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps;
+	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps; lp.kinline = svg_probe_inline(h);
 	lp.gap = h->dix.gap; lp.total_subreads = p->total_subreads;
 	lp.tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
 	lp.low = h->dix.start_base_offset;

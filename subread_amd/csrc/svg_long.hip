@@ -159,9 +159,12 @@ __global__ void __launch_bounds__(256) long_probe_kernel(LProbe lp)
 		if (!literal) {
 			uint2 rec;
 			if (khash_find(x, key, rec)) {
-				const uint32_t fwd = rec.y & 0xffffu, bwd = rec.y >> 16;
-				f = rec.x - bwd;
-				c = fwd + bwd;
+				if (svg_rec_inline(x.kinline, rec.y)) literal = true;   // a position, not the item
+				else {
+					const uint32_t fwd = rec.y & 0xffffu, bwd = rec.y >> 16;
+					f = rec.x - bwd;
+					c = fwd + bwd;
+				}
 			}
 		}
 	}

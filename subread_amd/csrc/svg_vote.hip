@@ -564,7 +564,8 @@ struct Wave {
 		STAMP(2);
 		// gather in visiting order (probe p, then mid..last, then mid-1..first), lane c = candidate
 		// c0 + c of the chunk; the next chunk's hit values are loaded while this one is voted
-		auto locate_cand = [&](uint32_t cc, uint32_t &item, int &off, int &kP1) __attribute__((always_inline)) {
+		// (inline key-hash records: a one-hit probe's "mid" is its position, DevIndex::kinline)
+		auto locate_cand = [&](uint32_t cc, uint32_t &item, int &off, int &kP1) __attribute__((always_inline)) -> bool {
 			int lo = 0, hi = np - 1;   // probe p with pcum[p] <= cc < pcum[p+1]
 			while (lo < hi) { int m = (lo + hi + 1) >> 1; if (L->pcum[m] <= cc) lo = m; else hi = m - 1; }
 			const int p = lo;
@@ -574,17 +575,17 @@ struct Wave {
 			item = j < fwd ? mid + j : mid - 1 - (j - fwd);
 			off = probe_off(E, p);
 			kP1 = p / gap + 1;
+			return svg_rec_inline(kp->ix.kinline, fwd | ((uint32_t)L->pbwd[E][s][p] << 16));
 		};
 		uint32_t nitem = 0, nval = 0;
 		int noff = 0, nkp1 = 0;
-		if ((uint32_t)lane < total) { locate_cand((uint32_t)lane, nitem, noff, nkp1); nval = kp->ix.vals[nitem]; }
+		if ((uint32_t)lane < total) nval = locate_cand((uint32_t)lane, nitem, noff, nkp1) ? nitem : kp->ix.vals[nitem];
 		for (uint32_t c0 = 0; c0 < total; c0 += CAND_CAP) {
 			const uint32_t cn = total - c0 < CAND_CAP ? total - c0 : CAND_CAP;
 			const uint32_t kv = nval - (uint32_t)noff;
 			const int kvv = (int)kv, kov = (int)cand_pack(kv, nkp1, noff);
 			if (c0 + CAND_CAP + (uint32_t)lane < total) {
-				locate_cand(c0 + CAND_CAP + (uint32_t)lane, nitem, noff, nkp1);
-				nval = kp->ix.vals[nitem];
+				nval = locate_cand(c0 + CAND_CAP + (uint32_t)lane, nitem, noff, nkp1) ? nitem : kp->ix.vals[nitem];
 			}
 			STAMP(2);
 			{
@@ -2199,7 +2200,7 @@ __global__ void __launch_bounds__(256) clear_khash_payload(uint32_t *kh, uint64_
 // count does not fit 8 bits (the sector image is then not used).
 template <bool SEC>
 __global__ void __launch_bounds__(256) build_khash(const uint32_t *bstart, const int16_t *keys, uint32_t nb, uint32_t *kh,
-                                                   uint64_t lines, uint32_t *ff)
+                                                   uint64_t lines, uint32_t *ff, const uint32_t *vals)
 {
 	for (uint32_t b = blockIdx.x * 256u + threadIdx.x; b < nb; b += gridDim.x * 256u) {
 		const uint32_t first = bstart[b], n = bstart[b + 1] - first;
@@ -2224,7 +2225,9 @@ __global__ void __launch_bounds__(256) build_khash(const uint32_t *bstart, const
 			qq = m - 1;
 			while (qq >= 0 && K[qq] == k16) qq--;
 			const uint32_t bwd = (uint32_t)(m - 1 - qq);
-			const uint32_t key = (uint32_t)(uint16_t)k16 * nb + b, rx = first + (uint32_t)m, ry = fwd | (bwd << 16);
+			// vals != NULL (DevIndex::kinline): a one-item run stores the item's value
+			const uint32_t key = (uint32_t)(uint16_t)k16 * nb + b, ry = fwd | (bwd << 16);
+			const uint32_t rx = vals && fwd + bwd == 1u ? vals[first + (uint32_t)m] : first + (uint32_t)m;
 			if (key == 0xffffffffu) { ff[1] = rx; ff[2] = ry; ff[0] = 1u; continue; }
 			if (SEC && (fwd > 255u || bwd > 255u)) { atomicOr(&ff[3], 1u); continue; }
 			uint64_t L = khash_line(key, lines);
@@ -2344,6 +2347,7 @@ int svg_index_finish_device(svg_index *h)
 	h->dix.khash_ff = NULL;
 	h->dix.khash_lines = 0;
 	h->dix.khash_sec = 0;
+	h->dix.kinline = 0;
 	h->dix.ksorted = NULL;
 	{
 		// 32-byte bucket codes when the key_hi range is small enough for them to hold ordinary
@@ -2364,11 +2368,22 @@ int svg_index_finish_device(svg_index *h)
 			}
 		}
 	}
-	if (!h->dix.bcode && !svg_get_option("no_compact") && !svg_get_option("no_khash")) {
+	// the key-hash image with one-item runs inline (kinline) is the probe image of every index
+	// whose HBM holds it (C3 full: ~52 GB); without inline values it is the image of indexes the
+	// bucket code does not fit.  The bucket code, when it fits, stays for the paths that need item
+	// indices (svg_probe_keys, fragile and sublong voting)
+	const bool want_inline = !svg_get_option("no_kinline");
+	if ((!h->dix.bcode || want_inline) && !svg_get_option("no_compact") && !svg_get_option("no_khash")) {
 		// key-hash image of the probe records: 32-byte sectors of 3 entries (lines ~ items / 1.8),
 		// or 64-byte lines of 5 entries (~ items / 3) when a run count needs more than 8 bits
 		for (int sec = svg_get_option("khash64") ? 0 : 1; sec >= 0 && !h->dix.khash; sec--) {
 			const uint64_t lines = (sec ? x->items * 5 / 9 : x->items / 3) + 1024, lb = sec ? 32 : 64;
+			// an optional image: leave room (8 GB) for the vote path's chunk buffers
+			size_t fre = 0, tot = 0;
+			if (h->dix.bcode && (hipMemGetInfo(&fre, &tot) != hipSuccess || fre < lines * lb + ((size_t)8 << 30))) {
+				(void)hipGetLastError();
+				break;
+			}
 			if (dmalloc(h, &h->d_khash, lines * lb + 64) != 0) {
 				h->d_khash = NULL;
 				(void)hipGetLastError();
@@ -2384,12 +2399,13 @@ int svg_index_finish_device(svg_index *h)
 			HIPCHK(hipGetLastError());
 			blocks = ((uint64_t)x->nb + 255) / 256;
 			if (blocks > bmax) blocks = bmax;
+			const uint32_t *iv = want_inline ? (const uint32_t *)h->d_vals : NULL;
 			if (sec)
 				hipLaunchKernelGGL(build_khash<true>, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
-				                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff);
+				                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff, iv);
 			else
 				hipLaunchKernelGGL(build_khash<false>, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
-				                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff);
+				                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff, iv);
 			HIPCHK(hipGetLastError());
 			uint32_t wide = 0;
 			HIPCHK(hipMemcpyAsync(&wide, ff + 3, 4, hipMemcpyDeviceToHost, h->stream));
@@ -2404,6 +2420,7 @@ int svg_index_finish_device(svg_index *h)
 			h->dix.khash_ff = ff;
 			h->dix.khash_lines = lines;
 			h->dix.khash_sec = sec;
+			h->dix.kinline = want_inline ? 1 : 0;
 		}
 		// which buckets are sorted: there the key-hash record is cellCounts' equal-key run too
 		if (h->dix.khash && dmalloc(h, &h->d_ksorted, ((size_t)x->nb + 31) / 32 * 4 + 64) == 0) {
@@ -2462,6 +2479,11 @@ int svg_index_finish_device(svg_index *h)
 	h->stats_on = 0;
 	h->max_read_len = 256;
 	return 0;
+}
+
+int svg_probe_inline(const svg_index *h)
+{
+	return h->dix.khash && h->dix.kinline && !svg_get_option("probe_v1") ? 1 : 0;
 }
 
 static int index_open_block(const char *prefix, int block, int device, svg_index **out)
@@ -2846,6 +2868,8 @@ int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, con
 	kp.err = h->d_err;
 	kp.p = *p;
 	kp.ix = h->dix;
+	// one-hit records carry positions only when the line kernel probes the inline key-hash image
+	kp.ix.kinline = svg_probe_inline(h);
 	kp.seq1 = r1->seq; kp.off1 = r1->offsets; kp.len1 = r1->lens;
 	if (r2) { kp.seq2 = r2->seq; kp.off2 = r2->offsets; kp.len2 = r2->lens; }
 	kp.n_reads = r1->n_reads;
