@@ -94,12 +94,18 @@ __global__ void __launch_bounds__(256) gather_kernel(GParams g)
 					int off = (int)(((int64_t)step * sk) >> 16);
 					if (gap > 1) off -= off % gap - x;
 					const uint16_t pk = (uint16_t)((sk + 1) | (off << 6));
-					for (uint32_t j = 0; j < hits; j++) {
-						const uint32_t item = j < fwd ? rec.x + j : rec.x - 1u - (j - fwd);
-						const size_t o = (size_t)(s * (uint32_t)g.cap + c + j) * g.cs + k;
-						g.cand[o] = g.vals[item] - (uint32_t)off;
+					if (svg_rec_inline(g.kinline, rec.y)) {
+						// one hit, its position in the record (inline key-hash image): no vals[] load
+						const size_t o = (size_t)(s * (uint32_t)g.cap + c) * g.cs + k;
+						g.cand[o] = rec.x - (uint32_t)off;
 						g.cpk[o] = pk;
-					}
+					} else
+						for (uint32_t j = 0; j < hits; j++) {
+							const uint32_t item = j < fwd ? rec.x + j : rec.x - 1u - (j - fwd);
+							const size_t o = (size_t)(s * (uint32_t)g.cap + c + j) * g.cs + k;
+							g.cand[o] = g.vals[item] - (uint32_t)off;
+							g.cpk[o] = pk;
+						}
 					c += hits;
 				}
 			}
@@ -111,6 +117,15 @@ __global__ void __launch_bounds__(256) gather_kernel(GParams g)
 // ---------------------------------------------------------------------------------------------
 // lane kernel
 // ---------------------------------------------------------------------------------------------
+struct LParams;
+// a candidate's position: the record's own word for an inline one-hit probe, else vals[item]; the
+// load's index is 0 for inline ones, so a load the compiler speculates stays inside vals[]
+template <class P>
+__device__ __forceinline__ uint32_t lval(const P &lp, bool inl, uint32_t it)
+{
+	const uint32_t v = lp.vals[inl ? 0u : it];
+	return inl ? it : v;
+}
 struct LParams {
 	const uint32_t *cand;
 	const uint16_t *cpk;
@@ -682,15 +697,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 				return svg_rec_inline(lp.kinline, ry[0]);   // item is the position itself
 			};
 			uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0, it = 0, pkn = 0;
-			if (0 < mycnt) { q0 = next(it, pkn) ? it : lp.vals[it]; k0 = pkn; }
-			if (1 < mycnt) { q1 = next(it, pkn) ? it : lp.vals[it]; k1 = pkn; }
-			if (2 < mycnt) { q2 = next(it, pkn) ? it : lp.vals[it]; k2 = pkn; }
-			if (3 < mycnt) { q3 = next(it, pkn) ? it : lp.vals[it]; k3 = pkn; }
+			if (0 < mycnt) { q0 = lval(lp, next(it, pkn), it); k0 = pkn; }
+			if (1 < mycnt) { q1 = lval(lp, next(it, pkn), it); k1 = pkn; }
+			if (2 < mycnt) { q2 = lval(lp, next(it, pkn), it); k2 = pkn; }
+			if (3 < mycnt) { q3 = lval(lp, next(it, pkn), it); k3 = pkn; }
 			for (int j = 0; j < mc; j++) {
 				const uint32_t val = q0, pk = k0;
 				q0 = q1; q1 = q2; q2 = q3;
 				k0 = k1; k1 = k2; k2 = k3;
-				if (j + 4 < mycnt) { q3 = next(it, pkn) ? it : lp.vals[it]; k3 = pkn; }
+				if (j + 4 < mycnt) { q3 = lval(lp, next(it, pkn), it); k3 = pkn; }
 				if (j < mycnt && !L.dfr) L.template vote<0>(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b, lp.gap);
 			}
 			}
@@ -1113,15 +1128,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 					return svg_rec_inline(lp.kinline, ry[0]);   // item is the position itself
 				};
 				uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0, it = 0, pkn = 0;
-				if (0 < mycnt) { q0 = next(it, pkn) ? it : lp.vals[it]; k0 = pkn; }
-				if (1 < mycnt) { q1 = next(it, pkn) ? it : lp.vals[it]; k1 = pkn; }
-				if (2 < mycnt) { q2 = next(it, pkn) ? it : lp.vals[it]; k2 = pkn; }
-				if (3 < mycnt) { q3 = next(it, pkn) ? it : lp.vals[it]; k3 = pkn; }
+				if (0 < mycnt) { q0 = lval(lp, next(it, pkn), it); k0 = pkn; }
+				if (1 < mycnt) { q1 = lval(lp, next(it, pkn), it); k1 = pkn; }
+				if (2 < mycnt) { q2 = lval(lp, next(it, pkn), it); k2 = pkn; }
+				if (3 < mycnt) { q3 = lval(lp, next(it, pkn), it); k3 = pkn; }
 				for (int j = 0; j < mc; j++) {
 					const uint32_t val = q0, pk = k0;
 					q0 = q1; q1 = q2; q2 = q3;
 					k0 = k1; k1 = k2; k2 = k3;
-					if (j + 4 < mycnt) { q3 = next(it, pkn) ? it : lp.vals[it]; k3 = pkn; }
+					if (j + 4 < mycnt) { q3 = lval(lp, next(it, pkn), it); k3 = pkn; }
 					if (j < mycnt && !L.dfr) L.template vote<E>(st, val - (pk >> 6), (int)(pk & 63u), (int)(pk >> 6), high_b[E], lp.gap);
 				}
 			};

@@ -579,13 +579,21 @@ struct Wave {
 		};
 		uint32_t nitem = 0, nval = 0;
 		int noff = 0, nkp1 = 0;
-		if ((uint32_t)lane < total) nval = locate_cand((uint32_t)lane, nitem, noff, nkp1) ? nitem : kp->ix.vals[nitem];
+		// (an inline one-hit record holds the position: the load index is 0 then, so a speculated
+		// load stays inside vals[])
+		if ((uint32_t)lane < total) {
+			const bool inl = locate_cand((uint32_t)lane, nitem, noff, nkp1);
+			const uint32_t v = kp->ix.vals[inl ? 0u : nitem];
+			nval = inl ? nitem : v;
+		}
 		for (uint32_t c0 = 0; c0 < total; c0 += CAND_CAP) {
 			const uint32_t cn = total - c0 < CAND_CAP ? total - c0 : CAND_CAP;
 			const uint32_t kv = nval - (uint32_t)noff;
 			const int kvv = (int)kv, kov = (int)cand_pack(kv, nkp1, noff);
 			if (c0 + CAND_CAP + (uint32_t)lane < total) {
-				nval = locate_cand(c0 + CAND_CAP + (uint32_t)lane, nitem, noff, nkp1) ? nitem : kp->ix.vals[nitem];
+				const bool inl = locate_cand(c0 + CAND_CAP + (uint32_t)lane, nitem, noff, nkp1);
+				const uint32_t v = kp->ix.vals[inl ? 0u : nitem];
+				nval = inl ? nitem : v;
 			}
 			STAMP(2);
 			{
