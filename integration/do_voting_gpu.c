@@ -34,6 +34,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
+#include <ctype.h>
 #include "subread.h"
 #include "core.h"
 #include "core-indel.h"
@@ -539,7 +540,307 @@ void svg_sam_finish(void)
 	svg_sam = NULL;
 }
 
+/*
+ * The reads of a chunk, parsed once (drop-in build).  The reference parses every read of a chunk
+ * in every pass over it -- the voting run of each index block and iteration two -- one read at a
+ * time under the input lock (fetch_next_read_pair, core.c:1121-1211), so with the vote on the GPU
+ * the serial parse is what iteration two waits on.  fetch_next_read_pair_svg is that function
+ * (same parser calls, same trimming, secondary-read skip, read numbering and -S reversal) with a
+ * cache: the first pass over a chunk parses and keeps each read as it hands it out; a later pass
+ * over the same chunk (the reference rewinds to the chunk start it saved,
+ * current_circle_start_position_file1, core.c:3487-3490,3523-3529) is served from the cache in the
+ * same order, and the input file is left where the rewind put it -- the reference seeks to the
+ * saved chunk end itself afterwards (go_chunk_nextchunk, core.c:3531-3537).  Colour space is never
+ * cached.
+ */
+#include "input-files.h"
+#include "gene-algorithms.h"
+
+typedef struct {
+	char *buf;                         /* name\0 text\0 qual\0 per read end, back to back */
+	uint64_t len, cap;
+	uint64_t *at;                      /* read r, end e: offset at[r * 2 + e] */
+	int *rl;                           /* read lengths, [r * 2 + e] */
+	uint64_t n, ncap;
+	int complete;                      /* the parse pass reached the chunk's end */
+	gene_inputfile_position_t start1;  /* the chunk's start (current_circle_start_position_file1) */
+} svg_read_cache;
+
+static svg_read_cache svg_rc;
+static int svg_pass_cached;            /* the current pass is served from svg_rc */
+
+static int rc_put(int e, const char *name, const char *text, const char *qual, int rl)
+{
+	const size_t nn = strlen(name) + 1, tn = (size_t)rl + 1, qn = qual ? strlen(qual) + 1 : 1;
+	if (svg_rc.len + nn + tn + qn > svg_rc.cap) {
+		uint64_t nc = (svg_rc.cap + nn + tn + qn) * 2 + (1 << 20);
+		char *nb = realloc(svg_rc.buf, nc);
+		if (!nb) return -1;
+		svg_rc.buf = nb;
+		svg_rc.cap = nc;
+	}
+	svg_rc.at[svg_rc.n * 2 + e] = svg_rc.len;
+	svg_rc.rl[svg_rc.n * 2 + e] = rl;
+	memcpy(svg_rc.buf + svg_rc.len, name, nn); svg_rc.len += nn;
+	memcpy(svg_rc.buf + svg_rc.len, text, tn); svg_rc.len += tn;
+	if (qual) memcpy(svg_rc.buf + svg_rc.len, qual, qn); else svg_rc.buf[svg_rc.len] = 0;
+	svg_rc.len += qn;
+	return 0;
+}
+
+static void rc_get(uint64_t r, int e, char *name, char *text, char *qual, int *rl)
+{
+	const char *p = svg_rc.buf + svg_rc.at[r * 2 + e];
+	const size_t nn = strlen(p) + 1;
+	strcpy(name, p);
+	*rl = svg_rc.rl[r * 2 + e];
+	memcpy(text, p + nn, (size_t)*rl + 1);
+	if (qual) strcpy(qual, p + nn + *rl + 1);
+}
+
+int fetch_next_read_pair_svg(global_context_t *gc, thread_context_t *tc, gene_input_t *ginp1, gene_input_t *ginp2,
+                             int *read_len_1, int *read_len_2, char *read_name_1, char *read_name_2, char *read_text_1,
+                             char *read_text_2, char *qual_text_1, char *qual_text_2, int remove_color_head,
+                             subread_read_number_t *read_no_in_chunk)
+{
+	(void)tc;
+	int rl1 = 0, rl2 = 0, is_second_R1, is_second_R2;
+	subread_read_number_t this_number = -1;
+	const int cacheable = gc->config.space_type != GENE_SPACE_COLOR && gc->input_reads.first_read_file.file_type != GENE_INPUT_BCL;
+	if (!svg_pass_cached) {
+		geinput_preload_buffer(ginp1, &gc->input_reads.input_lock);
+		if (ginp2) geinput_preload_buffer(ginp2, &gc->input_reads.input_lock);
+	}
+	subread_lock_occupy(&gc->input_reads.input_lock);
+	if (gc->running_processed_reads_in_chunk == 0) {
+		/* a pass begins: the same chunk as the complete cache -> serve it; else parse, refill */
+		svg_pass_cached = cacheable && svg_rc.complete &&
+		                  !memcmp(&svg_rc.start1, &gc->current_circle_start_position_file1, sizeof svg_rc.start1);
+		if (!svg_pass_cached && cacheable) {
+			svg_rc.n = svg_rc.len = 0;
+			svg_rc.complete = 0;
+			memcpy(&svg_rc.start1, &gc->current_circle_start_position_file1, sizeof svg_rc.start1);
+		}
+	}
+	if (svg_pass_cached) {
+		if (gc->running_processed_reads_in_chunk < (subread_read_number_t)svg_rc.n) {
+			this_number = gc->running_processed_reads_in_chunk++;
+			subread_lock_release(&gc->input_reads.input_lock);
+			rc_get((uint64_t)this_number, 0, read_name_1, read_text_1, qual_text_1, read_len_1);
+			if (ginp2) rc_get((uint64_t)this_number, 1, read_name_2, read_text_2, qual_text_2, read_len_2);
+			*read_no_in_chunk = this_number;
+			return 0;
+		}
+		subread_lock_release(&gc->input_reads.input_lock);
+		*read_no_in_chunk = -1;
+		return 1;
+	}
+	if (gc->running_processed_reads_in_chunk < gc->config.reads_per_chunk) {
+		do {
+			is_second_R1 = 0; is_second_R2 = 0;
+			rl1 = geinput_next_read_trim(ginp1, read_name_1, read_text_1, qual_text_1, gc->config.read_trim_5,
+			                             gc->config.read_trim_3, &is_second_R1);
+			if (gc->config.space_type == GENE_SPACE_COLOR && remove_color_head && isalpha(read_text_1[0])) {
+				int xk1;
+				for (xk1 = 2; read_text_1[xk1]; xk1++) read_text_1[xk1 - 2] = read_text_1[xk1];
+				read_text_1[xk1 - 2] = 0;
+			}
+			if (ginp2) {
+				rl2 = geinput_next_read_trim(ginp2, read_name_2, read_text_2, qual_text_2, gc->config.read_trim_5,
+				                             gc->config.read_trim_3, &is_second_R2);
+				if (gc->config.space_type == GENE_SPACE_COLOR && remove_color_head && isalpha(read_text_2[0])) {
+					int xk1;
+					for (xk1 = 2; read_text_2[xk1]; xk1++) read_text_2[xk1 - 2] = read_text_2[xk1];
+					read_text_2[xk1 - 2] = 0;
+				}
+			}
+			if (rl1 <= 0 || (rl2 <= 0 && ginp2)) break;
+		} while (is_second_R1 || is_second_R2);
+		if (rl1 > 0 || (rl2 > 0 && ginp2)) this_number = gc->running_processed_reads_in_chunk++;
+	}
+	int ok = this_number >= 0 && rl1 > 0 && (rl2 > 0 || !ginp2);
+	if (gc->config.space_type == GENE_SPACE_COLOR) { rl1 -= 1; rl2 -= 1; }
+	if (ok && gc->config.space_type != GENE_SPACE_COLOR) {
+		if (gc->config.is_first_read_reversed) {
+			reverse_read(read_text_1, rl1, gc->config.space_type);
+			if (qual_text_1) reverse_quality(qual_text_1, rl1);
+		}
+		if (ginp2 && gc->config.is_second_read_reversed) {
+			reverse_read(read_text_2, rl2, gc->config.space_type);
+			if (qual_text_2) reverse_quality(qual_text_2, rl2);
+		}
+		/* keep the read as handed out (the cache is filled in read-number order under the lock) */
+		if (cacheable && (uint64_t)this_number == svg_rc.n) {
+			if (svg_rc.n == svg_rc.ncap) {
+				svg_rc.ncap = svg_rc.ncap ? 2 * svg_rc.ncap : 1 << 16;
+				svg_rc.at = realloc(svg_rc.at, svg_rc.ncap * 2 * sizeof(uint64_t));
+				svg_rc.rl = realloc(svg_rc.rl, svg_rc.ncap * 2 * sizeof(int));
+			}
+			if (!svg_rc.at || !svg_rc.rl || rc_put(0, read_name_1, read_text_1, qual_text_1, rl1) ||
+			    (ginp2 && rc_put(1, read_name_2, read_text_2, qual_text_2, rl2)))
+				svg_rc.complete = -1;   /* out of memory: never served */
+			else svg_rc.n++;
+		}
+	} else if (this_number < 0 && cacheable && svg_rc.complete == 0) svg_rc.complete = 1;   /* the pass ended */
+	subread_lock_release(&gc->input_reads.input_lock);
+	if (ginp2 && rl1 * rl2 <= 0 && (rl1 > 0 || rl2 > 0)) {
+		if (!gc->input_reads.is_internal_error) SUBREADprintf("\nERROR: two input files have different amounts of reads.\n\n");
+		gc->input_reads.is_internal_error = 1;
+		*read_no_in_chunk = -1;
+		return 1;
+	} else if (rl1 > 0 && (rl2 > 0 || !ginp2) && this_number >= 0) {
+		if (gc->config.space_type == GENE_SPACE_COLOR) {
+			if (gc->config.is_first_read_reversed) {
+				reverse_read(read_text_1, rl1, gc->config.space_type);
+				if (qual_text_1) reverse_quality(qual_text_1, rl1);
+			}
+			if (ginp2 && gc->config.is_second_read_reversed) {
+				reverse_read(read_text_2, rl2, gc->config.space_type);
+				if (qual_text_2) reverse_quality(qual_text_2, rl2);
+			}
+		}
+		*read_no_in_chunk = this_number;
+		*read_len_1 = rl1;
+		if (ginp2) *read_len_2 = rl2;
+		return 0;
+	}
+	*read_no_in_chunk = -1;
+	return 1;
+}
+
 #ifdef SVG_DROPIN_DO_VOTING
+/*
+ * Harness build (linked with -Wl,--wrap=gehash_load,... in oracle/Makefile).  The reference's CPU hash table (gehash_load, sorted-hashtable.c:1390; read_chunk_circles loads
+ * one block at a time, core.c:3576) is what its own voting probes; with the vote on the GPU
+ * (svg_index_open holds every block in HBM) nothing of the align / subjunc paths reads it.  The
+ * drop-in therefore records the file and its index_gap (the one field the reference reads outside
+ * the table's own functions, core.c:3088, core-junction.c:5172) and loads the table only if a
+ * table function is ever called on it (long-indel reassembly, methylation mode).
+ */
+#include "sorted-hashtable.h"
+
+#define SVG_LAZY_MAX 8
+static struct { gehash_t *t; char fname[MAX_FILE_NAME_LENGTH + 40]; int loaded; } svg_lazy[SVG_LAZY_MAX];
+static pthread_mutex_t svg_lazy_mu = PTHREAD_MUTEX_INITIALIZER;
+
+int __real_gehash_load(gehash_t *the_table, const char fname[]);
+
+static int tab_index_gap(const char *fname, int *gap, int *padding)
+{
+	FILE *fp = fopen(fname, "rb");
+	char magic[8];
+	if (!fp) return -1;
+	int rc = -1;
+	if (fread(magic, 1, 8, fp) == 8 && !memcmp(magic, "2subindx", 8))
+		for (;;) {
+			short k, l, v = 0;
+			if (fread(&k, 2, 1, fp) != 1) break;
+			if (!k) { rc = 0; break; }
+			if (fread(&l, 2, 1, fp) != 1) break;
+			if (l == 2 && fread(&v, 2, 1, fp) == 1) {
+				if (k == 0x0101) *gap = v;
+				else if (k == 0x0102) *padding = v;
+			} else if (fseek(fp, l, SEEK_CUR)) break;
+		}
+	fclose(fp);
+	return rc;
+}
+
+int __wrap_gehash_load(gehash_t *t, const char fname[])
+{
+	int gap = 0, padding = 0, i;
+	if (tab_index_gap(fname, &gap, &padding) || gap < 1) return __real_gehash_load(t, fname);
+	pthread_mutex_lock(&svg_lazy_mu);
+	for (i = 0; i < SVG_LAZY_MAX && svg_lazy[i].t && svg_lazy[i].t != t; i++) ;
+	if (i == SVG_LAZY_MAX) { pthread_mutex_unlock(&svg_lazy_mu); return __real_gehash_load(t, fname); }
+	svg_lazy[i].t = t;
+	snprintf(svg_lazy[i].fname, sizeof svg_lazy[i].fname, "%s", fname);
+	svg_lazy[i].loaded = 0;
+	pthread_mutex_unlock(&svg_lazy_mu);
+	/* an empty table gehash_destory frees nothing from (core.c:3609) */
+	memset(t->malloc_ptr, 0, sizeof(t->malloc_ptr));
+	t->buckets = NULL;
+	t->buckets_number = 0;
+	t->current_items = 0;
+	t->index_gap = gap;
+	t->padding = padding;
+	t->is_small_table = 0;
+	t->free_item_only = 0;
+	return 0;
+}
+
+static void lazy_ensure(gehash_t *t)
+{
+	pthread_mutex_lock(&svg_lazy_mu);
+	for (int i = 0; i < SVG_LAZY_MAX; i++)
+		if (svg_lazy[i].t == t && !svg_lazy[i].loaded) {
+			svg_lazy[i].loaded = 1;
+			if (__real_gehash_load(t, svg_lazy[i].fname)) SUBREADprintf("lazy gehash_load of %s failed\n", svg_lazy[i].fname);
+		}
+	pthread_mutex_unlock(&svg_lazy_mu);
+}
+
+size_t __real_gehash_go_q(gehash_t *the_table, gehash_key_t raw_key, int offset, int read_len, int is_reversed,
+                          gene_vote_t *vote, int indel_tolerance, int subread_number, unsigned int low_border,
+                          unsigned int high_border);
+size_t __wrap_gehash_go_q(gehash_t *the_table, gehash_key_t raw_key, int offset, int read_len, int is_reversed,
+                          gene_vote_t *vote, int indel_tolerance, int subread_number, unsigned int low_border,
+                          unsigned int high_border)
+{
+	lazy_ensure(the_table);
+	return __real_gehash_go_q(the_table, raw_key, offset, read_len, is_reversed, vote, indel_tolerance, subread_number,
+	                          low_border, high_border);
+}
+
+size_t __real_gehash_go_X(gehash_t *the_table, gehash_key_t raw_key, int offset, int read_len, int is_reversed,
+                          gene_vote_t *vote, int indel_tolerance, int subread_number, unsigned int low_border,
+                          unsigned int high_border, int run_round, unsigned int *shift_indel_locs, unsigned int *shift_indel_NO);
+size_t __wrap_gehash_go_X(gehash_t *the_table, gehash_key_t raw_key, int offset, int read_len, int is_reversed,
+                          gene_vote_t *vote, int indel_tolerance, int subread_number, unsigned int low_border,
+                          unsigned int high_border, int run_round, unsigned int *shift_indel_locs, unsigned int *shift_indel_NO)
+{
+	lazy_ensure(the_table);
+	return __real_gehash_go_X(the_table, raw_key, offset, read_len, is_reversed, vote, indel_tolerance, subread_number,
+	                          low_border, high_border, run_round, shift_indel_locs, shift_indel_NO);
+}
+
+size_t __real_gehash_go_q_CtoT(gehash_t *the_table, gehash_key_t key, int offset, int read_len, int is_reversed,
+                               gene_vote_t *vote, gene_vote_number_t weight, int max_match_number, int indel_tolerance,
+                               int subread_number, int max_error_bases, unsigned int low_border, unsigned int high_border);
+size_t __wrap_gehash_go_q_CtoT(gehash_t *the_table, gehash_key_t key, int offset, int read_len, int is_reversed,
+                               gene_vote_t *vote, gene_vote_number_t weight, int max_match_number, int indel_tolerance,
+                               int subread_number, int max_error_bases, unsigned int low_border, unsigned int high_border)
+{
+	lazy_ensure(the_table);
+	return __real_gehash_go_q_CtoT(the_table, key, offset, read_len, is_reversed, vote, weight, max_match_number,
+	                               indel_tolerance, subread_number, max_error_bases, low_border, high_border);
+}
+
+size_t __real_gehash_go_q_tolerable(gehash_t *the_table, gehash_key_t key, int offset, int read_len, int is_reversed,
+                                    gene_vote_t *vote, gene_vote_number_t weight, gene_quality_score_t quality,
+                                    int max_match_number, int indel_tolerance, int subread_number, int max_error_bases,
+                                    int subread_len, unsigned int low_border, unsigned int high_border);
+size_t __wrap_gehash_go_q_tolerable(gehash_t *the_table, gehash_key_t key, int offset, int read_len, int is_reversed,
+                                    gene_vote_t *vote, gene_vote_number_t weight, gene_quality_score_t quality,
+                                    int max_match_number, int indel_tolerance, int subread_number, int max_error_bases,
+                                    int subread_len, unsigned int low_border, unsigned int high_border)
+{
+	lazy_ensure(the_table);
+	return __real_gehash_go_q_tolerable(the_table, key, offset, read_len, is_reversed, vote, weight, quality,
+	                                    max_match_number, indel_tolerance, subread_number, max_error_bases, subread_len,
+	                                    low_border, high_border);
+}
+
+/* harness build: core.o's fetch_next_read_pair is weak, every call site lands here */
+int fetch_next_read_pair(global_context_t *gc, thread_context_t *tc, gene_input_t *ginp1, gene_input_t *ginp2,
+                         int *read_len_1, int *read_len_2, char *read_name_1, char *read_name_2, char *read_text_1,
+                         char *read_text_2, char *qual_text_1, char *qual_text_2, int remove_color_head,
+                         subread_read_number_t *read_no_in_chunk)
+{
+	return fetch_next_read_pair_svg(gc, tc, ginp1, ginp2, read_len_1, read_len_2, read_name_1, read_name_2, read_text_1,
+	                                read_text_2, qual_text_1, qual_text_2, remove_color_head, read_no_in_chunk);
+}
+
 /* harness build: the reference's core.o is compiled with add_buffered_fragment weak (below) */
 void add_buffered_fragment(global_context_t *gc, thread_context_t *tc, subread_read_number_t pair_number,
 	char *read_name1, unsigned int flags1, char *chro_name1, unsigned int chro_position1, int mapping_quality1, char *cigar1,

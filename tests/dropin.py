@@ -18,7 +18,7 @@ import numpy as np
 
 from tests.common import ROOT
 
-REFBIN = os.path.join(ROOT, "oracle", "_ref")
+REFBIN = os.environ.get("SVG_TEST_REFBIN") or os.path.join(ROOT, "oracle", "_ref")
 
 
 def binary(program, kind):
