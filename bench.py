@@ -273,24 +273,31 @@ def main():
     log("[bench] packed host path: %.1f Mreads/s (%.1f ms/step; steps %s ms)" % (
         n * ends * args.steps / elapsed / 1e6, elapsed / args.steps * 1e3, step_ms))
 
-    # ---- secondary: the same kernels with reads and records already in HBM
-    def upload(b):
-        return (torch.from_numpy(b.seq).to(dev), torch.from_numpy(b.offsets.view(np.int64)).to(dev),
-                torch.from_numpy(b.lens.view(np.int16)).to(dev))
-    d1 = upload(rb)
-    d2 = upload(rb2) if rb2 is not None else None
+    # ---- secondary: the same kernels with the same 2-bit packed reads and the records already in
+    # HBM (svg_vote_batch_packed_device: no PCIe, no host expansion)
+    from subread_amd.abi import SvgPackedReads
+
+    def upload_packed(pk):
+        t = [torch.from_numpy(pk.bases.view(np.uint8)).to(dev), torch.from_numpy(pk.lens.view(np.uint8)).to(dev)]
+        if pk.xmask is not None:
+            t.append(torch.from_numpy(pk.xmask.view(np.uint8)).to(dev))
+        q = SvgPackedReads()
+        q.bases, q.lens = t[0].data_ptr(), t[1].data_ptr()
+        q.xmask = t[2].data_ptr() if pk.xmask is not None else None
+        q.starts, q.stride, q.n_reads = None, pk.stride, n
+        return q, t
+    q1, t1k = upload_packed(pk1)
+    q2, t2k = upload_packed(pk2) if pk2 is not None else (None, None)
     d_out = torch.empty(n * MAPPING_DTYPE.itemsize * mb * ends, dtype=torch.uint8, device=dev)
     d_jout = torch.empty(n * ends * mb * 16, dtype=torch.uint8, device=dev) if sj else None
     d_bm = torch.empty(n * ends * BIG_MARGIN_WORDS * 2, dtype=torch.uint8, device=dev) if sj else None
     ix.set_max_read_length(int(os.environ.get("SVG_BENCH_MAXLEN", L)))
     # the handle's own stream: a stream created now could share a hardware queue with the
     # library's second stream (HIP deals streams round-robin onto GPU_MAX_HW_QUEUES = 4 queues)
-    r1 = (d1[0].data_ptr(), d1[1].data_ptr(), d1[2].data_ptr(), n)
-    r2 = (d2[0].data_ptr(), d2[1].data_ptr(), d2[2].data_ptr(), n) if d2 is not None else None
 
     def dev_step():
-        ix.vote_device(p, r1, r2, d_out.data_ptr(), d_jout.data_ptr() if d_jout is not None else None,
-                       d_bm.data_ptr() if d_bm is not None else None, stream=None)
+        ix.vote_packed_device(p, q1, q2, d_out.data_ptr(), d_jout.data_ptr() if d_jout is not None else None,
+                              d_bm.data_ptr() if d_bm is not None else None)
     dev_step()
     torch.cuda.synchronize()
     ds = max(1, args.device_steps)
@@ -305,7 +312,8 @@ def main():
     ix.device_status()
     device_path = {"value": round(n * ends * ds / td / 1e6, 3), "unit": "Mreads/s", "steps": ds,
                    "ms_per_step": round(td / ds * 1e3, 3),
-                   "entry": "svg_vote_batch_device: reads and records resident in HBM (no PCIe)"}
+                   "entry": "svg_vote_batch_packed_device: the same 2-bit packed reads and the records resident in HBM "
+                            "(no PCIe, no host expansion)"}
 
     # algorithmic bytes from the kernels' own counters, outside the timed region
     ix.set_stats(True)

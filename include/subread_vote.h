@@ -375,8 +375,8 @@ int  svg_cpulist_parse(const char *list, uint8_t *mask, int max);
  *                               wave kernel, 3 no lane kernels (wave kernel only)
  *   lane_unfused, lane_bin      separate gather kernel; 2 = no count bins
  *   lane_cap, lane_pe_cap, lane_pairs, lane_mid   lane-path capacities (candidates, pairs)
- *   no_bcode, no_khash, khash64, no_bline, no_compact, no_kinline, probe_v1, no_window,
- *   probe_colmajor              probe images / probe kernel variants picked at index load
+ *   no_bcode, no_khash, khash64, no_bline, no_compact, kinline, khash_probe, probe_v1,
+ *   no_window, probe_colmajor   probe images / probe kernel variants picked at index load
  *   wave_cap                    resident wave-kernel blocks per CU beside the next chunk
  *   keys_literal, long_probes   svg_probe_keys / svg_long_vote_batch variants
  *   debug, pipe_debug, long_debug  diagnostics on stderr

@@ -43,7 +43,7 @@ static struct { const char *name; volatile int64_t value; } g_opts[] = {
 	{"host_threads", 0}, {"host_sub", 0}, {"chunk", 0}, {"overlap", -1},
 	{"lane", 0}, {"lane_unfused", 0}, {"lane_bin", 0}, {"lane_cap", 0}, {"lane_pe_cap", 0},
 	{"lane_pairs", 0}, {"lane_mid", 0},
-	{"no_bcode", 0}, {"no_khash", 0}, {"khash64", 0}, {"no_bline", 0}, {"no_compact", 0}, {"no_kinline", 0},
+	{"no_bcode", 0}, {"no_khash", 0}, {"khash64", 0}, {"no_bline", 0}, {"no_compact", 0}, {"kinline", 0}, {"khash_probe", 0},
 	{"probe_v1", 0}, {"no_window", 0}, {"probe_colmajor", 0},
 	{"wave_cap", -1}, {"keys_literal", 0}, {"long_probes", 0},
 	{"debug", 0}, {"pipe_debug", 0}, {"long_debug", 0},

@@ -2376,12 +2376,17 @@ int svg_index_finish_device(svg_index *h)
 			}
 		}
 	}
-	// the key-hash image with one-item runs inline (kinline) is the probe image of every index
-	// whose HBM holds it (C3 full: ~52 GB); without inline values it is the image of indexes the
-	// bucket code does not fit.  The bucket code, when it fits, stays for the paths that need item
-	// indices (svg_probe_keys, fragile and sublong voting)
-	const bool want_inline = !svg_get_option("no_kinline");
-	if ((!h->dix.bcode || want_inline) && !svg_get_option("no_compact") && !svg_get_option("no_khash")) {
+	// the key-hash image: the probe image of indexes the bucket code does not fit (gapped, small);
+	// beside the code on request (options kinline / khash_probe; C3 full: ~52 GB).  Measured at C3
+	// (profiles/r04/bench_c3_*.json): the key-hash probe kernel is 18% faster than the code's, but
+	// the lane / wave kernels slow by more than that (113.5 vs 110.6 ms/step), so the code stays the
+	// default probe image of -F -B indexes.  The code, when it fits, also serves the paths that need
+	// item indices (svg_probe_keys, fragile and sublong voting)
+	// option kinline: one-hit runs inline; option khash_probe: the key-hash image beside the bucket
+	// code, probed instead of it (A/B of the probe images)
+	const bool want_inline = svg_get_option("kinline") != 0;
+	const bool want_khash = !h->dix.bcode || want_inline || svg_get_option("khash_probe") != 0;
+	if (want_khash && !svg_get_option("no_compact") && !svg_get_option("no_khash")) {
 		// key-hash image of the probe records: 32-byte sectors of 3 entries (lines ~ items / 1.8),
 		// or 64-byte lines of 5 entries (~ items / 3) when a run count needs more than 8 bits
 		for (int sec = svg_get_option("khash64") ? 0 : 1; sec >= 0 && !h->dix.khash; sec--) {

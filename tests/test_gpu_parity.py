@@ -171,10 +171,11 @@ def test_gpu_pipelines_match_oracle(mode, gpu_indexes, index_cache, svgopt):
 
 
 def test_gpu_probe_images_match_oracle(svgopt):
-    """The probe images picked at index load: the key-hash of probe records with one-hit runs
-    inline (default: 32-byte sectors, the hit's position in place of its item; no_kinline: items
-    only), 32-byte unary bucket codes (no_kinline: the probe image of -F -B indexes, and the
-    image the side paths read), the key-hash without the code (no_bcode) or in 64-byte lines (+ khash64),
+    """The probe images picked at index load: 32-byte unary bucket codes (default for -F -B
+    indexes), the key-hash of probe records beside them (khash_probe) or with one-hit runs inline
+    (kinline: the hit's position in place of its item), the key-hash alone in 32-byte sectors
+    (no_bcode; the default of every index the code does not fit, e.g. gapped ones; + kinline) or
+    64-byte lines (+ khash64),
     64-byte bucket lines (+ no_khash), 16-bucket
     groups + u8 keys (+ no_bline), plain bounds + i16 keys (no_compact), and the
     one-kernel probe of the previous build (probe_v1).  The genome carries repeat families, so
@@ -187,8 +188,8 @@ def test_gpu_probe_images_match_oracle(svgopt):
     r1 = simulate_reads(g, 40000, 100, seed=5, sub=0.01, indel=0.001)
     p = default_params(PROGRAM_ALIGN, False)
     want = None
-    for env in ({}, {"no_kinline": 1}, {"no_bcode": 1}, {"no_bcode": 1, "no_kinline": 1}, {"no_bcode": 1, "khash64": 1},
-                {"no_bcode": 1, "no_khash": 1},
+    for env in ({}, {"kinline": 1}, {"khash_probe": 1}, {"no_bcode": 1}, {"no_bcode": 1, "kinline": 1},
+                {"no_bcode": 1, "khash64": 1}, {"no_bcode": 1, "khash64": 1, "kinline": 1}, {"no_bcode": 1, "no_khash": 1},
                 {"no_bcode": 1, "no_khash": 1, "no_bline": 1}, {"no_compact": 1},
                 {"probe_v1": 1}, {"probe_v1": 1, "no_bcode": 1}):
         for k, v in env.items():

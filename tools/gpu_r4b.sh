@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box, round 4 call B: the GPU test suite (inline key-hash image now the default probe image),
-# then C3 with it (the bench line + kernel record) and without it (no_kinline=1), then the
+# then C3 with it (the bench line + kernel record) and without it (the option then named no_kinline; now kinline=1 is opt-in), then the
 # serialised trace + HIP-event kernel record of the metric's path
 mkdir -p gpurun_out/r4b
 timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4b/gpu_tests.log 2>&1 && \
