@@ -307,6 +307,10 @@ static svg_fragile_result svg_frag;
 
 /* the chunk of the current run, shared by the run's threads (read and voted by thread 0) */
 static svg_chunk_reads svg_chunk;
+/* SVG_REF_TIMING=1: the voting phase's own split, cumulative over runs, printed by svg_sam_finish
+ * beside the reference's clocks (oracle/ref_dump_hook.c): reading the chunk, the vote call
+ * (packing + GPU), fragile voting, and the per-read tail (slowest thread of each run) */
+static double svg_t_read, svg_t_vote, svg_t_frag, svg_t_tail;
 static uint64_t *svg_win;       /* svg_win[r] .. svg_win[r+1]: read r's fragile windows in this block */
 
 /* thread 0 (or the only thread): the chunk's reads, the GPU vote (first block's run: every block),
@@ -316,12 +320,17 @@ static int vote_stage(global_context_t *gc, thread_context_t *tc)
 	int ends = 1 + gc->input_reads.is_paired_end_reads, rc;
 	memset(&svg_chunk, 0, sizeof svg_chunk);
 	svg_chunk_reads *c = &svg_chunk;
+	double t0 = miltime();
 	rc = read_chunk(gc, tc, ends, c);
+	svg_t_read += miltime() - t0;
 	/* a multi-block index: the library votes every block (all resident in HBM) in the first
 	 * block's run of read_chunk_circles (core.c:3567-3613); the later runs re-read the chunk
 	 * for the per-block host work */
 	if (!rc && c->n && gc->current_index_block_number == 0) {
+		t0 = miltime();
 		rc = vote_chunk(gc, ends, c);
+		svg_t_vote += miltime() - t0;
+		t0 = miltime();
 		/* fragile junction voting of every block, on the GPU (subjunc reads > 160 bp) */
 		svg_fragile_free(&svg_frag);
 		if (!rc && gc->config.do_breakpoint_detection) {
@@ -331,6 +340,7 @@ static int vote_stage(global_context_t *gc, thread_context_t *tc)
 			rc = svg_fragile_batch(svg_ix, &p, &a1, ends == 2 ? &a2 : NULL, &svg_frag);
 			if (rc) SUBREADprintf("svg_fragile_batch: %s\n", svg_last_error());
 		}
+		svg_t_frag += miltime() - t0;
 	}
 	/* this block's fragile windows are in (read, strand, end, window) order: read r's are
 	 * svg_win[r] .. svg_win[r+1]-1 */
@@ -423,7 +433,9 @@ static void run_end(global_context_t *gc)
 int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
 {
 	int rc = vote_stage(gc, tc);
+	const double t0 = miltime();
 	if (!rc) tail_stage(gc, tc, 0, svg_chunk.n);
+	svg_t_tail += miltime() - t0;
 	run_end(gc);
 	return rc ? 1 : 0;
 }
@@ -447,11 +459,13 @@ int do_voting_gpu_mt(global_context_t *gc, thread_context_t *tc, int nthreads)
 	const int tid = tc->thread_id;
 	if (tid == 0) svg_run_rc = vote_stage(gc, tc);
 	pthread_barrier_wait(&svg_bar);
+	const double t0 = miltime();
 	if (!svg_run_rc) {
 		const uint64_t n = svg_chunk.n;
 		tail_stage(gc, tc, n * (uint64_t)tid / (uint64_t)nthreads, n * (uint64_t)(tid + 1) / (uint64_t)nthreads);
 	}
 	pthread_barrier_wait(&svg_bar);
+	if (tid == 0) svg_t_tail += miltime() - t0;
 	const int rc = svg_run_rc;
 	if (tid == 0) run_end(gc);
 	return rc ? 1 : 0;
@@ -538,6 +552,9 @@ void svg_sam_finish(void)
 {
 	if (svg_sam && svg_sam_writer_close(svg_sam)) SUBREADprintf("svg_sam_writer_close: %s\n", svg_last_error());
 	svg_sam = NULL;
+	if (getenv("SVG_REF_TIMING"))
+		fprintf(stderr, "SVG_DROPIN_VOTING read_chunk=%.6f vote_call=%.6f fragile=%.6f tail=%.6f\n", svg_t_read, svg_t_vote,
+		        svg_t_frag, svg_t_tail);
 }
 
 /*
@@ -598,6 +615,78 @@ static void rc_get(uint64_t r, int e, char *name, char *text, char *qual, int *r
 	if (qual) strcpy(qual, p + nn + *rl + 1);
 }
 
+/*
+ * geinput_next_read_trim's plain-FASTQ branch (input-files.c:982-1093, with read_line_noempty
+ * :209-261 and SKIP_LINE :650) restated with the FILE's lock taken once per read (flockfile +
+ * getc_unlocked) instead of once per character (fgetc through geinput_getc, :197): the same bytes
+ * consumed, the same name / text / quality strings and return values, the file position where the
+ * reference's parse leaves it (chunk rewinds and saved positions see no difference).  Other input
+ * types take the reference's own function.
+ */
+int trim_read_inner(char *read_text, char *qual_text, int rlen, short t_5, short t_3);
+srInt_64 tell_current_line_no(gene_input_t *input);
+
+static int fq_line_noempty(FILE *fp, int max_len, char *buff)
+{
+	int ret = 0;
+	for (;;) {
+		const char ch = (char)getc_unlocked(fp);
+		if (ch == EOF) break;
+		if (ch == '\n') {
+			if (ret) break;
+		} else if (ret < max_len - 1) buff[ret++] = ch;
+	}
+	buff[ret] = 0;
+	return ret;
+}
+
+static int fq_next_read(gene_input_t *input, char *read_name, char *read_string, char *quality_string, short trim_5,
+                        short trim_3)
+{
+	FILE *fp = (FILE *)input->input_fp;
+	signed char nch;
+	int ret;
+	flockfile(fp);
+	do nch = (signed char)getc_unlocked(fp); while (nch == '\n');
+	if (nch == EOF) { funlockfile(fp); return -1; }
+	if (nch != '@') {
+		funlockfile(fp);
+		SUBREADprintf("ERROR: a format issue %d is found on the %lld-th line in input file '%s'.\nProgram aborted.\n", nch,
+		              (long long)tell_current_line_no(input), input->filename);
+		return -1;
+	}
+	fq_line_noempty(fp, MAX_READ_NAME_LEN, read_name);
+	for (int cursor = 1; read_name[cursor]; cursor++)
+		if (read_name[cursor] == ' ' || read_name[cursor] == '\t') { read_name[cursor] = 0; break; }
+	ret = fq_line_noempty(fp, MAX_READ_LENGTH, read_string);
+	do nch = (signed char)getc_unlocked(fp); while (nch == '\n');
+	if (nch != '+') {
+		funlockfile(fp);
+		SUBREADprintf("ERROR: a format issue %c is found on the %lld-th line in input file '%s'.\nProgram aborted.\n", nch,
+		              (long long)tell_current_line_no(input), input->filename);
+		return -1;
+	}
+	nch = ' ';
+	while (nch != EOF && nch != '\n') nch = (signed char)getc_unlocked(fp);
+	if (quality_string) fq_line_noempty(fp, MAX_READ_LENGTH, quality_string);
+	else {
+		int content = 0;
+		nch = ' ';
+		while (nch != EOF && (nch != '\n' || !content)) { nch = (signed char)getc_unlocked(fp); content += nch != '\n'; }
+	}
+	funlockfile(fp);
+	if (trim_5 || trim_3) ret = trim_read_inner(read_string, quality_string, ret, trim_5, trim_3);
+	return ret;
+}
+
+static int next_read_trim(gene_input_t *input, char *read_name, char *read_string, char *quality_string, short trim_5,
+                          short trim_3, int *is_secondary)
+{
+	if (input->file_type == GENE_INPUT_FASTQ && read_name)
+		return fq_next_read(input, read_name, read_string, quality_string, trim_5, trim_3);
+	return geinput_next_read_trim(input, read_name, read_string, quality_string, trim_5, trim_3, is_secondary);
+}
+
 int fetch_next_read_pair_svg(global_context_t *gc, thread_context_t *tc, gene_input_t *ginp1, gene_input_t *ginp2,
                              int *read_len_1, int *read_len_2, char *read_name_1, char *read_name_2, char *read_text_1,
                              char *read_text_2, char *qual_text_1, char *qual_text_2, int remove_color_head,
@@ -638,16 +727,16 @@ int fetch_next_read_pair_svg(global_context_t *gc, thread_context_t *tc, gene_in
 	if (gc->running_processed_reads_in_chunk < gc->config.reads_per_chunk) {
 		do {
 			is_second_R1 = 0; is_second_R2 = 0;
-			rl1 = geinput_next_read_trim(ginp1, read_name_1, read_text_1, qual_text_1, gc->config.read_trim_5,
-			                             gc->config.read_trim_3, &is_second_R1);
+			rl1 = next_read_trim(ginp1, read_name_1, read_text_1, qual_text_1, gc->config.read_trim_5,
+			                     gc->config.read_trim_3, &is_second_R1);
 			if (gc->config.space_type == GENE_SPACE_COLOR && remove_color_head && isalpha(read_text_1[0])) {
 				int xk1;
 				for (xk1 = 2; read_text_1[xk1]; xk1++) read_text_1[xk1 - 2] = read_text_1[xk1];
 				read_text_1[xk1 - 2] = 0;
 			}
 			if (ginp2) {
-				rl2 = geinput_next_read_trim(ginp2, read_name_2, read_text_2, qual_text_2, gc->config.read_trim_5,
-				                             gc->config.read_trim_3, &is_second_R2);
+				rl2 = next_read_trim(ginp2, read_name_2, read_text_2, qual_text_2, gc->config.read_trim_5,
+				                     gc->config.read_trim_3, &is_second_R2);
 				if (gc->config.space_type == GENE_SPACE_COLOR && remove_color_head && isalpha(read_text_2[0])) {
 					int xk1;
 					for (xk1 = 2; read_text_2[xk1]; xk1++) read_text_2[xk1 - 2] = read_text_2[xk1];

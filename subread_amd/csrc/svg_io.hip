@@ -618,11 +618,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	const bool jo = p->do_breakpoint_detection != 0, bmo = p->do_big_margin_filtering_for_junctions != 0;
 	const bool sjm = jo || bmo;   // subjunc: the wave kernel reads the text (donor scoring)
 	HIPCHK(hipSetDevice(h->device));
-	// copy streams on first use only: HIP deals a process's streams round-robin onto
-	// GPU_MAX_HW_QUEUES (4) hardware queues, and idle extra streams can land the chunk
-	// pipeline's second stream on the caller's queue
-	if (!h->up_stream) HIPCHK(hipStreamCreateWithFlags(&h->up_stream, hipStreamNonBlocking));
-	if (!h->down_stream) HIPCHK(hipStreamCreateWithFlags(&h->down_stream, hipStreamNonBlocking));
+	// (the copy streams are the handle's: the device's shared stream set, svg_vote.hip)
 	svg_hostio *io;
 	if ((rc = io_get(h, &io))) return rc;
 	{

@@ -32,6 +32,7 @@
 // the cold part (coverage start/end, 21-entry indel recorder) lives in a
 // per-wave HBM scratch that stays L2-resident.  Integer work only: no MFMA.
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
@@ -2304,6 +2305,53 @@ __global__ void __launch_bounds__(256) build_bline(const uint32_t *bstart, const
 	}
 }
 
+// The library's four streams of a device (probe + lane kernels, wave kernel + compaction, uploads,
+// downloads) are one set per process, created back to back and shared by every handle on the
+// device.  HIP deals a process's streams round-robin onto GPU_MAX_HW_QUEUES (4) hardware queues:
+// four consecutive creations land on four different queues, whereas per-handle streams created at
+// different times (a second index, a multi-block index's blocks, torch's own streams in between)
+// can put a handle's two kernel streams on one queue, where the wave kernel of chunk c and the
+// probe kernel of chunk c+1 run one after the other -- measured in a three-index process:
+// 152 ms/step against 110 with the same kernels (profiles/r04/ab_images_c3.json).  Handles on one
+// device then order their work on the same streams, which changes no result (each handle's
+// buffers are its own; its calls already wait for its previous call).
+static pthread_mutex_t g_streams_mu = PTHREAD_MUTEX_INITIALIZER;
+static struct { hipStream_t s[4]; int refs; } g_streams[64];
+
+static int streams_acquire(svg_index *h)
+{
+	if (h->device < 0 || h->device >= 64) { svg_set_error("device %d out of range", h->device); return SVG_E_ARG; }
+	pthread_mutex_lock(&g_streams_mu);
+	int rc = 0;
+	if (!g_streams[h->device].refs) {
+		for (int k = 0; k < 4 && !rc; k++)
+			if (hipStreamCreateWithFlags(&g_streams[h->device].s[k], hipStreamNonBlocking) != hipSuccess) {
+				svg_set_error("hipStreamCreate failed");
+				rc = SVG_E_DEVICE;
+				for (int j = 0; j < k; j++) hipStreamDestroy(g_streams[h->device].s[j]);
+			}
+	}
+	if (!rc) {
+		g_streams[h->device].refs++;
+		h->stream = g_streams[h->device].s[0];
+		h->stream2 = g_streams[h->device].s[1];
+		h->up_stream = g_streams[h->device].s[2];
+		h->down_stream = g_streams[h->device].s[3];
+	}
+	pthread_mutex_unlock(&g_streams_mu);
+	return rc;
+}
+
+static void streams_release(svg_index *h)
+{
+	if (!h->stream) return;
+	pthread_mutex_lock(&g_streams_mu);
+	if (--g_streams[h->device].refs == 0)
+		for (int k = 0; k < 4; k++) hipStreamDestroy(g_streams[h->device].s[k]);
+	pthread_mutex_unlock(&g_streams_mu);
+	h->stream = h->stream2 = h->up_stream = h->down_stream = NULL;
+}
+
 // common tail of svg_index_open / svg_index_build*: d_bstart/d_keys/d_vals already in HBM,
 // host part holds .array and the chromosome table
 int svg_index_finish_device(svg_index *h)
@@ -2314,8 +2362,7 @@ int svg_index_finish_device(svg_index *h)
 	HIPCHK(hipSetDevice(h->device));
 	if ((rc = dmalloc(h, &h->d_values, (size_t)x->values_bytes + 64)) || (rc = dmalloc(h, &h->d_chr, 4 * (size_t)x->n_chr + 64)))
 		return rc;
-	HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-	HIPCHK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+	if ((rc = streams_acquire(h))) return rc;
 	HIPCHK(hipEventCreateWithFlags(&h->ev_up[2], hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&h->ev_done[2], hipEventDisableTiming));
 	HIPCHK(hipEventCreateWithFlags(&h->ev_down[2], hipEventDisableTiming));
@@ -2598,10 +2645,7 @@ extern "C" void svg_index_close(svg_index *h)
 	hipFree(h->d_bgrp); hipFree(h->d_keys8); hipFree(h->d_bline); hipFree(h->d_bcode); hipFree(h->d_khash); hipFree(h->d_ksorted);
 	hipFree(h->d_scratch); hipFree(h->d_stats); hipFree(h->d_err);
 	if (h->ev_last) hipEventDestroy(h->ev_last);
-	if (h->stream) hipStreamDestroy(h->stream);
-	if (h->stream2) hipStreamDestroy(h->stream2);
-	if (h->up_stream) hipStreamDestroy(h->up_stream);
-	if (h->down_stream) hipStreamDestroy(h->down_stream);
+	streams_release(h);
 	svg_host_index_free(&h->host);
 	free(h);
 }

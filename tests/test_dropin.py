@@ -59,3 +59,57 @@ def test_sublong_oracle_dropin_matches_stock(cache, tmp_path):
     dropin.run_sublong("stock", pre, fq, str(tmp_path / "stock.sam"))
     dropin.run_sublong("oracle-dropin", pre, fq, str(tmp_path / "dropin.sam"))
     assert dropin.compare_sam(str(tmp_path / "stock.sam"), str(tmp_path / "dropin.sam")) > 30
+
+
+@pytest.mark.parametrize("trim", [(), ("--trim5", "3", "--trim3", "2")])
+def test_oracle_dropin_fastq_layouts_match_stock(trim, cache, tmp_path):
+    """The binding's plain-FASTQ parse (fq_next_read: geinput_next_read_trim's FASTQ branch,
+    input-files.c:982-1093, one stdio lock per read) against the reference's own parser inside
+    the stock aligner: read names cut at the first blank or tab after their first character,
+    empty names, blank lines between and inside records, '+' lines with text, CR bytes kept, a
+    read longer than MAX_READ_LENGTH cut to it, reads of every length, 5'/3' trimming -- the
+    same SAM / VCF byte for byte, with two threads (the chunk's reads are fetched once and
+    served to the later passes from the binding's cache)."""
+    from tests import dropin
+    c = Case("pe_gapped_errmut")
+    if not have(c.meta["program"], "oracle-dropin"):
+        pytest.skip("reference drop-in binaries not built (make -C oracle dropin)")
+    fq = str(tmp_path / "r.fq")
+    with open(fq, "wb") as f:
+        for i in range(len(c.r1)):
+            s = c.r1.read(i)
+            q = bytes(33 + (i * 5 + k * 11) % 41 for k in range(len(s)))
+            k = i % 9
+            if k == 0:
+                name = b"r%d extra comment" % i
+            elif k == 1:
+                name = b"r%d\tBX:Z:ACGT" % i
+            elif k == 2:
+                name = b" r%d" % i             # blank at position 0 is kept (the cut starts at 1)
+            elif k == 3:
+                name = b"x"
+            else:
+                name = b"r%d" % i
+            plus = b"+r%d" % i if k == 4 else b"+"
+            if k == 5:
+                s, q = s[:40], q[:40]
+            if i == 10:
+                s, q = (s * 16)[:1400], (q * 16)[:1400]   # past MAX_READ_LENGTH (1210): cut
+            if k == 6:
+                s, q = s + b"\r", q + b"\r"
+            sep = b"\n\n" if k == 7 else b"\n"
+            f.write(b"@" + name + sep + s + b"\n" + plus + sep + q + b"\n")
+            if k == 8:
+                f.write(b"\n")
+    pre = cache.get(c.index_key)
+    so, do = str(tmp_path / "stock.sam"), str(tmp_path / "dropin.sam")
+    dropin.run(c.meta["program"], "dump", pre, fq, None, so, 2, trim)
+    dropin.run(c.meta["program"], "oracle-dropin", pre, fq, None, do, 2, trim)
+    a, b = dropin.outputs(so), dropin.outputs(do)
+    assert sorted(a) == sorted(b)
+    for suf in a:
+        assert a[suf] == b[suf], "output %r differs" % (suf or ".sam")
+    # (CR bytes stay inside the records: split on LF only)
+    recs = [l for l in a[""].split(b"\n") if l and not l.startswith(b"@")]
+    assert len(recs) == len(c.r1)
+    assert sum(1 for l in recs if not int(l.split(b"\t")[1]) & 4) > 0

@@ -122,6 +122,10 @@ def parse_phases(stderr):
     for kv in m[-1].split():
         k, v = kv.split("=")
         d[k] = round(float(v), 3) if "." in v else int(v)
+    # the drop-in's split of its voting phase (integration/do_voting_gpu.c)
+    v = re.findall(r"SVG_DROPIN_VOTING (.*)", stderr)
+    if v:
+        d["voting_split"] = dict((kv.split("=")[0], round(float(kv.split("=")[1]), 3)) for kv in v[-1].split())
     return d
 
 
