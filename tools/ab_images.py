@@ -115,6 +115,11 @@ def main():
         if c["dev_ms"]:
             e["dev_ms_median"] = round(statistics.median(c["dev_ms"]), 2)
             e["dev_mreads_s"] = round(n / statistics.median(c["dev_ms"]) / 1e3, 1)
+            c["ix"].set_timing(True)
+            c["ix"].vote_packed_device(p, q, None, d_out.data_ptr(), None, None)
+            torch.cuda.synchronize()
+            e["dev_kernels"] = c["ix"].kernel_timing()
+            c["ix"].set_timing(False)
         res["configs"].append(e)
     s = json.dumps(res, indent=1)
     print(s)
