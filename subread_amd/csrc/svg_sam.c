@@ -25,39 +25,90 @@ typedef struct {
 	int all;          /* all_locations of the fragment (0: nothing put yet) */
 } sam_slot;
 
+/* A full staging buffer leaves the ring lock as a numbered batch: the thread that detached it
+ * writes it under the file lock once every earlier batch is written (batches leave in number
+ * order), so producers never wait on file I/O to put their text. */
+typedef struct sam_batch {
+	char *buf;
+	size_t len, cap;
+	uint64_t ticket;
+	int flush;                /* fflush after it (the chunk's last batch) */
+	struct sam_batch *next;   /* free list */
+} sam_batch;
+
 struct svg_sam_writer {
 	FILE *fp;
-	pthread_mutex_t mu;
+	pthread_mutex_t mu;       /* ring, staging, tickets */
 	sam_slot *ring;
 	uint64_t size;          /* power of two */
 	int64_t next;           /* oldest fragment not written yet */
 	int64_t pending;        /* fragments with text held in the ring */
 	int64_t chunk_end;      /* fragments in the chunk: flush once `next` reaches it */
-	char *out;              /* staging of drained fragments */
-	size_t out_len, out_cap;
+	sam_batch *out;         /* staging of drained fragments */
+	sam_batch *spare;       /* written batches, for reuse */
+	uint64_t tickets;       /* batches detached so far */
+	pthread_mutex_t wmu;      /* the FILE*; written / failed */
+	pthread_cond_t wcv;
+	uint64_t written;       /* batches written so far */
 	int failed;
 };
 
 #define OUT_FLUSH (4u << 20)
 
-static int out_flush(svg_sam_writer *w)
+static sam_batch *batch_new(svg_sam_writer *w)
 {
-	if (w->out_len && fwrite(w->out, 1, w->out_len, w->fp) != w->out_len) w->failed = 1;
-	w->out_len = 0;
-	return w->failed;
+	sam_batch *b = w->spare;
+	if (b) { w->spare = b->next; b->len = 0; b->flush = 0; return b; }
+	b = calloc(1, sizeof *b);
+	if (!b) return NULL;
+	b->cap = OUT_FLUSH;
+	b->buf = malloc(b->cap);
+	if (!b->buf) { free(b); return NULL; }
+	return b;
+}
+
+/* (ring lock held) the staging buffer becomes batch `ticket`; a fresh one takes its place */
+static sam_batch *out_detach(svg_sam_writer *w, int flush)
+{
+	sam_batch *b = w->out, *nb = batch_new(w);
+	if (!nb) return NULL;
+	b->ticket = w->tickets++;
+	b->flush = flush;
+	w->out = nb;
+	return b;
+}
+
+/* (no lock held) write batch b in ticket order, then hand it back to the spares */
+static int batch_write(svg_sam_writer *w, sam_batch *b)
+{
+	pthread_mutex_lock(&w->wmu);
+	while (w->written != b->ticket) pthread_cond_wait(&w->wcv, &w->wmu);
+	if (b->len && fwrite(b->buf, 1, b->len, w->fp) != b->len) w->failed = 1;
+	if (b->flush && fflush(w->fp)) w->failed = 1;
+	w->written++;
+	const int f = w->failed;
+	pthread_cond_broadcast(&w->wcv);
+	pthread_mutex_unlock(&w->wmu);
+	pthread_mutex_lock(&w->mu);
+	b->next = w->spare;
+	w->spare = b;
+	pthread_mutex_unlock(&w->mu);
+	return f ? SVG_E_IO : 0;
 }
 
 static int out_append(svg_sam_writer *w, const char *s, size_t n)
 {
-	if (w->out_len + n > w->out_cap) {
-		if (out_flush(w)) return SVG_E_IO;
-		if (n > w->out_cap) {     /* one fragment larger than the staging buffer: straight out */
-			if (fwrite(s, 1, n, w->fp) != n) w->failed = 1;
-			return w->failed ? SVG_E_IO : 0;
-		}
+	sam_batch *o = w->out;
+	if (o->len + n > o->cap) {
+		size_t nc = o->cap;
+		while (o->len + n > nc) nc *= 2;   /* (detached at OUT_FLUSH / 2: only a huge fragment grows it) */
+		char *nb = realloc(o->buf, nc);
+		if (!nb) return SVG_E_NOMEM;
+		o->buf = nb;
+		o->cap = nc;
 	}
-	memcpy(w->out + w->out_len, s, n);
-	w->out_len += n;
+	memcpy(o->buf + o->len, s, n);
+	o->len += n;
 	return 0;
 }
 
@@ -70,10 +121,14 @@ int svg_sam_writer_open(void *file, svg_sam_writer **out)
 	w->size = 1024;
 	w->ring = calloc(w->size, sizeof(sam_slot));
 	w->chunk_end = -1;
-	w->out_cap = OUT_FLUSH;
-	w->out = malloc(w->out_cap);
-	if (!w->ring || !w->out) { free(w->ring); free(w->out); free(w); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	w->out = batch_new(w);
+	if (!w->ring || !w->out) {
+		if (w->out) { free(w->out->buf); free(w->out); }
+		free(w->ring); free(w); svg_set_error("out of memory"); return SVG_E_NOMEM;
+	}
 	pthread_mutex_init(&w->mu, NULL);
+	pthread_mutex_init(&w->wmu, NULL);
+	pthread_cond_init(&w->wcv, NULL);
 	*out = w;
 	return 0;
 }
@@ -96,8 +151,9 @@ static int ring_reserve(svg_sam_writer *w, int64_t f)
 	return 0;
 }
 
-/* write every complete fragment from `next` on (lock held) */
-static int drain(svg_sam_writer *w)
+/* move every complete fragment from `next` on to the staging buffer (ring lock held); *out gets
+ * the batch to write once the lock is released (staging half full, or the chunk complete) */
+static int drain(svg_sam_writer *w, sam_batch **out)
 {
 	int rc = 0;
 	for (;;) {
@@ -109,8 +165,8 @@ static int drain(svg_sam_writer *w)
 		w->next++;
 		w->pending--;
 	}
-	if ((w->out_len >= OUT_FLUSH / 2 || w->next == w->chunk_end) && out_flush(w)) rc = SVG_E_IO;
-	if (w->next == w->chunk_end && fflush(w->fp)) { w->failed = 1; rc = SVG_E_IO; }
+	const int end = w->next == w->chunk_end;
+	if (!rc && (w->out->len >= OUT_FLUSH / 2 || end) && !(*out = out_detach(w, end))) rc = SVG_E_NOMEM;
 	return rc;
 }
 
@@ -121,6 +177,7 @@ int svg_sam_writer_put(svg_sam_writer *w, int64_t fragment, int location, int al
 		return SVG_E_ARG;
 	}
 	int rc = 0;
+	sam_batch *wb = NULL;
 	pthread_mutex_lock(&w->mu);
 	if (fragment < w->next) {
 		pthread_mutex_unlock(&w->mu);
@@ -136,7 +193,7 @@ int svg_sam_writer_put(svg_sam_writer *w, int64_t fragment, int location, int al
 		s->got = s->all = 0;
 		w->next++;
 		w->pending--;
-		if (!rc) rc = drain(w);
+		if (!rc) rc = drain(w, &wb);
 	} else {
 		if (s->len + len > s->cap) {
 			size_t nc = (s->len + len) * 2 + 256;
@@ -148,9 +205,15 @@ int svg_sam_writer_put(svg_sam_writer *w, int64_t fragment, int location, int al
 		memcpy(s->buf + s->len, text, len);
 		s->len += len;
 		s->got++;
-		if (fragment == w->next) rc = drain(w);
+		if (fragment == w->next) rc = drain(w, &wb);
 	}
 	pthread_mutex_unlock(&w->mu);
+	if (wb) {
+		const int wr = batch_write(w, wb);
+		if (!rc) rc = wr;
+	}
+	if (rc == SVG_E_IO) svg_set_error("svg_sam_writer_put: write failed");
+	else if (rc == SVG_E_NOMEM) svg_set_error("out of memory");
 	return rc;
 }
 
@@ -176,21 +239,29 @@ int64_t svg_sam_writer_pending(svg_sam_writer *w)
 
 int svg_sam_writer_failed(svg_sam_writer *w)
 {
-	return w ? w->failed : 0;
+	if (!w) return 0;
+	pthread_mutex_lock(&w->wmu);
+	const int f = w->failed;
+	pthread_mutex_unlock(&w->wmu);
+	return f;
 }
 
 int svg_sam_writer_close(svg_sam_writer *w)
 {
 	if (!w) return 0;
+	/* every producer has returned: the batches they detached are written; what is staged goes now */
 	pthread_mutex_lock(&w->mu);
-	int rc = out_flush(w) ? SVG_E_IO : 0;
-	if (fflush(w->fp)) rc = SVG_E_IO;
+	sam_batch *b = out_detach(w, 1);
 	const int64_t p = w->pending;
 	pthread_mutex_unlock(&w->mu);
+	int rc = b ? batch_write(w, b) : SVG_E_NOMEM;
 	for (uint64_t i = 0; i < w->size; i++) free(w->ring[i].buf);
 	free(w->ring);
-	free(w->out);
+	for (sam_batch *q = w->spare, *nx; q; q = nx) { nx = q->next; free(q->buf); free(q); }
+	if (w->out) { free(w->out->buf); free(w->out); }
 	pthread_mutex_destroy(&w->mu);
+	pthread_mutex_destroy(&w->wmu);
+	pthread_cond_destroy(&w->wcv);
 	free(w);
 	if (p) { svg_set_error("svg_sam_writer_close: %lld fragments never completed", (long long)p); return SVG_E_ARG; }
 	if (rc) svg_set_error("svg_sam_writer_close: write failed");
