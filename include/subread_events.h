@@ -130,6 +130,18 @@ int svg_events_merge(svg_events *dst, svg_events *const *tables, int n);
 int svg_events_anti_support(svg_events *t, const svg_params *p, const svg_event_params *ep, uint64_t n_reads, int ends,
                             const svg_mapping_result *out);
 
+/*
+ * remove_neighbour (core-indel.c:447-595) on a merged table after svg_events_anti_support, as
+ * the reference runs it before iteration two (core.c:3629-3630): redundant neighbour events
+ * become type 0 (CHRO_EVENT_TYPE_REMOVED) and leave the table's site lists.  Events of earlier
+ * passes already removed stay removed.
+ */
+int svg_events_remove_neighbour(svg_events *t);
+
+/* Append n events (e.g. a table kept from an earlier chunk, or the reference's own table) to t,
+ * each entered in its sides' site lists in order as put_new_event does (core-indel.c:1385). */
+int svg_events_load(svg_events *t, const svg_event *ev, int64_t n);
+
 int64_t svg_events_count(const svg_events *t);
 int     svg_events_get(const svg_events *t, svg_event *out);   /* svg_events_count() entries */
 

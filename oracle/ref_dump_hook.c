@@ -112,6 +112,27 @@ static void dump_events(global_context_t *gc, const char *fn)
 }
 
 int __real_anti_supporting_read_scan(global_context_t *global_context);
+void __real_remove_neighbour(global_context_t *global_context);
+
+/* SVG_REF_EVENTS_RN=<file>: the event types after remove_neighbour (core-indel.c:447, called
+ * right after anti_supporting_read_scan, core.c:3629-3630; removed events become type 0),
+ * appended chunk after chunk: u64 n_events, then n_events x u8 event_type */
+void __wrap_remove_neighbour(global_context_t *gc)
+{
+	__real_remove_neighbour(gc);
+	const char *fn = getenv("SVG_REF_EVENTS_RN");
+	if (!fn || !fn[0]) return;
+	FILE *fp = fopen(fn, "ab");
+	if (!fp) return;
+	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
+	unsigned long long n = ic ? ic->total_events : 0, i;
+	fwrite(&n, 8, 1, fp);
+	for (i = 0; i < n; i++) {
+		unsigned char t = (unsigned char)ic->event_space_dynamic[i].event_type;
+		fwrite(&t, 1, 1, fp);
+	}
+	fclose(fp);
+}
 int __real_write_indel_final_results(global_context_t *global_context);
 
 /* SVG_REF_TIMING=1: the reference's own phase clocks, accumulated over every chunk by

@@ -39,7 +39,7 @@ EXPORTS = [
     # host post-vote events (include/subread_events.h)
     "svg_event_params_default", "svg_genome_arrays_open", "svg_genome_arrays_close", "svg_events_create",
     "svg_events_destroy", "svg_events_add_batch", "svg_events_merge", "svg_events_count", "svg_events_get",
-    "svg_events_anti_support", "svg_events_add_batch2",
+    "svg_events_anti_support", "svg_events_add_batch2", "svg_events_remove_neighbour", "svg_events_load",
     # SAM emission (include/subread_sam.h)
     "svg_sam_writer_open", "svg_sam_writer_close", "svg_sam_writer_begin_chunk", "svg_sam_writer_put",
     "svg_sam_writer_pending", "svg_sam_writer_failed", "svg_sam_format",
@@ -171,6 +171,10 @@ def lib():
         L.svg_events_merge.restype = i32
         L.svg_events_anti_support.argtypes = [vp, vp, vp, u64, i32, vp]
         L.svg_events_anti_support.restype = i32
+        L.svg_events_remove_neighbour.argtypes = [vp]
+        L.svg_events_remove_neighbour.restype = i32
+        L.svg_events_load.argtypes = [vp, vp, ctypes.c_int64]
+        L.svg_events_load.restype = i32
         L.svg_events_count.argtypes = [vp]
         L.svg_events_count.restype = ctypes.c_int64
         L.svg_events_get.argtypes = [vp, vp]
@@ -301,6 +305,16 @@ class EventTable:
                                              ctypes.byref(event_params) if event_params is not None else None,
                                              int(n_reads), int(ends), mapping.ctypes.data), "svg_events_anti_support")
 
+    def load(self, events):
+        """svg_events_load: append an EVENT_DTYPE array (entered in the site lists in order)."""
+        from .abi import EVENT_DTYPE
+        a = np.ascontiguousarray(events).view(EVENT_DTYPE).reshape(-1)
+        _check(lib().svg_events_load(self.h, a.ctypes.data if len(a) else None, len(a)), "svg_events_load")
+
+    def remove_neighbour(self):
+        """svg_events_remove_neighbour: remove_neighbour (core-indel.c:447) on a merged table."""
+        _check(lib().svg_events_remove_neighbour(self.h), "svg_events_remove_neighbour")
+
     def events(self):
         from .abi import EVENT_DTYPE
         n = lib().svg_events_count(self.h)
@@ -320,14 +334,18 @@ class EventTable:
             pass
 
 
-def find_events(genome, params, r1, r2, records, first_read=0, anti_support=True, quals=None, fragile=None):
+def find_events(genome, params, r1, r2, records, first_read=0, anti_support=True, quals=None, fragile=None,
+                remove_neighbour=False):
     """Events of one batch, merged and sorted like the reference's table after the voting step,
-    with the anti-supporting read counts of the scan that follows it."""
+    with the anti-supporting read counts of the scan that follows it (and, remove_neighbour=True,
+    the redundant neighbours marked removed as the reference does next)."""
     t = EventTable()
     t.add_batch(genome, params, r1, r2, records, first_read, quals=quals, fragile=fragile)
     m = EventTable.merge([t])
     if anti_support:
         m.anti_support(params, len(r1), 2 if r2 is not None else 1, records[0])
+    if remove_neighbour:
+        m.remove_neighbour()
     ev = m.events()
     t.close()
     m.close()

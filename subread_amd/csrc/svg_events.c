@@ -1287,3 +1287,114 @@ int svg_events_anti_support(svg_events *t, const svg_params *p, const svg_event_
 	free(sm); free(lg); free(cnt); free(jobs); free(tid); free(started);
 	return 0;
 }
+
+/* events appended as given, each put in its sides' id lists (put_new_event) in order */
+int svg_events_load(svg_events *t, const svg_event *ev, int64_t n)
+{
+	if (!t || n < 0 || (n && !ev)) { svg_set_error("svg_events_load: bad argument"); return SVG_E_ARG; }
+	for (int64_t i = 0; i < n; i++) {
+		const uint64_t id = new_event(t);
+		t->ev[id] = ev[i];
+		put_event(t, id);
+	}
+	return 0;
+}
+
+/* ------------------------------------------------------------------ remove_neighbour */
+typedef struct { uint64_t *v; uint64_t n, cap; } idlist_t;
+
+static int idlist_push(idlist_t *l, uint64_t id)
+{
+	if (l->n == l->cap) {
+		uint64_t nc = l->cap ? 2 * l->cap : 1024;
+		uint64_t *nv = realloc(l->v, nc * sizeof(uint64_t));
+		if (!nv) return SVG_E_NOMEM;
+		l->v = nv;
+		l->cap = nc;
+	}
+	l->v[l->n++] = id;
+	return 0;
+}
+
+/* one id out of the site list at key (remove_neighbour's second loop, core-indel.c:572-590) */
+static void site_drop(svg_events *t, uint32_t key, uint64_t id)
+{
+	site_t *st = site_find(t, key);
+	if (!st) return;
+	int w = 0, k;
+	for (k = 0; k < EV_PER_SITE && st->ids[k]; k++) {
+		if (st->ids[k] - 1 == id) continue;
+		st->ids[w++] = st->ids[k];
+	}
+	for (; w < k; w++) st->ids[w] = 0;
+}
+
+/*
+ * remove_neighbour, core-indel.c:447-595 (no scRNA input, no fusion / long-deletion events): an
+ * indel with an indel of the same length within 3 bases of its small side is dropped unless the
+ * two are connected or it has the better quality (then the more supporting reads; on a tie the
+ * one at the higher coordinate stays); a junction / fusion event without the known-event mark
+ * (is_donor_found_or_annotation & 64) is dropped for a neighbour within 11 bases whose large
+ * side is within 4 of the shifted one and that has more supporting reads (a tie: the neighbour
+ * at the lower coordinate wins), or that has a smaller indel_at_junction over an intron of
+ * about the same length.  Every decision reads the table as it was before the pass; the
+ * dropped events become type 0 (CHRO_EVENT_TYPE_REMOVED) and leave their sides' id lists.
+ * The arithmetic is the reference's unsigned 32-bit coordinate arithmetic.
+ */
+int svg_events_remove_neighbour(svg_events *t)
+{
+	if (!t) { svg_set_error("svg_events_remove_neighbour: NULL argument"); return SVG_E_ARG; }
+	idlist_t rm = {NULL, 0, 0};
+	uint64_t i, ids[EV_PER_SITE];
+	int rc = 0;
+	for (i = 0; i < t->n && !rc; i++) {
+		const svg_event *e = &t->ev[i];
+		if (e->event_type == 0) continue;
+		if (e->event_type == SVG_EVENT_INDEL) {
+			/* (is_ambiguous_indel_score is 0, core-indel.h:214) */
+			for (int d = -3; d <= 3 && !rc; d++) {
+				const int nf = search_small(t, e->small_side + (uint32_t)d, SVG_EVENT_INDEL, ids);
+				for (int k = 0; k < nf && !rc; k++) {
+					const svg_event *nb = &t->ev[ids[k]];
+					const long long ld = (long long)nb->indel_length - e->indel_length;
+					if (ld == 0 && d == 0) continue;
+					if (ld != 0) continue;
+					if (e->small_side - (uint32_t)(int)e->connected_previous_event_distance + 1u == nb->large_side) continue;
+					if (nb->small_side - (uint32_t)(int)nb->connected_previous_event_distance + 1u == e->large_side) continue;
+					if (e->large_side + (uint32_t)(int)e->connected_next_event_distance - 1u == nb->small_side) continue;
+					if (nb->large_side + (uint32_t)(int)nb->connected_next_event_distance - 1u == e->small_side) continue;
+					if (e->event_quality < nb->event_quality ||
+					    (e->event_quality == nb->event_quality &&
+					     (e->supporting_reads < nb->supporting_reads || (e->supporting_reads == nb->supporting_reads && d < 0))))
+						rc = idlist_push(&rm, i);
+				}
+			}
+		} else {
+			if (e->is_donor_found_or_annotation & 64) continue;
+			for (int d = -11; d <= 11 && !rc; d++) {
+				if (!d) continue;
+				const int nf = search_small(t, e->small_side + (uint32_t)d, SVG_EVENT_JUNCTION | SVG_EVENT_FUSION, ids);
+				for (int k = 0; k < nf && !rc; k++) {
+					const svg_event *nb = &t->ev[ids[k]];
+					if (nb->indel_at_junction > e->indel_at_junction) continue;
+					const int32_t span = (int32_t)(nb->large_side - nb->small_side + (uint32_t)(int)nb->indel_at_junction -
+					                               e->large_side + e->small_side - (uint32_t)(int)e->indel_at_junction);
+					if (e->indel_at_junction > nb->indel_at_junction && abs(span) <= 16)
+						rc = idlist_push(&rm, i);
+					else if (nb->large_side >= e->large_side - 4u + (uint32_t)d && nb->large_side <= e->large_side + 4u + (uint32_t)d &&
+					         (e->supporting_reads < nb->supporting_reads || (e->supporting_reads == nb->supporting_reads && d < 0)))
+						rc = idlist_push(&rm, i);
+				}
+			}
+		}
+	}
+	if (rc) { free(rm.v); svg_set_error("out of memory"); return rc; }
+	for (i = 0; i < rm.n; i++) {
+		svg_event *e = &t->ev[rm.v[i]];
+		site_drop(t, e->small_side, rm.v[i]);
+		site_drop(t, e->large_side, rm.v[i]);
+		e->event_type = 0;
+	}
+	free(rm.v);
+	return 0;
+}

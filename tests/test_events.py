@@ -142,3 +142,51 @@ def test_gpu_records_give_reference_events(name, index_cache):
     got = sa.find_events(g, c.params, c.r1, c.r2, (out, jout, bm), **extras(c, windows))
     check(got, out["result_flags"].reshape(-1).view(np.uint16), want, wflags)
     g.close()
+
+
+RN_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLD, "events_rn", "*.npz")))
+
+
+@pytest.mark.parametrize("name", [n for n in RN_CASES if not n.startswith("rn_")])
+def test_remove_neighbour_after_event_stage_matches_reference(name, index_cache):
+    """The event stage, the anti-supporting read scan and remove_neighbour (core-indel.c:447) on
+    the reference's records give the reference's event types after remove_neighbour
+    (tests/golden/events_rn, made by tests/golden/make_removed.py with the reference itself).
+    These cases remove nothing; the rn_* cases below do."""
+    import subread_amd as sa
+    from oracle.pyoracle import OracleIndex
+    c = Case(name)
+    want = np.load(os.path.join(GOLD, "events_rn", name + ".npz"), allow_pickle=False)["types"]
+    pre = index_cache.get(c.index_key)
+    g = sa.GenomeArrays(pre)
+    recs = split_records(c)
+    windows = OracleIndex(pre).fragile(c.params, c.r1, c.r2) if long_subjunc(c) else None
+    got = sa.find_events(g, c.params, c.r1, c.r2, recs, remove_neighbour=True, **extras(c, windows))
+    g.close()
+    assert len(got) == len(want) and (got["event_type"] == want).all()
+
+
+@pytest.mark.parametrize("name", [n for n in RN_CASES if n.startswith("rn_")])
+def test_remove_neighbour_matches_reference(name):
+    """svg_events_remove_neighbour on the reference's own event table (dumped right before its
+    remove_neighbour) removes exactly the events the reference removes: same-length indels
+    within 3 bases (rn_se: 41 of 4789) and junctions within 11 bases (rn_sj: 8 of 11999), with
+    the reference's quality / support / coordinate tie-breaks."""
+    import subread_amd as sa
+    z = np.load(os.path.join(GOLD, "events_rn", name + ".npz"), allow_pickle=False)
+    before, want = z["events"], z["types"]
+    t = sa.EventTable()
+    t.load(before)
+    t.remove_neighbour()
+    got = t.events()
+    t.close()
+    assert len(got) == len(want)
+    removed_ref = np.nonzero(want == 0)[0]
+    removed_ours = np.nonzero(got["event_type"] == 0)[0]
+    assert len(removed_ref) > 0
+    assert (got["event_type"] == want).all(), "removed: ours %s, reference %s" % (
+        sorted(set(removed_ours) - set(removed_ref))[:8], sorted(set(removed_ref) - set(removed_ours))[:8])
+    # everything else unchanged
+    b = before.view(EVENT_DTYPE).reshape(-1)
+    keep = want != 0
+    assert (got[keep].view(np.uint8) == b[keep].view(np.uint8)).all()
