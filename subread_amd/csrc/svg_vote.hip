@@ -206,7 +206,6 @@ struct Wave {
 	uint32_t *shift_locs[2];
 	const KParams *kp;
 	ReadCtx rc;
-	unsigned long long st_probes, st_items, st_hits, st_results, st_batch, st_serial;
 	int items_v;            // lane 32*e + r: items[r] of table e (gene_vote_t.items)
 	int max_vote[2];        // gene_vote_t.max_vote per table (wave-uniform)
 	int nshift[2];          // shift_indel_NO per table (wave-uniform)
@@ -602,7 +601,10 @@ struct Wave {
 				unsigned long long serial = m == 64 ? ~0ull : ((1ull << m) - 1ull);
 				if (round == 0 && kp->ii_end == 5 && m >= 8) serial = batch_create<E>(kvv, kov, m, high_b);
 				if constexpr (!SJ) STAMP(6);   // diagnostics: batch mode (align variants; SJ uses 6 for junctions)
-				if (kp->stats) { st_batch += (unsigned long long)(m - __popcll(serial)); st_serial += (unsigned long long)__popcll(serial); }
+				if (kp->stats && lane == 0) {   // diagnostics: straight to the counters (no register kept live)
+					atomicAdd(&kp->stats[26], (unsigned long long)(m - __popcll(serial)));
+					atomicAdd(&kp->stats[27], (unsigned long long)__popcll(serial));
+				}
 				while (serial) {
 					const int j = __ffsll((long long)serial) - 1;
 					serial &= serial - 1ull;
@@ -1489,7 +1491,8 @@ struct Wave {
 		}
 		if (kp->stats) {
 			for (int e = 0; e < ENDS; e++)
-				for (int i = 0; i < p.multi_best; i++) st_results += rec_votes(L->res[e][i]) > 0;
+				for (int i = 0; i < p.multi_best; i++)
+					if (lane == 0 && rec_votes(L->res[e][i]) > 0) atomicAdd(&kp->stats[3], 1ull);
 		}
 		wsync();
 	}
@@ -1521,7 +1524,6 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	for (int k = 0; k < 4; k++) W.why[k] = 0;
 	W.t_last = __builtin_amdgcn_s_memtime();
 #endif
-	W.st_probes = W.st_items = W.st_hits = W.st_results = W.st_batch = W.st_serial = 0;
 	// direct: reads gw, gw+nw, ...; indirect: the deferred reads idx[gw], idx[gw+nw], ...
 	// deferred reads differ widely in cost (repeat families): taken from a work counter
 	const uint64_t n = kp.idx ? (uint64_t)*kp.idx_count : kp.n_reads;
@@ -1557,18 +1559,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 		for (int k = 0; k < 4; k++) atomicAdd(&kp.stats[28 + k], W.why[k]);
 	}
 #endif
-	if (kp.stats) {
-		unsigned long long a = W.st_items, h = W.st_hits;
-		for (int o = 32; o; o >>= 1) { a += __shfl_xor(a, o); h += __shfl_xor(h, o); }
-		if (lane_id() == 0) {
-			atomicAdd(&kp.stats[3], W.st_results);
-			atomicAdd(&kp.stats[26], W.st_batch);    // diagnostics: candidates settled by batch mode
-			atomicAdd(&kp.stats[27], W.st_serial);   //              candidates replayed serially
-			atomicAdd(&kp.stats[0], W.st_probes);
-			atomicAdd(&kp.stats[1], a);
-			atomicAdd(&kp.stats[2], h);
-		}
-	}
+	// (stats: results [3], batch-settled / serially replayed candidates [26] / [27] are added where
+	// they happen; probes, bucket items and hits [0..2] by the probe kernels)
 }
 
 // equal-key run of a bucket given as a bit mask over its items: gehash_go_X's binary search
