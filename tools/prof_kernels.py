@@ -9,9 +9,10 @@ Outputs: OUT.json (per-kernel launch time and HBM traffic per launch / per read;
 reads traffic_bytes_per_read of the dominant kernel from it) and OUT.md.
 
 Dispatch accounting: every step launches each kernel L times (one per chunk of reads).
-The trace holds (W + S) * L dispatches per kernel: the timed-region average drops the first
-W * L (warmup).  The PMC runs are 1 warmup + 1 step: half of each kernel's dispatches is one
-step.  probe_kernel = probe_line_kernel + probe_big_kernel (one probe launch of the library's
+The trace holds (W + S + X) * L dispatches per kernel (X: steps after the timed ones --
+prof_run.py's host mode runs one more, the HIP-event kernel record): the timed-region average
+is over dispatches W*L .. (W+S)*L.  The PMC runs are 1 warmup + 1 step (+ X): their second
+step's L dispatches are one step's traffic.  probe_kernel = probe_line_kernel + probe_big_kernel (one probe launch of the library's
 timing API brackets both), or the one-kernel probe when the index has no bucket codes/lines.
 
 Units and corrections (MI355X_MICROARCH.md, HBM / rocprofv3 section): FETCH_SIZE and
@@ -75,6 +76,7 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--extra", type=int, default=1, help="steps after the timed ones (prof_run.py host mode: 1)")
     ap.add_argument("--reads", type=int, default=50_000_000, help="reads per step (all chunks)")
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--bench-json", help="bench.py line of the traced run (launch_ms to compare)")
@@ -92,12 +94,13 @@ def main():
         if k not in per:
             continue
         d = per[k]
-        L = max(1, len(d) // (a.warmup + a.steps))
+        L = max(1, len(d) // (a.warmup + a.steps + a.extra))
         timed = d[a.warmup * L:(a.warmup + a.steps) * L]
         f, w = fe.get(k, []), wr.get(k, [])
-        nf = len(f) // 2
-        fb = sum(f[:nf]) * 1024.0
-        wb = sum(w[:nf]) * 1024.0
+        pl = max(1, len(f) // (2 + a.extra))      # the PMC runs' launches per step
+        nf = pl
+        fb = sum(f[pl:2 * pl]) * 1024.0
+        wb = sum(w[pl:2 * pl]) * 1024.0
         ent = {"launches_per_step": L, "timed_avg_ms": sum(timed) / max(1, len(timed)),
                "all_dispatch_avg_ms": stats.get(k, {}).get("avg_ms"), "calls": len(d),
                "fetch_bytes_per_read": fb / a.reads, "write_bytes_per_read": wb / a.reads,
