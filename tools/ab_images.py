@@ -49,12 +49,13 @@ def main():
     for c in args.config or ["base:"]:
         name, _, opts = c.partition(":")
         kv = [o.split("=", 1) for o in opts.split(",") if o]
+        prev = [(k, sa.get_option(k)) for k, _ in kv]
         for k, v in kv:
             sa.set_option(k, int(v))
         t0 = time.time()
         ix = sa.VoteIndex.build_genome(genome, gap=W.get("gap", 1), memory_mb=8000, force_one_block=True, device=0)
-        for k, _ in kv:
-            sa.set_option(k, 0)
+        for k, v in prev:   # back to what it was (options read at index load only)
+            sa.set_option(k, v)
         print("[ab] %s: index %.1f GB in %.1fs" % (name, ix.info.device_bytes / 1e9, time.time() - t0),
               file=sys.stderr, flush=True)
         configs.append({"name": name, "opts": dict((k, int(v)) for k, v in kv), "ix": ix, "ms": [], "dev_ms": []})
