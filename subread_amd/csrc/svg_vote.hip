@@ -1863,6 +1863,37 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 #define IMG_LINE  0
 #define IMG_CODE  1
 #define IMG_KHASH 2
+// a probe's record from its bucket's 32-byte code (q: key / nb, the key_hi the code counts):
+// the equal-key run's bounds by two selects on the code's zero bits, gehash_go_X's binary search
+// replayed on them for the first-hit midpoint; count byte 255 = the big-bucket list
+__device__ __forceinline__ void code_record(const uint4 u0, const uint4 u1, uint32_t q, uint32_t key, uint2 &rec, bool &big,
+                                            unsigned long long &st_i, unsigned long long &st_h)
+{
+	const uint32_t c = u0.y & 255u, first = u0.x;
+	big = c == 255u;
+	if (!big && c) {
+		const uint64_t z[4] = {~(((uint64_t)u0.y << 32) | u0.x) & ~0xffffffffffull, ~(((uint64_t)u0.w << 32) | u0.z),
+		                       ~(((uint64_t)u1.y << 32) | u1.x), ~(((uint64_t)u1.w << 32) | u1.z)};
+		const int k = (int)q;
+		const int fe = k ? code_zero(z, k - 1) - 40 - (k - 1) : 0;
+		const int ee = code_zero(z, k) - 40 - k;   // items with key_hi <= k
+		st_i += c;
+		if (ee > fe) {
+			const int le = ee - 1;
+			int lo = 0, hi = (int)c - 1, m;
+			for (;;) {
+				m = (lo + hi) >> 1;
+				if (m < fe) lo = m + 1;
+				else if (m > le) hi = m - 1;
+				else break;
+			}
+			rec = make_uint2(first + (uint32_t)m, (uint32_t)(le - m + 1) | ((uint32_t)(m - fe) << 16));
+			st_h += (unsigned)(ee - fe);
+		}
+	}
+	if (big) rec = make_uint2(key, 0xffffffffu);
+}
+
 template <int ENDS, bool PACKED, int IMG>
 __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 {
@@ -1879,7 +1910,59 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 	// contiguous group ranges per block: neighbouring reads stay on one XCD's L2
 	for (uint32_t g = blockIdx.x * per_blk; g < g_end; g++) {
 		const uint32_t r0 = g * G, nr = min(G, n - r0), np = nr * per_read, npr = (np + 255u) & ~255u;
-		for (uint32_t i = threadIdx.x; i < npr; i += 256u) {
+		// bucket code: two probes per thread and pass -- both keys, then both 32-byte code loads in
+		// flight together, then both decodes (the decode's selects and search replay no longer sit
+		// between one probe's load and the next one's)
+		if constexpr (IMG == IMG_CODE) for (uint32_t i0 = threadIdx.x; i0 < npr; i0 += 512u) {
+			const bool two = i0 + 256u < npr;   // block-uniform (npr is a multiple of 256)
+			uint32_t key[2] = {0u, 0u}, outidx[2] = {0u, 0u}, q[2] = {0u, 0u};
+			bool ok[2] = {false, false};
+#pragma unroll
+			for (int t = 0; t < 2; t++) {
+				const uint32_t i = i0 + 256u * (uint32_t)t;
+				if (i < np && (t == 0 || two)) {
+					const uint32_t rl = i / per_read, rem = i - rl * per_read, r = r0 + rl;
+					const int e = ENDS == 2 ? (int)(rem / (2 * nps)) : 0;
+					const uint32_t rem2 = rem - (uint32_t)e * 2 * nps;
+					const int s = rem2 >= nps ? 1 : 0;
+					const int p = (int)(rem2 - (uint32_t)s * nps);
+					outidx[t] = pp.soa ? rem * n + r : r * per_read + rem;
+					ok[t] = probe_key<ENDS, PACKED>(pp, r, e, s, p, key[t]);
+				}
+			}
+			uint4 u0[2], u1[2];
+#pragma unroll
+			for (int t = 0; t < 2; t++) {
+				u0[t] = u1[t] = make_uint4(0u, 0u, 0u, 0u);
+				if (ok[t]) {
+					q[t] = (uint32_t)__umul64hi((uint64_t)key[t], pp.nb_magic);
+					const uint4 *c4 = ix.bcode + 2 * (size_t)(key[t] - q[t] * ix.nb);
+					u0[t] = c4[0];
+					u1[t] = c4[1];
+				}
+			}
+#pragma unroll
+			for (int t = 0; t < 2; t++) {
+				if (t == 1 && !two) break;
+				const uint32_t i = i0 + 256u * (uint32_t)t;
+				uint2 rec = make_uint2(0u, 0u);
+				bool big = false;
+				if (ok[t]) {
+					st_p++;
+					code_record(u0[t], u1[t], q[t], key[t], rec, big, st_i, st_h);
+				}
+				const unsigned long long bm = ballot(big);
+				if (bm) {
+					const int leader = __ffsll((long long)bm) - 1;
+					uint32_t base = 0;
+					if (lane_id() == leader) base = atomicAdd(&s_big, (uint32_t)__popcll(bm));
+					base = __shfl(base, leader);
+					if (big) big_list[base + lanes_below(bm)] = outidx[t];
+				}
+				if (i < np) srec[i] = rec;
+			}
+		}
+		if constexpr (IMG != IMG_CODE) for (uint32_t i = threadIdx.x; i < npr; i += 256u) {
 			uint2 rec = make_uint2(0u, 0u);
 			bool big = false;
 			uint32_t outidx = 0;
@@ -1891,7 +1974,6 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 				const int p = (int)(rem2 - (uint32_t)s * nps);
 				outidx = pp.soa ? rem * n + r : r * per_read + rem;
 				uint32_t key;
-				constexpr bool CODE = IMG == IMG_CODE;
 				if (IMG == IMG_KHASH && probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
 					// the key's record from its 64-byte line (and the overflow chain)
 					st_p++;
@@ -1901,37 +1983,6 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 					}
 					khash_find(ix, key, rec);
 					if (pp.stats) st_h += (rec.y & 0xffffu) + (rec.y >> 16);
-				} else if (CODE && probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
-					const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
-					const uint32_t b = key - q * ix.nb;
-					// the bucket's 32-byte code: first item, count, unary key_hi counts
-					const uint4 *c4 = ix.bcode + 2 * (size_t)b;
-					const uint4 u0 = c4[0], u1 = c4[1];
-					const uint32_t c = u0.y & 255u, first = u0.x;
-					st_p++;
-					big = c == 255u;
-					if (!big && c) {
-						const uint64_t z[4] = {~(((uint64_t)u0.y << 32) | u0.x) & ~0xffffffffffull,
-						                       ~(((uint64_t)u0.w << 32) | u0.z), ~(((uint64_t)u1.y << 32) | u1.x),
-						                       ~(((uint64_t)u1.w << 32) | u1.z)};
-						const int k = (int)q;
-						const int fe = k ? code_zero(z, k - 1) - 40 - (k - 1) : 0;
-						const int ee = code_zero(z, k) - 40 - k;   // items with key_hi <= k
-						st_i += c;
-						if (ee > fe) {
-							const int le = ee - 1;
-							int lo = 0, hi = (int)c - 1, m;
-							for (;;) {
-								m = (lo + hi) >> 1;
-								if (m < fe) lo = m + 1;
-								else if (m > le) hi = m - 1;
-								else break;
-							}
-							rec = make_uint2(first + (uint32_t)m, (uint32_t)(le - m + 1) | ((uint32_t)(m - fe) << 16));
-							st_h += (unsigned)(ee - fe);
-						}
-					}
-					if (big) rec = make_uint2(key, 0xffffffffu);
 				} else if (IMG == IMG_LINE && probe_key<ENDS, PACKED>(pp, r, e, s, p, key)) {
 					const uint32_t q = (uint32_t)__umul64hi((uint64_t)key, pp.nb_magic);
 					const uint32_t b = key - q * ix.nb;
