@@ -98,27 +98,32 @@ __device__ __forceinline__ uint64_t khash_line(uint32_t key, uint64_t lines)
 	return ((uint64_t)(key * 0x9E3779B1u) * lines) >> 32;
 }
 
-// the probe record (mid item, fwd | bwd << 16) stored under key in DevIndex::khash; rec is left
-// unchanged (and false returned) when the key has no record
-__device__ __forceinline__ bool khash_find(const DevIndex &ix, uint32_t key, uint2 &rec)
+// one 32-byte key-hash sector (3 entries: keys, midpoints, 8-bit run counts; the top half of the
+// last word flags an overflow into the next sector): the key's record, or *more when the key may
+// continue in the next sector
+__device__ __forceinline__ bool khash_sector(const uint4 a, const uint4 b4, uint32_t key, uint2 &rec, bool &more)
 {
-	if (key == 0xffffffffu) {
-		if (!ix.khash_ff[0]) return false;
-		rec = make_uint2(ix.khash_ff[1], ix.khash_ff[2]);
-		return true;
-	}
-	uint64_t L = khash_line(key, ix.khash_lines);
+	const uint32_t ks[3] = {a.x, a.y, a.z}, mid[3] = {a.w, b4.x, b4.y};
+	const uint32_t fb[3] = {b4.z & 0xffffu, b4.z >> 16, b4.w & 0xffffu};
+	bool found = false;
+#pragma unroll
+	for (int k = 0; k < 3; k++)
+		if (ks[k] == key) { rec = make_uint2(mid[k], (fb[k] & 0xffu) | ((fb[k] >> 8) << 16)); found = true; }
+	more = !found && (b4.w >> 16);
+	return found;
+}
+
+// the probe record (mid item, fwd | bwd << 16) stored under key in DevIndex::khash, looked up from
+// line L on; rec is left unchanged (and false returned) when the key has no record
+__device__ __forceinline__ bool khash_find_from(const DevIndex &ix, uint32_t key, uint64_t L, uint2 &rec)
+{
 	bool found = false;
 	if (ix.khash_sec) {
 		for (;;) {
 			const uint4 *l4 = (const uint4 *)(ix.khash + 8 * L);
-			const uint4 a = l4[0], b4 = l4[1];
-			const uint32_t ks[3] = {a.x, a.y, a.z}, mid[3] = {a.w, b4.x, b4.y};
-			const uint32_t fb[3] = {b4.z & 0xffffu, b4.z >> 16, b4.w & 0xffffu};
-#pragma unroll
-			for (int k = 0; k < 3; k++)
-				if (ks[k] == key) { rec = make_uint2(mid[k], (fb[k] & 0xffu) | ((fb[k] >> 8) << 16)); found = true; }
-			if (found || !(b4.w >> 16)) break;
+			bool more;
+			found = khash_sector(l4[0], l4[1], key, rec, more);
+			if (!more) break;
 			L = L + 1 == ix.khash_lines ? 0 : L + 1;
 		}
 	} else for (;;) {
@@ -134,6 +139,16 @@ __device__ __forceinline__ bool khash_find(const DevIndex &ix, uint32_t key, uin
 		L = L + 1 == ix.khash_lines ? 0 : L + 1;
 	}
 	return found;
+}
+
+__device__ __forceinline__ bool khash_find(const DevIndex &ix, uint32_t key, uint2 &rec)
+{
+	if (key == 0xffffffffu) {
+		if (!ix.khash_ff[0]) return false;
+		rec = make_uint2(ix.khash_ff[1], ix.khash_ff[2]);
+		return true;
+	}
+	return khash_find_from(ix, key, khash_line(key, ix.khash_lines), rec);
 }
 
 #define SVG_MAX_BLOCKS 64

@@ -1962,7 +1962,60 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 				if (i < np) srec[i] = rec;
 			}
 		}
-		if constexpr (IMG != IMG_CODE) for (uint32_t i = threadIdx.x; i < npr; i += 256u) {
+		// key-hash image in 32-byte sectors: the same two-probe pass (first sectors of both probes in
+		// flight together; an overflow chain continues from the next sector)
+		if (IMG == IMG_KHASH && ix.khash_sec) for (uint32_t i0 = threadIdx.x; i0 < npr; i0 += 512u) {
+			const bool two = i0 + 256u < npr;   // block-uniform
+			uint32_t key[2] = {0u, 0u}, outidx[2] = {0u, 0u};
+			uint64_t L[2] = {0u, 0u};
+			bool ok[2] = {false, false};
+#pragma unroll
+			for (int t = 0; t < 2; t++) {
+				const uint32_t i = i0 + 256u * (uint32_t)t;
+				if (i < np && (t == 0 || two)) {
+					const uint32_t rl = i / per_read, rem = i - rl * per_read, r = r0 + rl;
+					const int e = ENDS == 2 ? (int)(rem / (2 * nps)) : 0;
+					const uint32_t rem2 = rem - (uint32_t)e * 2 * nps;
+					const int s = rem2 >= nps ? 1 : 0;
+					const int p = (int)(rem2 - (uint32_t)s * nps);
+					outidx[t] = pp.soa ? rem * n + r : r * per_read + rem;
+					ok[t] = probe_key<ENDS, PACKED>(pp, r, e, s, p, key[t]);
+				}
+			}
+			uint4 a[2], b4[2];
+#pragma unroll
+			for (int t = 0; t < 2; t++) {
+				a[t] = b4[t] = make_uint4(0u, 0u, 0u, 0u);
+				if (ok[t] && key[t] != 0xffffffffu) {
+					L[t] = khash_line(key[t], ix.khash_lines);
+					const uint4 *l4 = (const uint4 *)(ix.khash + 8 * L[t]);
+					a[t] = l4[0];
+					b4[t] = l4[1];
+				}
+			}
+#pragma unroll
+			for (int t = 0; t < 2; t++) {
+				if (t == 1 && !two) break;
+				const uint32_t i = i0 + 256u * (uint32_t)t;
+				uint2 rec = make_uint2(0u, 0u);
+				if (ok[t]) {
+					st_p++;
+					if (pp.stats) {
+						const uint32_t q = (uint32_t)__umul64hi((uint64_t)key[t], pp.nb_magic), b = key[t] - q * ix.nb;
+						st_i += ix.bstart[b + 1] - ix.bstart[b];
+					}
+					if (key[t] == 0xffffffffu) khash_find(ix, key[t], rec);
+					else {
+						bool more;
+						if (!khash_sector(a[t], b4[t], key[t], rec, more) && more)
+							khash_find_from(ix, key[t], L[t] + 1 == ix.khash_lines ? 0 : L[t] + 1, rec);
+					}
+					if (pp.stats) st_h += (rec.y & 0xffffu) + (rec.y >> 16);
+				}
+				if (i < np) srec[i] = rec;   // (the key-hash image has no big-bucket list)
+			}
+		}
+		if (IMG != IMG_CODE && !(IMG == IMG_KHASH && ix.khash_sec)) for (uint32_t i = threadIdx.x; i < npr; i += 256u) {
 			uint2 rec = make_uint2(0u, 0u);
 			bool big = false;
 			uint32_t outidx = 0;
