@@ -216,3 +216,30 @@ def test_calls_on_different_streams_are_ordered(gpu_indexes):
     for c, o, _ in outs:
         got = o.cpu().numpy().reshape(len(c.r1), -1)
         assert (got == c.expected).all(), describe_mismatch(got, c.expected, 1, 3)
+
+
+def test_handles_share_the_device_stream_set(index_cache):
+    """Every handle on a device uses the device's one set of library streams (svg_vote.hip
+    streams_acquire: four streams created back to back, so the chunk pipeline's two kernel
+    streams sit on different hardware queues however many indexes a process holds).  Three
+    handles of two indexes, host-path calls interleaved without synchronisation, handles closed
+    in between (the set lives while any handle does, and is made again after the last close):
+    every call gives the reference's golden records."""
+    import subread_amd as sa
+    a, b = Case("se_full_errmut"), Case("pe_gapped_errmut")
+    for rnd in range(2):
+        h1 = sa.VoteIndex(index_cache.get(a.index_key), device=0)
+        h2 = sa.VoteIndex(index_cache.get(b.index_key), device=0)
+        h3 = sa.VoteIndex(index_cache.get(a.index_key), device=0)
+        try:
+            for k, (h, c) in enumerate(((h1, a), (h2, b), (h3, a), (h2, b), (h1, a))):
+                out, _, _ = h.vote(c.params, c.r1, c.r2)
+                got = pack_records(out, None, None)
+                assert (got == c.expected).all(), "round %d call %d: %s" % (rnd, k, describe_mismatch(got, c.expected, c.ends, 3))
+                if k == 2:
+                    h3.close()
+                    h3 = None
+        finally:
+            for h in (h1, h2, h3):
+                if h is not None:
+                    h.close()
