@@ -1863,6 +1863,12 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 #define IMG_LINE  0
 #define IMG_CODE  1
 #define IMG_KHASH 2
+// probes per thread and pass of the code / key-hash line kernels (their loads in flight
+// together): 3 for single-end packed reads, 2 otherwise -- the most that stay within the 64 VGPRs
+// of 8 waves per SIMD without spilling (4 spills 46 registers)
+template <int ENDS, bool PACKED>
+struct ProbeDepth { static constexpr int value = ENDS == 1 && PACKED ? 3 : 2; };
+
 // a probe's record from its bucket's 32-byte code (q: key / nb, the key_hi the code counts):
 // the equal-key run's bounds by two selects on the code's zero bits, gehash_go_X's binary search
 // replayed on them for the first-hit midpoint; count byte 255 = the big-bucket list
@@ -1910,17 +1916,18 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 	// contiguous group ranges per block: neighbouring reads stay on one XCD's L2
 	for (uint32_t g = blockIdx.x * per_blk; g < g_end; g++) {
 		const uint32_t r0 = g * G, nr = min(G, n - r0), np = nr * per_read, npr = (np + 255u) & ~255u;
-		// bucket code: two probes per thread and pass -- both keys, then both 32-byte code loads in
-		// flight together, then both decodes (the decode's selects and search replay no longer sit
-		// between one probe's load and the next one's)
-		if constexpr (IMG == IMG_CODE) for (uint32_t i0 = threadIdx.x; i0 < npr; i0 += 512u) {
-			const bool two = i0 + 256u < npr;   // block-uniform (npr is a multiple of 256)
-			uint32_t key[2] = {0u, 0u}, outidx[2] = {0u, 0u}, q[2] = {0u, 0u};
-			bool ok[2] = {false, false};
+		// bucket code: ProbeDepth<ENDS, PACKED>::value probes per thread and pass -- their keys, then their 32-byte code loads
+		// in flight together, then their decodes (the decode's selects and search replay no longer
+		// sit between one probe's load and the next one's)
+		if constexpr (IMG == IMG_CODE) for (uint32_t i0 = threadIdx.x; i0 < npr; i0 += 256u * ProbeDepth<ENDS, PACKED>::value) {
+			uint32_t key[ProbeDepth<ENDS, PACKED>::value], outidx[ProbeDepth<ENDS, PACKED>::value], q[ProbeDepth<ENDS, PACKED>::value];
+			bool ok[ProbeDepth<ENDS, PACKED>::value];
 #pragma unroll
-			for (int t = 0; t < 2; t++) {
+			for (int t = 0; t < ProbeDepth<ENDS, PACKED>::value; t++) {
 				const uint32_t i = i0 + 256u * (uint32_t)t;
-				if (i < np && (t == 0 || two)) {
+				key[t] = outidx[t] = q[t] = 0u;
+				ok[t] = false;
+				if (i < np) {
 					const uint32_t rl = i / per_read, rem = i - rl * per_read, r = r0 + rl;
 					const int e = ENDS == 2 ? (int)(rem / (2 * nps)) : 0;
 					const uint32_t rem2 = rem - (uint32_t)e * 2 * nps;
@@ -1930,9 +1937,9 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 					ok[t] = probe_key<ENDS, PACKED>(pp, r, e, s, p, key[t]);
 				}
 			}
-			uint4 u0[2], u1[2];
+			uint4 u0[ProbeDepth<ENDS, PACKED>::value], u1[ProbeDepth<ENDS, PACKED>::value];
 #pragma unroll
-			for (int t = 0; t < 2; t++) {
+			for (int t = 0; t < ProbeDepth<ENDS, PACKED>::value; t++) {
 				u0[t] = u1[t] = make_uint4(0u, 0u, 0u, 0u);
 				if (ok[t]) {
 					q[t] = (uint32_t)__umul64hi((uint64_t)key[t], pp.nb_magic);
@@ -1942,9 +1949,9 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 				}
 			}
 #pragma unroll
-			for (int t = 0; t < 2; t++) {
-				if (t == 1 && !two) break;
+			for (int t = 0; t < ProbeDepth<ENDS, PACKED>::value; t++) {
 				const uint32_t i = i0 + 256u * (uint32_t)t;
+				if (i - threadIdx.x >= npr) break;   // block-uniform (npr is a multiple of 256)
 				uint2 rec = make_uint2(0u, 0u);
 				bool big = false;
 				if (ok[t]) {
@@ -1962,17 +1969,19 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 				if (i < np) srec[i] = rec;
 			}
 		}
-		// key-hash image in 32-byte sectors: the same two-probe pass (first sectors of both probes in
-		// flight together; an overflow chain continues from the next sector)
-		if (IMG == IMG_KHASH && ix.khash_sec) for (uint32_t i0 = threadIdx.x; i0 < npr; i0 += 512u) {
-			const bool two = i0 + 256u < npr;   // block-uniform
-			uint32_t key[2] = {0u, 0u}, outidx[2] = {0u, 0u};
-			uint64_t L[2] = {0u, 0u};
-			bool ok[2] = {false, false};
+		// key-hash image in 32-byte sectors: the same pass (the probes' first sectors in flight
+		// together; an overflow chain continues from the next sector)
+		if (IMG == IMG_KHASH && ix.khash_sec) for (uint32_t i0 = threadIdx.x; i0 < npr; i0 += 256u * ProbeDepth<ENDS, PACKED>::value) {
+			uint32_t key[ProbeDepth<ENDS, PACKED>::value], outidx[ProbeDepth<ENDS, PACKED>::value];
+			uint64_t L[ProbeDepth<ENDS, PACKED>::value];
+			bool ok[ProbeDepth<ENDS, PACKED>::value];
 #pragma unroll
-			for (int t = 0; t < 2; t++) {
+			for (int t = 0; t < ProbeDepth<ENDS, PACKED>::value; t++) {
 				const uint32_t i = i0 + 256u * (uint32_t)t;
-				if (i < np && (t == 0 || two)) {
+				key[t] = outidx[t] = 0u;
+				L[t] = 0u;
+				ok[t] = false;
+				if (i < np) {
 					const uint32_t rl = i / per_read, rem = i - rl * per_read, r = r0 + rl;
 					const int e = ENDS == 2 ? (int)(rem / (2 * nps)) : 0;
 					const uint32_t rem2 = rem - (uint32_t)e * 2 * nps;
@@ -1982,9 +1991,9 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 					ok[t] = probe_key<ENDS, PACKED>(pp, r, e, s, p, key[t]);
 				}
 			}
-			uint4 a[2], b4[2];
+			uint4 a[ProbeDepth<ENDS, PACKED>::value], b4[ProbeDepth<ENDS, PACKED>::value];
 #pragma unroll
-			for (int t = 0; t < 2; t++) {
+			for (int t = 0; t < ProbeDepth<ENDS, PACKED>::value; t++) {
 				a[t] = b4[t] = make_uint4(0u, 0u, 0u, 0u);
 				if (ok[t] && key[t] != 0xffffffffu) {
 					L[t] = khash_line(key[t], ix.khash_lines);
@@ -1994,9 +2003,9 @@ __global__ void __launch_bounds__(256, 8) probe_line_kernel(PParams pp)
 				}
 			}
 #pragma unroll
-			for (int t = 0; t < 2; t++) {
-				if (t == 1 && !two) break;
+			for (int t = 0; t < ProbeDepth<ENDS, PACKED>::value; t++) {
 				const uint32_t i = i0 + 256u * (uint32_t)t;
+				if (i - threadIdx.x >= npr) break;   // block-uniform
 				uint2 rec = make_uint2(0u, 0u);
 				if (ok[t]) {
 					st_p++;
