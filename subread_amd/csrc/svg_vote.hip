@@ -1864,10 +1864,10 @@ __global__ void __launch_bounds__(256, BPC) probe_kernel(PParams pp)
 #define IMG_CODE  1
 #define IMG_KHASH 2
 // probes per thread and pass of the code / key-hash line kernels (their loads in flight
-// together): 3 for single-end packed reads, 2 otherwise -- the most that stay within the 64 VGPRs
-// of 8 waves per SIMD without spilling (4 spills 46 registers)
+// together): 2 -- C3 0.976 -> 0.913 ms per launch, 469.6 Mreads/s (profiles/r04/bench_c3_probe2.json);
+// 3 measured the same (0.920 ms, 467.0, bench_c3_r4i.json) and 4 spills 46 registers at 8 waves/SIMD
 template <int ENDS, bool PACKED>
-struct ProbeDepth { static constexpr int value = ENDS == 1 && PACKED ? 3 : 2; };
+struct ProbeDepth { static constexpr int value = 2; };
 
 // a probe's record from its bucket's 32-byte code (q: key / nb, the key_hi the code counts):
 // the equal-key run's bounds by two selects on the code's zero bits, gehash_go_X's binary search
