@@ -1524,30 +1524,34 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	for (int k = 0; k < 4; k++) W.why[k] = 0;
 	W.t_last = __builtin_amdgcn_s_memtime();
 #endif
-	// direct: reads gw, gw+nw, ...; indirect: the deferred reads idx[gw], idx[gw+nw], ...
-	// deferred reads differ widely in cost (repeat families): taken from a work counter
+	// direct: reads gw, gw+nw, ...; indirect: the deferred reads idx[pos].  Deferred reads differ
+	// widely in cost (repeat families): the first three quarters of the list are dealt out
+	// statically (positions gw, gw+nw, ... below n_static: no atomic), the rest come from the work
+	// counter, one read ahead (the atomic's result is consumed a whole read later).  Each loop
+	// trip knows the current and the next position; the next read's index is needed for its
+	// prefetch (run_read), the position after it is computed or requested during the read.
 	const uint64_t n = kp.idx ? (uint64_t)*kp.idx_count : kp.n_reads;
-	// (the next index is grabbed one read ahead, so the atomic's latency hides behind a read)
-	uint64_t i, in;
-	if (kp.idx) {
+	const uint64_t n_static = kp.idx ? (n * 3 / 4) / nw * nw : n;
+	auto grab = [&]() -> uint64_t {   // a dynamic position, synchronously (twice per wave at most)
 		uint32_t a = 0;
-		if (lane_id() == 0) a = atomicAdd(kp.work, 2u);
-		i = (uint64_t)(uint32_t)__shfl((int)a, 0);
-		in = i + 1;
-	} else {
-		i = gw;
-		in = gw + nw;
-	}
+		if (lane_id() == 0) a = atomicAdd(kp.work, 1u);
+		return n_static + (uint64_t)(uint32_t)__shfl((int)a, 0);
+	};
+	auto dyn_after = [&](uint64_t p) { return kp.idx && p + nw >= n_static; };   // p's successor is dynamic
+	uint64_t i = !kp.idx || gw < n_static ? gw : (n ? grab() : n);
+	uint64_t in = i >= n ? n : (dyn_after(i) ? grab() : i + nw);
 	uint64_t r = i < n ? (kp.idx ? kp.idx[i] : i) : 0;
 	if (i < n) { W.prefetch_text(r); W.prefetch_recs(r); }
 	while (i < n) {
+		const bool dyn = in < n && dyn_after(in);
 		uint32_t nxt = 0;
-		if (kp.idx && lane_id() == 0) nxt = atomicAdd(kp.work, 1u);   // consumed after this read
+		if (dyn && lane_id() == 0) nxt = atomicAdd(kp.work, 1u);   // consumed after this read
 		const uint64_t rn = in < n ? (kp.idx ? kp.idx[in] : in) : kp.n_reads;
 		W.run_read(r, rn);
+		const uint64_t in2 = in >= n ? n : (dyn ? n_static + (uint64_t)(uint32_t)__shfl((int)nxt, 0) : in + nw);
 		i = in;
 		r = rn;
-		in = kp.idx ? (uint64_t)(uint32_t)__shfl((int)nxt, 0) : in + nw;
+		in = in2;
 #ifdef SVG_STAMPS
 		{ unsigned long long _t = __builtin_amdgcn_s_memtime(); W.acc[5] += _t - W.t_last; W.t_last = _t; }
 #endif
