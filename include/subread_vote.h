@@ -378,6 +378,8 @@ int  svg_cpulist_parse(const char *list, uint8_t *mask, int max);
  *   no_bcode, no_khash, khash64, no_bline, no_compact, kinline, khash_probe, probe_v1,
  *   no_window, probe_colmajor   probe images / probe kernel variants picked at index load
  *   wave_cap                    resident wave-kernel blocks per CU beside the next chunk
+ *   wave_static                 eighths (0-8) of a chunk's deferred reads the wave kernel deals
+ *                               out statically before its work counter (default 6)
  *   keys_literal, long_probes   svg_probe_keys / svg_long_vote_batch variants
  *   debug, pipe_debug, long_debug  diagnostics on stderr
  * svg_set_option returns SVG_E_ARG for an unknown name; svg_get_option returns the current value

@@ -256,6 +256,7 @@ struct KParams {
 	const uint32_t *idx;      // NULL: reads 0..n_reads-1; else the reads idx[0..*idx_count) (deferred by lane_kernel)
 	const uint32_t *idx_count;
 	uint32_t *work;           // indirect mode: zeroed work counter (waves grab deferred reads dynamically)
+	int32_t static_eighths;   // indirect mode: eighths of the deferred reads dealt out statically
 	int stored;               // records already hold earlier index blocks' results (multi-block, block > 0)
 	uint32_t *err;            // sticky device error word (svg_device_status): bit 0 = a read needs more
 	                          // probes than the announced read-length bound provides, bit 1 = a read
