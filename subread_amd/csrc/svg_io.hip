@@ -641,7 +641,22 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		if ((rc = host_ensure((void **)&io->h_stage[s], &io->h_stage_cap[s], CL.bytes, io->node))) return rc;
 	}
 	const int saved_len = h->max_read_len;
-	const uint64_t nsub = (n + sub - 1) / sub;
+	// sub-batch boundaries: full sub-batches, ramped at both ends (sub/4, sub/2 first and last) when
+	// the batch holds at least 8 of them -- the pipeline fills with a short upload and drains with
+	// a short wave kernel + compaction + download + expansion after the last probe kernel; option
+	// host_ramp 0 = uniform sub-batches
+	std::vector<uint64_t> sb{0};
+	{
+		const bool ramp = svg_get_option("host_ramp") != 0 && n >= 8 * sub && sub >= 64;
+		const uint64_t q4 = sub / 4, q2 = sub / 2;
+		if (ramp) { sb.push_back(q4); sb.push_back(q4 + q2); }
+		const uint64_t tail = ramp ? q2 + q4 : 0, body_end = n - tail;
+		while (sb.back() < body_end) sb.push_back(sb.back() + sub < body_end ? sb.back() + sub : body_end);
+		if (ramp) { sb.push_back(body_end + q2); sb.push_back(n); }
+	}
+	const uint64_t nsub = sb.size() - 1;
+	auto sb_b = [&](uint64_t k) { return sb[k]; };
+	auto sb_m = [&](uint64_t k) { return sb[k + 1] - sb[k]; };
 	hipStream_t st = h->stream;
 	if (h->last_pending) HIPCHK(hipStreamWaitEvent(st, h->ev_last, 0));
 	for (int k = 0; k < h->nblocks; k++) {
@@ -662,7 +677,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		HIPCHK(hipEventSynchronize(h->ev_done[s3]));
 		if (dbg) w_done += now() - t0;
 		const uint64_t cnt_rec = io->h_cnt[4 * s3], cnt_j = io->h_cnt[4 * s3 + 1];
-		const uint64_t m = j + 1 < nsub ? sub : n - j * sub;
+		const uint64_t m = sb_m(j);
 		const CompLayout C = comp_layout(m, R, ends, jo, bmo);
 		t0 = dbg ? now() : 0;
 		io->pool->wait(s3);   // staging slot free: expansion of sub-batch j-3 done
@@ -680,7 +695,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	auto expand = [&](uint64_t k) -> int {
 		const int s3 = (int)(k % 3);
 		HIPCHK(hipEventSynchronize(h->ev_down[s3]));
-		const uint64_t b = k * sub, m = k + 1 < nsub ? sub : n - b;
+		const uint64_t b = sb_b(k), m = sb_m(k);
 		const CompLayout C = comp_layout(m, R, ends, jo, bmo);
 		const uint8_t *stg = io->h_stage[s3];
 		const uint32_t tiles = C.tiles, per_job = 128;   // 8192 reads per job
@@ -740,7 +755,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	} up[3];
 	auto upload = [&](uint64_t u) -> int {
 		const int s3 = (int)(u % 3);
-		const uint64_t b = u * sub, m = u + 1 < nsub ? sub : n - b;
+		const uint64_t b = sb_b(u), m = sb_m(u);
 		Up &U = up[s3];
 		memset(&U, 0, sizeof U);
 		int rc2;
@@ -804,7 +819,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		if (i >= nsub) goto tail;
 		{
 		const int s = (int)(i & 1), s3 = (int)(i % 3);
-		const uint64_t b = i * sub, m = i + 1 < nsub ? sub : n - b;
+		const uint64_t b = sb_b(i), m = sb_m(i);
 		double tu = dbg ? now() : 0;
 		if (i + 1 < nsub && (rc = upload(i + 1))) break;
 		if (dbg) { w_up += now() - tu; tu = now(); }

@@ -71,9 +71,12 @@ def test_compacted_pipeline_small_subbatches(mode, entry, gpu_indexes, index_cac
     ref, rj, rbm, _ = OracleIndex(pre).vote(p, r1, r2, threads=16)
     want = pack_records(ref, rj if mode == "sj" else None, rbm if mode == "sj" else None)
     ix = gpu_indexes(key)
-    for sub, th in (("3001", "1"), ("7777", "3"), ("64", "8")):
+    # (2000 and 64: the ramped schedule -- sub/4, sub/2, full ones, the remainder, sub/2, sub/4;
+    # 3001 / 7777 and host_ramp 0: uniform sub-batches)
+    for sub, th, ramp in (("3001", "1", 1), ("7777", "3", 1), ("64", "8", 1), ("2000", "4", 1), ("2000", "2", 0)):
         svgopt.set("host_sub", int(sub))
         svgopt.set("host_threads", int(th))
+        svgopt.set("host_ramp", ramp)
         if entry == "ascii":
             out, jout, bm = ix.vote(p, r1, r2)
         else:
