@@ -1530,44 +1530,28 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	// counter, one read ahead (the atomic's result is consumed a whole read later).  Each loop
 	// trip knows the current and the next position; the next read's index is needed for its
 	// prefetch (run_read), the position after it is computed or requested during the read.
-	// (positions are 32-bit and wave-uniform -- readfirstlane keeps them in scalar registers)
-	auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
-	const uint32_t n = uni(kp.idx ? *kp.idx_count : (uint32_t)kp.n_reads);
-	const uint32_t w0 = (uint32_t)gw, wn = (uint32_t)nw;
-	const uint32_t n_static = kp.idx ? (uint32_t)(((uint64_t)n * (uint32_t)kp.static_eighths / 8u) / wn * wn) : n;
-	auto grab = [&]() -> uint32_t {   // a dynamic position, synchronously (twice per wave at most)
+	const uint64_t n = kp.idx ? (uint64_t)*kp.idx_count : kp.n_reads;
+	const uint64_t n_static = kp.idx ? (n * (uint64_t)kp.static_eighths / 8) / nw * nw : n;
+	auto grab = [&]() -> uint64_t {   // a dynamic position, synchronously (twice per wave at most)
 		uint32_t a = 0;
 		if (lane_id() == 0) a = atomicAdd(kp.work, 1u);
-		return n_static + uni((uint32_t)__shfl((int)a, 0));
+		return n_static + (uint64_t)(uint32_t)__shfl((int)a, 0);
 	};
-	auto dyn_after = [&](uint32_t p) { return kp.idx && p + wn >= n_static; };   // p's successor is dynamic
-	// the read indices of this wave's static positions w0 + k*wn, k < 64, loaded together up front:
-	// lane k holds the k-th, so a read's successor index is a lane read, not a dependent load at
-	// the start of every read (k: the position's static step, carried along)
-	uint32_t my_idx = 0;
-	const uint32_t n_mine = kp.idx && w0 < n_static ? (n_static - w0 + wn - 1) / wn : 0u;
-	if ((uint32_t)lane_id() < n_mine) my_idx = kp.idx[w0 + (uint32_t)lane_id() * wn];
-	auto idx_at = [&](uint32_t p, uint32_t k) -> uint32_t {
-		if (!kp.idx) return p;
-		if (p < n_static && k < 64u) return (uint32_t)__builtin_amdgcn_readlane((int)my_idx, (int)k);
-		return kp.idx[p];
-	};
-	uint32_t i = !kp.idx || w0 < n_static ? w0 : (n ? grab() : n), ki = 0;
-	uint32_t in = i >= n ? n : (dyn_after(i) ? grab() : i + wn), kin = 1;
-	uint64_t r = i < n ? idx_at(i, ki) : 0;
+	auto dyn_after = [&](uint64_t p) { return kp.idx && p + nw >= n_static; };   // p's successor is dynamic
+	uint64_t i = !kp.idx || gw < n_static ? gw : (n ? grab() : n);
+	uint64_t in = i >= n ? n : (dyn_after(i) ? grab() : i + nw);
+	uint64_t r = i < n ? (kp.idx ? kp.idx[i] : i) : 0;
 	if (i < n) { W.prefetch_text(r); W.prefetch_recs(r); }
 	while (i < n) {
 		const bool dyn = in < n && dyn_after(in);
 		uint32_t nxt = 0;
 		if (dyn && lane_id() == 0) nxt = atomicAdd(kp.work, 1u);   // consumed after this read
-		const uint64_t rn = in < n ? idx_at(in, kin) : kp.n_reads;
+		const uint64_t rn = in < n ? (kp.idx ? kp.idx[in] : in) : kp.n_reads;
 		W.run_read(r, rn);
-		const uint32_t in2 = in >= n ? n : (dyn ? n_static + uni((uint32_t)__shfl((int)nxt, 0)) : in + wn);
+		const uint64_t in2 = in >= n ? n : (dyn ? n_static + (uint64_t)(uint32_t)__shfl((int)nxt, 0) : in + nw);
 		i = in;
-		ki = kin;
 		r = rn;
-		in = uni(in2);
-		kin = ki + 1;
+		in = in2;
 #ifdef SVG_STAMPS
 		{ unsigned long long _t = __builtin_amdgcn_s_memtime(); W.acc[5] += _t - W.t_last; W.t_last = _t; }
 #endif
