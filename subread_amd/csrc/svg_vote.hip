@@ -32,6 +32,7 @@
 // the cold part (coverage start/end, 21-entry indel recorder) lives in a
 // per-wave HBM scratch that stays L2-resident.  Integer work only: no MFMA.
 #include <hip/hip_runtime.h>
+#include <vector>
 #include <pthread.h>
 #include <stdint.h>
 #include <string.h>
@@ -3254,9 +3255,21 @@ static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads 
 		fprintf(stderr, "[svg] batch of %llu reads: chunks of %llu, chunk pipeline %s\n", (unsigned long long)n,
 		        (unsigned long long)chunk, overlap ? "on" : "off");
 	bool slot_busy[2] = {false, false};
-	for (uint64_t c0 = 0; c0 < n && !rc; c0 += chunk) {
-		const uint64_t cn = n - c0 < chunk ? n - c0 : chunk;
-		const int slot = overlap ? (int)((c0 / chunk) & 1) : 0;
+	// chunk boundaries: ramped at both ends (chunk/4, chunk/2 first and last, option host_ramp) when
+	// the batch holds at least 8 chunks -- the second stream gets work sooner and the last wave
+	// kernel, which nothing overlaps, is short
+	std::vector<uint64_t> cb{0};
+	{
+		const bool ramp = overlap && svg_get_option("host_ramp") != 0 && n >= 8 * chunk && chunk >= 64;
+		const uint64_t q4 = chunk / 4, q2 = chunk / 2;
+		if (ramp) { cb.push_back(q4); cb.push_back(q4 + q2); }
+		const uint64_t body_end = n - (ramp ? q2 + q4 : 0);
+		while (cb.back() < body_end) cb.push_back(cb.back() + chunk < body_end ? cb.back() + chunk : body_end);
+		if (ramp) { cb.push_back(body_end + q2); cb.push_back(n); }
+	}
+	for (size_t k = 0; k + 1 < cb.size() && !rc; k++) {
+		const uint64_t c0 = cb[k], cn = cb[k + 1] - cb[k];
+		const int slot = overlap ? (int)(k & 1) : 0;
 		if (slot_busy[slot]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[slot], 0));
 		rc = svg_vote_chunk(h, &job, c0, cn, slot, st, st2);
 		if (!rc && overlap) {

@@ -135,7 +135,11 @@ def _to_dev(a, dev):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).to(dev)
 
 
-def test_packed_device_entry(gpu_indexes):
+@pytest.mark.parametrize("chunking", ["default", "ramped", "flat"])
+def test_packed_device_entry(chunking, gpu_indexes, svgopt):
+    """svg_vote_batch_packed_device on the golden pairs, with the default chunk (one chunk) and
+    with small chunks on the two-stream chunk pipeline -- ramped at both ends (chunk/4, chunk/2
+    first and last) or uniform (host_ramp 0)."""
     import torch
     import subread_amd as sa
     from subread_amd.abi import SvgPackedReads
@@ -160,6 +164,11 @@ def test_packed_device_entry(gpu_indexes):
         keep.append(t)
         return q
     n, mb = len(c.r1), c.params.multi_best
+    if chunking != "default":
+        assert n >= 8 * 97
+        svgopt.set("chunk", 97)
+        svgopt.set("overlap", 1)
+        svgopt.set("host_ramp", 1 if chunking == "ramped" else 0)
     ix.set_max_read_length(int(max(c.r1.lens.max(), c.r2.lens.max())))
     for stride in (None, 100):
         d_out = torch.zeros(n * 2 * mb * 68, dtype=torch.uint8, device=dev)
