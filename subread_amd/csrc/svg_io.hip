@@ -584,7 +584,7 @@ extern "C" int svg_vote_batch_packed_device(svg_index *h, const svg_params *p, c
 }
 
 // ============================================================================ the host pipeline
-// Sub-batch i (<= one probe-record chunk) in device slot s = i & 1:
+// Sub-batch i (<= one probe-record chunk) in device slot s = i % 3 (option host_slots 2: i & 1):
 //   up_stream : upload of the reads into d_in[s]
 //   stream    : [unpack] + probe + lane kernels             (svg_vote_chunk)
 //   stream2   : wave kernel + record compaction + counts    (single-end align: beside the next
@@ -595,7 +595,7 @@ extern "C" int svg_vote_batch_packed_device(svg_index *h, const svg_params *p, c
 //               writing the compact records into mapped host memory from the compaction kernel
 //               itself measured slower: 237 vs 318 Mreads/s at C3, the PCIe-bound kernel then
 //               sits on the wave kernels' stream)
-// Device slots are reused by sub-batch i+2 once ev_done (vote + compaction) has fired, compact
+// Device slots are reused by sub-batch i+3 (i+2) once ev_done (vote + compaction) has fired, compact
 // slots by i+3 once ev_down (download) has, a staging slot once its expansion jobs are done.
 static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1, const svg_reads *a2,
                          const svg_packed_reads *q1, const svg_packed_reads *q2, svg_mapping_result *out,
@@ -634,7 +634,10 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	const size_t rec_b = (size_t)R * 68, j_b = jo ? (size_t)R * 16 : 0, bm_b = bmo ? (size_t)ends * SVG_BIG_MARGIN_WORDS * 2 : 0;
 	const CompLayout CL = comp_layout(sub, R, ends, jo, bmo);
 	const size_t o_j = (sub * rec_b + 255) & ~(size_t)255, o_bm = (o_j + sub * j_b + 255) & ~(size_t)255;
-	for (int s = 0; s < 2; s++)
+	// device slots (probe records, lane lists, full records): 3 by default, so the first stream
+	// may run two sub-batches ahead of the second (option host_slots 2: one)
+	const int NS = svg_get_option("host_slots") == 2 ? 2 : 3;
+	for (int s = 0; s < NS; s++)
 		if ((rc = svg_ensure(h, &h->d_out[s], &h->d_out_cap[s], o_bm + sub * bm_b + 64))) return rc;
 	for (int s = 0; s < 3; s++) {
 		if ((rc = svg_ensure(h, &io->d_comp[s], &io->d_comp_cap[s], CL.bytes))) return rc;
@@ -818,7 +821,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	for (uint64_t i = 0; i < nsub + 3 && !rc; i++) {
 		if (i >= nsub) goto tail;
 		{
-		const int s = (int)(i & 1), s3 = (int)(i % 3);
+		const int s = (int)(i % (uint64_t)NS), s3 = (int)(i % 3);
 		const uint64_t b = sb_b(i), m = sb_m(i);
 		double tu = dbg ? now() : 0;
 		if (i + 1 < nsub && (rc = upload(i + 1))) break;
@@ -830,7 +833,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 		uint8_t *din = (uint8_t *)h->d_in[s3];
 		// ---- vote on stream (probe, lane) / stream2 (wave); slot s free once sub-batch i-2 is done
 		HIPCHK(hipStreamWaitEvent(st, h->ev_up[s3], 0));
-		if (i >= 2) HIPCHK(hipStreamWaitEvent(st, h->ev_done[(i - 2) % 3], 0));
+		if (i >= (uint64_t)NS) HIPCHK(hipStreamWaitEvent(st, h->ev_done[(i - NS) % 3], 0));
 		h->max_read_len = U.maxlen;
 		svg_reads dr[2];
 		svg_packed_reads pk[2];
