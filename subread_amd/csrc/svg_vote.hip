@@ -3065,7 +3065,7 @@ int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, con
 	if (chunk < 1) chunk = 1;
 	job->chunk = chunk;
 	// chunk pipeline: the wave kernel of chunk c runs on stream2 while the probe and lane kernels
-	// of chunk c+1 run on st; slot c & 1 holds a chunk's probe records and lane buffers until its
+	// of chunk c+1 run on st; slot c % 3 holds a chunk's probe records and lane buffers until its
 	// wave kernel is done.  On by default for single-end align only (C3: 289 -> 304 Mreads/s; PE
 	// and subjunc, whose wave kernels are 2-3x longer, lost 1-2%: the kernels time-share the CUs
 	// there).  Option "overlap" 0/1 forces it off/on.
@@ -3254,7 +3254,10 @@ static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads 
 	if (svg_get_option("debug"))
 		fprintf(stderr, "[svg] batch of %llu reads: chunks of %llu, chunk pipeline %s\n", (unsigned long long)n,
 		        (unsigned long long)chunk, overlap ? "on" : "off");
-	bool slot_busy[2] = {false, false};
+	// chunk slots (probe records, lane lists): 3 (option host_slots 2), so the probe / lane stream
+	// may run two chunks ahead of the wave kernel's
+	const int NS = svg_get_option("host_slots") == 2 ? 2 : 3;
+	bool slot_busy[3] = {false, false, false};
 	// chunk boundaries: ramped at both ends (chunk/4, chunk/2 first and last, option host_ramp) when
 	// the batch holds at least 8 chunks -- the second stream gets work sooner and the last wave
 	// kernel, which nothing overlaps, is short
@@ -3269,7 +3272,7 @@ static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads 
 	}
 	for (size_t k = 0; k + 1 < cb.size() && !rc; k++) {
 		const uint64_t c0 = cb[k], cn = cb[k + 1] - cb[k];
-		const int slot = overlap ? (int)(k & 1) : 0;
+		const int slot = overlap ? (int)(k % (size_t)NS) : 0;
 		if (slot_busy[slot]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[slot], 0));
 		rc = svg_vote_chunk(h, &job, c0, cn, slot, st, st2);
 		if (!rc && overlap) {
@@ -3278,7 +3281,7 @@ static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads 
 		}
 	}
 	// join: the caller's stream sees every wave kernel of the batch
-	for (int s = 0; s < 2 && overlap; s++)
+	for (int s = 0; s < NS && overlap; s++)
 		if (slot_busy[s]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[s], 0));
 	if (rc) return rc;
 	HIPCHK(hipEventRecord(h->ev_last, st));
