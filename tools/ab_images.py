@@ -30,6 +30,8 @@ def main():
                     help="name:opt=v,opt=v (options applied while this configuration's index is built)")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--device", action="store_true", help="also alternate the HBM-resident entry")
+    ap.add_argument("--hipmalloc", action="store_true",
+                    help="HBM-resident entry: records into a hipMalloc'd array instead of a torch tensor")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -79,7 +81,18 @@ def main():
         tl = torch.from_numpy(pk.lens.view(np.uint8)).to(dev)
         q = SvgPackedReads()
         q.bases, q.lens, q.xmask, q.starts, q.stride, q.n_reads = tb.data_ptr(), tl.data_ptr(), None, None, pk.stride, n
-        d_out = torch.empty(n * MAPPING_DTYPE.itemsize * p.multi_best, dtype=torch.uint8, device=dev)
+        if args.hipmalloc:
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            ptr = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(ptr), ctypes.c_size_t(n * MAPPING_DTYPE.itemsize * p.multi_best)) == 0
+
+            class _Raw:
+                def data_ptr(self):
+                    return ptr.value
+            d_out = _Raw()
+        else:
+            d_out = torch.empty(n * MAPPING_DTYPE.itemsize * p.multi_best, dtype=torch.uint8, device=dev)
         for c in configs:
             c["ix"].set_max_read_length(L)
 
