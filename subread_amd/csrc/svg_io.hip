@@ -381,8 +381,8 @@ extern "C" void svg_host_free(void *p)
 struct svg_hostio {
 	SvgPool *pool;
 	uint32_t *d_cnt;                         // [slot][4]: compact mapping / subjunc record counts
-	void *d_text[2]; size_t d_text_cap[2];   // unpacked reads (packed input), per device slot
-	void *d_offs[2]; size_t d_offs_cap[2];
+	void *d_text[3]; size_t d_text_cap[3];   // unpacked reads (packed input), per device slot
+	void *d_offs[3]; size_t d_offs_cap[3];
 	void *d_comp[3]; size_t d_comp_cap[3];   // compacted sub-batch (same layout as a staging slot)
 	uint32_t *h_cnt;                         // pinned [slot][4] (3 slots): compact record counts
 	uint8_t *h_stage[3]; size_t h_stage_cap[3];   // pinned host staging of compacted sub-batches
@@ -397,7 +397,7 @@ void svg_io_free(svg_index *h)
 	if (!io) return;
 	delete io->pool;
 	hipFree(io->d_cnt);
-	for (int s = 0; s < 2; s++) {
+	for (int s = 0; s < 3; s++) {
 		hipFree(io->d_text[s]);
 		hipFree(io->d_offs[s]);
 	}
@@ -502,6 +502,7 @@ static int launch_unpack(svg_index *h, svg_hostio *io, int slot, uint64_t stride
                          const uint32_t *xmask, const uint64_t *starts, const uint16_t *lens, uint64_t m, int maxlen,
                          int end, svg_reads *dr, hipStream_t st)
 {
+	if (slot < 0 || slot > 2) { svg_set_error("chunk slot %d out of range", slot); return SVG_E_ARG; }   // [3]-slot buffers
 	// text of end e at [e * m * S, (e + 1) * m * S) of the slot's buffer, offsets likewise
 	const uint32_t S = (uint32_t)((maxlen + 3) & ~3);
 	size_t need = 2 * m * (size_t)S + 2048, needo = 2 * m * 8 + 64;

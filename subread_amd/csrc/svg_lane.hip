@@ -1647,6 +1647,7 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
                       const uint64_t *off1, const char *seq2, const uint64_t *off2, unsigned long long *stats,
                       uint32_t **defer_list, uint32_t **defer_count, hipStream_t st)
 {
+	if (slot < 0 || slot > 2) { svg_set_error("chunk slot %d out of range", slot); return SVG_E_ARG; }   // [3]-slot buffers
 	const size_t o_l1 = 0, o_cnt = (o_l1 + (size_t)4 * n + 255) & ~(size_t)255, need = o_cnt + 256;
 	if (need > h->lane_cap[slot]) {
 		hipFree(h->d_lane[slot]);
@@ -1727,6 +1728,7 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
                    uint8_t *out, uint8_t *jout, uint16_t *bm, const char *seq, const uint64_t *off,
                    unsigned long long *stats, uint32_t **defer_list, uint32_t **defer_count, hipStream_t st)
 {
+	if (slot < 0 || slot > 2) { svg_set_error("chunk slot %d out of range", slot); return SVG_E_ARG; }   // [3]-slot buffers
 	// buffers: cand/cpk/cnt over n columns (unfused gather), deferral list, counters, count bins
 	const size_t o_c1 = 0, o_p1 = o_c1 + (size_t)8 * LANE_CAP1 * n, o_n1 = o_p1 + (size_t)4 * LANE_CAP1 * n;
 	const size_t o_l1 = (o_n1 + (size_t)4 * n + 255) & ~(size_t)255;

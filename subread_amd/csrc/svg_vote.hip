@@ -3099,6 +3099,7 @@ int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slo
 
 int svg_vote_chunk_probe(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slot, hipStream_t st)
 {
+	if (slot < 0 || slot > 2) { svg_set_error("chunk slot %d out of range", slot); return SVG_E_ARG; }   // [3]-slot buffers
 	const KParams &kp = job->kp;
 	int rc;
 	if ((rc = svg_ensure(h, &h->d_prec[slot], &h->prec_cap[slot], cn * job->per_read * 8))) return rc;
