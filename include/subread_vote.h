@@ -379,7 +379,7 @@ int  svg_cpulist_parse(const char *list, uint8_t *mask, int max);
  *   no_window, probe_colmajor   probe images / probe kernel variants picked at index load
  *   wave_cap                    resident wave-kernel blocks per CU beside the next chunk
  *   host_ramp                   host-buffer entries: sub-batches ramped at both ends (default 1)
- *   host_slots                  host-buffer entries: device slots per sub-batch ring, 2 or 3 (default)
+ *   host_slots                  device slots of the chunk pipeline, 2 (default) or 3
  *   wave_static                 eighths (0-8) of a chunk's deferred reads the wave kernel deals
  *                               out statically before its work counter (default 6)
  *   keys_literal, long_probes   svg_probe_keys / svg_long_vote_batch variants

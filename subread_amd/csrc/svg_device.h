@@ -169,7 +169,8 @@ struct svg_index {
 	int wave_cap;   // > 0: blocks per CU cap of the wave kernel (set while it overlaps the probe kernel)
 	int max_read_len;        // announced read-length bound (svg_set_max_read_length), picks the kernel variant
 	// chunk pipeline: probe + lane kernels of chunk c run on the caller's stream while the wave
-	// kernel of chunk c-1 runs on stream2, so the per-chunk buffers come in three slots (c % 3)
+	// kernel of chunk c-1 runs on stream2, so the per-chunk buffers come in two slots (c & 1; three
+	// with option host_slots 3)
 	hipStream_t stream2;
 	hipEvent_t ev_lane[3], ev_wave[3], ev_probe[3];   // slot's records + deferral list ready / wave kernel done / probe records ready
 	void *d_prec[3]; size_t prec_cap[3];   // probe records of one chunk

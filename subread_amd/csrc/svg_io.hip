@@ -585,7 +585,7 @@ extern "C" int svg_vote_batch_packed_device(svg_index *h, const svg_params *p, c
 }
 
 // ============================================================================ the host pipeline
-// Sub-batch i (<= one probe-record chunk) in device slot s = i % 3 (option host_slots 2: i & 1):
+// Sub-batch i (<= one probe-record chunk) in device slot s = i & 1 (option host_slots 3: i % 3):
 //   up_stream : upload of the reads into d_in[s]
 //   stream    : [unpack] + probe + lane kernels             (svg_vote_chunk)
 //   stream2   : wave kernel + record compaction + counts    (single-end align: beside the next
@@ -596,7 +596,7 @@ extern "C" int svg_vote_batch_packed_device(svg_index *h, const svg_params *p, c
 //               writing the compact records into mapped host memory from the compaction kernel
 //               itself measured slower: 237 vs 318 Mreads/s at C3, the PCIe-bound kernel then
 //               sits on the wave kernels' stream)
-// Device slots are reused by sub-batch i+3 (i+2) once ev_done (vote + compaction) has fired, compact
+// Device slots are reused by sub-batch i+2 (i+3) once ev_done (vote + compaction) has fired, compact
 // slots by i+3 once ev_down (download) has, a staging slot once its expansion jobs are done.
 static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1, const svg_reads *a2,
                          const svg_packed_reads *q1, const svg_packed_reads *q2, svg_mapping_result *out,
@@ -635,9 +635,12 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	const size_t rec_b = (size_t)R * 68, j_b = jo ? (size_t)R * 16 : 0, bm_b = bmo ? (size_t)ends * SVG_BIG_MARGIN_WORDS * 2 : 0;
 	const CompLayout CL = comp_layout(sub, R, ends, jo, bmo);
 	const size_t o_j = (sub * rec_b + 255) & ~(size_t)255, o_bm = (o_j + sub * j_b + 255) & ~(size_t)255;
-	// device slots (probe records, lane lists, full records): 3 by default, so the first stream
-	// may run two sub-batches ahead of the second (option host_slots 2: one)
-	const int NS = svg_get_option("host_slots") == 2 ? 2 : 3;
+	// device slots (probe records, lane lists, full records): 2 -- the probe / lane stream runs one
+	// sub-batch ahead of the wave kernel's.  Option host_slots 3 lets it run two ahead: measured
+	// 114.4-114.9 vs 101.9-102.2 ms/step at C3 (profiles/r04/n/sweep_slots.txt) -- the probe kernel
+	// speeds up, but the lane and wave kernels then read probe records that no longer sit in the
+	// 256 MB infinity cache (160 MB per sub-batch)
+	const int NS = svg_get_option("host_slots") == 3 ? 3 : 2;
 	for (int s = 0; s < NS; s++)
 		if ((rc = svg_ensure(h, &h->d_out[s], &h->d_out_cap[s], o_bm + sub * bm_b + 64))) return rc;
 	for (int s = 0; s < 3; s++) {

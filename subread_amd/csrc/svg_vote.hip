@@ -3065,7 +3065,7 @@ int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, con
 	if (chunk < 1) chunk = 1;
 	job->chunk = chunk;
 	// chunk pipeline: the wave kernel of chunk c runs on stream2 while the probe and lane kernels
-	// of chunk c+1 run on st; slot c % 3 holds a chunk's probe records and lane buffers until its
+	// of chunk c+1 run on st; slot c & 1 holds a chunk's probe records and lane buffers until its
 	// wave kernel is done.  On by default for single-end align only (C3: 289 -> 304 Mreads/s; PE
 	// and subjunc, whose wave kernels are 2-3x longer, lost 1-2%: the kernels time-share the CUs
 	// there).  Option "overlap" 0/1 forces it off/on.
@@ -3255,9 +3255,9 @@ static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads 
 	if (svg_get_option("debug"))
 		fprintf(stderr, "[svg] batch of %llu reads: chunks of %llu, chunk pipeline %s\n", (unsigned long long)n,
 		        (unsigned long long)chunk, overlap ? "on" : "off");
-	// chunk slots (probe records, lane lists): 3 (option host_slots 2), so the probe / lane stream
-	// may run two chunks ahead of the wave kernel's
-	const int NS = svg_get_option("host_slots") == 2 ? 2 : 3;
+	// chunk slots (probe records, lane lists): 2, as in the host pipeline (option host_slots 3:
+	// measured slower there -- the records must stay in the infinity cache)
+	const int NS = svg_get_option("host_slots") == 3 ? 3 : 2;
 	bool slot_busy[3] = {false, false, false};
 	// chunk boundaries: ramped at both ends (chunk/4, chunk/2 first and last, option host_ramp) when
 	// the batch holds at least 8 chunks -- the second stream gets work sooner and the last wave
