@@ -638,8 +638,8 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	// device slots (probe records, lane lists, full records): 2 -- the probe / lane stream runs one
 	// sub-batch ahead of the wave kernel's.  Option host_slots 3 lets it run two ahead: measured
 	// 114.4-114.9 vs 101.9-102.2 ms/step at C3 (profiles/r04/n/sweep_slots.txt) -- the probe kernel
-	// speeds up, but the lane and wave kernels then read probe records that no longer sit in the
-	// 256 MB infinity cache (160 MB per sub-batch)
+	// speeds up, the lane and wave kernels slow down more (more kernels on the CUs at once; the
+	// probe records, 160 MB per sub-batch, outlive the 256 MB infinity cache)
 	const int NS = svg_get_option("host_slots") == 3 ? 3 : 2;
 	for (int s = 0; s < NS; s++)
 		if ((rc = svg_ensure(h, &h->d_out[s], &h->d_out_cap[s], o_bm + sub * bm_b + 64))) return rc;
