@@ -381,7 +381,8 @@ int  svg_cpulist_parse(const char *list, uint8_t *mask, int max);
  *   host_ramp                   host-buffer entries: sub-batches ramped at both ends (default 1)
  *   host_slots                  device slots of the chunk pipeline, 2 (default) or 3
  *   wave_static                 eighths (0-8) of a chunk's deferred reads the wave kernel deals
- *                               out statically before its work counter (default 6)
+ *                               out statically before its work counter (default 6 single-end,
+ *                               0 pairs)
  *   keys_literal, long_probes   svg_probe_keys / svg_long_vote_batch variants
  *   debug, pipe_debug, long_debug  diagnostics on stderr
  * svg_set_option returns SVG_E_ARG for an unknown name; svg_get_option returns the current value

@@ -3202,9 +3202,12 @@ int svg_vote_chunk_vote(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, in
 		kc.idx = dl;
 		kc.idx_count = dc;
 		kc.work = dc + 2;
-		{   // option wave_static: eighths of the deferral list dealt out without the work counter
+		{   // option wave_static: eighths of the deferral list dealt out without the work counter.
+			// Single-end: 6 (C3 1.67 -> 1.535 ms per wave-kernel launch); pairs, whose deferred
+			// reads cost far more and vary more: 0, all from the counter (C4 with 6: 272 vs 235
+			// ms/step, profiles/r04/r/bench_c4.json)
 			const int64_t ws = svg_get_option("wave_static");
-			kc.static_eighths = ws >= 0 && ws <= 8 ? (int32_t)ws : 6;
+			kc.static_eighths = ws >= 0 && ws <= 8 ? (int32_t)ws : (ends == 1 ? 6 : 0);
 		}
 	}
 	if (st2 != st) {
