@@ -378,6 +378,7 @@ int  svg_cpulist_parse(const char *list, uint8_t *mask, int max);
  *   no_bcode, no_khash, khash64, no_bline, no_compact, kinline, khash_probe, probe_v1,
  *   no_window, probe_colmajor   probe images / probe kernel variants picked at index load
  *   wave_cap                    resident wave-kernel blocks per CU beside the next chunk
+ *   probe_cap                   probe line kernel grid, blocks per CU (default 32)
  *   host_ramp                   host-buffer entries: sub-batches ramped at both ends (default 1)
  *   host_slots                  device slots of the chunk pipeline, 2 (default) or 3
  *   wave_static                 eighths (0-8) of a chunk's deferred reads the wave kernel deals

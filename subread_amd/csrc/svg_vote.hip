@@ -3129,7 +3129,9 @@ int svg_vote_chunk_probe(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, i
 		if (pp.group > 64) pp.group = 64;
 		if (pp.group < 1) pp.group = 1;
 		const uint64_t ng = (cn + pp.group - 1) / pp.group;
-		uint64_t gb = ng, gmax = (uint64_t)h->n_cu * 8 * 4;
+		// grid: 32 blocks per CU (4 rounds of the 8 resident); option probe_cap sets blocks per CU
+		const int64_t pc = svg_get_option("probe_cap");
+		uint64_t gb = ng, gmax = (uint64_t)h->n_cu * (pc > 0 ? (uint64_t)pc : 32u);
 		if (gb > gmax) gb = gmax;
 		// one list region per line-kernel block, sized for all of its probes; per-block counts
 		const uint64_t per_blk = (ng + gb - 1) / gb, stride = per_blk * pp.group * job->per_read;
