@@ -379,6 +379,9 @@ int  svg_cpulist_parse(const char *list, uint8_t *mask, int max);
  *   no_window, probe_colmajor   probe images / probe kernel variants picked at index load
  *   wave_cap                    resident wave-kernel blocks per CU beside the next chunk
  *   probe_cap                   probe line kernel grid, blocks per CU (default 32)
+ *   wave_cus, lane_cus_excl     CU masks of the device's streams (read when they are created, at
+ *                               the first index load): the wave-kernel stream on CUs 0..wave_cus-1,
+ *                               the probe / lane stream on the others with lane_cus_excl 1
  *   host_ramp                   host-buffer entries: sub-batches ramped at both ends (default 1)
  *   host_slots                  device slots of the chunk pipeline, 2 (default) or 3
  *   wave_static                 eighths (0-8) of a chunk's deferred reads the wave kernel deals

@@ -2434,12 +2434,30 @@ static int streams_acquire(svg_index *h)
 	pthread_mutex_lock(&g_streams_mu);
 	int rc = 0;
 	if (!g_streams[h->device].refs) {
-		for (int k = 0; k < 4 && !rc; k++)
-			if (hipStreamCreateWithFlags(&g_streams[h->device].s[k], hipStreamNonBlocking) != hipSuccess) {
+		// options wave_cus = K (0: off): the second stream (wave kernel, compaction) runs on CUs
+		// 0..K-1 only; lane_cus_excl 1: the first stream (probe, lane kernels) on the others
+		hipDeviceProp_t prop;
+		const int ncu = hipGetDeviceProperties(&prop, h->device) == hipSuccess ? prop.multiProcessorCount : 0;
+		const int64_t K = svg_get_option("wave_cus");
+		uint32_t mask[2][32];
+		const bool masked = K > 0 && K < ncu && ncu <= 1024;
+		if (masked) {
+			memset(mask, 0, sizeof mask);
+			for (int c = 0; c < ncu; c++) mask[c < K ? 1 : 0][c >> 5] |= 1u << (c & 31);
+		}
+		const bool excl = masked && svg_get_option("lane_cus_excl") != 0;
+		for (int k = 0; k < 4 && !rc; k++) {
+			hipError_t e;
+			if (masked && (k == 1 || (k == 0 && excl)))
+				e = hipExtStreamCreateWithCUMask(&g_streams[h->device].s[k], (uint32_t)((ncu + 31) / 32), mask[k == 1 ? 1 : 0]);
+			else
+				e = hipStreamCreateWithFlags(&g_streams[h->device].s[k], hipStreamNonBlocking);
+			if (e != hipSuccess) {
 				svg_set_error("hipStreamCreate failed");
 				rc = SVG_E_DEVICE;
 				for (int j = 0; j < k; j++) hipStreamDestroy(g_streams[h->device].s[j]);
 			}
+		}
 	}
 	if (!rc) {
 		g_streams[h->device].refs++;
