@@ -654,12 +654,20 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	// host_ramp 0 = uniform sub-batches
 	std::vector<uint64_t> sb{0};
 	{
-		const bool ramp = svg_get_option("host_ramp") != 0 && n >= 8 * sub && sub >= 64;
-		const uint64_t q4 = sub / 4, q2 = sub / 2;
-		if (ramp) { sb.push_back(q4); sb.push_back(q4 + q2); }
-		const uint64_t tail = ramp ? q2 + q4 : 0, body_end = n - tail;
+		// (host_ramp 2: 1/8, 1/4, 1/2 at both ends)
+		const int64_t rl = svg_get_option("host_ramp");
+		const bool ramp = rl != 0 && n >= 8 * sub && sub >= 64;
+		std::vector<uint64_t> steps;   // the ramp's sub-batch sizes, smallest first
+		if (ramp) {
+			if (rl >= 2) steps.push_back(sub / 8);
+			steps.push_back(sub / 4);
+			steps.push_back(sub / 2);
+		}
+		uint64_t tail = 0;
+		for (uint64_t x : steps) { sb.push_back(sb.back() + x); tail += x; }
+		const uint64_t body_end = n - tail;
 		while (sb.back() < body_end) sb.push_back(sb.back() + sub < body_end ? sb.back() + sub : body_end);
-		if (ramp) { sb.push_back(body_end + q2); sb.push_back(n); }
+		for (size_t k = steps.size(); k-- > 0;) sb.push_back(sb.back() + steps[k]);
 	}
 	const uint64_t nsub = sb.size() - 1;
 	auto sb_b = [&](uint64_t k) { return sb[k]; };
