@@ -1581,7 +1581,9 @@ __global__ void __launch_bounds__(256) lane_bin_kernel(LParams lp)
 //                   it saves (64-slot tables: 5 waves/CU, long row walks, and most repeat-family
 //                   reads still overflow), so the wave kernel takes pass 1's deferrals directly.
 // ---------------------------------------------------------------------------------------------
+#ifndef LANE_K1
 #define LANE_K1 20   // slots per lane: 10 KB LDS per wave = the 4 waves/SIMD the VGPRs allow
+#endif
 #define LANE_NPF 10   // probe records per strand held in registers by the fused light pass
 #define LANE_NPF_SJ 14   // subjunc: -n 14
 #define LANE_CAP1 40
