@@ -1582,7 +1582,11 @@ __global__ void __launch_bounds__(256) lane_bin_kernel(LParams lp)
 //                   reads still overflow), so the wave kernel takes pass 1's deferrals directly.
 // ---------------------------------------------------------------------------------------------
 #ifndef LANE_K1
-#define LANE_K1 20   // slots per lane: 10 KB LDS per wave = the 4 waves/SIMD the VGPRs allow
+// slots per lane: 16 = 8 KB LDS per wave.  20 (10 KB) filled the 4 waves/SIMD the VGPRs allow, but
+// beside the wave kernel of the previous chunk (~89 KB of a CU's LDS) the lane kernel then fits 7
+// waves per CU instead of 9: 16 measured faster at C3 in one process, 100.9 vs 106.8 ms/step
+// (profiles/r04/y/ab_k20_vs_k16.txt), though a few more reads need the wave kernel
+#define LANE_K1 16
 #endif
 #define LANE_NPF 10   // probe records per strand held in registers by the fused light pass
 #define LANE_NPF_SJ 14   // subjunc: -n 14
