@@ -1584,8 +1584,9 @@ __global__ void __launch_bounds__(256) lane_bin_kernel(LParams lp)
 #ifndef LANE_K1
 // slots per lane: 16 = 8 KB LDS per wave.  20 (10 KB) filled the 4 waves/SIMD the VGPRs allow, but
 // beside the wave kernel of the previous chunk (~89 KB of a CU's LDS) the lane kernel then fits 7
-// waves per CU instead of 9: 16 measured faster at C3 in one process, 100.9 vs 106.8 ms/step
-// (profiles/r04/y/ab_k20_vs_k16.txt), though a few more reads need the wave kernel
+// waves per CU instead of 8: 16 measured faster at C3 in one process, 99.8 vs 101.8 ms/step with
+// either build first (profiles/r04/z/ab_k20_vs_k16.txt, r04/y/), though 3% more reads need the
+// wave kernel (5.94M vs 5.77M per 50M)
 #define LANE_K1 16
 #endif
 #define LANE_NPF 10   // probe records per strand held in registers by the fused light pass
