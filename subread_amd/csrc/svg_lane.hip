@@ -1589,6 +1589,11 @@ __global__ void __launch_bounds__(256) lane_bin_kernel(LParams lp)
 // wave kernel (5.94M vs 5.77M per 50M)
 #define LANE_K1 16
 #endif
+// subjunc and the unfused (gather kernel) path keep 20: a deferred subjunc read costs the wave
+// kernel far more (C5 with 16: 148.4 vs 164.8 Mreads/s, profiles/r04/aa/bench_c5.json)
+#ifndef LANE_K1_WIDE
+#define LANE_K1_WIDE 20
+#endif
 #define LANE_NPF 10   // probe records per strand held in registers by the fused light pass
 #define LANE_NPF_SJ 14   // subjunc: -n 14
 #define LANE_CAP1 40
@@ -1810,8 +1815,8 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 			else hipLaunchKernelGGL(lane_bin_kernel<LANE_NPF>, dim3((unsigned)bb), dim3(256), 0, st, lp);
 			HIPCHK(hipGetLastError());
 		}
-		if (!fused) rc = lane_launch<LANE_K1, 0>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
-		else if (sjm) rc = lane_launch<LANE_K1, LANE_NPF_SJ>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
+		if (!fused) rc = lane_launch<LANE_K1_WIDE, 0>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
+		else if (sjm) rc = lane_launch<LANE_K1_WIDE, LANE_NPF_SJ>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
 		else rc = lane_launch<LANE_K1, LANE_NPF>(h, lp, &h->d_lscratch, &h->lscratch_words, st);
 	}
 	if (rc) return rc;
