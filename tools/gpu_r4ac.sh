@@ -8,3 +8,4 @@ for wl in c5 c3g; do
   timeout -k 10 400 python -u bench.py --workload $wl --steps 5 --warmup 2 --no-cpu --ascii-reads 0 --long-reads 0 --device-steps 3 \
     > gpurun_out/r4ac/bench_$wl.json 2> gpurun_out/r4ac/bench_$wl.err || exit $?
 done
+timeout -k 10 400 python -u tools/ab_libs.py c3 10 subread_amd/lib/libsubread_amd_k12.so subread_amd/lib/libsubread_amd.so > gpurun_out/r4ac/ab_k12_vs_k16.txt 2>&1
