@@ -45,6 +45,11 @@ int  svg_sam_writer_begin_chunk(svg_sam_writer *w, int64_t n_fragments);
  * this fragment.  Thread-safe; never waits for other producers. */
 int  svg_sam_writer_put(svg_sam_writer *w, int64_t fragment, int location, int all_locations,
                         const char *text, size_t len);
+/* the complete text of `count` consecutive fragments first .. first+count-1 (all their
+ * locations, in order) in one put: the same as putting each fragment whole, with one lock
+ * round trip.  A producer that owns a run of fragments (svg_realign_chunk's workers take blocks
+ * of them) puts the run this way.  Empty text is allowed (fragments that write nothing). */
+int  svg_sam_writer_put_block(svg_sam_writer *w, int64_t first, int64_t count, const char *text, size_t len);
 /* fragments put but not yet written (waiting for an earlier one) */
 int64_t svg_sam_writer_pending(svg_sam_writer *w);
 /* 1 once a write came up short (the reference's output_sam_is_full, core.c:1869-1871) */

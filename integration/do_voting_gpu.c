@@ -311,6 +311,7 @@ static svg_chunk_reads svg_chunk;
  * beside the reference's clocks (oracle/ref_dump_hook.c): reading the chunk, the vote call
  * (packing + GPU), fragile voting, and the per-read tail (slowest thread of each run) */
 static double svg_t_read, svg_t_vote, svg_t_frag, svg_t_tail;
+static double svg_t_realign;   /* the library's iteration two (drop-in build), cumulative */
 static uint64_t *svg_win;       /* svg_win[r] .. svg_win[r+1]: read r's fragile windows in this block */
 
 /* thread 0 (or the only thread): the chunk's reads, the GPU vote (first block's run: every block),
@@ -553,8 +554,8 @@ void svg_sam_finish(void)
 	if (svg_sam && svg_sam_writer_close(svg_sam)) SUBREADprintf("svg_sam_writer_close: %s\n", svg_last_error());
 	svg_sam = NULL;
 	if (getenv("SVG_REF_TIMING"))
-		fprintf(stderr, "SVG_DROPIN_VOTING read_chunk=%.6f vote_call=%.6f fragile=%.6f tail=%.6f\n", svg_t_read, svg_t_vote,
-		        svg_t_frag, svg_t_tail);
+		fprintf(stderr, "SVG_DROPIN_VOTING read_chunk=%.6f vote_call=%.6f fragile=%.6f tail=%.6f realign=%.6f\n", svg_t_read,
+		        svg_t_vote, svg_t_frag, svg_t_tail, svg_t_realign);
 }
 
 /*
@@ -956,6 +957,222 @@ void add_buffered_fragment(global_context_t *gc, thread_context_t *tc, subread_r
  * stay sequential; then every voting thread does the per-read host work of its slice of the
  * chunk (do_voting_gpu_mt).  The device is SVG_DEVICE (default 0).
  */
+
+/*
+ * Iteration two (harness build: core.o's do_iteration_two is weak; the reference's own stays
+ * reachable as ref_do_iteration_two, an alias oracle/Makefile adds).  run_maybe_threads
+ * (core.c:3379-3461) calls do_iteration_two from each of the run's -T threads after the chunk's
+ * anti-supporting read scan and remove_neighbour (core.c:3629-3638); thread 0 (or the only
+ * caller) runs the library's iteration two (include/subread_realign.h, svg_realign_chunk) over
+ * the whole chunk with -T worker threads and the others return at once.  Inputs are the chunk's
+ * reads as fetch_next_read_pair handed them out (the read cache above), the bigtable records,
+ * the reference's merged event table, its value arrays and contig table; outputs go where the
+ * reference's go: SAM lines to the ordered sink, final_counted_reads / junction flanking back
+ * into the event table (add_realignment_event_support, core.c:2364-2379; the VCF / BED writers
+ * read them), the counters into the thread context (core.c:3433-3444), the expected-TLEN state
+ * into the global context.  Configurations the library does not cover (BAM output, colour space,
+ * fusion / long-deletion detection, annotation exon scoring, scRNA input) and SVG_REF_ITER2=1
+ * keep the reference's own iteration two.
+ */
+#include "subread_realign.h"
+
+int ref_do_iteration_two(global_context_t *gc, thread_context_t *tc);
+void print_in_box(int line_width, int is_boundary, int options, char *pattern, ...);
+
+static svg_genome_arrays *svg_it2_g;
+static svg_realign *svg_it2;
+
+static int svg_it2_supported(global_context_t *gc)
+{
+	const char *e = getenv("SVG_REF_ITER2");
+	if (e && e[0] == '1') return 0;
+	return !gc->config.is_BAM_output && gc->config.space_type == GENE_SPACE_BASE && !gc->config.convert_color_to_base &&
+	       !gc->config.do_fusion_detection && !gc->config.do_long_del_detection && !gc->exonic_region_bitmap &&
+	       !gc->config.scRNA_input_mode && !gc->config.do_big_margin_filtering_for_reads &&
+	       gc->input_reads.first_read_file.file_type != GENE_INPUT_BCL && svg_rc.complete == 1 &&
+	       (subread_read_number_t)svg_rc.n == gc->processed_reads_in_chunk &&
+	       !memcmp(&svg_rc.start1, &gc->current_circle_start_position_file1, sizeof svg_rc.start1);
+}
+
+static int svg_it2_setup(global_context_t *gc)
+{
+	if (svg_it2) return 0;
+	svg_value_block blk[100];
+	int nb = gc->index_block_number, b;
+	for (b = 0; b < nb; b++) {
+		gene_value_index_t *v = &gc->all_value_indexes[b];
+		blk[b].values = v->values;
+		blk[b].start_point = v->start_point;
+		blk[b].length = v->length;
+		blk[b].start_base_offset = v->start_base_offset;
+		blk[b].values_bytes = v->values_bytes;
+	}
+	gene_offset_t *ct = &gc->chromosome_table;
+	int rc = svg_genome_arrays_wrap(blk, nb, ct->read_offsets, ct->read_names, MAX_CHROMOSOME_NAME_LEN, (uint32_t)ct->total_offsets,
+	                                ct->padding, 1, &svg_it2_g);
+	if (rc) return rc;
+	svg_realign_params p;
+	memset(&p, 0, sizeof p);
+	p.paired = gc->input_reads.is_paired_end_reads;
+	p.multi_best = gc->config.multi_best_reads;
+	p.reported_multi_best = gc->config.reported_multi_best_reads;
+	p.report_multi_mapping = gc->config.report_multi_mapping_reads;
+	p.min_votes_first = gc->config.minimum_subread_for_first_read;
+	p.min_votes_second = gc->config.minimum_subread_for_second_read;
+	p.experiment_type = gc->config.experiment_type;
+	p.max_mismatch_exonic = gc->config.max_mismatch_exonic_reads;
+	p.max_mismatch_junction = gc->config.max_mismatch_junction_reads;
+	p.min_mapped_fraction = gc->config.min_mapped_fraction;
+	p.show_soft_clipping = gc->config.show_soft_cliping;
+	p.realignment_minimum_variant_distance = gc->config.realignment_minimum_variant_distance;
+	p.limited_tree_scan = gc->config.limited_tree_scan;
+	p.maximise_sensitivity_indel = gc->config.maximise_sensitivity_indel;
+	p.minimum_exonic_subread_fraction = gc->config.minimum_exonic_subread_fraction;
+	p.no_tlen_preference = gc->config.no_TLEN_preference;
+	p.min_pair_distance = gc->config.minimum_pair_distance;
+	p.max_pair_distance = gc->config.maximum_pair_distance;
+	p.is_first_read_reversed = gc->config.is_first_read_reversed;
+	p.is_second_read_reversed = gc->config.is_second_read_reversed;
+	p.do_breakpoint_detection = gc->config.do_breakpoint_detection;
+	p.ignore_unmapped_reads = gc->config.ignore_unmapped_reads;
+	p.phred_offset = gc->config.phred_score_format == FASTQ_PHRED64 ? 64 : 33;
+	snprintf(p.read_group_id, sizeof p.read_group_id, "%s", gc->config.read_group_id);
+	rc = svg_realign_create(svg_it2_g, &p, &svg_it2);
+	if (rc) { svg_genome_arrays_close(svg_it2_g); svg_it2_g = NULL; }
+	return rc;
+}
+
+/* chromosome_event_t <-> svg_event: the fields iteration two reads and writes */
+static int svg_it2_events_in(global_context_t *gc)
+{
+	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
+	int64_t n = ic->total_events, i;
+	svg_event *ev = calloc((size_t)(n ? n : 1), sizeof(svg_event));
+	if (!ev) return SVG_E_NOMEM;
+	for (i = 0; i < n; i++) {
+		const chromosome_event_t *e = ic->event_space_dynamic + i;
+		svg_event *o = &ev[i];
+		o->small_side = e->event_small_side;
+		o->large_side = e->event_large_side;
+		o->indel_length = e->indel_length;
+		o->junction_flanking_left = e->junction_flanking_left;
+		o->junction_flanking_right = e->junction_flanking_right;
+		o->indel_at_junction = e->indel_at_junction;
+		o->is_negative_strand = e->is_negative_strand;
+		o->is_strand_jumped = e->is_strand_jumped;
+		o->is_donor_found_or_annotation = e->is_donor_found_or_annotation;
+		o->small_side_increasing_coordinate = e->small_side_increasing_coordinate;
+		o->large_side_increasing_coordinate = e->large_side_increasing_coordinate;
+		o->connected_next_event_distance = e->connected_next_event_distance;
+		o->connected_previous_event_distance = e->connected_previous_event_distance;
+		o->supporting_reads = e->supporting_reads;
+		o->anti_supporting_reads = e->anti_supporting_reads;
+		o->final_counted_reads = e->final_counted_reads;
+		o->final_reads_mismatches = e->final_reads_mismatches;
+		o->event_type = e->event_type;
+		o->critical_read_id = e->critical_read_id;
+		o->event_quality = e->event_quality;
+		o->critical_supporting_reads = e->critical_supporting_reads;
+	}
+	int rc = svg_realign_set_events(svg_it2, ev, n);
+	free(ev);
+	return rc;
+}
+
+static int svg_it2_events_out(global_context_t *gc)
+{
+	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
+	int64_t n = ic->total_events, i;
+	svg_event *ev = calloc((size_t)(n ? n : 1), sizeof(svg_event));
+	if (!ev) return SVG_E_NOMEM;
+	int rc = svg_realign_get_events(svg_it2, ev);
+	for (i = 0; !rc && i < n; i++) {
+		chromosome_event_t *e = ic->event_space_dynamic + i;
+		e->final_counted_reads = ev[i].final_counted_reads;
+		e->junction_flanking_left = ev[i].junction_flanking_left;
+		e->junction_flanking_right = ev[i].junction_flanking_right;
+	}
+	free(ev);
+	return rc;
+}
+
+static int svg_iteration_two(global_context_t *gc, thread_context_t *tc)
+{
+	double t0 = miltime();
+	int rc = svg_it2_setup(gc);
+	if (!rc) rc = svg_it2_events_in(gc);
+	const int ends = 1 + gc->input_reads.is_paired_end_reads;
+	const uint64_t n = svg_rc.n;
+	uint64_t *offs = NULL;
+	uint16_t *lens = NULL;
+	if (!rc) {
+		offs = malloc(sizeof(uint64_t) * 3 * (n * ends + 1));
+		lens = malloc(sizeof(uint16_t) * (n * ends + 1));
+		if (!offs || !lens) rc = SVG_E_NOMEM;
+	}
+	if (!rc) {
+		uint64_t r;
+		int e;
+		for (r = 0; r < n; r++)
+			for (e = 0; e < ends; e++) {
+				const uint64_t k = r * ends + e, at = svg_rc.at[r * 2 + e];
+				const int rl = svg_rc.rl[r * 2 + e];
+				offs[k] = at;
+				offs[n * ends + k] = at + strlen(svg_rc.buf + at) + 1;
+				offs[2 * n * ends + k] = offs[n * ends + k] + (uint64_t)rl + 1;
+				lens[k] = (uint16_t)rl;
+			}
+	}
+	svg_sam_writer *sink = NULL;
+	if (!rc) {
+		pthread_mutex_lock(&svg_sam_mu);
+		if (!svg_sam && svg_sam_writer_open(gc->output_sam_fp, &svg_sam)) rc = SVG_E_IO;
+		if (!rc) {
+			rc = svg_sam_writer_begin_chunk(svg_sam, (int64_t)n);
+			gc->last_written_fragment_number = -2;
+			sink = svg_sam;
+		}
+		pthread_mutex_unlock(&svg_sam_mu);
+	}
+	if (!rc) {
+		svg_fragment_reads R = {svg_rc.buf, offs, offs + n * ends, offs + 2 * n * ends, lens, n};
+		svg_realign_stats st;
+		memset(&st, 0, sizeof st);
+		const unsigned int tlen_n0 = gc->expected_TLEN_read_numbers;
+		svg_realign_set_tlen_state(svg_it2, gc->expected_TLEN_read_numbers, (int64_t)gc->expected_TLEN_sum);
+		rc = svg_realign_chunk(svg_it2, &R, (svg_mapping_result *)_global_retrieve_alignment_ptr(gc, 0, 0, 0), sink, NULL, NULL,
+		                       gc->config.all_threads, &st);
+		int64_t tn, ts;
+		svg_realign_get_tlen_state(svg_it2, &tn, &ts);
+		gc->expected_TLEN_read_numbers = (unsigned int)tn;
+		gc->expected_TLEN_sum = (unsigned long long)ts;
+		if (tlen_n0 < READPAIRS_FOR_CALC_EXPT_TLEN && tn >= READPAIRS_FOR_CALC_EXPT_TLEN)
+			print_in_box(80, 0, 0, "  Estimated fragment length : %d bp\n", (int)(gc->expected_TLEN_sum / gc->expected_TLEN_read_numbers));
+		if (!rc) rc = svg_it2_events_out(gc);
+#define SVG_ADD(f) do { if (tc) tc->f += st.f; else gc->f += st.f; } while (0)
+		SVG_ADD(all_mapped_reads); SVG_ADD(all_correct_PE_reads); SVG_ADD(not_properly_pairs_wrong_arrangement);
+		SVG_ADD(not_properly_pairs_different_chro); SVG_ADD(not_properly_different_strands); SVG_ADD(not_properly_pairs_TLEN_wrong);
+		SVG_ADD(all_unmapped_reads); SVG_ADD(not_properly_pairs_only_one_end_mapped); SVG_ADD(all_multimapping_reads);
+		SVG_ADD(all_uniquely_mapped_reads);
+#undef SVG_ADD
+	}
+	free(offs);
+	free(lens);
+	if (rc) {
+		SUBREADprintf("svg iteration two: %s\n", svg_last_error());
+		gc->output_sam_is_full = 1;
+	}
+	svg_t_realign += miltime() - t0;
+	return 0;
+}
+
+int do_iteration_two(global_context_t *gc, thread_context_t *tc)
+{
+	if (!svg_it2_supported(gc)) return ref_do_iteration_two(gc, tc);
+	if (tc && tc->thread_id != 0) return 0;
+	return svg_iteration_two(gc, tc);
+}
+
 int do_voting(global_context_t *gc, thread_context_t *tc)
 {
 	pthread_mutex_lock(&svg_sam_mu_init);

@@ -42,7 +42,11 @@ EXPORTS = [
     "svg_events_anti_support", "svg_events_add_batch2", "svg_events_remove_neighbour", "svg_events_load",
     # SAM emission (include/subread_sam.h)
     "svg_sam_writer_open", "svg_sam_writer_close", "svg_sam_writer_begin_chunk", "svg_sam_writer_put",
-    "svg_sam_writer_pending", "svg_sam_writer_failed", "svg_sam_format",
+    "svg_sam_writer_pending", "svg_sam_writer_failed", "svg_sam_format", "svg_sam_writer_put_block",
+    # iteration two (include/subread_realign.h)
+    "svg_realign_params_default", "svg_realign_create", "svg_realign_destroy", "svg_realign_set_events",
+    "svg_realign_get_events", "svg_realign_set_tlen_state", "svg_realign_get_tlen_state", "svg_realign_chunk",
+    "svg_genome_arrays_contigs", "svg_genome_arrays_wrap",
 ]
 
 _lib = None
@@ -115,6 +119,8 @@ def lib():
         L.svg_sam_writer_begin_chunk.restype = i32
         L.svg_sam_writer_put.argtypes = [vp, ctypes.c_int64, i32, i32, vp, ctypes.c_size_t]
         L.svg_sam_writer_put.restype = i32
+        L.svg_sam_writer_put_block.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, vp, ctypes.c_size_t]
+        L.svg_sam_writer_put_block.restype = i32
         L.svg_sam_writer_pending.argtypes = [vp]
         L.svg_sam_writer_pending.restype = ctypes.c_int64
         L.svg_sam_writer_failed.argtypes = [vp]

@@ -41,28 +41,61 @@ void svg_event_params_default(svg_event_params *e)
 }
 
 /* ------------------------------------------------------------------ base arrays */
-typedef struct {
-	uint32_t start_point, length, start_base_offset, values_bytes;
-	uint8_t *values;
-} garray;
-
-struct svg_genome_arrays {
-	int nblocks;
-	garray *blk;
-	uint32_t n_chr;
-	uint32_t *chr_end;
-	int padding;
-	int gap;               /* index_gap of the first table (1 full, 3 gapped): GENE_SLIDING_STEP */
-};
-
+/* (garray and struct svg_genome_arrays are in svg_internal.h: svg_realign.c reads them too) */
 void svg_genome_arrays_close(svg_genome_arrays *g)
 {
 	int b;
 	if (!g) return;
-	for (b = 0; b < g->nblocks; b++) free(g->blk[b].values);
+	if (g->owned)
+		for (b = 0; b < g->nblocks; b++) free(g->blk[b].values);
 	free(g->blk);
 	free(g->chr_end);
+	free(g->chr_name);
 	free(g);
+}
+
+int svg_genome_arrays_wrap(const svg_value_block *blocks, int nblocks, const uint32_t *chr_end, const char *names,
+                           int name_stride, uint32_t n_chr, int padding, int gap, svg_genome_arrays **out)
+{
+	if (!blocks || nblocks < 1 || !chr_end || !out || (n_chr && !names) || name_stride < 1) {
+		svg_set_error("svg_genome_arrays_wrap: bad argument");
+		return SVG_E_ARG;
+	}
+	svg_genome_arrays *g = calloc(1, sizeof *g);
+	if (!g) { svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	g->blk = calloc((size_t)nblocks, sizeof(garray));
+	g->chr_end = malloc(4 * ((size_t)n_chr + 1));
+	g->chr_name = calloc((size_t)n_chr + 1, SVG_CHR_NAME_LEN);
+	if (!g->blk || !g->chr_end || !g->chr_name) { svg_genome_arrays_close(g); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	for (int b = 0; b < nblocks; b++) {
+		g->blk[b].values = (uint8_t *)blocks[b].values;
+		g->blk[b].start_point = blocks[b].start_point;
+		g->blk[b].length = blocks[b].length;
+		g->blk[b].start_base_offset = blocks[b].start_base_offset;
+		g->blk[b].values_bytes = blocks[b].values_bytes;
+	}
+	g->nblocks = nblocks;
+	g->owned = 0;
+	for (uint32_t c = 0; c < n_chr; c++) {
+		g->chr_end[c] = chr_end[c];
+		snprintf(g->chr_name + (size_t)c * SVG_CHR_NAME_LEN, SVG_CHR_NAME_LEN, "%s", names + (size_t)c * name_stride);
+	}
+	g->n_chr = n_chr;
+	g->padding = padding;
+	g->gap = gap;
+	*out = g;
+	return 0;
+}
+
+int svg_genome_arrays_contigs(const svg_genome_arrays *g, uint32_t *n, const char **names, uint32_t *lengths)
+{
+	if (!g || !n) { svg_set_error("svg_genome_arrays_contigs: NULL argument"); return SVG_E_ARG; }
+	*n = g->n_chr;
+	for (uint32_t c = 0; c < g->n_chr; c++) {
+		if (names) names[c] = g->chr_name + (size_t)c * SVG_CHR_NAME_LEN;
+		if (lengths) lengths[c] = g->chr_end[c] - (c ? g->chr_end[c - 1] : 0) - (uint32_t)g->padding;
+	}
+	return 0;
 }
 
 /* gvindex_load (gene-value-index.c:190-228) per block; load_offsets' .reads table
@@ -79,6 +112,7 @@ int svg_genome_arrays_open(const char *prefix, svg_genome_arrays **out)
 	if (nb < 1) { svg_set_error("index table '%s.00.b.tab' not found", prefix); return SVG_E_IO; }
 	g = calloc(1, sizeof *g);
 	g->blk = calloc((size_t)nb, sizeof(garray));
+	g->owned = 1;
 	g->padding = 1210;
 	for (b = 0; b < nb; b++) {
 		garray *a = &g->blk[b];
@@ -120,13 +154,25 @@ int svg_genome_arrays_open(const char *prefix, svg_genome_arrays **out)
 	snprintf(fn, sizeof fn, "%s.reads", prefix);
 	if (!(fp = fopen(fn, "r"))) { svg_genome_arrays_close(g); svg_set_error("cannot open '%s'", fn); return SVG_E_IO; }
 	{
+		/* load_offsets (gene-algorithms.c:1326-1368): "<end offset>\t<name>" per line, the name
+		 * cut at MAX_CHROMOSOME_NAME_LEN - 1 bytes */
 		char line[4096];
 		uint32_t cap = 64;
 		g->chr_end = malloc(4 * cap);
+		g->chr_name = calloc(cap, SVG_CHR_NAME_LEN);
 		while (fgets(line, sizeof line, fp)) {
-			if (strlen(line) < 2) continue;
-			if (g->n_chr == cap) { cap *= 2; g->chr_end = realloc(g->chr_end, 4 * cap); }
-			g->chr_end[g->n_chr++] = (uint32_t)strtoull(line, NULL, 10);
+			size_t ll = strlen(line);
+			while (ll && (line[ll - 1] == '\n' || line[ll - 1] == '\r')) line[--ll] = 0;
+			if (ll < 2) continue;
+			if (g->n_chr == cap) {
+				cap *= 2;
+				g->chr_end = realloc(g->chr_end, 4 * cap);
+				g->chr_name = realloc(g->chr_name, (size_t)cap * SVG_CHR_NAME_LEN);
+			}
+			g->chr_end[g->n_chr] = (uint32_t)strtoull(line, NULL, 10);
+			char *tab = strchr(line, '\t');
+			snprintf(g->chr_name + (size_t)g->n_chr * SVG_CHR_NAME_LEN, SVG_CHR_NAME_LEN, "%s", tab ? tab + 1 : "");
+			g->n_chr++;
 		}
 	}
 	fclose(fp);
@@ -1295,7 +1341,9 @@ int svg_events_load(svg_events *t, const svg_event *ev, int64_t n)
 	for (int64_t i = 0; i < n; i++) {
 		const uint64_t id = new_event(t);
 		t->ev[id] = ev[i];
-		put_event(t, id);
+		/* an event remove_neighbour already took out of the site lists stays out of them
+		 * (core-indel.c:573-593): it keeps its slot in the array, not in a list */
+		if (ev[i].event_type) put_event(t, id);
 	}
 	return 0;
 }

@@ -3,6 +3,8 @@
 #define SVG_INTERNAL_H
 #include <stdint.h>
 #include "subread_vote.h"
+#include "subread_events.h"
+#include "subread_realign.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -40,6 +42,24 @@ int  svg_index_count_blocks(const char *prefix);
 void svg_host_index_free(svg_host_index *ix);
 
 uint32_t svg_bucket_count(uint64_t expected_items, int gap);
+
+/* host copy (or a wrap, owned = 0) of the index's base arrays and contig table
+ * (subread_events.h svg_genome_arrays_open / subread_realign.h svg_genome_arrays_wrap) */
+#define SVG_CHR_NAME_LEN 200   /* MAX_CHROMOSOME_NAME_LEN */
+typedef struct {
+	uint32_t start_point, length, start_base_offset, values_bytes;
+	uint8_t *values;
+} garray;
+struct svg_genome_arrays {
+	int nblocks;
+	garray *blk;
+	uint32_t n_chr;
+	uint32_t *chr_end;
+	char *chr_name;        /* n_chr x SVG_CHR_NAME_LEN */
+	int padding;
+	int gap;               /* index_gap of the first table (1 full, 3 gapped): GENE_SLIDING_STEP */
+	int owned;             /* the value arrays are freed with the image */
+};
 
 /* normalised genome (check_and_convert_FastA semantics, index-builder.c:789-992) */
 typedef struct svg_contig {

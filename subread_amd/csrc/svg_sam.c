@@ -23,6 +23,7 @@ typedef struct {
 	size_t len, cap;
 	int got;          /* locations put so far */
 	int all;          /* all_locations of the fragment (0: nothing put yet) */
+	int64_t span;     /* fragments the text covers (svg_sam_writer_put_block; 1 otherwise) */
 } sam_slot;
 
 /* A full staging buffer leaves the ring lock as a numbered batch: the thread that detached it
@@ -160,9 +161,11 @@ static int drain(svg_sam_writer *w, sam_batch **out)
 		sam_slot *s = &w->ring[(uint64_t)w->next & (w->size - 1)];
 		if (!s->all || s->got < s->all) break;
 		if (!rc) rc = out_append(w, s->buf, s->len);
+		const int64_t span = s->span > 0 ? s->span : 1;
 		s->len = 0;
 		s->got = s->all = 0;
-		w->next++;
+		s->span = 0;
+		w->next += span;
 		w->pending--;
 	}
 	const int end = w->next == w->chunk_end;
@@ -213,6 +216,57 @@ int svg_sam_writer_put(svg_sam_writer *w, int64_t fragment, int location, int al
 		if (!rc) rc = wr;
 	}
 	if (rc == SVG_E_IO) svg_set_error("svg_sam_writer_put: write failed");
+	else if (rc == SVG_E_NOMEM) svg_set_error("out of memory");
+	return rc;
+}
+
+int svg_sam_writer_put_block(svg_sam_writer *w, int64_t first, int64_t count, const char *text, size_t len)
+{
+	if (!w || first < 0 || count < 1 || (len && !text)) {
+		svg_set_error("svg_sam_writer_put_block: bad argument");
+		return SVG_E_ARG;
+	}
+	int rc = 0;
+	sam_batch *wb = NULL;
+	pthread_mutex_lock(&w->mu);
+	if (first < w->next) {
+		pthread_mutex_unlock(&w->mu);
+		svg_set_error("svg_sam_writer_put_block: fragment %lld was already written", (long long)first);
+		return SVG_E_ARG;
+	}
+	if ((rc = ring_reserve(w, first))) { pthread_mutex_unlock(&w->mu); return rc; }
+	sam_slot *s = &w->ring[(uint64_t)first & (w->size - 1)];
+	if (s->all) {
+		pthread_mutex_unlock(&w->mu);
+		svg_set_error("svg_sam_writer_put_block: fragment %lld was already put", (long long)first);
+		return SVG_E_ARG;
+	}
+	w->pending++;
+	if (first == w->next) {
+		/* the oldest missing fragments arriving whole: straight to the staging buffer */
+		rc = out_append(w, text, len);
+		w->next += count;
+		w->pending--;
+		if (!rc) rc = drain(w, &wb);
+	} else {
+		if (len > s->cap) {
+			size_t nc = len * 2 + 256;
+			char *nb = realloc(s->buf, nc);
+			if (!nb) { w->pending--; pthread_mutex_unlock(&w->mu); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+			s->buf = nb;
+			s->cap = nc;
+		}
+		memcpy(s->buf, text, len);
+		s->len = len;
+		s->got = s->all = 1;
+		s->span = count;
+	}
+	pthread_mutex_unlock(&w->mu);
+	if (wb) {
+		const int wr = batch_write(w, wb);
+		if (!rc) rc = wr;
+	}
+	if (rc == SVG_E_IO) svg_set_error("svg_sam_writer_put_block: write failed");
 	else if (rc == SVG_E_NOMEM) svg_set_error("out of memory");
 	return rc;
 }

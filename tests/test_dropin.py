@@ -1,11 +1,14 @@
 """CPU: the drop-in binding (integration/do_voting_gpu.c) inside the reference's own
 subread-align / subjunc, with the vote answered by the CPU restatement
-(oracle/dropin_oracle.c), gives the stock reference's SAM / VCF / junction BED / event table
-byte for byte.  This pins the binding's host logic -- chunk reading, bigtable layout,
-big-margin staging, the post-vote tail's text/quality orientation, fragile junction voting of
-long subjunc reads, the multi-block run loop, -T > 1 -- apart from the kernels;
-tests/test_gpu_dropin.py runs the same binding with the GPU library.  Needs the binaries
-built from /root/reference (this container; skipped where they are absent)."""
+(oracle/dropin_oracle.c) and iteration two run by the library (svg_realign_chunk,
+include/subread_realign.h -- host C, no GPU), gives the stock reference's SAM / VCF / junction
+BED / event table byte for byte.  This pins the binding's host logic -- chunk reading, bigtable
+layout, big-margin staging, the post-vote tail's text/quality orientation, fragile junction
+voting of long subjunc reads, the multi-block run loop, -T > 1 -- and the library's iteration
+two (realignment against the event table, candidate choice, SAM fields, event support for the
+VCF / BED) apart from the kernels; tests/test_gpu_dropin.py runs the same binding with the GPU
+library.  Needs the binaries built from /root/reference (this container; skipped where they
+are absent)."""
 import os
 
 import pytest
@@ -21,10 +24,14 @@ def cache(tmp_path_factory):
 
 @pytest.mark.parametrize("name,threads", [
     ("pe_gapped_errmut", 1),            # PE align, test-err-mut pairs
+    ("pe_gapped_errmut", 4),            # the same at -T 4 (iteration two's worker threads)
+    ("sj_pe_gapped_junc", 1),           # subjunc PE, junction reads: junction events, XS tags, BED support
     ("sj_pe_gapped_long", 1),           # subjunc PE > 160 bp: fragile junction voting in the binding
     ("sj_pe_mb_long_gappedM6", 1),      # subjunc PE on a 4-block index (block loop)
     ("sj_se_mb_synth_long_fullM1", 1),  # subjunc SE > 160 bp on a 4-block index: fragile windows per block
     ("se_gapped_mixed_n14_I16", 4),     # -n 14 -I 16, N / lowercase / IUPAC, -T 4
+    ("se_mb_synth_fullM1", 1),          # SE on a 4-block index: iteration two's value-index choice per record
+    ("pe_mb_synth_gappedM1", 1),        # PE on a 2-block index
 ])
 def test_oracle_dropin_matches_stock_reference(name, threads, cache, tmp_path):
     c = Case(name)
@@ -113,3 +120,33 @@ def test_oracle_dropin_fastq_layouts_match_stock(trim, cache, tmp_path):
     recs = [l for l in a[""].split(b"\n") if l and not l.startswith(b"@")]
     assert len(recs) == len(c.r1)
     assert sum(1 for l in recs if not int(l.split(b"\t")[1]) & 4) > 0
+
+
+@pytest.mark.parametrize("extra,threads", [
+    (("--multiMapping", "-B", "3"), 4),           # multi-mapping reads: up to 3 locations, HI / NH, MAPQ
+    # no records for unmapped fragments; RG tag (-T 1: the stock aligner hangs at -T > 1 with
+    # --ignoreUnmapped: add_buffered_fragment waits for a fragment that is never written, core.c:2435)
+    (("--ignoreUnmapped", "--rg-id", "grp1", "--rg", "SM:x"), 1),
+    (("-d", "150", "-D", "400", "--noTLENpreference"), 1),
+    (("-M", "1", "--complexIndels"), 1),            # mismatch limit, realignment variant distance 1
+    (("-P", "6",), 1),                               # Phred+64 qualities: converted in the SAM
+])
+def test_oracle_dropin_realign_options(extra, threads, cache, tmp_path):
+    """iteration two's options through the library's realignment: stock vs drop-in, same bytes."""
+    from tests import dropin
+    c = Case("pe_gapped_errmut")
+    if not have(c.meta["program"], "oracle-dropin"):
+        pytest.skip("reference drop-in binaries not built (make -C oracle dropin)")
+    f1, f2 = dropin.fastq_pair(str(tmp_path), c.name, c.r1, c.r2)
+    if "-P" in extra:   # the same reads with Phred+64 qualities
+        for f in (f1, f2):
+            lines = open(f, "rb").read().split(b"\n")
+            for i in range(3, len(lines), 4):
+                lines[i] = bytes(min(b + 31, 126) for b in lines[i])
+            open(f, "wb").write(b"\n".join(lines))
+    pre = cache.get(c.index_key)
+    so, do = str(tmp_path / "stock.sam"), str(tmp_path / "dropin.sam")
+    dropin.run(c.meta["program"], "dump", pre, f1, f2, so, threads, extra)
+    dropin.run(c.meta["program"], "oracle-dropin", pre, f1, f2, do, threads, extra)
+    rep = dropin.compare(so, do)
+    assert rep["mapped"] > 0

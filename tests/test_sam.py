@@ -111,3 +111,82 @@ def test_sam_writer_orders_fragments_across_threads(tmp_path, threads):
     assert L.svg_sam_writer_close(w) == 0
     libc.fclose(fp)
     assert open(path, "rb").read() == b"".join(want)
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_sam_writer_blocks_and_big_chunks(tmp_path, threads):
+    """svg_sam_writer_put_block (the runs of fragments svg_realign_chunk's workers put) mixed with
+    single puts, chunks of more than 8 MB from 8 threads, one fragment larger than 4 MB (the
+    staging buffer's growth) and empty fragments (--ignoreUnmapped writes nothing for a fragment):
+    fragment order, chunk after chunk."""
+    L = sa.lib()
+    rng = random.Random(100 + threads)
+    path = str(tmp_path / "big.sam")
+    fp = libc.fopen(path.encode(), b"w")
+    w = ctypes.c_void_p()
+    assert L.svg_sam_writer_open(fp, ctypes.byref(w)) == 0
+    want = []
+    for chunk in range(2):
+        n = 6000
+        assert L.svg_sam_writer_begin_chunk(w, n) == 0
+        texts = []
+        for k in range(n):
+            if k == 1234 and chunk == 1:
+                t = b"huge %d " % k + b"y" * (5 << 20) + b"\n"
+            elif k % 97 == 0:
+                t = b""
+            else:
+                t = b"c%d f%d %s\n" % (chunk, k, b"x" * rng.randrange(1000, 3000))
+            texts.append(t)
+            want.append(t)
+        # runs of 1..300 fragments, put as blocks (a run of one as a single put), in shuffled order
+        runs, k = [], 0
+        while k < n:
+            m = min(n - k, rng.randrange(1, 300))
+            runs.append((k, m))
+            k += m
+        rng.shuffle(runs)
+        parts = [runs[t::threads] for t in range(threads)]
+        errs = []
+
+        def work(rs):
+            for (b, m) in rs:
+                txt = b"".join(texts[b:b + m])
+                if m == 1 and txt:
+                    rc = L.svg_sam_writer_put(w, b, 0, 1, txt, len(txt))
+                else:
+                    rc = L.svg_sam_writer_put_block(w, b, m, txt, len(txt))
+                if rc:
+                    errs.append((b, m, rc))
+        th = [threading.Thread(target=work, args=(p,)) for p in parts]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs
+        assert L.svg_sam_writer_pending(w) == 0
+    assert L.svg_sam_writer_failed(w) == 0
+    assert L.svg_sam_writer_close(w) == 0
+    libc.fclose(fp)
+    got = open(path, "rb").read()
+    assert len(got) > 16 << 20
+    assert got == b"".join(want)
+
+
+def test_sam_writer_reports_a_failed_write():
+    """A short write (a full device) sets svg_sam_writer_failed and fails the put that wrote it and
+    the close -- the reference's output_sam_is_full (core.c:1869-1871)."""
+    import os
+    if not os.path.exists("/dev/full"):
+        pytest.skip("no /dev/full")
+    L = sa.lib()
+    fp = libc.fopen(b"/dev/full", b"w")
+    w = ctypes.c_void_p()
+    assert L.svg_sam_writer_open(fp, ctypes.byref(w)) == 0
+    assert L.svg_sam_writer_begin_chunk(w, 3) == 0
+    t = b"x" * (3 << 20) + b"\n"
+    rcs = [L.svg_sam_writer_put(w, k, 0, 1, t, len(t)) for k in range(3)]
+    assert any(rcs) or L.svg_sam_writer_failed(w)
+    assert L.svg_sam_writer_failed(w) == 1
+    assert L.svg_sam_writer_close(w) != 0
+    libc.fclose(fp)
