@@ -35,6 +35,7 @@
 #include <string.h>
 #include <pthread.h>
 #include <ctype.h>
+#include <unistd.h>
 #include "subread.h"
 #include "core.h"
 #include "core-indel.h"
@@ -496,9 +497,8 @@ void add_buffered_fragment_svg(global_context_t *gc, thread_context_t *tc, subre
 	int all_locations, int this_location)
 {
 	const int pe = gc->input_reads.is_paired_end_reads;
-	if (gc->config.is_BAM_output) {
-		/* the reference's unordered per-thread BAM path (core.c:1847-1852); ordered BAM output
-		 * (--keepReadOrder) is not taken by this binding */
+	if (gc->config.is_BAM_output && !gc->config.is_input_read_order_required) {
+		/* the reference's unordered per-thread BAM path (core.c:1849-1853) */
 		SamBam_writer_add_read(gc->output_bam_writer, tc->thread_id, read_name1, flags1, chro_name1, chro_position1,
 		                       mapping_quality1, cigar1, next_chro_name1, next_chro_pos1, temp_len1, read_len1, read_text1,
 		                       qual_text1, additional_columns1, !pe);
@@ -508,14 +508,41 @@ void add_buffered_fragment_svg(global_context_t *gc, thread_context_t *tc, subre
 			                       read_text2, qual_text2, additional_columns2, 1);
 		return;
 	}
+	if (gc->config.is_BAM_output) {
+		/* --keepReadOrder with BAM output: the reference's ordered path (core.c:1855-1881) -- wait
+		 * for the fragments before this one, then write through the ordered writer (-1 / -2) */
+		for (;;) {
+			int fin = 0;
+			subread_lock_occupy(&gc->output_lock);
+			if (gc->last_written_fragment_number == pair_number - 1) {
+				SamBam_writer_add_read(gc->output_bam_writer, -1, read_name1, flags1, chro_name1, chro_position1, mapping_quality1,
+				                       cigar1, next_chro_name1, next_chro_pos1, temp_len1, read_len1, read_text1, qual_text1,
+				                       additional_columns1, !pe);
+				if (pe)
+					SamBam_writer_add_read(gc->output_bam_writer, -2, read_name2, flags2, chro_name2, chro_position2, mapping_quality2,
+					                       cigar2, next_chro_name2, next_chro_pos2, temp_len2, read_len2, read_text2, qual_text2,
+					                       additional_columns2, 1);
+				if (all_locations <= this_location + 1) gc->last_written_fragment_number = pair_number;
+				fin = 1;
+			}
+			subread_lock_release(&gc->output_lock);
+			if (fin) return;
+			usleep(2);
+		}
+	}
 	pthread_mutex_lock(&svg_sam_mu);
 	if (!svg_sam && svg_sam_writer_open(gc->output_sam_fp, &svg_sam))
 		SUBREADprintf("svg_sam_writer_open: %s\n", svg_last_error());
 	/* run_maybe_threads sets last_written_fragment_number = -1 before every iteration two
 	 * (core.c:3384-3386), which this function otherwise leaves alone: a new chunk */
 	if (svg_sam && gc->last_written_fragment_number == -1) {
-		if (svg_sam_writer_begin_chunk(svg_sam, gc->processed_reads_in_chunk))
+		if (svg_sam_writer_begin_chunk(svg_sam, gc->processed_reads_in_chunk)) {
+			/* fragments of the last chunk never completed (a fragment that was never put): the
+			 * reference's error path for a short output (output_sam_is_full) rather than a
+			 * silently truncated SAM */
 			SUBREADprintf("svg_sam_writer_begin_chunk: %s\n", svg_last_error());
+			gc->output_sam_is_full = 1;
+		}
 		gc->last_written_fragment_number = -2;
 	}
 	pthread_mutex_unlock(&svg_sam_mu);
@@ -549,13 +576,17 @@ void add_buffered_fragment_svg(global_context_t *gc, thread_context_t *tc, subre
 
 /* the sink is flushed at each chunk's last fragment; closed (and its FILE* flushed) once the
  * run is over -- the harness calls this from its end-of-run hook */
-void svg_sam_finish(void)
+int svg_sam_finish(void)
 {
-	if (svg_sam && svg_sam_writer_close(svg_sam)) SUBREADprintf("svg_sam_writer_close: %s\n", svg_last_error());
+	int rc = 0;
+	/* a fragment never put (or a short write) fails the run as the reference's output_sam_is_full
+	 * does (destroy_global_context, core.c:4270-4275: no output file, exit status 1) */
+	if (svg_sam && (rc = svg_sam_writer_close(svg_sam))) SUBREADprintf("svg_sam_writer_close: %s\n", svg_last_error());
 	svg_sam = NULL;
 	if (getenv("SVG_REF_TIMING"))
 		fprintf(stderr, "SVG_DROPIN_VOTING read_chunk=%.6f vote_call=%.6f fragile=%.6f tail=%.6f realign=%.6f\n", svg_t_read,
 		        svg_t_vote, svg_t_frag, svg_t_tail, svg_t_realign);
+	return rc;
 }
 
 /*

@@ -143,11 +143,11 @@ int __real_write_indel_final_results(global_context_t *global_context);
  * write_indel_final_results (core.c:1220) once, after the last chunk, so the clocks are final
  * here; the wall clock of the whole run so far (start_time, core.c:4013) is printed beside them. */
 /* the drop-in's ordered SAM sink (integration/do_voting_gpu.c), when linked */
-void svg_sam_finish(void) __attribute__((weak));
+int svg_sam_finish(void) __attribute__((weak));
 
 int __wrap_write_indel_final_results(global_context_t *gc)
 {
-	if (svg_sam_finish) svg_sam_finish();
+	if (svg_sam_finish && svg_sam_finish()) gc->output_sam_is_full = 1;
 	double t0 = miltime();
 	int rc = __real_write_indel_final_results(gc);
 	if (getenv("SVG_REF_TIMING"))

@@ -150,3 +150,42 @@ def test_oracle_dropin_realign_options(extra, threads, cache, tmp_path):
     dropin.run(c.meta["program"], "oracle-dropin", pre, f1, f2, do, threads, extra)
     rep = dropin.compare(so, do)
     assert rep["mapped"] > 0
+
+
+def _bam_records(path):
+    """The alignment records of a BAM file (BGZF members concatenated, header text and reference
+    list skipped: the header's @PG line holds the program path)."""
+    import gzip
+    import struct
+    b = gzip.open(path, "rb").read()
+    assert b[:4] == b"BAM\x01"
+    lt = struct.unpack("<i", b[4:8])[0]
+    p = 8 + lt
+    nref = struct.unpack("<i", b[p:p + 4])[0]
+    p += 4
+    for _ in range(nref):
+        ln = struct.unpack("<i", b[p:p + 4])[0]
+        p += 4 + ln + 4
+    return b[p:]
+
+
+def test_oracle_dropin_bam_keep_read_order(cache, tmp_path):
+    """BAM output with --keepReadOrder at -T 4: the drop-in keeps the reference's ordered writer
+    path (add_buffered_fragment, core.c:1855-1881; iteration two is the reference's for BAM), so
+    the records come out in read order, identical to the stock aligner's."""
+    from tests import dropin
+    c = Case("pe_gapped_errmut")
+    if not have(c.meta["program"], "oracle-dropin"):
+        pytest.skip("reference drop-in binaries not built (make -C oracle dropin)")
+    f1, f2 = dropin.fastq_pair(str(tmp_path), c.name, c.r1, c.r2)
+    pre = cache.get(c.index_key)
+    outs = {}
+    for kind in ("dump", "oracle-dropin"):
+        o = str(tmp_path / (kind + ".bam"))
+        args = [dropin.binary(0, kind), "-T", "4", "-i", pre, "-r", f1, "-R", f2, "-o", o, "-t", "1", "--keepReadOrder"]
+        import subprocess
+        r = subprocess.run(args, capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[kind] = _bam_records(o)
+    assert len(outs["dump"]) > 100000
+    assert outs["dump"] == outs["oracle-dropin"]

@@ -31,7 +31,9 @@ def main():
     ap.add_argument("--reads", type=int, default=2_000_000)
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--workdir", default="")
-    ap.add_argument("--kinds", default="dump,dropin", help="which binaries: dump (stock), dropin (GPU vote)")
+    ap.add_argument("--kinds", default="dump,dropin,dropin_refit2",
+                    help="which binaries: dump (stock), dropin (GPU vote + the library's iteration two), "
+                         "dropin_refit2 (GPU vote + the reference's own iteration two, SVG_REF_ITER2=1)")
     ap.add_argument("--out", default="", help="also write the JSON line here")
     args = ap.parse_args()
     kinds = args.kinds.split(",")
@@ -63,23 +65,26 @@ def main():
     res, start, phases = {}, {}, {}
     env = {"SVG_REF_TIMING": "1"}
     for kind in kinds:
+        binkind = "dropin" if kind == "dropin_refit2" else kind
+        kenv = dict(env, SVG_REF_ITER2="1") if kind == "dropin_refit2" else env
         # the fixed cost first (index load(s), voting space, output files): the same program on one read
-        out = os.path.join(wd, "one_" + kind)
+        out = os.path.join(wd, "one_%s.sam" % kind)
         ts = time.perf_counter()
-        dropin.run(0, kind, pre, fq1, None, out, threads=T, timeout=1500, env=env)
+        dropin.run(0, binkind, pre, fq1, None, out, threads=T, timeout=1500, env=kenv)
         start[kind] = time.perf_counter() - ts
-        out = os.path.join(wd, "out_" + kind)
+        out = os.path.join(wd, "out_%s.sam" % kind)
         ts = time.perf_counter()
-        r = dropin.run(0, kind, pre, fq, None, out, threads=T, timeout=1500, env=env)
+        r = dropin.run(0, binkind, pre, fq, None, out, threads=T, timeout=1500, env=kenv)
         res[kind] = time.perf_counter() - ts
         phases[kind] = parse_phases(r.stderr)
         log("[e2e] %s: %.1f s (%.1f s on one read) phases %s" % (kind, res[kind], start[kind], phases[kind]))
     stop.set()
     same = None
-    if len(kinds) == 2:
-        dropin.compare(os.path.join(wd, "out_" + kinds[0]), os.path.join(wd, "out_" + kinds[1]))
+    if len(kinds) >= 2:
+        for k in kinds[1:]:
+            dropin.compare(os.path.join(wd, "out_%s.sam" % kinds[0]), os.path.join(wd, "out_%s.sam" % k))
         same = True
-        log("[e2e] SAM / VCF byte-identical")
+        log("[e2e] SAM / VCF byte-identical (%s)" % ", ".join(kinds))
     if len(kinds) == 1:
         k = kinds[0]
         line = {"metric": "end-to-end subread-align phases", "kind": k, "seconds": round(res[k], 2),
@@ -101,6 +106,9 @@ def main():
                              "dropin_value": round(args.reads / max(1e-9, res["dropin"] - start["dropin"]) / 1e6, 4),
                              "note": "whole-program time minus the same program's time on one read"},
             "outputs_identical": same, "threads": T,
+            "dropin_refit2": ({"seconds": round(res["dropin_refit2"], 2),
+                               "note": "the same drop-in with the reference's own iteration two (SVG_REF_ITER2=1)"}
+                              if "dropin_refit2" in res else None),
             "phases_s": phases,
             "phases_note": "the reference's own clocks (read_chunk_circles, core.c:3552-3641), printed by "
                            "oracle/ref_dump_hook.c: load_index, voting, before_realign (anti-support scan + "
