@@ -10,6 +10,9 @@
  * VCF and junction BED of that binary with the stock reference's, byte for byte.
  *
  *   svg_attach           once, after load_global_context (core.c:4013) has the index prefix
+ *   svg_attach_devices   the same for several GPUs: one handle (a full index replica) per device;
+ *                        each chunk's reads are then split into contiguous ranges, one per handle,
+ *                        voted by one host thread per handle into the one bigtable
  *   do_voting_gpu        per chunk and index block, from ONE host thread per GPU
  *                        (run_in_thread, core.c:3366)
  *   do_voting_gpu_mt     the same from each of the run's -T threads: thread 0 reads and votes
@@ -41,6 +44,7 @@
 #include "core-indel.h"
 #include "core-junction.h"
 #include "input-files.h"
+#include "gene-algorithms.h"
 #include "subread_vote.h"
 
 /* defined in core.c (non-static there, not declared in a header) */
@@ -56,16 +60,35 @@ int has_better_mapping(global_context_t *global_context, thread_context_t *threa
                        subread_read_number_t current_read_number, int is_second_read, int this_aln_id);
 int find_subread_end(int len, int TOTAL_SUBREADS, int subread);   /* input-files.c:1371 */
 
-static svg_index *svg_ix;   /* one per process, one process per GPU */
+/* The handles: svg_ix[0 .. svg_nix-1], one per device (svg_attach_devices), each with a full index
+ * replica in its HBM.  The reads of a chunk are independent, so handle k votes the k-th contiguous
+ * range of them straight into the bigtable rows of those reads -- the fan-out of run_maybe_threads
+ * (core.c:3379-3461), with GPUs in the role of its threads; no exchange between devices. */
+#define SVG_MAX_DEV 16
+static svg_index *svg_ix[SVG_MAX_DEV];
+static int svg_nix;
 static pthread_mutex_t svg_sam_mu_init = PTHREAD_MUTEX_INITIALIZER;   /* one-time setup of the shared state */
+
+int svg_attach_devices(global_context_t *gc, const int *devices, int n)
+{
+	char prefix[MAX_FILE_NAME_LENGTH + 1];
+	int k, rc = 0;
+	if (n < 1 || n > SVG_MAX_DEV) {
+		SUBREADprintf("GPU voting: %d devices (1 .. %d)\n", n, SVG_MAX_DEV);
+		return 1;
+	}
+	snprintf(prefix, sizeof prefix, "%s", gc->config.index_prefix);
+	for (k = 0; k < n && !rc; k++) {
+		rc = svg_index_open(prefix, devices[k], &svg_ix[k]);
+		if (rc) SUBREADprintf("GPU voting unavailable on device %d: %s\n", devices[k], svg_last_error());
+		else svg_nix = k + 1;
+	}
+	return rc;
+}
 
 int svg_attach(global_context_t *gc, int device)
 {
-	char prefix[MAX_FILE_NAME_LENGTH + 1];
-	snprintf(prefix, sizeof prefix, "%s", gc->config.index_prefix);
-	int rc = svg_index_open(prefix, device, &svg_ix);
-	if (rc) SUBREADprintf("GPU voting unavailable: %s\n", svg_last_error());
-	return rc;
+	return svg_attach_devices(gc, &device, 1);
 }
 
 static void svg_fill_params(global_context_t *gc, svg_params *p)
@@ -162,7 +185,29 @@ static int read_chunk(global_context_t *gc, thread_context_t *tc, int ends, svg_
 	return 0;
 }
 
-/* 2. one packed call for the whole chunk, records into the bigtable */
+/* one handle's share of a chunk: reads [r0, r1) of the packed chunk, records into their rows */
+typedef struct {
+	svg_index *ix;
+	const svg_params *p;
+	int ends;
+	svg_packed_reads pk[2];
+	svg_mapping_result *out;
+	svg_subjunc_result *jout;
+	uint16_t *bm;
+	int rc;
+	char err[256];
+} svg_share;
+
+static void *svg_share_run(void *v)
+{
+	svg_share *s = v;
+	s->rc = svg_vote_batch_packed(s->ix, s->p, &s->pk[0], s->ends == 2 ? &s->pk[1] : NULL, s->out, s->jout, s->bm);
+	if (s->rc) snprintf(s->err, sizeof s->err, "%s", svg_last_error());
+	return NULL;
+}
+
+/* 2. the chunk's packed reads voted into the bigtable: one call, or with several handles one
+ * contiguous range of reads per handle, each from its own host thread */
 static int vote_chunk(global_context_t *gc, int ends, const svg_chunk_reads *c)
 {
 	svg_params p;
@@ -189,13 +234,50 @@ static int vote_chunk(global_context_t *gc, int ends, const svg_chunk_reads *c)
 		bm = malloc(sizeof(uint16_t) * SVG_BIG_MARGIN_WORDS * ends * (c->n + 1));
 		if (!bm) rc = SVG_E_NOMEM;
 	}
-	if (!rc)
-		rc = svg_vote_batch_packed(svg_ix, &p, &pk[0], ends == 2 ? &pk[1] : NULL,
-		                           (svg_mapping_result *)_global_retrieve_alignment_ptr(gc, 0, 0, 0),
-		                           p.do_breakpoint_detection ? (svg_subjunc_result *)_global_retrieve_subjunc_ptr(gc, 0, 0, 0) : NULL,
-		                           bm);
-	if (rc) SUBREADprintf("svg_vote_batch_packed: %s\n", svg_last_error());
-	else if (bm) {
+	if (!rc) {
+		svg_mapping_result *out = (svg_mapping_result *)_global_retrieve_alignment_ptr(gc, 0, 0, 0);
+		svg_subjunc_result *jout = p.do_breakpoint_detection ? (svg_subjunc_result *)_global_retrieve_subjunc_ptr(gc, 0, 0, 0) : NULL;
+		const uint64_t per = (uint64_t)ends * (uint64_t)p.multi_best;
+		int nh = svg_nix, k;
+		if ((uint64_t)nh > c->n) nh = c->n ? (int)c->n : 1;
+		svg_share sh[SVG_MAX_DEV];
+		pthread_t th[SVG_MAX_DEV];
+		int started[SVG_MAX_DEV];
+		memset(sh, 0, sizeof sh);
+		for (k = 0; k < nh; k++) {
+			const uint64_t r0 = c->n * (uint64_t)k / (uint64_t)nh, r1 = c->n * (uint64_t)(k + 1) / (uint64_t)nh;
+			int e;
+			sh[k].ix = svg_ix[k];
+			sh[k].p = &p;
+			sh[k].ends = ends;
+			for (e = 0; e < ends; e++) {
+				/* the range's starts / lengths / count; the packed codes and the exception mask stay
+				 * shared (starts are absolute base offsets) */
+				sh[k].pk[e] = pk[e];
+				sh[k].pk[e].starts = pk[e].starts + r0;
+				sh[k].pk[e].lens = pk[e].lens + r0;
+				sh[k].pk[e].n_reads = r1 - r0;
+			}
+			sh[k].out = out + r0 * per;
+			sh[k].jout = jout ? jout + r0 * per : NULL;
+			sh[k].bm = bm ? bm + r0 * ends * SVG_BIG_MARGIN_WORDS : NULL;
+			started[k] = 0;
+		}
+		if (nh == 1) svg_share_run(&sh[0]);
+		else {
+			for (k = 0; k < nh; k++) started[k] = pthread_create(&th[k], NULL, svg_share_run, &sh[k]) == 0;
+			for (k = 0; k < nh; k++) {
+				if (started[k]) pthread_join(th[k], NULL);
+				else svg_share_run(&sh[k]);
+			}
+		}
+		for (k = 0; k < nh && !rc; k++)
+			if (sh[k].rc) {
+				rc = sh[k].rc;
+				SUBREADprintf("svg_vote_batch_packed (handle %d): %s\n", k, sh[k].err);
+			}
+	}
+	if (!rc && bm) {
 		uint64_t r;
 		int words = gc->config.big_margin_record_size;
 		for (r = 0; r < c->n; r++)
@@ -339,7 +421,7 @@ static int vote_stage(global_context_t *gc, thread_context_t *tc)
 			svg_params p;
 			svg_fill_params(gc, &p);
 			svg_reads a1 = {c->text[0], c->off[0], c->len[0], c->n}, a2 = {c->text[1], c->off[1], c->len[1], c->n};
-			rc = svg_fragile_batch(svg_ix, &p, &a1, ends == 2 ? &a2 : NULL, &svg_frag);
+			rc = svg_fragile_batch(svg_ix[0], &p, &a1, ends == 2 ? &a2 : NULL, &svg_frag);
 			if (rc) SUBREADprintf("svg_fragile_batch: %s\n", svg_last_error());
 		}
 		svg_t_frag += miltime() - t0;
@@ -1067,7 +1149,11 @@ static int svg_it2_setup(global_context_t *gc)
 	p.do_breakpoint_detection = gc->config.do_breakpoint_detection;
 	p.ignore_unmapped_reads = gc->config.ignore_unmapped_reads;
 	p.phred_offset = gc->config.phred_score_format == FASTQ_PHRED64 ? 64 : 33;
-	snprintf(p.read_group_id, sizeof p.read_group_id, "%s", gc->config.read_group_id);
+	{   /* (the tag the reference writes is cut at 310 bytes anyway, core.c:2053) */
+		const size_t rg = strnlen(gc->config.read_group_id, sizeof p.read_group_id - 1);
+		memcpy(p.read_group_id, gc->config.read_group_id, rg);
+		p.read_group_id[rg] = 0;
+	}
 	rc = svg_realign_create(svg_it2_g, &p, &svg_it2);
 	if (rc) { svg_genome_arrays_close(svg_it2_g); svg_it2_g = NULL; }
 	return rc;
@@ -1208,9 +1294,20 @@ int do_voting(global_context_t *gc, thread_context_t *tc)
 {
 	pthread_mutex_lock(&svg_sam_mu_init);
 	int rc = 0;
-	if (!svg_ix) {
-		const char *d = getenv("SVG_DEVICE");
-		rc = svg_attach(gc, d ? atoi(d) : 0);
+	if (!svg_nix) {
+		/* SVG_DEVICES=0,1,...: one handle per listed device (a device may repeat: several replicas on
+		 * one GPU); else SVG_DEVICE (default 0) */
+		const char *ds = getenv("SVG_DEVICES"), *d = getenv("SVG_DEVICE");
+		if (ds && ds[0]) {
+			int devs[SVG_MAX_DEV], n = 0;
+			const char *q = ds;
+			while (*q && n < SVG_MAX_DEV) {
+				devs[n++] = atoi(q);
+				while (*q && *q != ',') q++;
+				if (*q == ',') q++;
+			}
+			rc = svg_attach_devices(gc, devs, n);
+		} else rc = svg_attach(gc, d ? atoi(d) : 0);
 	}
 	pthread_mutex_unlock(&svg_sam_mu_init);
 	if (rc) return 1;

@@ -41,12 +41,6 @@ struct DevIndex {
 	const uint32_t *khash_ff;
 	uint64_t khash_lines;
 	int32_t khash_sec;        // 1: 32-byte sectors of 3 entries (8-bit run counts), 0: 64-byte lines
-	//   kinline: a key whose equal-key run is ONE item keeps that item's VALUE (its linear
-	//            position, vals[item]) in the record's first word instead of the item index: the
-	//            probe then delivers the hit itself and the vote kernels skip the dependent random
-	//            load of vals[] for it (svg_rec_value).  Paths that need the item (prefill_votes,
-	//            gehash_go_q / go_QQ runs) take the literal search for such keys.
-	int32_t kinline;
 	//   ksorted: bit b set when bucket b's keys are non-decreasing as shorts (built with khash), so
 	//            that its key-hash record is also prefill_votes's equal-key run (svg_probe_keys)
 	const uint32_t *ksorted;
@@ -56,13 +50,6 @@ struct DevIndex {
 // probe-image helpers shared by the vote path's probe kernels (svg_vote.hip) and the key
 // lookups (svg_keys.hip)
 
-// hit j of a probe record (x, fwd | bwd << 16) in gehash_go_X's visiting order (mid..last,
-// mid-1..first; sorted-hashtable.c:984-1120): its linear position.  With an inline key-hash
-// image a one-item run carries the position itself (DevIndex::kinline).
-__device__ __forceinline__ bool svg_rec_inline(int32_t kinline, uint32_t y)
-{
-	return kinline && y == 1u;   // fwd = 1, bwd = 0
-}
 
 // position (0..63) of the j-th (0-based) set bit of x; x has more than j set bits
 __device__ __forceinline__ int select64(uint64_t x, int j)
@@ -306,8 +293,6 @@ int svg_vote_chunk(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slo
 // the two halves of svg_vote_chunk: the probe kernels (into the slot's probe records), then the
 // lane kernels on st and the wave kernel on st2
 int svg_vote_chunk_probe(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slot, hipStream_t st);
-// 1 when the vote path's probe records of this index carry one-hit positions inline (DevIndex::kinline)
-int svg_probe_inline(const svg_index *h);
 int svg_vote_chunk_vote(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, int slot, hipStream_t st, hipStream_t st2);
 int svg_vote_batch_device_packed(svg_index *h, const svg_params *p, const svg_reads *r1, const svg_reads *r2,
                                  const svg_packed_reads *pk, svg_mapping_result *out, svg_subjunc_result *jout,

@@ -267,7 +267,7 @@ __device__ __forceinline__ void go_run(const DevIndex &x, uint32_t key, uint32_t
 		uint2 rec;
 		const bool hit = khash_find(x, key, rec);
 		if (!hit) return;
-		if (!svg_rec_inline(x.kinline, rec.y)) {   // (an inline record holds a position: literal search)
+		{
 			const uint32_t fwd = rec.y & 0xffffu, bwd = rec.y >> 16;
 			f = rec.x - bwd;
 			c = fwd + bwd;

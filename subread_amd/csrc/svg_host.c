@@ -40,13 +40,11 @@ int svg_abi_version(void) { return SVG_ABI_VERSION; }
 /* Implementation options (include/subread_vote.h): explicit, process-wide, never read from the
  * environment, and none of them changes a record. */
 static struct { const char *name; volatile int64_t value; } g_opts[] = {
-	{"host_threads", 0}, {"host_sub", 0}, {"chunk", 0}, {"overlap", -1},
-	{"lane", 0}, {"lane_unfused", 0}, {"lane_bin", 0}, {"lane_cap", 0}, {"lane_pe_cap", 0},
-	{"lane_pairs", 0}, {"lane_mid", 0},
-	{"no_bcode", 0}, {"no_khash", 0}, {"khash64", 0}, {"no_bline", 0}, {"no_compact", 0}, {"kinline", 0}, {"khash_probe", 0},
-	{"probe_v1", 0}, {"no_window", 0}, {"probe_colmajor", 0},
-	{"wave_cap", -1}, {"wave_static", -1}, {"host_ramp", 1}, {"host_slots", 2}, {"probe_cap", 0}, {"wave_cus", 0}, {"lane_cus_excl", 0}, {"keys_literal", 0}, {"long_probes", 0},
-	{"debug", 0}, {"pipe_debug", 0}, {"long_debug", 0},
+	{"host_threads", 0}, {"host_sub", 0}, {"host_ramp", 1}, {"chunk", 0}, {"overlap", -1},
+	{"lane", 0}, {"lane_unfused", 0}, {"lane_cap", 0},
+	{"no_bcode", 0}, {"no_khash", 0}, {"khash64", 0}, {"no_bline", 0}, {"no_compact", 0}, {"keys_literal", 0},
+	{"wave_cap", -1}, {"wave_static", -1}, {"probe_cap", 0}, {"long_probes", 0},
+	{"debug", 0},   /* bits: 1 vote-path batches, 2 host pipeline, 4 sublong chunks */
 };
 #define N_OPTS ((int)(sizeof g_opts / sizeof g_opts[0]))
 

@@ -585,7 +585,7 @@ extern "C" int svg_vote_batch_packed_device(svg_index *h, const svg_params *p, c
 }
 
 // ============================================================================ the host pipeline
-// Sub-batch i (<= one probe-record chunk) in device slot s = i & 1 (option host_slots 3: i % 3):
+// Sub-batch i (<= one probe-record chunk) in device slot s = i & 1:
 //   up_stream : upload of the reads into d_in[s]
 //   stream    : [unpack] + probe + lane kernels             (svg_vote_chunk)
 //   stream2   : wave kernel + record compaction + counts    (single-end align: beside the next
@@ -636,11 +636,11 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	const CompLayout CL = comp_layout(sub, R, ends, jo, bmo);
 	const size_t o_j = (sub * rec_b + 255) & ~(size_t)255, o_bm = (o_j + sub * j_b + 255) & ~(size_t)255;
 	// device slots (probe records, lane lists, full records): 2 -- the probe / lane stream runs one
-	// sub-batch ahead of the wave kernel's.  Option host_slots 3 lets it run two ahead: measured
+	// sub-batch ahead of the wave kernel's.  Three slots (two ahead) were measured slower,
 	// 114.4-114.9 vs 101.9-102.2 ms/step at C3 (profiles/r04/n/sweep_slots.txt) -- the probe kernel
 	// speeds up, the lane and wave kernels slow down more (more kernels on the CUs at once; the
 	// probe records, 160 MB per sub-batch, outlive the 256 MB infinity cache)
-	const int NS = svg_get_option("host_slots") == 3 ? 3 : 2;
+	const int NS = 2;
 	for (int s = 0; s < NS; s++)
 		if ((rc = svg_ensure(h, &h->d_out[s], &h->d_out_cap[s], o_bm + sub * bm_b + 64))) return rc;
 	for (int s = 0; s < 3; s++) {
@@ -682,7 +682,7 @@ static int host_pipeline(svg_index *h, const svg_params *p, const svg_reads *a1,
 	}
 
 	// SVG_PIPE_DEBUG=1: where the host thread waits (seconds per batch)
-	const bool dbg = svg_get_option("pipe_debug") != 0;
+	const bool dbg = (svg_get_option("debug") & 2) != 0;
 	double w_done = 0, w_pool = 0, w_up = 0, w_vote = 0;
 	auto now = []() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
 	// D2H of the compacted sub-batch j (compact slot j % 3) into staging slot j % 3

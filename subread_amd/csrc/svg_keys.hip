@@ -114,8 +114,7 @@ __global__ void __launch_bounds__(256) probe_keys_kernel(KeyParams kp)
 			if (!literal) {
 				uint2 rec;
 				if (khash_find(kp.ix, sub, rec)) {
-					if (svg_rec_inline(kp.ix.kinline, rec.y)) literal = true;   // a position, not the item
-					else {
+					{
 						const uint32_t fwd = rec.y & 0xffffu, bwd = rec.y >> 16;
 						f = rec.x - bwd - kp.bstart[b];
 						c = fwd + bwd;

@@ -62,7 +62,6 @@ struct GParams {
 	uint32_t cs;             // column stride of cand/cpk/ccnt
 	const uint32_t *idx;     // NULL: column r = read r; else column k = read idx[k], k < min(*idx_count, cs)
 	const uint32_t *idx_count;
-	int kinline;             // DevIndex::kinline: one-hit records carry the position itself
 };
 
 __global__ void __launch_bounds__(256) gather_kernel(GParams g)
@@ -94,18 +93,12 @@ __global__ void __launch_bounds__(256) gather_kernel(GParams g)
 					int off = (int)(((int64_t)step * sk) >> 16);
 					if (gap > 1) off -= off % gap - x;
 					const uint16_t pk = (uint16_t)((sk + 1) | (off << 6));
-					if (svg_rec_inline(g.kinline, rec.y)) {
-						// one hit, its position in the record (inline key-hash image): no vals[] load
-						const size_t o = (size_t)(s * (uint32_t)g.cap + c) * g.cs + k;
-						g.cand[o] = rec.x - (uint32_t)off;
+					for (uint32_t j = 0; j < hits; j++) {
+						const uint32_t item = j < fwd ? rec.x + j : rec.x - 1u - (j - fwd);
+						const size_t o = (size_t)(s * (uint32_t)g.cap + c + j) * g.cs + k;
+						g.cand[o] = g.vals[item] - (uint32_t)off;
 						g.cpk[o] = pk;
-					} else
-						for (uint32_t j = 0; j < hits; j++) {
-							const uint32_t item = j < fwd ? rec.x + j : rec.x - 1u - (j - fwd);
-							const size_t o = (size_t)(s * (uint32_t)g.cap + c + j) * g.cs + k;
-							g.cand[o] = g.vals[item] - (uint32_t)off;
-							g.cpk[o] = pk;
-						}
+					}
 					c += hits;
 				}
 			}
@@ -145,7 +138,6 @@ struct LParams {
 	const uint2 *precs;           // fused gather (NPF > 0): probe records, SoA [(end * 2 + strand) * nps + p][n]
 	const uint32_t *vals;
 	int nps;
-	int kinline;                  // DevIndex::kinline: one-hit probe records carry the position itself
 	// subjunc (lane_kernel<..., SJ = true>)
 	uint8_t *jout;                // subjunc_result_t records of the chunk
 	uint16_t *bm_out;             // big-margin records of the chunk
@@ -694,7 +686,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) la
 				int off = (int)(((int64_t)step * sk) >> 16);
 				if (lp.gap > 1) off -= off % lp.gap - x;
 				pk = (uint32_t)(sk + 1) | ((uint32_t)off << 6);
-				return svg_rec_inline(lp.kinline, ry[0]);   // item is the position itself
+				return false;
 			};
 			uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0, it = 0, pkn = 0;
 			if (0 < mycnt) { q0 = lval(lp, next(it, pkn), it); k0 = pkn; }
@@ -1125,7 +1117,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) la
 					int off = (int)(((int64_t)step[E] * sk) >> 16);
 					if (lp.gap > 1) off -= off % lp.gap - x;
 					pk = (uint32_t)(sk + 1) | ((uint32_t)off << 6);
-					return svg_rec_inline(lp.kinline, ry[0]);   // item is the position itself
+					return false;
 				};
 				uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, k0 = 0, k1 = 0, k2 = 0, k3 = 0, it = 0, pkn = 0;
 				if (0 < mycnt) { q0 = lval(lp, next(it, pkn), it); k0 = pkn; }
@@ -1675,8 +1667,7 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	LParams lp;
 	memset(&lp, 0, sizeof lp);
 	lp.len = len1; lp.len2 = len2; lp.n = n; lp.cap = LANE_PE_CAP;
-	if (svg_get_option("lane_pe_cap") > 0) lp.cap = (int)svg_get_option("lane_pe_cap");   // candidates per end and strand
-	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps; lp.kinline = svg_probe_inline(h);
+	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps;
 	lp.gap = h->dix.gap; lp.total_subreads = p->total_subreads;
 	lp.tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
 	lp.low = h->dix.start_base_offset;
@@ -1686,7 +1677,7 @@ int svg_lane_pe_chunk(svg_index *h, int slot, const svg_params *p, const uint16_
 	lp.chr_end = h->dix.chr_end; lp.n_chr = (int)h->dix.n_chr; lp.padding = h->dix.padding;
 	lp.min_pair = p->min_pair_distance; lp.max_pair = p->max_pair_distance; lp.mvc = p->max_vote_combinations;
 	// 96 -> 256: C5pe deferrals 34% -> 21% of the pairs, 942 -> 779 ms/step (profiles/r03/sweeps/c5pe_pairs_*.json)
-	lp.max_pairs = svg_get_option("lane_pairs") > 0 ? (int)svg_get_option("lane_pairs") : 256;
+	lp.max_pairs = 256;   // measured: 96 -> 256 pairs cut C5pe deferrals 8.57M -> 5.18M of 25M; 1024 the same
 	lp.out = out;
 	lp.jout = jout;
 	lp.bm_out = jout ? bm_out : NULL;
@@ -1757,7 +1748,7 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 	uint32_t *cnt = (uint32_t *)(b + o_cnt);
 	HIPCHK(hipMemsetAsync(cnt, 0, 32, st));
 	GParams g;
-	g.precs = precs; g.len = len; g.vals = h->dix.vals; g.n = n; g.nps = nps; g.gap = h->dix.gap; g.kinline = svg_probe_inline(h);
+	g.precs = precs; g.len = len; g.vals = h->dix.vals; g.n = n; g.nps = nps; g.gap = h->dix.gap;
 	g.total_subreads = p->total_subreads; g.cap = LANE_CAP1;
 	g.cand = (uint32_t *)(b + o_c1); g.cpk = (uint16_t *)(b + o_p1); g.ccnt = (uint16_t *)(b + o_n1);
 	g.cs = n; g.idx = NULL; g.idx_count = NULL;
@@ -1769,7 +1760,7 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 	if (!fused && (rc = gather_launch(h, g, st))) return rc;
 	LParams lp;
 	lp.cand = g.cand; lp.cpk = g.cpk; lp.ccnt = g.ccnt; lp.len = len; lp.n = n; lp.cap = LANE_CAP1;
-	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps; lp.kinline = svg_probe_inline(h);
+	lp.precs = precs; lp.vals = h->dix.vals; lp.nps = nps;
 	lp.gap = h->dix.gap; lp.total_subreads = p->total_subreads;
 	lp.tol = p->max_indel_length < 16 ? p->max_indel_length : 16;
 	lp.low = h->dix.start_base_offset;
@@ -1805,7 +1796,7 @@ int svg_lane_chunk(svg_index *h, int slot, const svg_params *p, const uint16_t *
 		if (oc > LANE_CAP1 && fused) lp.cap = oc < 64 ? oc : 64;
 		// count bins for the fused single-pass path: one thread per read sorts the chunk's reads into
 		// LBINS lists by candidate count (and defers the over-cap ones) before the lane kernel
-		if (fused && svg_get_option("lane_bin") != 2) {
+		if (fused) {
 			lp.bins = (uint32_t *)(b + o_bin);
 			lp.bin_count = cnt + 4;
 			uint64_t bb = ((uint64_t)n + LBT - 1) / LBT, bmax = (uint64_t)h->n_cu * 8;

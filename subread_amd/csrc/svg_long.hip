@@ -159,8 +159,7 @@ __global__ void __launch_bounds__(256) long_probe_kernel(LProbe lp)
 		if (!literal) {
 			uint2 rec;
 			if (khash_find(x, key, rec)) {
-				if (svg_rec_inline(x.kinline, rec.y)) literal = true;   // a position, not the item
-				else {
+				{
 					const uint32_t fwd = rec.y & 0xffffu, bwd = rec.y >> 16;
 					f = rec.x - bwd;
 					c = fwd + bwd;
@@ -559,7 +558,7 @@ int long_chunk(svg_index *h, const svg_long_reads *R, uint64_t r0, uint64_t r1, 
 	svg_longws *w = h->lws;
 	const uint32_t n = (uint32_t)(r1 - r0);
 	*too_big = false;
-	const bool dbg = svg_get_option("long_debug") != 0;
+	const bool dbg = (svg_get_option("debug") & 4) != 0;
 	auto now = [] { struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6; };
 	const double t0 = dbg ? now() : 0;
 	double t_up = 0, t_probe = 0, t_seg = 0, t_keep = 0, t_dev = 0;
@@ -825,7 +824,7 @@ extern "C" int svg_long_vote_batch(svg_index *h, const svg_long_reads *R, svg_lo
 			const int rc = long_chunk(h, R, r0, r1, ccap, res, counts, &big, T, par, pend);
 			if (rc) { pend.join(); free(res.votes); free(res.order); return rc; }
 			if (!big) break;
-			if (svg_get_option("long_debug")) fprintf(stderr, "[svg_long] split %llu reads\n", (unsigned long long)(r1 - r0));
+			if (svg_get_option("debug") & 4) fprintf(stderr, "[svg_long] split %llu reads\n", (unsigned long long)(r1 - r0));
 			r1 = r0 + (r1 - r0) / 2;   // too many candidates: half the reads
 		}
 		r0 = r1;

@@ -565,7 +565,6 @@ struct Wave {
 		STAMP(2);
 		// gather in visiting order (probe p, then mid..last, then mid-1..first), lane c = candidate
 		// c0 + c of the chunk; the next chunk's hit values are loaded while this one is voted
-		// (inline key-hash records: a one-hit probe's "mid" is its position, DevIndex::kinline)
 		auto locate_cand = [&](uint32_t cc, uint32_t &item, int &off, int &kP1) __attribute__((always_inline)) -> bool {
 			int lo = 0, hi = np - 1;   // probe p with pcum[p] <= cc < pcum[p+1]
 			while (lo < hi) { int m = (lo + hi + 1) >> 1; if (L->pcum[m] <= cc) lo = m; else hi = m - 1; }
@@ -576,12 +575,10 @@ struct Wave {
 			item = j < fwd ? mid + j : mid - 1 - (j - fwd);
 			off = probe_off(E, p);
 			kP1 = p / gap + 1;
-			return svg_rec_inline(kp->ix.kinline, fwd | ((uint32_t)L->pbwd[E][s][p] << 16));
+			return false;
 		};
 		uint32_t nitem = 0, nval = 0;
 		int noff = 0, nkp1 = 0;
-		// (an inline one-hit record holds the position: the load index is 0 then, so a speculated
-		// load stays inside vals[])
 		if ((uint32_t)lane < total) {
 			const bool inl = locate_cand((uint32_t)lane, nitem, noff, nkp1);
 			const uint32_t v = kp->ix.vals[inl ? 0u : nitem];
@@ -2319,7 +2316,7 @@ __global__ void __launch_bounds__(256) clear_khash_payload(uint32_t *kh, uint64_
 // count does not fit 8 bits (the sector image is then not used).
 template <bool SEC>
 __global__ void __launch_bounds__(256) build_khash(const uint32_t *bstart, const int16_t *keys, uint32_t nb, uint32_t *kh,
-                                                   uint64_t lines, uint32_t *ff, const uint32_t *vals)
+                                                   uint64_t lines, uint32_t *ff)
 {
 	for (uint32_t b = blockIdx.x * 256u + threadIdx.x; b < nb; b += gridDim.x * 256u) {
 		const uint32_t first = bstart[b], n = bstart[b + 1] - first;
@@ -2344,9 +2341,8 @@ __global__ void __launch_bounds__(256) build_khash(const uint32_t *bstart, const
 			qq = m - 1;
 			while (qq >= 0 && K[qq] == k16) qq--;
 			const uint32_t bwd = (uint32_t)(m - 1 - qq);
-			// vals != NULL (DevIndex::kinline): a one-item run stores the item's value
 			const uint32_t key = (uint32_t)(uint16_t)k16 * nb + b, ry = fwd | (bwd << 16);
-			const uint32_t rx = vals && fwd + bwd == 1u ? vals[first + (uint32_t)m] : first + (uint32_t)m;
+			const uint32_t rx = first + (uint32_t)m;
 			if (key == 0xffffffffu) { ff[1] = rx; ff[2] = ry; ff[0] = 1u; continue; }
 			if (SEC && (fwd > 255u || bwd > 255u)) { atomicOr(&ff[3], 1u); continue; }
 			uint64_t L = khash_line(key, lines);
@@ -2434,24 +2430,10 @@ static int streams_acquire(svg_index *h)
 	pthread_mutex_lock(&g_streams_mu);
 	int rc = 0;
 	if (!g_streams[h->device].refs) {
-		// options wave_cus = K (0: off): the second stream (wave kernel, compaction) runs on CUs
-		// 0..K-1 only; lane_cus_excl 1: the first stream (probe, lane kernels) on the others
-		hipDeviceProp_t prop;
-		const int ncu = hipGetDeviceProperties(&prop, h->device) == hipSuccess ? prop.multiProcessorCount : 0;
-		const int64_t K = svg_get_option("wave_cus");
-		uint32_t mask[2][32];
-		const bool masked = K > 0 && K < ncu && ncu <= 1024;
-		if (masked) {
-			memset(mask, 0, sizeof mask);
-			for (int c = 0; c < ncu; c++) mask[c < K ? 1 : 0][c >> 5] |= 1u << (c & 31);
-		}
-		const bool excl = masked && svg_get_option("lane_cus_excl") != 0;
+		// (round 4 measured CU-masked streams for the wave kernel: 64 / 96 / 128 / 192 of 256 CUs
+		// gave 219.8 / 162.4 / 144.5 / 101.7 ms/step against 100.7 unmasked)
 		for (int k = 0; k < 4 && !rc; k++) {
-			hipError_t e;
-			if (masked && (k == 1 || (k == 0 && excl)))
-				e = hipExtStreamCreateWithCUMask(&g_streams[h->device].s[k], (uint32_t)((ncu + 31) / 32), mask[k == 1 ? 1 : 0]);
-			else
-				e = hipStreamCreateWithFlags(&g_streams[h->device].s[k], hipStreamNonBlocking);
+			const hipError_t e = hipStreamCreateWithFlags(&g_streams[h->device].s[k], hipStreamNonBlocking);
 			if (e != hipSuccess) {
 				svg_set_error("hipStreamCreate failed");
 				rc = SVG_E_DEVICE;
@@ -2530,7 +2512,6 @@ int svg_index_finish_device(svg_index *h)
 	h->dix.khash_ff = NULL;
 	h->dix.khash_lines = 0;
 	h->dix.khash_sec = 0;
-	h->dix.kinline = 0;
 	h->dix.ksorted = NULL;
 	{
 		// 32-byte bucket codes when the key_hi range is small enough for them to hold ordinary
@@ -2552,26 +2533,17 @@ int svg_index_finish_device(svg_index *h)
 		}
 	}
 	// the key-hash image: the probe image of indexes the bucket code does not fit (gapped, small);
-	// beside the code on request (options kinline / khash_probe; C3 full: ~52 GB).  Measured at C3
-	// (profiles/r04/bench_c3_*.json): the key-hash probe kernel is 18% faster than the code's, but
-	// the lane / wave kernels slow by more than that (113.5 vs 110.6 ms/step), so the code stays the
-	// default probe image of -F -B indexes.  The code, when it fits, also serves the paths that need
-	// item indices (svg_probe_keys, fragile and sublong voting)
-	// option kinline: one-hit runs inline; option khash_probe: the key-hash image beside the bucket
-	// code, probed instead of it (A/B of the probe images)
-	const bool want_inline = svg_get_option("kinline") != 0;
-	const bool want_khash = !h->dix.bcode || want_inline || svg_get_option("khash_probe") != 0;
-	if (want_khash && !svg_get_option("no_compact") && !svg_get_option("no_khash")) {
+	// beside the code it was measured at C3 (profiles/r04/bench_c3_*.json): the key-hash probe
+	// kernel is 18% faster than the code's, but the lane / wave kernels slow by more than that
+	// (113.5 vs 110.6 ms/step), so the code is the probe image of -F -B indexes.  The code, when it fits, also serves the paths that need
+	// item indices (svg_probe_keys, fragile and sublong voting).  (Round 4 also measured the key-hash
+	// image beside the code with one-hit runs inline -- the hit's position in the probe record, no
+	// vals[] load -- 52 GB at C3, slower: 113.5 vs 110.6 ms/step; removed.)
+	if (!h->dix.bcode && !svg_get_option("no_compact") && !svg_get_option("no_khash")) {
 		// key-hash image of the probe records: 32-byte sectors of 3 entries (lines ~ items / 1.8),
 		// or 64-byte lines of 5 entries (~ items / 3) when a run count needs more than 8 bits
 		for (int sec = svg_get_option("khash64") ? 0 : 1; sec >= 0 && !h->dix.khash; sec--) {
 			const uint64_t lines = (sec ? x->items * 5 / 9 : x->items / 3) + 1024, lb = sec ? 32 : 64;
-			// an optional image: leave room (8 GB) for the vote path's chunk buffers
-			size_t fre = 0, tot = 0;
-			if (h->dix.bcode && (hipMemGetInfo(&fre, &tot) != hipSuccess || fre < lines * lb + ((size_t)8 << 30))) {
-				(void)hipGetLastError();
-				break;
-			}
 			if (dmalloc(h, &h->d_khash, lines * lb + 64) != 0) {
 				h->d_khash = NULL;
 				(void)hipGetLastError();
@@ -2587,13 +2559,12 @@ int svg_index_finish_device(svg_index *h)
 			HIPCHK(hipGetLastError());
 			blocks = ((uint64_t)x->nb + 255) / 256;
 			if (blocks > bmax) blocks = bmax;
-			const uint32_t *iv = want_inline ? (const uint32_t *)h->d_vals : NULL;
 			if (sec)
 				hipLaunchKernelGGL(build_khash<true>, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
-				                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff, iv);
+				                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff);
 			else
 				hipLaunchKernelGGL(build_khash<false>, dim3((unsigned)blocks), dim3(256), 0, h->stream, (const uint32_t *)h->d_bstart,
-				                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff, iv);
+				                   (const int16_t *)h->d_keys, x->nb, (uint32_t *)h->d_khash, lines, ff);
 			HIPCHK(hipGetLastError());
 			uint32_t wide = 0;
 			HIPCHK(hipMemcpyAsync(&wide, ff + 3, 4, hipMemcpyDeviceToHost, h->stream));
@@ -2608,7 +2579,6 @@ int svg_index_finish_device(svg_index *h)
 			h->dix.khash_ff = ff;
 			h->dix.khash_lines = lines;
 			h->dix.khash_sec = sec;
-			h->dix.kinline = want_inline ? 1 : 0;
 		}
 		// which buckets are sorted: there the key-hash record is cellCounts' equal-key run too
 		if (h->dix.khash && dmalloc(h, &h->d_ksorted, ((size_t)x->nb + 31) / 32 * 4 + 64) == 0) {
@@ -2667,11 +2637,6 @@ int svg_index_finish_device(svg_index *h)
 	h->stats_on = 0;
 	h->max_read_len = 256;
 	return 0;
-}
-
-int svg_probe_inline(const svg_index *h)
-{
-	return h->dix.khash && h->dix.kinline && !svg_get_option("probe_v1") ? 1 : 0;
 }
 
 static int index_open_block(const char *prefix, int block, int device, svg_index **out)
@@ -2974,7 +2939,7 @@ static int launch_t(svg_index *h, KParams &kp, hipStream_t st)
 	if (per_cu < 1) { svg_set_error("kernel LDS too large"); return SVG_E_DEVICE; }
 	if (per_cu > 4 * OCC / WPB) per_cu = 4 * OCC / WPB;   // 4 SIMDs x OCC waves
 	if (h->wave_cap > 0 && per_cu > h->wave_cap) per_cu = h->wave_cap;
-	if (svg_get_option("debug"))
+	if (svg_get_option("debug") & 1)
 		fprintf(stderr, "[svg] vote_kernel<%d,%d,%d,%d,%d,%d>: LDS %zu B/wave, %d blocks/CU\n", ENDS, MAXL,
 		        MAXP, WPB, OCC, (int)SJ, sizeof(LT), per_cu);
 	uint64_t blocks = (uint64_t)h->n_cu * per_cu;
@@ -3054,7 +3019,6 @@ int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, con
 	kp.p = *p;
 	kp.ix = h->dix;
 	// one-hit records carry positions only when the line kernel probes the inline key-hash image
-	kp.ix.kinline = svg_probe_inline(h);
 	kp.seq1 = r1->seq; kp.off1 = r1->offsets; kp.len1 = r1->lens;
 	if (r2) { kp.seq2 = r2->seq; kp.off2 = r2->offsets; kp.len2 = r2->lens; }
 	kp.n_reads = r1->n_reads;
@@ -3103,8 +3067,8 @@ int svg_vote_prepare(svg_index *h, const svg_params *p, const svg_reads *r1, con
 	            !h->stored;   // later blocks of a multi-block index merge with stored records: wave kernel
 	kp.stored = h->stored;
 	pp.soa = job->lane ? 1 : 0;
-	pp.window = h->dix.nb >= 131073u && !svg_get_option("no_window");   // key_hi <= 32767: int16 order == key order
-	pp.readmajor = !svg_get_option("probe_colmajor");
+	pp.window = h->dix.nb >= 131073u;   // key_hi <= 32767: int16 order == key order
+	pp.readmajor = 1;
 	return 0;
 }
 
@@ -3141,7 +3105,7 @@ int svg_vote_chunk_probe(svg_index *h, VoteJob *job, uint64_t c0, uint64_t cn, i
 		}
 	}
 #define PROBE_LAUNCH(E, L, P) hipLaunchKernelGGL((probe_kernel<E, 8, L, P>), dim3((unsigned)pb), dim3(256), 0, st, pp)
-	if ((h->dix.bline || h->dix.bcode || h->dix.khash) && !svg_get_option("probe_v1")) {
+	if (h->dix.bline || h->dix.bcode || h->dix.khash) {
 		// bucket lines: grouped probe kernel + the big-bucket kernel on its list
 		pp.group = (uint32_t)(PROBE_GROUP_RECS / job->per_read);
 		if (pp.group > 64) pp.group = 64;
@@ -3275,12 +3239,12 @@ static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads 
 	const uint64_t n = r1->n_reads;
 	const bool overlap = job.overlap_mode && chunk < n;
 	hipStream_t st2 = overlap ? h->stream2 : st;
-	if (svg_get_option("debug"))
+	if (svg_get_option("debug") & 1)
 		fprintf(stderr, "[svg] batch of %llu reads: chunks of %llu, chunk pipeline %s\n", (unsigned long long)n,
 		        (unsigned long long)chunk, overlap ? "on" : "off");
-	// chunk slots (probe records, lane lists): 2, as in the host pipeline (option host_slots 3:
-	// measured slower there -- the records must stay in the infinity cache)
-	const int NS = svg_get_option("host_slots") == 3 ? 3 : 2;
+	// chunk slots (probe records, lane lists): 2, as in the host pipeline (three were measured slower
+	// there -- the records must stay in the infinity cache)
+	const int NS = 2;
 	bool slot_busy[3] = {false, false, false};
 	// chunk boundaries: ramped at both ends (chunk/4, chunk/2 first and last, option host_ramp) when
 	// the batch holds at least 8 chunks -- the second stream gets work sooner and the last wave

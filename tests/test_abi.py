@@ -16,7 +16,7 @@ ensure_built()
 
 def header_symbols():
     syms = set()
-    for h in ("subread_vote.h", "subread_events.h", "subread_long.h", "subread_sam.h"):
+    for h in ("subread_vote.h", "subread_events.h", "subread_long.h", "subread_sam.h", "subread_realign.h"):
         txt = open(os.path.join(ROOT, "include", h)).read()
         txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
         syms |= set(re.findall(r"\b(svg_[a-z0-9_]+)\s*\(", txt))

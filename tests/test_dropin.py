@@ -189,3 +189,17 @@ def test_oracle_dropin_bam_keep_read_order(cache, tmp_path):
         outs[kind] = _bam_records(o)
     assert len(outs["dump"]) > 100000
     assert outs["dump"] == outs["oracle-dropin"]
+
+
+@pytest.mark.parametrize("name,threads", [("pe_gapped_errmut", 1), ("sj_pe_gapped_long", 2), ("sj_pe_mb_long_gappedM6", 1),
+                                          ("se_gapped_mixed_n14_I16", 4)])
+def test_oracle_dropin_several_handles(name, threads, cache, tmp_path):
+    """SVG_DEVICES=0,0,0: the binding with three handles (svg_attach_devices) splits each chunk into
+    three contiguous read ranges voted by three host threads into the one bigtable (the GPU fan-out
+    of run_maybe_threads, core.c:3379-3461) -- the stock reference's outputs byte for byte, incl.
+    the multi-block loop and fragile junction voting (on the first handle)."""
+    c = Case(name)
+    if not have(c.meta["program"], "oracle-dropin"):
+        pytest.skip("reference drop-in binaries not built (make -C oracle dropin)")
+    rep = check_case(c, cache.get(c.index_key), str(tmp_path), "oracle-dropin", threads, env={"SVG_DEVICES": "0,0,0"})
+    assert rep["mapped"] > 0

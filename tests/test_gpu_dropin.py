@@ -47,6 +47,19 @@ def test_gpu_dropin_matches_stock_reference(name, threads, cache, tmp_path):
     print(name, rep)
 
 
+@pytest.mark.parametrize("name,threads", [
+    ("pe_gapped_errmut", 1), ("sj_pe_gapped_junc", 2), ("sj_pe_mb_long_gappedM6", 1), ("se_gapped_mixed_n14_I16", 4)])
+def test_gpu_dropin_two_handles(name, threads, cache, tmp_path):
+    """SVG_DEVICES=0,0: two handles (two index replicas; this box has one GPU, so both on device 0),
+    each chunk split into two contiguous read ranges voted by two host threads into the one
+    bigtable -- the stock outputs byte for byte.  On an 8-GPU node SVG_DEVICES=0,...,7 gives each
+    device one range."""
+    c = Case(name)
+    _need(c.meta["program"])
+    rep = check_case(c, cache.get(c.index_key), str(tmp_path), "dropin", threads, env={"SVG_DEVICES": "0,0"})
+    assert rep["mapped"] > 0
+
+
 @pytest.mark.timeout(600)
 def test_gpu_dropin_c2_200k(tmp_path):
     """200k C2 reads (bench.py workload c2's genome and read generator) through the drop-in, -T 8."""
@@ -64,6 +77,10 @@ def test_gpu_dropin_c2_200k(tmp_path):
     run(0, "dump", pre, f1, None, so, threads=8)
     run(0, "dropin", pre, f1, None, do, threads=8)
     rep = compare(so, do)
+    # the same with two handles (contiguous halves of the chunk)
+    do2 = str(tmp_path / "c2.dropin2.sam")
+    run(0, "dropin", pre, f1, None, do2, threads=8, env={"SVG_DEVICES": "0,0"})
+    compare(so, do2)
     votes = np.fromfile(do + ".votes", dtype=np.uint8)
     assert votes.size == 200_000 * 3 * 68
     assert rep["sam_records"] >= 200_000 and rep["mapped"] > 190_000, rep

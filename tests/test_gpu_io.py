@@ -73,13 +73,10 @@ def test_compacted_pipeline_small_subbatches(mode, entry, gpu_indexes, index_cac
     ix = gpu_indexes(key)
     # (2000 and 64: the ramped schedule -- sub/4, sub/2, full ones, the remainder, sub/2, sub/4;
     # 3001 / 7777 and host_ramp 0: uniform sub-batches)
-    # (host_slots: device slots 3 -- the default -- or 2)
-    for sub, th, ramp, slots in (("3001", "1", 1, 3), ("7777", "3", 1, 2), ("64", "8", 1, 3), ("2000", "4", 1, 3),
-                                 ("2000", "2", 0, 2)):
+    for sub, th, ramp in (("3001", "1", 1), ("7777", "3", 1), ("64", "8", 1), ("2000", "4", 1), ("2000", "2", 0)):
         svgopt.set("host_sub", int(sub))
         svgopt.set("host_threads", int(th))
         svgopt.set("host_ramp", ramp)
-        svgopt.set("host_slots", slots)
         if entry == "ascii":
             out, jout, bm = ix.vote(p, r1, r2)
         else:

@@ -172,14 +172,11 @@ def test_gpu_pipelines_match_oracle(mode, gpu_indexes, index_cache, svgopt):
 
 def test_gpu_probe_images_match_oracle(svgopt):
     """The probe images picked at index load: 32-byte unary bucket codes (default for -F -B
-    indexes), the key-hash of probe records beside them (khash_probe) or with one-hit runs inline
-    (kinline: the hit's position in place of its item), the key-hash alone in 32-byte sectors
-    (no_bcode; the default of every index the code does not fit, e.g. gapped ones; + kinline) or
-    64-byte lines (+ khash64),
-    64-byte bucket lines (+ no_khash), 16-bucket
-    groups + u8 keys (+ no_bline), plain bounds + i16 keys (no_compact), and the
-    one-kernel probe of the previous build (probe_v1).  The genome carries repeat families, so
-    that buckets past a code's 169 keys / a line's 59 keys take the big-bucket search."""
+    indexes), the key-hash of probe records in 32-byte sectors (no_bcode; the default of every
+    index the code does not fit, e.g. gapped ones) or 64-byte lines (+ khash64), 64-byte bucket
+    lines (+ no_khash), 16-bucket groups + u8 keys (+ no_bline), plain bounds + i16 keys
+    (no_compact).  The genome carries repeat families, so that buckets past a code's 169 keys / a
+    line's 59 keys take the big-bucket search."""
     import subread_amd as sa
     from oracle.pyoracle import OracleIndex
     from subread_amd.abi import default_params, PROGRAM_ALIGN
@@ -188,18 +185,15 @@ def test_gpu_probe_images_match_oracle(svgopt):
     r1 = simulate_reads(g, 40000, 100, seed=5, sub=0.01, indel=0.001)
     p = default_params(PROGRAM_ALIGN, False)
     want = None
-    for env in ({}, {"kinline": 1}, {"khash_probe": 1}, {"no_bcode": 1}, {"no_bcode": 1, "kinline": 1},
-                {"no_bcode": 1, "khash64": 1}, {"no_bcode": 1, "khash64": 1, "kinline": 1}, {"no_bcode": 1, "no_khash": 1},
-                {"no_bcode": 1, "no_khash": 1, "no_bline": 1}, {"no_compact": 1},
-                {"probe_v1": 1}, {"probe_v1": 1, "no_bcode": 1}):
+    for env in ({}, {"no_bcode": 1}, {"no_bcode": 1, "khash64": 1}, {"no_bcode": 1, "no_khash": 1},
+                {"no_bcode": 1, "no_khash": 1, "no_bline": 1}, {"no_compact": 1}):
         for k, v in env.items():
             svgopt.set(k, v)
         # repeat threshold 400 (-f 400): keys with up to 400 occurrences stay, so some buckets
         # exceed a code's 169 items too
         ix = sa.VoteIndex.build_genome(g, gap=1, force_one_block=True, repeat_threshold=400, device=0)
-        if "probe_v1" not in env:
-            for k in env:
-                svgopt.reset(k)
+        for k in env:
+            svgopt.reset(k)
         if want is None:
             a = ix.export()
             sizes = np.diff(a["bstart"].astype(np.int64))

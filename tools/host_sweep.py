@@ -29,7 +29,7 @@ pk = sa.pack_reads(rb, 100, threads=16, alloc=pinned)
 pk.lens = pinned(n, np.uint16)
 pk.lens[:] = rb.lens
 o = pinned(n * 3, sa.MAPPING_DTYPE).reshape(n, 1, 3)
-sa.set_option("pipe_debug", 1)
+sa.set_option("debug", 2)
 for sub in os.environ.get("SUBS", "262144 524288 1048576 2097152").split():
     for th in os.environ.get("THREADS", "8 16").split():
         sa.set_option("host_sub", int(sub))
