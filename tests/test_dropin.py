@@ -191,7 +191,7 @@ def test_oracle_dropin_bam_keep_read_order(cache, tmp_path):
     assert outs["dump"] == outs["oracle-dropin"]
 
 
-@pytest.mark.parametrize("name,threads", [("pe_gapped_errmut", 1), ("sj_pe_gapped_long", 2), ("sj_pe_mb_long_gappedM6", 1),
+@pytest.mark.parametrize("name,threads", [("pe_gapped_errmut", 1), ("sj_pe_gapped_long", 1), ("sj_pe_mb_long_gappedM6", 1),
                                           ("se_gapped_mixed_n14_I16", 4)])
 def test_oracle_dropin_several_handles(name, threads, cache, tmp_path):
     """SVG_DEVICES=0,0,0: the binding with three handles (svg_attach_devices) splits each chunk into

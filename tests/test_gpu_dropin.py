@@ -48,7 +48,7 @@ def test_gpu_dropin_matches_stock_reference(name, threads, cache, tmp_path):
 
 
 @pytest.mark.parametrize("name,threads", [
-    ("pe_gapped_errmut", 1), ("sj_pe_gapped_junc", 2), ("sj_pe_mb_long_gappedM6", 1), ("se_gapped_mixed_n14_I16", 4)])
+    ("pe_gapped_errmut", 1), ("sj_pe_gapped_junc", 1), ("sj_pe_mb_long_gappedM6", 1), ("se_gapped_mixed_n14_I16", 4)])
 def test_gpu_dropin_two_handles(name, threads, cache, tmp_path):
     """SVG_DEVICES=0,0: two handles (two index replicas; this box has one GPU, so both on device 0),
     each chunk split into two contiguous read ranges voted by two host threads into the one
