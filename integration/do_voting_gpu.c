@@ -67,6 +67,7 @@ int find_subread_end(int len, int TOTAL_SUBREADS, int subread);   /* input-files
 #define SVG_MAX_DEV 16
 static svg_index *svg_ix[SVG_MAX_DEV];
 static int svg_nix;
+static double svg_t_open;      /* SVG_REF_TIMING: svg_index_open of every handle (the index files into HBM) */
 static pthread_mutex_t svg_sam_mu_init = PTHREAD_MUTEX_INITIALIZER;   /* one-time setup of the shared state */
 
 int svg_attach_devices(global_context_t *gc, const int *devices, int n)
@@ -78,11 +79,13 @@ int svg_attach_devices(global_context_t *gc, const int *devices, int n)
 		return 1;
 	}
 	snprintf(prefix, sizeof prefix, "%s", gc->config.index_prefix);
+	const double t0 = miltime();
 	for (k = 0; k < n && !rc; k++) {
 		rc = svg_index_open(prefix, devices[k], &svg_ix[k]);
 		if (rc) SUBREADprintf("GPU voting unavailable on device %d: %s\n", devices[k], svg_last_error());
 		else svg_nix = k + 1;
 	}
+	svg_t_open += miltime() - t0;
 	return rc;
 }
 
@@ -666,8 +669,8 @@ int svg_sam_finish(void)
 	if (svg_sam && (rc = svg_sam_writer_close(svg_sam))) SUBREADprintf("svg_sam_writer_close: %s\n", svg_last_error());
 	svg_sam = NULL;
 	if (getenv("SVG_REF_TIMING"))
-		fprintf(stderr, "SVG_DROPIN_VOTING read_chunk=%.6f vote_call=%.6f fragile=%.6f tail=%.6f realign=%.6f\n", svg_t_read,
-		        svg_t_vote, svg_t_frag, svg_t_tail, svg_t_realign);
+		fprintf(stderr, "SVG_DROPIN_VOTING index_open=%.6f read_chunk=%.6f vote_call=%.6f fragile=%.6f tail=%.6f realign=%.6f\n",
+		        svg_t_open, svg_t_read, svg_t_vote, svg_t_frag, svg_t_tail, svg_t_realign);
 	return rc;
 }
 

@@ -35,6 +35,11 @@ def main():
                     help="which binaries: dump (stock), dropin (GPU vote + the library's iteration two), "
                          "dropin_refit2 (GPU vote + the reference's own iteration two, SVG_REF_ITER2=1)")
     ap.add_argument("--out", default="", help="also write the JSON line here")
+    ap.add_argument("--genome", default="synth", choices=["synth", "c3"],
+                    help="synth: --mbp Mbp with repeat families; c3: bench.py's C3 genome (3.0 Gbp, 24 contigs)")
+    ap.add_argument("--gpu-build", action="store_true", help="write the index files with the GPU builder "
+                    "(svg_index_build_mem + save_prefix; the same bytes as the CPU builder, minutes faster at 3 Gbp)")
+    ap.add_argument("--no-startup", action="store_true", help="skip the one-read runs (fixed cost) of each binary")
     args = ap.parse_args()
     kinds = args.kinds.split(",")
     import subread_amd as sa
@@ -45,10 +50,18 @@ def main():
     T = args.threads or cpu["usable_cpus"]
     wd = args.workdir or tempfile.mkdtemp(prefix="svg_e2e_")
     t0 = time.time()
-    g = random_genome(c3_lengths(args.mbp * 1_000_000), 3000, repeats=(args.mbp * 300, 300, 200, 0.12))
+    if args.genome == "c3":   # bench.py's c3 workload genome
+        g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))
+    else:
+        g = random_genome(c3_lengths(args.mbp * 1_000_000), 3000, repeats=(args.mbp * 300, 300, 200, 0.12))
     fa, pre = os.path.join(wd, "g.fa"), os.path.join(wd, "g_full")
-    g.write_fasta(fa)
-    sa.build_index(fa, pre, gap=1, force_one_block=True)
+    if args.gpu_build:
+        ix = sa.VoteIndex.build_genome(g, gap=1, memory_mb=8000, force_one_block=True, device=0, save_prefix=pre)
+        ix.close()
+    else:
+        g.write_fasta(fa)
+        sa.build_index(fa, pre, gap=1, force_one_block=True)
+    tab_bytes = os.path.getsize(pre + ".00.b.tab")
     log("[e2e] genome %.0f Mbp + index files in %.1fs" % (g.length / 1e6, time.time() - t0))
     rb = simulate_reads(g, args.reads, 100, seed=20261015, sub=0.01, indel=0.001)
     fq, fq1 = os.path.join(wd, "r.fq"), os.path.join(wd, "r1.fq")
@@ -70,7 +83,8 @@ def main():
         # the fixed cost first (index load(s), voting space, output files): the same program on one read
         out = os.path.join(wd, "one_%s.sam" % kind)
         ts = time.perf_counter()
-        dropin.run(0, binkind, pre, fq1, None, out, threads=T, timeout=1500, env=kenv)
+        if not args.no_startup:
+            dropin.run(0, binkind, pre, fq1, None, out, threads=T, timeout=1500, env=kenv)
         start[kind] = time.perf_counter() - ts
         out = os.path.join(wd, "out_%s.sam" % kind)
         ts = time.perf_counter()
@@ -114,7 +128,8 @@ def main():
                            "oracle/ref_dump_hook.c: load_index, voting, before_realign (anti-support scan + "
                            "remove_neighbour), realign (iteration two incl. SAM writing)",
             "cpu_model": cpu["model"],
-            "config": {"genome_mbp": round(g.length / 1e6, 1), "reads": args.reads, "read_len": 100, "mode": "SE, -t 1 (DNA)",
+            "config": {"genome_mbp": round(g.length / 1e6, 1), "genome": args.genome, "tab_bytes": tab_bytes,
+                       "reads": args.reads, "read_len": 100, "mode": "SE, -t 1 (DNA)",
                        "index": "full one-block files (our builder, md5-identical to subread-buildindex -F -B)"}}
     print(json.dumps(line), flush=True)
     if args.out:
