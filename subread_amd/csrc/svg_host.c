@@ -22,7 +22,15 @@
 #include <unistd.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <time.h>
 #include "svg_internal.h"
+
+static double t_now(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 
 static __thread char g_err[1024];
 
@@ -135,6 +143,8 @@ static int load_tab(const char *fn, svg_host_index *ix, int threads)
 	uint32_t b;
 	if (fd < 0) { svg_set_error("index table '%s' not found", fn); return SVG_E_IO; }
 	if (fstat(fd, &st) || st.st_size < 32) { close(fd); svg_set_error("index table '%s' unreadable", fn); return SVG_E_IO; }
+	const int dbg = (svg_get_option("debug") & 8) != 0;
+	double t0 = t_now();
 	ix->map_len = st.st_size;
 	ix->map = mmap(NULL, ix->map_len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
 	close(fd);
@@ -165,6 +175,7 @@ static int load_tab(const char *fn, svg_host_index *ix, int threads)
 	ix->keys = malloc(2 * ix->items + 64);
 	ix->vals = malloc(4 * ix->items + 64);
 	if (!ix->bstart || !hdr || !ix->keys || !ix->vals) { free(hdr); svg_set_error("out of host memory loading index"); return SVG_E_NOMEM; }
+	const double t1 = t_now();
 	for (b = 0; b < ix->nb; b++) {
 		int32_t n;
 		if (p + 8 > end) { free(hdr); svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT; }
@@ -176,6 +187,7 @@ static int load_tab(const char *fn, svg_host_index *ix, int threads)
 	}
 	ix->bstart[ix->nb] = (uint32_t)cur;
 	if (cur != ix->items || p > end) { free(hdr); svg_set_error("'%s': bucket sizes do not add up", fn); return SVG_E_FORMAT; }
+	const double t2 = t_now();
 	{
 		int t, nt = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
 		pthread_t th[64];
@@ -190,8 +202,12 @@ static int load_tab(const char *fn, svg_host_index *ix, int threads)
 			if (th[t]) pthread_join(th[t], NULL);   /* 0: that range ran inline */
 	}
 	free(hdr);
+	const double t3 = t_now();
 	munmap(ix->map, ix->map_len);
 	ix->map = NULL;
+	if (dbg)
+		fprintf(stderr, "[svg] load_tab %s: %.2f GB, mmap+populate %.3f s, bucket headers %.3f s, copy (%d threads) %.3f s, unmap %.3f s\n",
+		        fn, (double)ix->map_len / 1e9, t1 - t0, t2 - t1, threads, t3 - t2, t_now() - t3);
 	return 0;
 }
 
@@ -209,23 +225,76 @@ int svg_index_count_blocks(const char *prefix)
 	return n;
 }
 
+/* The .tab of a block mapped for a streaming load (svg_vote.hip index_open_block): the header
+ * (options, items, buckets) parsed, *first = the first bucket header.  Bucket b's header is then at
+ * first + 8 b + 6 bstart[b] (header {i32 n, i32 space}, then i16 keys[n], u32 vals[n]). */
+int svg_tab_map(const char *fn, svg_host_index *ix, const uint8_t **first)
+{
+	int fd = open(fn, O_RDONLY);
+	struct stat st;
+	if (fd < 0) { svg_set_error("index table '%s' not found", fn); return SVG_E_IO; }
+	if (fstat(fd, &st) || st.st_size < 32) { close(fd); svg_set_error("index table '%s' unreadable", fn); return SVG_E_IO; }
+	ix->map_len = st.st_size;
+	ix->map = mmap(NULL, ix->map_len, PROT_READ, MAP_PRIVATE, fd, 0);
+	close(fd);
+	if (ix->map == MAP_FAILED) { ix->map = NULL; svg_set_error("mmap of '%s' failed", fn); return SVG_E_IO; }
+	madvise(ix->map, ix->map_len, MADV_SEQUENTIAL);
+	const uint8_t *m = ix->map, *p = m + 8, *end = m + ix->map_len;
+	if (memcmp(m, "2subindx", 8)) { svg_set_error("'%s' is not a v2 subread index (magic)", fn); return SVG_E_FORMAT; }
+	for (;;) {
+		int16_t k, l;
+		if (p + 4 > end) { svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT; }
+		memcpy(&k, p, 2); p += 2;
+		if (!k) break;
+		memcpy(&l, p, 2); p += 2;
+		if (k == 0x0101) { int16_t v; memcpy(&v, p, 2); ix->gap = v; }
+		else if (k == 0x0102) { int16_t v; memcpy(&v, p, 2); ix->padding = v; }
+		p += l;
+	}
+	int64_t items; int32_t nb;
+	if (p + 12 > end) { svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT; }
+	memcpy(&items, p, 8); p += 8;
+	memcpy(&nb, p, 4); p += 4;
+	if (items < 1 || (uint64_t)items > 0xffffffffull || nb < 1) { svg_set_error("'%s': bad item/bucket count", fn); return SVG_E_FORMAT; }
+	if (ix->gap < 1) { svg_set_error("'%s': no index gap option", fn); return SVG_E_FORMAT; }
+	ix->items = items; ix->nb = nb;
+	*first = p;
+	return 0;
+}
+
+/* one block's .array and the chromosome table of <prefix>.reads (gvindex_load, load_offsets) */
+static int load_meta(const char *prefix, int block, svg_host_index *ix);
+
+int svg_host_index_load_meta(const char *prefix, int block, svg_host_index *ix)
+{
+	return load_meta(prefix, block, ix);   /* (on an error the caller frees ix: the .tab may still be mapped) */
+}
+
 /* one block: <prefix>.NN.b.tab and .NN.b.array (gehash_load / gvindex_load of read_chunk_circles,
- * core.c:3553-3582), plus the chromosome table of <prefix>.reads */
+ * core.c:3553-3582), plus the chromosome table of <prefix>.reads, into host arrays */
 int svg_host_index_load_block(const char *prefix, int block, svg_host_index *ix, int threads)
 {
 	char fn[4096];
-	FILE *fp;
 	int rc;
 	memset(ix, 0, sizeof *ix);
 	snprintf(fn, sizeof fn, "%s.%02d.b.tab", prefix, block);
 	rc = load_tab(fn, ix, threads);
 	if (rc) { svg_host_index_free(ix); return rc; }
+	rc = load_meta(prefix, block, ix);
+	if (rc) svg_host_index_free(ix);
+	return rc;
+}
+
+static int load_meta(const char *prefix, int block, svg_host_index *ix)
+{
+	char fn[4096];
+	FILE *fp;
 
 	snprintf(fn, sizeof fn, "%s.%02d.b.array", prefix, block);
 	fp = fopen(fn, "rb");
-	if (!fp) { svg_host_index_free(ix); svg_set_error("'%s' not found", fn); return SVG_E_IO; }
+	if (!fp) { svg_set_error("'%s' not found", fn); return SVG_E_IO; }
 	if (fread(&ix->start_point, 4, 1, fp) != 1 || fread(&ix->length, 4, 1, fp) != 1) {
-		fclose(fp); svg_host_index_free(ix); svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT;
+		fclose(fp); svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT;
 	}
 	ix->start_base_offset = ix->start_point - ix->start_point % 4;
 	{
@@ -233,14 +302,14 @@ int svg_host_index_load_block(const char *prefix, int block, svg_host_index *ix,
 		ix->values_bytes = useful + 1;
 		ix->values = calloc((size_t)ix->values_bytes + 64, 1);
 		if (fread(ix->values, 1, useful + 1, fp) < useful) {
-			fclose(fp); svg_host_index_free(ix); svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT;
+			fclose(fp); svg_set_error("'%s' truncated", fn); return SVG_E_FORMAT;
 		}
 	}
 	fclose(fp);
 
 	snprintf(fn, sizeof fn, "%s.reads", prefix);
 	fp = fopen(fn, "r");
-	if (!fp) { svg_host_index_free(ix); svg_set_error("'%s' not found", fn); return SVG_E_IO; }
+	if (!fp) { svg_set_error("'%s' not found", fn); return SVG_E_IO; }
 	{
 		char line[4096];
 		uint32_t cap = 64;
@@ -263,7 +332,7 @@ int svg_host_index_load_block(const char *prefix, int block, svg_host_index *ix,
 		}
 	}
 	fclose(fp);
-	if (!ix->n_chr) { svg_host_index_free(ix); svg_set_error("'%s' is empty", fn); return SVG_E_FORMAT; }
+	if (!ix->n_chr) { svg_set_error("'%s' is empty", fn); return SVG_E_FORMAT; }
 	return 0;
 }
 

@@ -39,6 +39,9 @@ typedef struct svg_host_index {
 int  svg_host_index_load(const char *prefix, svg_host_index *out, int threads);
 int  svg_host_index_load_block(const char *prefix, int block, svg_host_index *out, int threads);
 int  svg_index_count_blocks(const char *prefix);
+/* streaming load (svg_vote.hip): the .tab mapped and its header parsed; the .array / .reads */
+int  svg_tab_map(const char *fn, svg_host_index *ix, const uint8_t **first);
+int  svg_host_index_load_meta(const char *prefix, int block, svg_host_index *ix);
 void svg_host_index_free(svg_host_index *ix);
 
 uint32_t svg_bucket_count(uint64_t expected_items, int gap);

@@ -33,7 +33,14 @@
 // per-wave HBM scratch that stays L2-resident.  Integer work only: no MFMA.
 #include <hip/hip_runtime.h>
 #include <vector>
+#include <chrono>
+#include <atomic>
+#include <deque>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <pthread.h>
+#include <sys/mman.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
@@ -2639,32 +2646,233 @@ int svg_index_finish_device(svg_index *h)
 	return 0;
 }
 
+// One block from its files into HBM.  The .tab is a chain of bucket records {i32 n, i32 space,
+// i16 keys[n], u32 vals[n]}: where bucket b + 1 starts is known only from bucket b's n, and a
+// serial walk of the chain is one dependent memory load per bucket (C3: 93M buckets, 11.7 s).
+// The walk is split instead: worker t finds, from byte S_t = t/T of the file on, the first offset
+// where a run of WALK_SYNC consecutive records is well formed (n == space -- what gehash_dump and
+// our builder write, sorted-hashtable.c:1867-1870 --, sizes inside the file) and walks the chain
+// from there; worker t's walk must land exactly on worker t+1's start (the last one on the file's
+// final byte), which proves every start right -- otherwise one serial walk is done instead.
+// Then bucket starts are a prefix sum, and the workers gather runs of buckets (~LOAD_ITEMS items)
+// from the mapped file into pinned staging buffers and copy them to d_keys / d_vals on streams of
+// their own; the .array and .reads load beside them.  No host copy of the 21 GB arrays is made
+// (round 4 read them into malloc'd arrays, then uploaded pageable memory: 19.1 s at C3).
+#define LOAD_ITEMS (4u << 20)
+#define LOAD_WORKERS 16
+#define LOAD_BUFS 2
+#define WALK_SYNC 32
+
+// a well-formed run of WALK_SYNC records from p (the file's buckets end at `last`)
+static bool tab_sync_ok(const uint8_t *p, const uint8_t *last)
+{
+	for (int k = 0; k < WALK_SYNC; k++) {
+		if (p == last) return k > 0;
+		if (p + 8 > last) return false;
+		int32_t n, sp;
+		memcpy(&n, p, 4);
+		memcpy(&sp, p + 4, 4);
+		if (n < 0 || n != sp || (uint64_t)(last - p) < 8 + 6 * (uint64_t)(uint32_t)n) return false;
+		p += 8 + 6 * (size_t)(uint32_t)n;
+	}
+	return true;
+}
+
+// the bucket sizes of the chain from `first` to `last`, in order; false: not a chain of nb buckets
+static bool tab_walk(const uint8_t *first, const uint8_t *last, uint32_t nb, uint32_t *sizes, int nt)
+{
+	const uint64_t len = (uint64_t)(last - first);
+	std::vector<const uint8_t *> start(nt + 1, NULL);
+	std::vector<std::vector<uint32_t>> part(nt);
+	std::vector<const uint8_t *> stop(nt, NULL);
+	start[0] = first;
+	start[nt] = last;
+	// starts: candidate offsets keep first's parity (every record is an even number of bytes)
+	{
+		std::vector<std::thread> th;
+		for (int t = 1; t < nt; t++)
+			th.emplace_back([&, t] {
+				const uint8_t *q = first + len * (uint64_t)t / (uint64_t)nt;
+				if ((q - first) & 1) q++;
+				const uint8_t *lim = first + len * (uint64_t)(t + 1) / (uint64_t)nt;
+				for (; q < lim; q += 2)
+					if (tab_sync_ok(q, last)) { start[t] = q; return; }
+			});
+		for (auto &x : th) x.join();
+	}
+	// segments without a start merge into the one before them
+	std::vector<int> seg;
+	for (int t = 0; t < nt; t++) if (start[t]) seg.push_back(t);
+	const int ns = (int)seg.size();
+	std::vector<const uint8_t *> s0(ns + 1);
+	for (int k = 0; k < ns; k++) s0[k] = start[seg[k]];
+	s0[ns] = last;
+	{
+		std::vector<std::thread> th;
+		for (int k = 0; k < ns; k++)
+			th.emplace_back([&, k] {
+				const uint8_t *p = s0[k], *until = s0[k + 1];
+				std::vector<uint32_t> &v = part[k];
+				v.reserve((size_t)((until - p) / 150 + 16));
+				while (p < until) {
+					if (p + 8 > last) break;
+					int32_t n;
+					memcpy(&n, p, 4);
+					if (n < 0 || (uint64_t)(last - p) < 8 + 6 * (uint64_t)(uint32_t)n) break;
+					v.push_back((uint32_t)n);
+					p += 8 + 6 * (size_t)(uint32_t)n;
+				}
+				stop[k] = p;
+			});
+		for (auto &x : th) x.join();
+	}
+	bool ok = true;
+	uint64_t total = 0;
+	for (int k = 0; k < ns; k++) {
+		if (stop[k] != s0[k + 1]) ok = false;
+		total += part[k].size();
+	}
+	if (ok && total == nb) {
+		uint64_t b = 0;
+		for (int k = 0; k < ns; k++) {
+			memcpy(sizes + b, part[k].data(), 4 * part[k].size());
+			b += part[k].size();
+		}
+		return true;
+	}
+	// one serial walk
+	const uint8_t *p = first;
+	for (uint32_t b = 0; b < nb; b++) {
+		if (p + 8 > last) return false;
+		int32_t n;
+		memcpy(&n, p, 4);
+		if (n < 0 || (uint64_t)(last - p) < 8 + 6 * (uint64_t)(uint32_t)n) return false;
+		sizes[b] = (uint32_t)n;
+		p += 8 + 6 * (size_t)(uint32_t)n;
+	}
+	return p == last;
+}
+
 static int index_open_block(const char *prefix, int block, int device, svg_index **out)
 {
 	*out = NULL;
 	svg_index *h = (svg_index *)calloc(1, sizeof(svg_index));
+	if (!h) { svg_set_error("out of memory"); return SVG_E_NOMEM; }
 	h->device = device;
 	h->nblocks = 1;
-	int rc = svg_host_index_load_block(prefix, block, &h->host, 16);
-	if (rc) { free(h); return rc; }
+	const bool dbg = (svg_get_option("debug") & 8) != 0;
+	auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+	const double t0 = now();
 	svg_host_index *x = &h->host;
-	if ((rc = dmalloc(h, &h->d_bstart, 4 * ((size_t)x->nb + 1))) || (rc = dmalloc(h, &h->d_keys, 2 * x->items + 64)) ||
-	    (rc = dmalloc(h, &h->d_vals, 4 * x->items + 64))) {
-		svg_index_close(h);
-		return rc;
+	char fn[4096];
+	snprintf(fn, sizeof fn, "%s.%02d.b.tab", prefix, block);
+	const uint8_t *first = NULL;
+	int rc = svg_tab_map(fn, x, &first);
+	if (rc) { svg_host_index_free(x); free(h); return rc; }
+	// the .array and the contig table on a thread of their own
+	int meta_rc = 0;
+	std::thread meta([&] { meta_rc = svg_host_index_load_meta(prefix, block, x); });
+	// the buckets end one byte before the file does (gehash_dump's is_small_table byte)
+	const uint8_t *const last = (const uint8_t *)x->map + x->map_len - 1;
+	uint32_t *bstart = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)x->nb + 1));
+	if (!bstart) { rc = SVG_E_NOMEM; svg_set_error("out of memory"); }
+	if (!rc && ((rc = dmalloc(h, &h->d_bstart, 4 * ((size_t)x->nb + 1))) || (rc = dmalloc(h, &h->d_keys, 2 * x->items + 64)) ||
+	            (rc = dmalloc(h, &h->d_vals, 4 * x->items + 64))))
+		;
+	double t_walk = 0, t_copy = 0;
+	if (!rc) {
+		if (!tab_walk(first, last, x->nb, bstart, LOAD_WORKERS)) {
+			rc = SVG_E_FORMAT;
+			svg_set_error("'%s': the bucket records do not make %u buckets", fn, x->nb);
+		} else {
+			uint64_t cur = 0;
+			for (uint32_t b = 0; b < x->nb; b++) {
+				const uint32_t n = bstart[b];
+				bstart[b] = (uint32_t)cur;
+				cur += n;
+			}
+			bstart[x->nb] = (uint32_t)cur;
+			if (cur != x->items) { rc = SVG_E_FORMAT; svg_set_error("'%s': bucket sizes do not add up", fn); }
+		}
+		t_walk = now() - t0;
 	}
-	if (hipMemcpy(h->d_bstart, x->bstart, 4 * ((size_t)x->nb + 1), hipMemcpyHostToDevice) != hipSuccess ||
-	    hipMemcpy(h->d_keys, x->keys, 2 * x->items, hipMemcpyHostToDevice) != hipSuccess ||
-	    hipMemcpy(h->d_vals, x->vals, 4 * x->items, hipMemcpyHostToDevice) != hipSuccess) {
-		svg_set_error("upload of the index to HBM failed");
-		svg_index_close(h);
-		return SVG_E_DEVICE;
+	if (!rc) {
+		// runs of buckets [b0, b1) of about LOAD_ITEMS items
+		std::vector<std::pair<uint32_t, uint32_t>> jobs;
+		for (uint32_t b0 = 0, b = 0; b < x->nb; b++)
+			if ((uint64_t)bstart[b + 1] - bstart[b0] >= LOAD_ITEMS || b + 1 == x->nb) {
+				jobs.emplace_back(b0, b + 1);
+				b0 = b + 1;
+			}
+		std::atomic<size_t> next(0);
+		std::atomic<int> werr(0);
+		auto worker = [&]() {
+			hipStream_t st = NULL;
+			uint8_t *buf[LOAD_BUFS] = {NULL, NULL};
+			hipEvent_t ev[LOAD_BUFS] = {NULL, NULL};
+			bool used[LOAD_BUFS] = {false, false};
+			int k = 0;
+			if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) werr = 1;
+			for (int i = 0; i < LOAD_BUFS && !werr; i++)
+				if (hipHostMalloc((void **)&buf[i], 6 * (size_t)LOAD_ITEMS, hipHostMallocDefault) != hipSuccess ||
+				    hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
+					werr = 1;
+			for (;;) {
+				const size_t jn = next.fetch_add(1);
+				if (jn >= jobs.size() || werr) break;
+				const uint32_t b0 = jobs[jn].first, b1 = jobs[jn].second;
+				const uint64_t i0 = bstart[b0], cnt = (uint64_t)bstart[b1] - i0;
+				if (!cnt) continue;
+				if (cnt > LOAD_ITEMS) {   // one bucket larger than a staging buffer: straight from the map
+					const uint8_t *src = first + 8ull * b0 + 6ull * i0 + 8;
+					if (hipMemcpy((uint8_t *)h->d_keys + 2 * i0, src, 2 * cnt, hipMemcpyHostToDevice) != hipSuccess ||
+					    hipMemcpy((uint8_t *)h->d_vals + 4 * i0, src + 2 * cnt, 4 * cnt, hipMemcpyHostToDevice) != hipSuccess)
+						werr = 1;
+					continue;
+				}
+				if (used[k] && hipEventSynchronize(ev[k]) != hipSuccess) { werr = 1; break; }
+				uint8_t *kb = buf[k], *vb = buf[k] + 2 * (size_t)LOAD_ITEMS;
+				for (uint32_t b = b0; b < b1; b++) {
+					const uint64_t n = (uint64_t)bstart[b + 1] - bstart[b], at = (uint64_t)bstart[b] - i0;
+					if (!n) continue;
+					const uint8_t *src = first + 8ull * b + 6ull * bstart[b] + 8;
+					memcpy(kb + 2 * at, src, 2 * n);
+					memcpy(vb + 4 * at, src + 2 * n, 4 * n);
+				}
+				if (hipMemcpyAsync((uint8_t *)h->d_keys + 2 * i0, kb, 2 * cnt, hipMemcpyHostToDevice, st) != hipSuccess ||
+				    hipMemcpyAsync((uint8_t *)h->d_vals + 4 * i0, vb, 4 * cnt, hipMemcpyHostToDevice, st) != hipSuccess ||
+				    hipEventRecord(ev[k], st) != hipSuccess)
+					werr = 1;
+				used[k] = true;
+				k = (k + 1) % LOAD_BUFS;
+			}
+			if (st) { if (hipStreamSynchronize(st) != hipSuccess) werr = 1; hipStreamDestroy(st); }
+			for (int i = 0; i < LOAD_BUFS; i++) {
+				if (ev[i]) hipEventDestroy(ev[i]);
+				if (buf[i]) hipHostFree(buf[i]);
+			}
+		};
+		std::vector<std::thread> ws;
+		for (int t = 0; t < LOAD_WORKERS; t++) ws.emplace_back(worker);
+		for (auto &w : ws) w.join();
+		if (werr) { rc = SVG_E_DEVICE; svg_set_error("upload of the index to HBM failed"); }
+		if (!rc && hipMemcpy(h->d_bstart, bstart, 4 * ((size_t)x->nb + 1), hipMemcpyHostToDevice) != hipSuccess) {
+			rc = SVG_E_DEVICE;
+			svg_set_error("upload of the index to HBM failed");
+		}
+		t_copy = now() - t0;
 	}
-	// the flat key/value arrays now live in HBM; keep only the small host parts
-	free(x->bstart); x->bstart = NULL;
-	free(x->keys); x->keys = NULL;
-	free(x->vals); x->vals = NULL;
+	meta.join();
+	free(bstart);
+	munmap(x->map, x->map_len);
+	x->map = NULL;
+	if (!rc && meta_rc) rc = meta_rc;
+	if (rc) { svg_index_close(h); return rc; }
+	const double t1 = now();
 	if ((rc = svg_index_finish_device(h))) { svg_index_close(h); return rc; }
+	if (dbg)
+		fprintf(stderr, "[svg] index block %d: %.2f GB .tab, bucket walk %.3f s, keys/values in HBM %.3f s, .array + contigs %.3f s, "
+		        "device images %.3f s\n", block, (double)x->map_len / 1e9, t_walk, t_copy, t1 - t0, now() - t1);
 	*out = h;
 	return 0;
 }
