@@ -95,6 +95,51 @@ def cpu_info():
     return {"model": model, "logical_cpus": ncpu, "usable_cpus": usable, "cgroup_quota_cpus": quota}
 
 
+def ref_binary(kind):
+    """The reference aligner built from its own sources with the voting-step clock (oracle/Makefile
+    votetime; oracle/ref_votetime.c) -- git-ignored, travels with the tree like our own .so files."""
+    return os.path.join(ROOT, "oracle", "_ref", "subjunc-votetime" if kind in ("sj", "sjpe") else "subread-align-votetime")
+
+
+def reference_cpu_run(kind, prefix, rb, rb2, chunk, chunks, threads, wd):
+    """The reference's own voting step on the CPU (SURVEY.md §8(d) cpu_baseline, kind "reference"):
+    the first chunk*chunks reads (pairs) of the timed batch as FASTQ, one run of the reference
+    aligner over the same index files with -T threads, the reads in `chunks` chunks of one process
+    (one index load; SVG_REF_CHUNK), each chunk's voting step clocked from its first read handed
+    out to its last (votes, bigtable writes, final-run tail; FASTQ parsing before the clock,
+    iteration two not run).  Returns (per-chunk (seconds, reads), the vote records the reference
+    dumped for the sample (raw bytes, read order), wall seconds)."""
+    import re
+    import subprocess
+    from subread_amd.sim import write_fastq
+    m = min(len(rb), chunk * chunks)
+    f1 = os.path.join(wd, "cpu_r1.fq")
+    write_fastq(f1, rb.slice(0, m))
+    args = [ref_binary(kind), "-T", str(threads), "-i", prefix, "-r", f1, "-o", os.path.join(wd, "cpu.sam"),
+            "--SAMoutput"]
+    if kind not in ("sj", "sjpe"):
+        args += ["-t", "1"]
+    if rb2 is not None:
+        f2 = os.path.join(wd, "cpu_r2.fq")
+        write_fastq(f2, rb2.slice(0, m))
+        args += ["-R", f2]
+    dump = os.path.join(wd, "cpu.votes")
+    if os.path.exists(dump):
+        os.remove(dump)
+    t = time.perf_counter()
+    r = subprocess.run(args, capture_output=True, text=True, timeout=900,
+                       env=dict(os.environ, SVG_REF_CHUNK=str(chunk), SVG_REF_VOTETIME="1", SVG_REF_DUMP=dump))
+    wall = time.perf_counter() - t
+    lines = re.findall(r"SVG_REF_CHUNK_VOTING_S (\d+) ([0-9.]+) (\d+)", r.stderr)
+    if r.returncode != 0 or sum(int(x[2]) for x in lines) != m:
+        raise RuntimeError("reference run failed (%d): %s" % (r.returncode, (r.stdout + r.stderr)[-1500:]))
+    votes = np.fromfile(dump, dtype=np.uint8)
+    for f in [f1, dump, os.path.join(wd, "cpu.sam")] + ([f2] if rb2 is not None else []):
+        if os.path.exists(f):
+            os.remove(f)
+    return [(float(x[1]), int(x[2])) for x in lines], votes, wall
+
+
 def committed_fracs(wl, kernel, bytes_per_launch):
     """The dominant kernel's roofline fraction recomputed from the committed evidence: the newest
     profiles/r*_<wl>_kernel_record.json (HIP events of a GPU run, per launch) and the newest
@@ -127,6 +172,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=20_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="default: the CPUs this process may use")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--ref-chunk", type=int, default=600_000,
+                    help="reads (pairs) per chunk of the reference's timed CPU run (3 chunks: 3 repetitions)")
+    ap.add_argument("--ref-chunks", type=int, default=3)
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--device-steps", type=int, default=5, help="timed steps of the HBM-resident secondary figure")
     ap.add_argument("--ascii-reads", type=int, default=8_000_000, help="reads of the ASCII host-entry figure (0: skip)")
@@ -176,6 +224,7 @@ def main():
     genome = random_genome(W["lengths"], W["gseed"], repeats=W["repeats"])
     log("[bench] genome %.3f Gbp in %.1fs" % (genome.length / 1e9, time.time() - t0))
     prefix = None
+    prefix_cpu = None        # reference-format index files of this genome (the reference's CPU run)
     if args.workload == "c2":
         # the drop-in path: reference-format files written by our builder, loaded by svg_index_open
         prefix = os.path.join(wd, "genome_full")
@@ -188,11 +237,16 @@ def main():
             dist.barrier()
         t1 = time.time()
         ix = sa.VoteIndex(prefix, device=device)
+        prefix_cpu = prefix
     else:
-        # 3 Gbp: build the same index straight into this GPU's HBM (replicated per rank)
+        # 3 Gbp: build the same index straight into this GPU's HBM (replicated per rank); rank 0 of an
+        # N=1 run also writes it to reference-format files for the reference's timed CPU run
         t1 = time.time()
         gap = W.get("gap", 1)
-        ix = sa.VoteIndex.build_genome(genome, gap=gap, memory_mb=8000, force_one_block=gap == 1, device=device)
+        if rank == 0 and world == 1 and not args.no_cpu and os.path.exists(ref_binary(W["kind"])):
+            prefix_cpu = os.path.join(wd, "index_%s" % args.workload)
+        ix = sa.VoteIndex.build_genome(genome, gap=gap, memory_mb=8000, force_one_block=gap == 1, device=device,
+                                       save_prefix=prefix_cpu)
     log("[bench] index in HBM (%.1f GB, %d items) in %.1fs" % (ix.info.device_bytes / 1e9, ix.info.items,
                                                             time.time() - t1))
 
@@ -488,7 +542,40 @@ def main():
             log("[bench] sublong figure failed: %s" % ex)
     cpu_base = None
     if rank == 0 and world == 1 and not args.no_cpu:   # the CPU baseline is an N=1 figure
-        # bounded CPU sample: chunks of the same reads until >= 10 s of CPU work
+        cpu_base = {"unit": "Mreads/s", "cores": threads, "cpu_model": cpu["model"],
+                    "host_logical_cpus": cpu["logical_cpus"], "usable_cpus": cpu["usable_cpus"],
+                    "cgroup_quota_cpus": cpu["cgroup_quota_cpus"]}
+        # (1) the reference itself, timed in this run (oracle/_ref/*-votetime, same index and reads)
+        if prefix_cpu and os.path.exists(ref_binary(kind)):
+            try:
+                per, votes, wall = reference_cpu_run(kind, prefix_cpu, rb, rb2, args.ref_chunk, args.ref_chunks,
+                                                     threads, wd)
+                rates = sorted(r_ * ends / s_ / 1e6 for s_, r_ in per)
+                med = rates[len(rates) // 2] if len(rates) % 2 else 0.5 * (rates[len(rates) // 2 - 1] + rates[len(rates) // 2])
+                m = sum(r_ for _, r_ in per)
+                mine = [out[:m].view(np.uint8).reshape(m, -1)]
+                if sj:
+                    mine += [jout[:m].view(np.uint8).reshape(m, -1), bmo[:m].view(np.uint8).reshape(m, -1)]
+                mine = np.concatenate(mine, 1).reshape(-1)
+                cpu_base.update({
+                    "value": round(med, 4), "kind": "reference",
+                    "sample": "first %d %s of the timed batch in %d chunks of one run of the reference aligner (%s, "
+                              "built from its sources, -T %d, same index files); value = median over the chunks of "
+                              "the voting step's rate, FASTQ parsing and index loading outside the clock" % (
+                                  m, "pairs" if ends == 2 else "reads", len(per), os.path.basename(ref_binary(kind)), threads),
+                    "reps": [{"seconds": round(s_, 4), "reads": r_ * ends, "value": round(r_ * ends / s_ / 1e6, 4)}
+                             for s_, r_ in per],
+                    "spread": {"min": round(rates[0], 4), "max": round(rates[-1], 4)},
+                    "run_wall_s": round(wall, 1),
+                    # the GPU host path's records of the same reads against the reference's own
+                    # post-vote records (SVG_REF_DUMP, oracle/ref_dump_hook.c)
+                    "records_identical_to_gpu": bool(votes.size == mine.size and (votes == mine).all())})
+                log("[bench] reference CPU voting: %s Mreads/s per chunk (median %.3f), records vs GPU %s" % (
+                    [round(x, 3) for x in rates], med, "IDENTICAL" if cpu_base["records_identical_to_gpu"] else "DIFFERENT"))
+            except Exception as ex:   # noqa: BLE001
+                cpu_base["reference_error"] = "%s: %s" % (type(ex).__name__, ex)
+                log("[bench] reference CPU run failed: %s" % ex)
+        # (2) the restatement (oracle/svoracle.c): chunks of the same reads until >= 10 s of CPU work
         done, cs, chunk = 0, 0.0, 200000
         while cs < 10.0 and done < min(n, args.cpu_sample):
             b = min(chunk, n - done)
@@ -497,24 +584,13 @@ def main():
                     threads=threads)
             cs += time.perf_counter() - t1
             done += b
-        cpu_base = {"value": round(done * ends / cs / 1e6, 4), "unit": "Mreads/s", "cores": threads, "kind": "port",
-                    "sample": "first %d reads of the timed batch, oracle/svoracle.c restatement, %d pthreads, %.1f s" % (
-                        done, threads, cs),
-                    "cpu_model": cpu["model"], "host_logical_cpus": cpu["logical_cpus"],
-                    "usable_cpus": cpu["usable_cpus"], "cgroup_quota_cpus": cpu["cgroup_quota_cpus"]}
-        # tools/cpu_calibration.py: the reference's voting step over this restatement, same reads and
-        # index; the newest calibration taken on this CPU model, else the newest
-        import glob
-        cals = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_cpu_calibration.json")))
-        same = [c for c in cals if json.load(open(c)).get("cpu_model") == cpu["model"]]
-        cal = (same or cals or [None])[-1]
-        if cal:
-            c = json.load(open(cal))
-            cpu_base["reference_over_port"] = c.get("reference_over_port")
-            cpu_base["reference_equiv_value"] = round(cpu_base["value"] * c["reference_over_port"], 4)
-            cpu_base["calibration"] = "%s: %s" % (os.path.relpath(cal, ROOT), c.get("summary", ""))
-            cpu_base["calibration_same_cpu_model"] = bool(same)
-
+        port = {"value": round(done * ends / cs / 1e6, 4), "kind": "port",
+                "sample": "first %d reads of the timed batch, oracle/svoracle.c restatement, %d pthreads, %.1f s" % (
+                    done, threads, cs)}
+        if "value" in cpu_base:
+            cpu_base["port"] = port
+        else:
+            cpu_base.update(port)
     total_reads = n * ends * world * args.steps
     value = total_reads / elapsed / 1e6
     if rank == 0:

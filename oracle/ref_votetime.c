@@ -16,7 +16,14 @@
  * bigtable writes and the final-run tail of every read, FASTQ parsing excluded).
  * SVG_REF_VOTETIME=1 prints "SVG_REF_VOTING_S <seconds> <reads>" to stderr at exit.
  *
- * Single chunk only (reads <= reads_per_chunk), base space only: the calibration's inputs.
+ * Two modes.  Default: a single chunk (reads <= reads_per_chunk), the reference's iteration two
+ * and SAM as usual.  SVG_REF_CHUNK=S (the bench's cpu_baseline): reads_per_chunk is set to S at
+ * the first call, so the reads go through ceil(n/S) chunks of one process (one index load), and
+ * do_iteration_two -- weak in core-vt.o, answered here -- returns at once: each chunk is timed
+ * from its first read handed out to its last "no more reads" answer, and
+ * "SVG_REF_CHUNK_VOTING_S <chunk> <seconds> <reads>" is printed per chunk.  The vote, the
+ * bigtable writes and the final-run tail are the reference's own; iteration two and SAM are not
+ * run in that mode (nothing they do is on the timed path).  One-block indexes only.
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -34,6 +41,23 @@ static pthread_mutex_t rv_mu = PTHREAD_MUTEX_INITIALIZER;
 static int rv_parsed, rv_pass;
 static long rv_served;
 static double rv_t0, rv_t1;
+// chunked vote-only mode (SVG_REF_CHUNK)
+#define RV_MAX_CHUNKS 64
+static long rv_chunk_size, rv_base, rv_chunk_reads[RV_MAX_CHUNKS];
+static int rv_chunk = -1, rv_it2_seen;
+static double rv_ct0[RV_MAX_CHUNKS], rv_ct1[RV_MAX_CHUNKS];
+
+int ref_do_iteration_two(global_context_t *gc, thread_context_t *tc);
+
+// run_in_thread's STEP_ITERATION_TWO call (core.c:3370): in chunked mode the chunk's voting is over
+int do_iteration_two(global_context_t *gc, thread_context_t *tc)
+{
+	if (!rv_chunk_size) return ref_do_iteration_two(gc, tc);
+	pthread_mutex_lock(&rv_mu);
+	rv_it2_seen = 1;
+	pthread_mutex_unlock(&rv_mu);
+	return 0;
+}
 
 static double rv_now(void)
 {
@@ -57,8 +81,9 @@ static void rv_parse(global_context_t *gc, gene_input_t *in, struct rv_end *e)
 			e->len = realloc(e->len, e->cap * sizeof(int));
 		}
 		e->name[e->n] = strdup(name);
-		e->text[e->n] = strdup(text);
-		e->qual[e->n] = strdup(qual);
+		// text and quality by length: a read may hold NUL bytes (the reference works on rl bytes)
+		e->text[e->n] = memcpy(malloc(rl + 1), text, rl + 1);
+		e->qual[e->n] = memcpy(malloc(rl + 1), qual, rl + 1);
 		e->len[e->n] = rl;
 		e->n++;
 	}
@@ -71,38 +96,65 @@ int fetch_next_read_pair(global_context_t *gc, thread_context_t *tc, gene_input_
                          subread_read_number_t *read_no_in_chunk)
 {
 	(void)tc; (void)remove_color_head;
-	long num = -1;
+	long num = -1, at = -1;
 	pthread_mutex_lock(&rv_mu);
 	if (!rv_parsed) {
 		rv_parse(gc, ginp1, &rv[0]);
 		if (ginp2) rv_parse(gc, ginp2, &rv[1]);
 		if (ginp2 && rv[0].n != rv[1].n) { fprintf(stderr, "ref_votetime: unequal read counts\n"); exit(2); }
-		if (rv[0].n > (long)gc->config.reads_per_chunk) { fprintf(stderr, "ref_votetime: one chunk only\n"); exit(2); }
+		const char *cs = getenv("SVG_REF_CHUNK");
+		if (cs && atol(cs) > 0) {
+			rv_chunk_size = atol(cs);
+			if (rv_chunk_size > (long)gc->config.reads_per_chunk) { fprintf(stderr, "ref_votetime: chunk too large\n"); exit(2); }
+			if ((rv[0].n + rv_chunk_size - 1) / rv_chunk_size >= RV_MAX_CHUNKS) { fprintf(stderr, "ref_votetime: too many chunks\n"); exit(2); }
+			gc->config.reads_per_chunk = rv_chunk_size;
+			rv_it2_seen = 1;
+		} else if (rv[0].n > (long)gc->config.reads_per_chunk) { fprintf(stderr, "ref_votetime: one chunk only\n"); exit(2); }
 		rv_parsed = 1;
 		rv_t0 = rv_now();
 	}
-	if (gc->running_processed_reads_in_chunk < gc->config.reads_per_chunk && gc->running_processed_reads_in_chunk < rv[0].n) {
-		num = (long)gc->running_processed_reads_in_chunk++;
-		if (num == 0 && rv_served) rv_pass++;   // the counter was reset: a later pass (iteration two, three)
-		rv_served++;
-	} else if (rv_pass == 0) {
-		rv_t1 = rv_now();                       // a thread's last answer of the voting pass
+	if (rv_chunk_size) {
+		if (rv_it2_seen) {           // the first call of a chunk's voting pass
+			if (rv_chunk >= 0) rv_base += rv_chunk_reads[rv_chunk];
+			rv_chunk++;
+			rv_it2_seen = 0;
+			rv_ct0[rv_chunk] = rv_now();
+			rv_ct1[rv_chunk] = rv_ct0[rv_chunk];
+		}
+		if (gc->running_processed_reads_in_chunk < gc->config.reads_per_chunk &&
+		    rv_base + (long)gc->running_processed_reads_in_chunk < rv[0].n) {
+			num = (long)gc->running_processed_reads_in_chunk++;
+			at = rv_base + num;
+			rv_chunk_reads[rv_chunk] = num + 1;
+		} else {
+			rv_ct1[rv_chunk] = rv_now();
+		}
+		pthread_mutex_unlock(&rv_mu);
+	} else {
+		if (gc->running_processed_reads_in_chunk < gc->config.reads_per_chunk && gc->running_processed_reads_in_chunk < rv[0].n) {
+			num = (long)gc->running_processed_reads_in_chunk++;
+			at = num;
+			if (num == 0 && rv_served) rv_pass++;   // the counter was reset: a later pass (iteration two, three)
+			rv_served++;
+		} else if (rv_pass == 0) {
+			rv_t1 = rv_now();                       // a thread's last answer of the voting pass
+		}
+		pthread_mutex_unlock(&rv_mu);
 	}
-	pthread_mutex_unlock(&rv_mu);
 	if (num < 0) { *read_no_in_chunk = -1; return 1; }
-	strcpy(read_name_1, rv[0].name[num]);
-	strcpy(read_text_1, rv[0].text[num]);
-	if (qual_text_1) strcpy(qual_text_1, rv[0].qual[num]);
-	*read_len_1 = rv[0].len[num];
+	strcpy(read_name_1, rv[0].name[at]);
+	memcpy(read_text_1, rv[0].text[at], rv[0].len[at] + 1);
+	if (qual_text_1) memcpy(qual_text_1, rv[0].qual[at], rv[0].len[at] + 1);
+	*read_len_1 = rv[0].len[at];
 	if (gc->config.is_first_read_reversed) {
 		reverse_read(read_text_1, *read_len_1, gc->config.space_type);
 		if (qual_text_1) reverse_quality(qual_text_1, *read_len_1);
 	}
 	if (ginp2) {
-		strcpy(read_name_2, rv[1].name[num]);
-		strcpy(read_text_2, rv[1].text[num]);
-		if (qual_text_2) strcpy(qual_text_2, rv[1].qual[num]);
-		*read_len_2 = rv[1].len[num];
+		strcpy(read_name_2, rv[1].name[at]);
+		memcpy(read_text_2, rv[1].text[at], rv[1].len[at] + 1);
+		if (qual_text_2) memcpy(qual_text_2, rv[1].qual[at], rv[1].len[at] + 1);
+		*read_len_2 = rv[1].len[at];
 		if (gc->config.is_second_read_reversed) {
 			reverse_read(read_text_2, *read_len_2, gc->config.space_type);
 			if (qual_text_2) reverse_quality(qual_text_2, *read_len_2);
@@ -115,6 +167,11 @@ int fetch_next_read_pair(global_context_t *gc, thread_context_t *tc, gene_input_
 __attribute__((destructor)) static void rv_report(void)
 {
 	const char *e = getenv("SVG_REF_VOTETIME");
-	if (e && e[0] == '1' && rv_parsed)
-		fprintf(stderr, "SVG_REF_VOTING_S %.6f %ld\n", rv_t1 - rv_t0, rv[0].n);
+	if (e && e[0] == '1' && rv_parsed) {
+		if (rv_chunk_size) {
+			for (int c = 0; c <= rv_chunk; c++)
+				if (rv_chunk_reads[c]) fprintf(stderr, "SVG_REF_CHUNK_VOTING_S %d %.6f %ld\n", c, rv_ct1[c] - rv_ct0[c], rv_chunk_reads[c]);
+		} else
+			fprintf(stderr, "SVG_REF_VOTING_S %.6f %ld\n", rv_t1 - rv_t0, rv[0].n);
+	}
 }

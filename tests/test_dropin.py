@@ -11,6 +11,7 @@ library.  Needs the binaries built from /root/reference (this container; skipped
 are absent)."""
 import os
 
+import numpy as np
 import pytest
 
 from tests.common import Case, IndexCache
@@ -41,7 +42,8 @@ def test_oracle_dropin_matches_stock_reference(name, threads, cache, tmp_path):
     assert rep["mapped"] > 0
 
 
-@pytest.mark.parametrize("name,threads", [("pe_gapped_errmut", 4), ("sj_pe_gapped_long", 1)])
+@pytest.mark.parametrize("name,threads", [("pe_gapped_errmut", 4), ("sj_pe_gapped_long", 1),
+                                          ("se_gapped_mixed_n14_I16", 2)])   # reads holding NUL bytes
 def test_votetime_harness_matches_stock_reference(name, threads, cache, tmp_path):
     """The CPU-baseline timing harness (oracle/ref_votetime.c: reads parsed before the clock,
     served from memory) changes nothing the aligner writes."""
@@ -50,6 +52,31 @@ def test_votetime_harness_matches_stock_reference(name, threads, cache, tmp_path
         pytest.skip("reference timing binaries not built (make -C oracle votetime)")
     rep = check_case(c, cache.get(c.index_key), str(tmp_path), "votetime", threads)
     assert rep["mapped"] > 0
+
+
+@pytest.mark.parametrize("name,threads", [("pe_gapped_errmut", 4), ("se_gapped_mixed_n14_I16", 2)])
+def test_votetime_chunked_mode_votes_every_read(name, threads, cache, tmp_path):
+    """bench.py's cpu_baseline timing of the reference (SVG_REF_CHUNK: the reads in chunks of one
+    process, iteration two skipped): one clock line per chunk, every read voted once, and the
+    vote records of the chunks, one after another, are the golden records of the case."""
+    import math
+    import re
+    from tests.dropin import fastq_pair, run, case_extra
+    c = Case(name)
+    if not have(c.meta["program"], "votetime"):
+        pytest.skip("reference timing binaries not built (make -C oracle votetime)")
+    n = len(c.r1)
+    size = math.ceil(n / 3)
+    f1, f2 = fastq_pair(str(tmp_path), c.name, c.r1, c.r2)
+    out = str(tmp_path / "vt.sam")
+    r = run(c.meta["program"], "votetime", cache.get(c.index_key), f1, f2, out, threads, case_extra(c),
+            env={"SVG_REF_CHUNK": str(size), "SVG_REF_VOTETIME": "1"})
+    lines = re.findall(r"SVG_REF_CHUNK_VOTING_S (\d+) ([0-9.]+) (\d+)", r.stderr)
+    assert [int(x[0]) for x in lines] == list(range(math.ceil(n / size)))
+    assert [int(x[2]) for x in lines] == [min(size, n - k * size) for k in range(len(lines))]
+    assert all(float(x[1]) > 0 for x in lines)
+    votes = np.fromfile(out + ".votes", dtype=np.uint8)
+    assert votes.size == c.expected.size and (votes.reshape(c.expected.shape) == c.expected).all()
 
 
 def test_sublong_oracle_dropin_matches_stock(cache, tmp_path):
