@@ -1879,7 +1879,7 @@ int svg_realign_chunk(svg_realign *ra, const svg_fragment_reads *R, svg_mapping_
 		}
 	}
 	for (int t = 0; t < threads; t++) worker_free(wk[t]);
-	if (getenv("SVG_REALIGN_PROF"))
+	if (svg_get_option("debug") & 16)
 		fprintf(stderr, "svg_realign_chunk: %llu fragments, %d threads: setup+ordered %.4f s (%lld in order), parallel %.4f s, merge %.4f s\n",
 		        (unsigned long long)R->n, threads, t1 - t0, (long long)r, t2 - t1, now_s() - t2);
 	if (rc && rc != SVG_E_NOMEM) svg_set_error("svg_realign_chunk: SAM output failed (error %d)", rc);
