@@ -852,8 +852,26 @@ static void topk(readctx *c)
 }
 
 /* one read (pair): do_voting body, core.c:3091-3235 */
+/* diagnostics (tools/table_hist.py): per read, the most candidates one (strand, end) table took and
+ * the most slots one table used, as a joint histogram -- sizes the wave kernel's vote table */
+#define DH_C 7
+#define DH_S 8
+static uint64_t g_dhist[DH_C * DH_S];
+static int dh_cbin(uint64_t h) { return h <= 40 ? 0 : h <= 64 ? 1 : h <= 96 ? 2 : h <= 128 ? 3 : h <= 160 ? 4 : h <= 256 ? 5 : 6; }
+static int dh_sbin(int u) { return u <= 16 ? 0 : u <= 32 ? 1 : u <= 64 ? 2 : u <= 128 ? 3 : u <= 192 ? 4 : u <= 256 ? 5 : u <= 384 ? 6 : 7; }
+void svo_diag_hist(uint64_t *out, int reset)
+{
+	int i;
+	for (i = 0; i < DH_C * DH_S; i++) {
+		out[i] = __atomic_load_n(&g_dhist[i], __ATOMIC_RELAXED);
+		if (reset) __atomic_store_n(&g_dhist[i], 0, __ATOMIC_RELAXED);
+	}
+}
+
 static void vote_read(readctx *c)
 {
+	uint64_t dh_hits = 0;
+	int dh_used = 0;
 	const svg_params *p = c->p;
 	const svo_index *ix = c->ix;
 	int strand, e, gap = ix->gap;
@@ -887,6 +905,7 @@ static void vote_read(readctx *c)
 			c->applied[e] = applied;
 			hb = high - (uint32_t)rl;
 			for (round = 0; round < 2; round++) {
+				const uint64_t h0 = c->st.hits;
 				vt_reset(v);
 				for (k = 0; k < applied; k++)
 					for (x = 0; x < gap; x++) {
@@ -894,6 +913,12 @@ static void vote_read(readctx *c)
 						if (gap > 1) off -= off % gap - x;
 						probe_X(ix, pack16(c->text[e] + off), off, strand, v, tol, k, low, hb, round, shift_locs, &shift_no, &c->st);
 					}
+				if (c->st.hits - h0 > dh_hits) dh_hits = c->st.hits - h0;
+				{
+					int u = 0, i;
+					for (i = 0; i < TAB_ROWS; i++) u += v->items[i];
+					if (u > dh_used) dh_used = u;
+				}
 				if (shift_no == 0) break;
 			}
 		}
@@ -908,6 +933,7 @@ static void vote_read(readctx *c)
 		if (strand == 0)
 			for (e = 0; e < c->ends; e++) revcomp(c->text[e], c->rl[e]);
 	}
+	__atomic_fetch_add(&g_dhist[dh_cbin(dh_hits) * DH_S + dh_sbin(dh_used)], 1, __ATOMIC_RELAXED);
 }
 
 /* ------------------------------------------------------------------ batch driver */

@@ -217,7 +217,6 @@ struct Wave {
 	int items_v;            // lane 32*e + r: items[r] of table e (gene_vote_t.items)
 	int max_vote[2];        // gene_vote_t.max_vote per table (wave-uniform)
 	int nshift[2];          // shift_indel_NO per table (wave-uniform)
-	int lseg, lslot;        // fixed lane map of the 3-row fetch (vote_one)
 	uint32_t *ovf;          // PE: compacted end-0 entries beyond the LDS list (HBM scratch)
 	uint32_t wb[2];         // subjunc: first .array byte of the left / right donor window
 	int cur_strand;
@@ -363,17 +362,21 @@ struct Wave {
 		const int n0 = rd(items_v, E * 32 + (int)r0);
 		bool found = false;
 		if (kp->ii_end == 5) {
-			// rows r0, r0+1, r0-1 (iix = 0, +5, -5) in one LDS round trip with a fixed lane map:
-			// lanes 0-23 row r0, 24-47 row r0+1, 48-63 slots 0-15 of row r0-1 (ballot order =
-			// the reference's scan order); slots 16-23 of row r0-1 (rare) in a second group
+			// rows r0, r0+1, r0-1 (iix = 0, +5, -5) in one LDS round trip, lanes packed over the used
+			// slots in the reference's scan order (lane l = the l-th used slot of r0, then rp, then
+			// rm; ballot order = scan order).  Rows hold a few slots each (C3 deferred reads: ~4), so
+			// the three runs sit in distinct banks -- a fixed 24/24/16 lane map made rp's slots 16-23
+			// and rm's 0-7 share banks on every fetch (29% of the kernel's LDS cycles in conflicts).
+			// More than 64 used slots (rare): a second group, after the first found nothing.
 			const uint32_t rp = (pk >> 22) & 31u, rm = pk >> 27;
 			const int np_ = rd(items_v, E * 32 + (int)rp), nm = rd(items_v, E * 32 + (int)rm);
-			if (n0 + np_ + nm) {
-				const uint32_t row = lseg == 0 ? r0 : (lseg == 1 ? rp : rm);
-				const int cnt = lseg == 0 ? n0 : (lseg == 1 ? np_ : nm);
-				found = vote_group<E>(lslot < cnt, (int)row * SPACE + lslot, kv, kP1, off, round);
-				if (!found && nm > 16)
-					found = vote_group<E>(lane < nm - 16, (int)rm * SPACE + 16 + lane, kv, kP1, off, round);
+			const int tot = n0 + np_ + nm;
+			for (int g = 0; g < tot && !found; g += 64) {
+				const int l = g + lane;
+				const bool in0 = l < n0, in1 = !in0 && l < n0 + np_;
+				const uint32_t row = in0 ? r0 : (in1 ? rp : rm);
+				const int sl = in0 ? l : (in1 ? l - n0 : l - n0 - np_);
+				found = vote_group<E>(l < tot, (int)row * SPACE + sl, kv, kP1, off, round);
 			}
 		} else {
 			for (int iix = 0; iix <= kp->ii_end && !found; iix = iix > 0 ? -iix : (-iix + 5)) {
@@ -1514,8 +1517,6 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	Wave<ENDS, MAXL, MAXP, SJ> W;
 	W.L = reinterpret_cast<LT *>(lds_raw + (size_t)wib * ((sizeof(LT) + 15) & ~(size_t)15));
 	W.kp = &kp;
-	W.lseg = lane_id() < 24 ? 0 : (lane_id() < 48 ? 1 : 2);
-	W.lslot = lane_id() - 24 * W.lseg;
 	const size_t per_end = (size_t)NSLOT * COLD_WORDS + NSLOT;   // cold + shift_locs
 	const size_t per_wave = per_end * ENDS + (ENDS == 2 ? (size_t)NSLOT * 4 : 0);   // + PE overflow list
 	uint32_t *base = kp.scratch + gw * per_wave;
