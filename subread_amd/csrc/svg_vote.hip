@@ -50,8 +50,13 @@
 #include "svg_device.h"
 
 #define ROWS 30
-#define SPACE 24
-#define NSLOT (ROWS * SPACE)
+#define SPACE 24              // GENE_VOTE_SPACE: slots a row may hold
+// LDS row stride of the vote table, in slots: 25 x 8 B = 50 dwords, so the rows of the 30-row
+// table start on 30 different bank pairs (a 24-slot stride puts every row on one of 4 and made
+// batch mode's per-lane random-row scans 8-way bank conflicts).  Slot ids (LDS index, cold state,
+// top-K handles) are row * PSTR + slot.
+#define PSTR 25
+#define NSLOT (ROWS * PSTR)
 #define REC_LEN 21
 #define COLD_WORDS 8          // per slot: cs|ce<<16, rec[21] as bytes, pad
 #define JCW 17
@@ -376,14 +381,14 @@ struct Wave {
 				const bool in0 = l < n0, in1 = !in0 && l < n0 + np_;
 				const uint32_t row = in0 ? r0 : (in1 ? rp : rm);
 				const int sl = in0 ? l : (in1 ? l - n0 : l - n0 - np_);
-				found = vote_group<E>(l < tot, (int)row * SPACE + sl, kv, kP1, off, round);
+				found = vote_group<E>(l < tot, (int)row * PSTR + sl, kv, kP1, off, round);
 			}
 		} else {
 			for (int iix = 0; iix <= kp->ii_end && !found; iix = iix > 0 ? -iix : (-iix + 5)) {
 				uint32_t r = iix ? ((kv + (uint32_t)iix) / 5u) % ROWS : r0;
 				int cnt = iix ? rd(items_v, E * 32 + (int)r) : n0;
 				if (!cnt) continue;
-				found = vote_group<E>(lane < cnt, (int)r * SPACE + lane, kv, kP1, off, round);
+				found = vote_group<E>(lane < cnt, (int)r * PSTR + lane, kv, kP1, off, round);
 			}
 		}
 		if (!found && kv >= kp->low && kv <= high_b && n0 < SPACE) {
@@ -399,7 +404,7 @@ struct Wave {
 			if (lane == 0) {
 				// a new slot: recorder (k+1, k+1, 0), coverage off..off+16, all in the meta
 				const int x = gap_x(off, kp->ix.gap);
-				L->pm[(int)r0 * SPACE + n0] = make_uint2(kv, m_pack_u(1, kP1, sh, x, kP1, x));
+				L->pm[(int)r0 * PSTR + n0] = make_uint2(kv, m_pack_u(1, kP1, sh, x, kP1, x));
 			}
 			if (lane == E * 32 + (int)r0) items_v = n0 + 1;
 			if (max_vote[E] == 0) max_vote[E] = 1;
@@ -447,7 +452,7 @@ struct Wave {
 				for (int k = 0; k < 4; k++) {
 					const int q = q0 + k < tot ? q0 + k : tot - 1;
 					const uint32_t row = q < n0 ? r0 : (q < n0 + np_ ? rp : rm);
-					at[k] = (int)row * SPACE + (q < n0 ? q : (q < n0 + np_ ? q - n0 : q - n0 - np_));
+					at[k] = (int)row * PSTR + (q < n0 ? q : (q < n0 + np_ ? q - n0 : q - n0 - np_));
 					e[k] = L->pm[at[k]];
 				}
 #pragma unroll
@@ -534,7 +539,7 @@ struct Wave {
 		int nv = 0;
 		if (mk) {
 			nv = __popcll(eqm);
-			L->pm[(int)r0 * SPACE + n0 + rank] =
+			L->pm[(int)r0 * PSTR + n0 + rank] =
 				make_uint2(kv, m_pack_u(nv, kl, 0, gap_x(ol, kp->ix.gap), kP1, gap_x(off, kp->ix.gap)));   // no cold state
 		}
 		if (isB && (grp & ~le) == 0ull) {   // the group's last vote: votes += group size, last = its kP1
@@ -988,7 +993,7 @@ struct Wave {
 		for (int r = 0; r < ROWS - 1; r++) row += (rd(rs_v, e * 32 + r) <= f);
 		int start = __shfl(rs_v, (e * 32 + row - 1) & 63);
 		if (row == 0) start = 0;
-		return row * SPACE + (f - start);
+		return row * PSTR + (f - start);
 	}
 
 	// ---------------------------------------------------------------- phase K
