@@ -142,7 +142,12 @@ static int chunk_push(svg_chunk_reads *c, int e, const char *text, const char *q
 	memcpy(c->qual[e] + c->bytes[e], qual, len);
 	c->off[e][c->n] = c->bytes[e];
 	c->len[e][c->n] = (uint16_t)len;
-	snprintf(c->name[e] + c->n * (MAX_READ_NAME_LEN + 1), MAX_READ_NAME_LEN + 1, "%s", name);
+	{
+		char *dn = c->name[e] + c->n * (MAX_READ_NAME_LEN + 1);
+		const size_t nl = strnlen(name, MAX_READ_NAME_LEN);
+		memcpy(dn, name, nl);
+		dn[nl] = 0;
+	}
 	c->bytes[e] += len;
 	return 0;
 }
@@ -155,14 +160,19 @@ static void chunk_free(svg_chunk_reads *c)
 	}
 }
 
-/* 1. the chunk's reads, in chunk read-number order (one thread: numbers are sequential) */
+static void fqb_begin(gene_input_t *ginp1, gene_input_t *ginp2);
+static void fqb_end(void);
+
+/* 1. the chunk's reads, in chunk read-number order (one thread: numbers are sequential); plain
+ * FASTQ input is read in bulk meanwhile (fqb_begin / fqb_end, below) */
 static int read_chunk(global_context_t *gc, thread_context_t *tc, int ends, svg_chunk_reads *c)
 {
 	gene_input_t *ginp1 = NULL, *ginp2 = NULL;
 	char text[2][MAX_READ_LENGTH + 1], qual[2][MAX_READ_LENGTH + 1], name[2][MAX_READ_NAME_LEN + 1];
-	int len[2] = {0, 0}, e;
+	int len[2] = {0, 0}, e, rc = 0;
 	subread_read_number_t rno = 0;
 	init_chunk_scanning_parameters(gc, tc, &ginp1, &ginp2);
+	fqb_begin(ginp1, ginp2);
 	for (;;) {
 		fetch_next_read_pair(gc, tc, ginp1, ginp2, &len[0], &len[1], name[0], name[1], text[0], text[1], qual[0],
 		                     qual[1], 1, &rno);
@@ -170,7 +180,8 @@ static int read_chunk(global_context_t *gc, thread_context_t *tc, int ends, svg_
 		if ((uint64_t)rno != c->n) {
 			SUBREADprintf("do_voting_gpu: read numbers are not sequential (%lld after %llu reads)\n",
 			              (long long)rno, (unsigned long long)c->n);
-			return 1;
+			rc = 1;
+			break;
 		}
 		if (c->n == c->cap) {
 			c->cap = c->cap ? 2 * c->cap : 1 << 16;
@@ -178,14 +189,17 @@ static int read_chunk(global_context_t *gc, thread_context_t *tc, int ends, svg_
 				c->len[e] = realloc(c->len[e], c->cap * sizeof(uint16_t));
 				c->off[e] = realloc(c->off[e], c->cap * sizeof(uint64_t));
 				c->name[e] = realloc(c->name[e], c->cap * (MAX_READ_NAME_LEN + 1));
-				if (!c->len[e] || !c->off[e] || !c->name[e]) return 1;
+				if (!c->len[e] || !c->off[e] || !c->name[e]) rc = 1;
 			}
+			if (rc) break;
 		}
-		for (e = 0; e < ends; e++)
-			if (chunk_push(c, e, text[e], qual[e], name[e], len[e])) return 1;
+		for (e = 0; e < ends && !rc; e++)
+			if (chunk_push(c, e, text[e], qual[e], name[e], len[e])) rc = 1;
+		if (rc) break;
 		c->n++;
 	}
-	return 0;
+	fqb_end();
+	return rc;
 }
 
 /* one handle's share of a chunk: reads [r0, r1) of the packed chunk, records into their rows */
@@ -757,10 +771,158 @@ static int fq_line_noempty(FILE *fp, int max_len, char *buff)
 	return ret;
 }
 
+/*
+ * Bulk reading of plain FASTQ while the binding's own chunk read runs (read_chunk): the parse
+ * below takes its bytes from a 4 MB buffer filled by fread and finds line ends with memchr instead
+ * of one getc per character; at the end of the chunk read the FILE is put back (fseeko) exactly
+ * where the character-wise parse would have left it -- nothing else touches the FILE in between
+ * (preloading is a no-op for plain files, input-files.c:199-203), and the reference's own
+ * position bookkeeping (geinput_tell = ftello, :684-698) only runs outside.  A byte 0xFF ends a
+ * line or the input as the reference's `char` comparisons with EOF make it do.
+ */
+typedef struct {
+	FILE *fp;
+	char *buf;
+	size_t cap, lo, hi;               /* unread bytes buf[lo..hi) */
+	off_t pos;                        /* file offset of buf[hi] */
+	int on, eof;
+} svg_fqbuf;
+static svg_fqbuf svg_fqb[2];
+
+static void fqb_begin(gene_input_t *ginp1, gene_input_t *ginp2)
+{
+	gene_input_t *in[2] = {ginp1, ginp2};
+	for (int e = 0; e < 2; e++) {
+		svg_fqbuf *b = &svg_fqb[e];
+		b->on = 0;
+		if (!in[e] || in[e]->file_type != GENE_INPUT_FASTQ) continue;
+		if (!b->buf) {
+			b->cap = (size_t)4 << 20;
+			if (!(b->buf = malloc(b->cap))) continue;
+		}
+		b->fp = (FILE *)in[e]->input_fp;
+		b->pos = ftello(b->fp);
+		if (b->pos < 0) continue;
+		b->lo = b->hi = 0;
+		b->eof = 0;
+		b->on = 1;
+	}
+}
+
+static void fqb_end(void)
+{
+	for (int e = 0; e < 2; e++) {
+		svg_fqbuf *b = &svg_fqb[e];
+		if (!b->on) continue;
+		fseeko(b->fp, b->pos - (off_t)(b->hi - b->lo), SEEK_SET);
+		b->on = 0;
+	}
+}
+
+static svg_fqbuf *fqb_of(FILE *fp)
+{
+	for (int e = 0; e < 2; e++)
+		if (svg_fqb[e].on && svg_fqb[e].fp == fp) return &svg_fqb[e];
+	return NULL;
+}
+
+/* more bytes: 0 at the end of the file */
+static size_t fqb_fill(svg_fqbuf *b)
+{
+	if (b->lo == b->hi) b->lo = b->hi = 0;
+	else if (b->lo > 0) {
+		memmove(b->buf, b->buf + b->lo, b->hi - b->lo);
+		b->hi -= b->lo;
+		b->lo = 0;
+	}
+	if (b->eof || b->hi == b->cap) return b->hi - b->lo;
+	const size_t got = fread(b->buf + b->hi, 1, b->cap - b->hi, b->fp);
+	if (got == 0) b->eof = 1;
+	b->hi += got;
+	b->pos += (off_t)got;
+	return got;
+}
+
+/* getc_unlocked as a signed char (EOF = -1, and so is byte 0xFF) */
+static inline int fqb_getc(svg_fqbuf *b)
+{
+	if (b->lo == b->hi && fqb_fill(b) == 0) return -1;
+	return (signed char)b->buf[b->lo++];
+}
+
+/* fq_line_noempty from the buffer: leading newlines skipped, the line copied up to max_len - 1
+ * characters (the rest consumed), ended by '\n' (consumed), 0xFF (consumed) or the end of file */
+static int fqb_line_noempty(svg_fqbuf *b, int max_len, char *buff)
+{
+	int ret = 0;
+	for (;;) {
+		if (b->lo == b->hi && fqb_fill(b) == 0) break;
+		const char *p = b->buf + b->lo;
+		size_t n = b->hi - b->lo;
+		if (ret == 0) {
+			size_t k = 0;
+			while (k < n && p[k] == '\n') k++;
+			b->lo += k;
+			if (k == n) continue;
+			p += k;
+			n -= k;
+		}
+		const char *nl = memchr(p, '\n', n);
+		size_t take = nl ? (size_t)(nl - p) : n;
+		const char *ff = memchr(p, 0xff, take);
+		if (ff) take = (size_t)(ff - p);
+		const size_t room = ret < max_len - 1 ? (size_t)(max_len - 1 - ret) : 0;
+		const size_t cp = take < room ? take : room;
+		memcpy(buff + ret, p, cp);
+		ret += (int)cp;
+		b->lo += take;
+		if (ff || nl) { b->lo++; break; }   /* the terminating '\n' or 0xFF byte is consumed */
+	}
+	buff[ret] = 0;
+	return ret;
+}
+
+static int fq_next_read_bulk(svg_fqbuf *b, gene_input_t *input, char *read_name, char *read_string, char *quality_string,
+                             short trim_5, short trim_3)
+{
+	int nch, ret;
+	do nch = fqb_getc(b); while (nch == '\n');
+	if (nch == -1) return -1;
+	if (nch != '@') {
+		fseeko(b->fp, b->pos - (off_t)(b->hi - b->lo), SEEK_SET);   /* the message counts lines up to here */
+		SUBREADprintf("ERROR: a format issue %d is found on the %lld-th line in input file '%s'.\nProgram aborted.\n", nch,
+		              (long long)tell_current_line_no(input), input->filename);
+		return -1;
+	}
+	fqb_line_noempty(b, MAX_READ_NAME_LEN, read_name);
+	for (int cursor = 1; read_name[cursor]; cursor++)
+		if (read_name[cursor] == ' ' || read_name[cursor] == '\t') { read_name[cursor] = 0; break; }
+	ret = fqb_line_noempty(b, MAX_READ_LENGTH, read_string);
+	do nch = fqb_getc(b); while (nch == '\n');
+	if (nch != '+') {
+		fseeko(b->fp, b->pos - (off_t)(b->hi - b->lo), SEEK_SET);
+		SUBREADprintf("ERROR: a format issue %c is found on the %lld-th line in input file '%s'.\nProgram aborted.\n", nch,
+		              (long long)tell_current_line_no(input), input->filename);
+		return -1;
+	}
+	nch = ' ';
+	while (nch != -1 && nch != '\n') nch = fqb_getc(b);
+	if (quality_string) fqb_line_noempty(b, MAX_READ_LENGTH, quality_string);
+	else {
+		int content = 0;
+		nch = ' ';
+		while (nch != -1 && (nch != '\n' || !content)) { nch = fqb_getc(b); content += nch != '\n'; }
+	}
+	if (trim_5 || trim_3) ret = trim_read_inner(read_string, quality_string, ret, trim_5, trim_3);
+	return ret;
+}
+
 static int fq_next_read(gene_input_t *input, char *read_name, char *read_string, char *quality_string, short trim_5,
                         short trim_3)
 {
 	FILE *fp = (FILE *)input->input_fp;
+	svg_fqbuf *bq = fqb_of(fp);
+	if (bq) return fq_next_read_bulk(bq, input, read_name, read_string, quality_string, trim_5, trim_3);
 	signed char nch;
 	int ret;
 	flockfile(fp);

@@ -149,6 +149,38 @@ def test_oracle_dropin_fastq_layouts_match_stock(trim, cache, tmp_path):
     assert sum(1 for l in recs if not int(l.split(b"\t")[1]) & 4) > 0
 
 
+def test_oracle_dropin_fastq_bulk_read_matches_stock(cache, tmp_path):
+    """The binding's bulk FASTQ reading (a 4 MB buffer refilled by fread, memchr line ends, the FILE
+    put back where the character-wise parse would leave it): 30k reads, about 7 MB, so records
+    straddle buffer refills; some quality lines end in a 0xFF byte (the reference's `char` compare
+    with EOF ends the line there); reads of many lengths -- the stock SAM byte for byte."""
+    from tests import dropin
+    c = Case("pe_gapped_errmut")
+    if not have(c.meta["program"], "oracle-dropin"):
+        pytest.skip("reference drop-in binaries not built (make -C oracle dropin)")
+    fq = str(tmp_path / "r.fq")
+    n0 = len(c.r1)
+    with open(fq, "wb") as f:
+        for i in range(30000):
+            s = c.r1.read(i % n0)
+            L = 30 + (i * 37) % (len(s) - 29) if i % 5 == 0 else len(s)
+            s = s[:L]
+            q = bytes(33 + (i * 3 + k * 7) % 41 for k in range(len(s)))
+            if i % 11 == 0:
+                q = q[:-1] + b"\xff"
+            f.write(b"@q%d desc %d\n" % (i, i) + s + b"\n+\n" + q + b"\n")
+    pre = cache.get(c.index_key)
+    so, do = str(tmp_path / "stock.sam"), str(tmp_path / "dropin.sam")
+    dropin.run(c.meta["program"], "dump", pre, fq, None, so, 2)
+    dropin.run(c.meta["program"], "oracle-dropin", pre, fq, None, do, 2)
+    a, b = dropin.outputs(so), dropin.outputs(do)
+    assert sorted(a) == sorted(b)
+    for suf in a:
+        assert a[suf] == b[suf], "output %r differs" % (suf or ".sam")
+    recs = [l for l in a[""].split(b"\n") if l and not l.startswith(b"@")]
+    assert len(recs) == 30000
+
+
 @pytest.mark.parametrize("extra,threads", [
     (("--multiMapping", "-B", "3"), 4),           # multi-mapping reads: up to 3 locations, HI / NH, MAPQ
     # no records for unmapped fragments; RG tag (-T 1: the stock aligner hangs at -T > 1 with
