@@ -412,6 +412,7 @@ static svg_chunk_reads svg_chunk;
  * (packing + GPU), fragile voting, and the per-read tail (slowest thread of each run) */
 static double svg_t_read, svg_t_vote, svg_t_frag, svg_t_tail;
 static double svg_t_realign;   /* the library's iteration two (drop-in build), cumulative */
+static double svg_t_anti;      /* the library's anti-supporting read scan (drop-in build), cumulative */
 static uint64_t *svg_win;       /* svg_win[r] .. svg_win[r+1]: read r's fragile windows in this block */
 
 /* thread 0 (or the only thread): the chunk's reads, the GPU vote (first block's run: every block),
@@ -683,8 +684,8 @@ int svg_sam_finish(void)
 	if (svg_sam && (rc = svg_sam_writer_close(svg_sam))) SUBREADprintf("svg_sam_writer_close: %s\n", svg_last_error());
 	svg_sam = NULL;
 	if (getenv("SVG_REF_TIMING"))
-		fprintf(stderr, "SVG_DROPIN_VOTING index_open=%.6f read_chunk=%.6f vote_call=%.6f fragile=%.6f tail=%.6f realign=%.6f\n",
-		        svg_t_open, svg_t_read, svg_t_vote, svg_t_frag, svg_t_tail, svg_t_realign);
+		fprintf(stderr, "SVG_DROPIN_VOTING index_open=%.6f read_chunk=%.6f vote_call=%.6f fragile=%.6f tail=%.6f anti=%.6f realign=%.6f\n",
+		        svg_t_open, svg_t_read, svg_t_vote, svg_t_frag, svg_t_tail, svg_t_anti, svg_t_realign);
 	return rc;
 }
 
@@ -1324,13 +1325,15 @@ static int svg_it2_setup(global_context_t *gc)
 	return rc;
 }
 
-/* chromosome_event_t <-> svg_event: the fields iteration two reads and writes */
-static int svg_it2_events_in(global_context_t *gc)
+/* chromosome_event_t -> svg_event: the fields iteration two and the anti-supporting read scan
+ * read (a calloc'd array of ic->total_events entries, NULL when out of memory) */
+static svg_event *svg_events_from_gc(global_context_t *gc, int64_t *n_out)
 {
 	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
 	int64_t n = ic->total_events, i;
 	svg_event *ev = calloc((size_t)(n ? n : 1), sizeof(svg_event));
-	if (!ev) return SVG_E_NOMEM;
+	*n_out = n;
+	if (!ev) return NULL;
 	for (i = 0; i < n; i++) {
 		const chromosome_event_t *e = ic->event_space_dynamic + i;
 		svg_event *o = &ev[i];
@@ -1356,9 +1359,64 @@ static int svg_it2_events_in(global_context_t *gc)
 		o->event_quality = e->event_quality;
 		o->critical_supporting_reads = e->critical_supporting_reads;
 	}
+	return ev;
+}
+
+static int svg_it2_events_in(global_context_t *gc)
+{
+	int64_t n;
+	svg_event *ev = svg_events_from_gc(gc, &n);
+	if (!ev) return SVG_E_NOMEM;
 	int rc = svg_realign_set_events(svg_it2, ev, n);
 	free(ev);
 	return rc;
+}
+
+/*
+ * anti_supporting_read_scan (core-indel.c:177-330), weakened in the drop-in build like do_voting:
+ * the chunk's merged event table and its bigtable records go through svg_events_anti_support
+ * (sorted side lists, one binary search per record side, threads over reads); the counts come back
+ * into the reference's table.  Fusion / long-deletion detection and colour space keep the
+ * reference's scan (ref_anti_supporting_read_scan, the alias oracle/Makefile adds), as does
+ * SVG_REF_ANTI=1.
+ */
+int ref_anti_supporting_read_scan(global_context_t *gc);
+int anti_supporting_read_scan(global_context_t *gc)
+{
+	const char *env = getenv("SVG_REF_ANTI");
+	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
+	if ((env && env[0] == '1') || gc->config.do_fusion_detection || gc->config.do_long_del_detection ||
+	    gc->config.space_type != GENE_SPACE_BASE || gc->config.multi_best_reads > 3)
+		return ref_anti_supporting_read_scan(gc);
+	if (ic->total_events < 1) return 0;
+	const double t0 = miltime();
+	int64_t n, i;
+	int rc = 0;
+	svg_event *ev = svg_events_from_gc(gc, &n);
+	svg_events *t = NULL;
+	if (!ev) rc = SVG_E_NOMEM;
+	if (!rc) rc = svg_events_create(&t);
+	if (!rc) rc = svg_events_load(t, ev, n);
+	if (!rc) {
+		svg_params p;
+		svg_event_params ep;
+		svg_fill_params(gc, &p);
+		svg_event_params_default(&ep);
+		ep.report_multi_mapping_reads = gc->config.report_multi_mapping_reads;
+		rc = svg_events_anti_support(t, &p, &ep, (uint64_t)gc->processed_reads_in_chunk, 1 + gc->input_reads.is_paired_end_reads,
+		                             (const svg_mapping_result *)_global_retrieve_alignment_ptr(gc, 0, 0, 0));
+	}
+	if (!rc && svg_events_count(t) != n) rc = SVG_E_ARG;
+	if (!rc) rc = svg_events_get(t, ev);
+	for (i = 0; !rc && i < n; i++) ic->event_space_dynamic[i].anti_supporting_reads = ev[i].anti_supporting_reads;
+	if (t) svg_events_destroy(t);
+	free(ev);
+	svg_t_anti += miltime() - t0;
+	if (rc) {
+		SUBREADprintf("svg anti-supporting read scan: %s\n", svg_last_error());
+		return 1;
+	}
+	return 0;
 }
 
 static int svg_it2_events_out(global_context_t *gc)
