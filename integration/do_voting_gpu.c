@@ -1381,13 +1381,22 @@ static int svg_it2_events_in(global_context_t *gc)
  * SVG_REF_ANTI=1.
  */
 int ref_anti_supporting_read_scan(global_context_t *gc);
-int anti_supporting_read_scan(global_context_t *gc)
+void ref_remove_neighbour(global_context_t *gc);
+static svg_events *svg_anti_t;   /* the chunk's table after the library's scan, for remove_neighbour */
+
+static int svg_anti_supported(global_context_t *gc)
 {
 	const char *env = getenv("SVG_REF_ANTI");
+	return !(env && env[0] == '1') && !gc->config.do_fusion_detection && !gc->config.do_long_del_detection &&
+	       gc->config.space_type == GENE_SPACE_BASE && gc->config.multi_best_reads <= 3 &&
+	       !(gc->config.do_remove_neighbour_for_scRNA && gc->config.scRNA_input_mode);
+}
+
+int anti_supporting_read_scan(global_context_t *gc)
+{
 	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
-	if ((env && env[0] == '1') || gc->config.do_fusion_detection || gc->config.do_long_del_detection ||
-	    gc->config.space_type != GENE_SPACE_BASE || gc->config.multi_best_reads > 3)
-		return ref_anti_supporting_read_scan(gc);
+	if (svg_anti_t) { svg_events_destroy(svg_anti_t); svg_anti_t = NULL; }
+	if (!svg_anti_supported(gc)) return ref_anti_supporting_read_scan(gc);
 	if (ic->total_events < 1) return 0;
 	const double t0 = miltime();
 	int64_t n, i;
@@ -1409,7 +1418,8 @@ int anti_supporting_read_scan(global_context_t *gc)
 	if (!rc && svg_events_count(t) != n) rc = SVG_E_ARG;
 	if (!rc) rc = svg_events_get(t, ev);
 	for (i = 0; !rc && i < n; i++) ic->event_space_dynamic[i].anti_supporting_reads = ev[i].anti_supporting_reads;
-	if (t) svg_events_destroy(t);
+	if (!rc) svg_anti_t = t;   /* remove_neighbour, next, starts from it */
+	else if (t) svg_events_destroy(t);
 	free(ev);
 	svg_t_anti += miltime() - t0;
 	if (rc) {
@@ -1434,6 +1444,61 @@ static int svg_it2_events_out(global_context_t *gc)
 	}
 	free(ev);
 	return rc;
+}
+
+/*
+ * remove_neighbour (core-indel.c:447-595), weakened like anti_supporting_read_scan: the decisions
+ * come from svg_events_remove_neighbour on the table the library's scan just counted (pinned to
+ * the reference's own removals, §5e of DESIGN.md), and each newly removed event is then taken
+ * out of the reference's site lists (event_entry_table) and typed CHRO_EVENT_TYPE_REMOVED exactly
+ * as the reference's removal loop does (core-indel.c:569-593) -- the VCF / BED writers and any
+ * later pass see the reference's own state.
+ */
+void remove_neighbour(global_context_t *gc)
+{
+	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
+	svg_events *t = svg_anti_t;
+	svg_anti_t = NULL;
+	if (!svg_anti_supported(gc) || !t || svg_events_count(t) != ic->total_events) {
+		if (t) svg_events_destroy(t);
+		ref_remove_neighbour(gc);
+		return;
+	}
+	const double t0 = miltime();
+	const int64_t n = ic->total_events;
+	svg_event *ev = calloc((size_t)(n ? n : 1), sizeof(svg_event));
+	int rc = ev ? svg_events_remove_neighbour(t) : SVG_E_NOMEM;
+	if (!rc) rc = svg_events_get(t, ev);
+	svg_events_destroy(t);
+	if (rc) {
+		free(ev);
+		ref_remove_neighbour(gc);   /* the table is untouched: the reference decides */
+		return;
+	}
+	HashTable *event_table = ic->event_entry_table;
+	chromosome_event_t *event_space = ic->event_space_dynamic;
+	for (int64_t no = 0; no < n; no++) {
+		chromosome_event_t *del = &event_space[no];
+		if (ev[no].event_type != CHRO_EVENT_TYPE_REMOVED || del->event_type == CHRO_EVENT_TYPE_REMOVED) continue;
+		for (int side = 0; side < 2; side++) {
+			const unsigned int pos = side ? del->event_large_side : del->event_small_side;
+			unsigned int *res = HashTableGet(event_table, NULL + pos);
+			if (!res) continue;
+			const int cur = res[0] & 0x0fffffff;
+			int w = 1;
+			for (int k = 1; k < cur + 1; k++) {
+				if (!res[k]) break;
+				if ((int64_t)res[k] - 1 == no) continue;
+				if (w != k) res[w] = res[k];
+				w++;
+			}
+			if (w < cur + 1) res[w] = 0;
+		}
+		if (del->event_type == CHRO_EVENT_TYPE_INDEL && del->inserted_bases) free(del->inserted_bases);
+		del->event_type = CHRO_EVENT_TYPE_REMOVED;
+	}
+	free(ev);
+	svg_t_anti += miltime() - t0;
 }
 
 static int svg_iteration_two(global_context_t *gc, thread_context_t *tc)

@@ -2803,13 +2803,18 @@ static int index_open_block(const char *prefix, int block, int device, svg_index
 		t_walk = now() - t0;
 	}
 	if (!rc) {
-		// runs of buckets [b0, b1) of about LOAD_ITEMS items
+		// runs of buckets [b0, b1) of at most LOAD_ITEMS items (a staging buffer), or a single
+		// bucket larger than that (copied straight from the map below)
 		std::vector<std::pair<uint32_t, uint32_t>> jobs;
-		for (uint32_t b0 = 0, b = 0; b < x->nb; b++)
-			if ((uint64_t)bstart[b + 1] - bstart[b0] >= LOAD_ITEMS || b + 1 == x->nb) {
-				jobs.emplace_back(b0, b + 1);
-				b0 = b + 1;
-			}
+		{
+			uint32_t b0 = 0;
+			for (uint32_t b = 0; b < x->nb; b++)
+				if (b > b0 && (uint64_t)bstart[b + 1] - bstart[b0] > LOAD_ITEMS) {
+					jobs.emplace_back(b0, b);
+					b0 = b;
+				}
+			if (b0 < x->nb) jobs.emplace_back(b0, x->nb);
+		}
 		std::atomic<size_t> next(0);
 		std::atomic<int> werr(0);
 		auto worker = [&]() {
@@ -2829,7 +2834,7 @@ static int index_open_block(const char *prefix, int block, int device, svg_index
 				const uint32_t b0 = jobs[jn].first, b1 = jobs[jn].second;
 				const uint64_t i0 = bstart[b0], cnt = (uint64_t)bstart[b1] - i0;
 				if (!cnt) continue;
-				if (cnt > LOAD_ITEMS) {   // one bucket larger than a staging buffer: straight from the map
+				if (cnt > LOAD_ITEMS) {   // one bucket larger than a staging buffer (b1 == b0 + 1): straight from the map
 					const uint8_t *src = first + 8ull * b0 + 6ull * i0 + 8;
 					if (hipMemcpy((uint8_t *)h->d_keys + 2 * i0, src, 2 * cnt, hipMemcpyHostToDevice) != hipSuccess ||
 					    hipMemcpy((uint8_t *)h->d_vals + 4 * i0, src + 2 * cnt, 4 * cnt, hipMemcpyHostToDevice) != hipSuccess)

@@ -181,6 +181,40 @@ def test_oracle_dropin_fastq_bulk_read_matches_stock(cache, tmp_path):
     assert len(recs) == 30000
 
 
+@pytest.mark.parametrize("kind", ["se", "sj"])
+def test_oracle_dropin_remove_neighbour_matches_stock(kind, tmp_path):
+    """The binding's anti-supporting read scan and remove_neighbour (the library's decisions, the
+    removals mirrored into the reference's site lists) on the two data sets where remove_neighbour
+    removes events (tests/golden/make_removed.py): subread-align on 2%-indel reads over a 150 kb
+    genome, subjunc on spliced reads over a genome with repeat families.  Event tables before and
+    after remove_neighbour (the reference's own dump hook), SAM, VCF and BED identical to stock."""
+    from tests import dropin
+    from subread_amd import build_index
+    from subread_amd.abi import PROGRAM_ALIGN, PROGRAM_SUBJUNC
+    from subread_amd.sim import random_genome, simulate_reads, simulate_spliced_reads
+    prog = PROGRAM_ALIGN if kind == "se" else PROGRAM_SUBJUNC
+    if not have(prog, "oracle-dropin"):
+        pytest.skip("reference drop-in binaries not built (make -C oracle dropin)")
+    if kind == "se":
+        g = random_genome([150_000], 78)
+        reads = simulate_reads(g, 120_000, 100, seed=4, sub=0.005, indel=0.02)
+    else:
+        g = random_genome([1_000_000, 700_000], 77, repeats=(200, 300, 20, 0.02))
+        reads = simulate_spliced_reads(g, 30000, 100, seed=6, spliced=0.5, max_intron=3000)
+    fa, pre = str(tmp_path / "g.fa"), str(tmp_path / "idx")
+    g.write_fasta(fa)
+    build_index(fa, pre, gap=1, force_one_block=True)
+    fq = str(tmp_path / "r.fq")
+    dropin.write_fastq(fq, reads)
+    so, do = str(tmp_path / "stock.sam"), str(tmp_path / "dropin.sam")
+    dropin.run(prog, "dump", pre, fq, None, so, 1, env={"SVG_REF_EVENTS_RN": so + ".rn"})
+    dropin.run(prog, "oracle-dropin", pre, fq, None, do, 1, env={"SVG_REF_EVENTS_RN": do + ".rn"})
+    rn = np.fromfile(so + ".rn", np.uint8)[8:]
+    assert (rn == 0).sum() > 0   # remove_neighbour removed events here
+    rep = dropin.compare(so, do)
+    assert ".rn" in rep["files"] and rep["mapped"] > 0
+
+
 @pytest.mark.parametrize("extra,threads", [
     (("--multiMapping", "-B", "3"), 4),           # multi-mapping reads: up to 3 locations, HI / NH, MAPQ
     # no records for unmapped fragments; RG tag (-T 1: the stock aligner hangs at -T > 1 with

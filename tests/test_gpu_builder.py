@@ -41,3 +41,22 @@ def test_gpu_built_index_votes_identically(index_cache):
     out, _, _ = ix.vote(c.params, c.r1, c.r2)
     assert (pack_records(out, None, None) == c.expected).all()
     ix.close()
+
+
+def test_index_open_from_files_equals_built_index(tmp_path):
+    """svg_index_open's streamed load (parallel bucket-chain walk, ~4M-item staging runs on 16
+    streams) of a 60 Mbp index (~60M items: many staging runs, repeat-family buckets) gives the
+    same arrays in HBM as the index built there, array for array."""
+    import subread_amd as sa
+    from subread_amd.sim import random_genome
+    g = random_genome([25_000_000, 20_000_000, 15_000_000], 606, repeats=(20_000, 300, 40, 0.12))
+    pre = str(tmp_path / "g60")
+    built = sa.VoteIndex.build_genome(g, gap=1, memory_mb=8000, force_one_block=True, device=0, save_prefix=pre)
+    opened = sa.VoteIndex(pre, device=0)
+    a, b = built.export(), opened.export()
+    assert a["items"] > 50_000_000
+    for f in ("bstart", "keys", "vals", "chr_end"):
+        assert (a[f] == b[f]).all(), f
+    assert (a["values"][:a["values_bytes"]] == b["values"][:b["values_bytes"]]).all()
+    built.close()
+    opened.close()

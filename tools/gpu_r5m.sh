@@ -1,7 +1,10 @@
 #!/bin/bash
-# GPU box, round 5 call M: the wave kernel's per-phase cycles (stamps build, C3 deferred reads),
-# then end to end at human scale with the round-5 loader (C3 genome, 3M reads: stock vs drop-in)
+# GPU box, round 5 call M: the streamed index open against the built index (60 Mbp), the drop-in
+# GPU tests (bulk FASTQ read, library anti-support scan), then end to end: C3 genome (3.0 Gbp)
+# and the 200 Mbp genome, 3M reads each, stock vs drop-in
 mkdir -p gpurun_out/r5m
-SVG_LIB=subread_amd/lib/libsubread_amd_stamps.so timeout -k 10 400 python -u tools/phase_profile.py c3 5000000 > gpurun_out/r5m/phases_c3.txt 2> gpurun_out/r5m/phases_c3.err &&
-timeout -k 10 1000 python -u tools/e2e_dropin.py --genome c3 --gpu-build --reads 3000000 --kinds dump,dropin --no-startup \
-    --out gpurun_out/r5m/e2e_c3.json > gpurun_out/r5m/e2e.out 2> gpurun_out/r5m/e2e.err
+timeout -k 10 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread -m gpu tests/test_gpu_builder.py tests/test_gpu_dropin.py > gpurun_out/r5m/tests.txt 2>&1 &&
+timeout -k 10 900 python -u tools/e2e_dropin.py --genome c3 --gpu-build --reads 3000000 --kinds dump,dropin --no-startup \
+    --out gpurun_out/r5m/e2e_c3.json > gpurun_out/r5m/e2e_c3.out 2> gpurun_out/r5m/e2e_c3.err &&
+timeout -k 10 900 python -u tools/e2e_dropin.py --mbp 200 --reads 3000000 --kinds dump,dropin,dropin_refit2 \
+    --out gpurun_out/r5m/e2e_c200m.json > gpurun_out/r5m/e2e_c200m.out 2> gpurun_out/r5m/e2e_c200m.err
