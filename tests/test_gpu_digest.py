@@ -41,3 +41,32 @@ def test_c2_10m_records_match_reference_digest():
         assert int((out["selected_votes"][:, 0, 0] > 0).sum()) == want["reads_with_votes"]
     finally:
         ix.close()
+
+
+@pytest.mark.timeout(900)
+def test_c3_50m_records_match_reference_digest():
+    """The bench workload itself: all 50M C3 reads (3.0 Gbp genome with repeat families, full
+    index built in HBM) through svg_vote_batch_packed, against tests/golden/c3_digest.json --
+    the SHA-256 of the reference aligner's own post-vote records of the same reads
+    (tools/c3_reference_digest.py)."""
+    import subread_amd as sa
+    from subread_amd.abi import default_params
+    from subread_amd.sim import random_genome, simulate_reads, c3_lengths
+    want = json.load(open(os.path.join(GOLD, "c3_digest.json")))
+    n = want["n_reads"]
+    g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))
+    ix = sa.VoteIndex.build_genome(g, gap=1, memory_mb=8000, force_one_block=True, device=0)
+    try:
+        rb = simulate_reads(g, n, 100, seed=20261015, first=0, sub=0.01, indel=0.001)
+        del g
+        pk = sa.pack_reads(rb, 100, threads=16)
+        del rb
+        out, _, _ = ix.vote_packed(default_params(), pk)
+        raw = out.view(np.uint8).reshape(n, -1)
+        B = want["block_reads"]
+        got_blocks = [hashlib.sha256(raw[a:a + B].tobytes()).hexdigest() for a in range(0, n, B)]
+        bad = [i for i, (a, b) in enumerate(zip(got_blocks, want["block_sha256"])) if a != b]
+        assert not bad, "records differ from the reference in 1M-read blocks %s" % bad[:10]
+        assert int((out["selected_votes"][:, 0, 0] > 0).sum()) == want["reads_with_votes"]
+    finally:
+        ix.close()
