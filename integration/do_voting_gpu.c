@@ -413,6 +413,10 @@ static svg_chunk_reads svg_chunk;
 static double svg_t_read, svg_t_vote, svg_t_frag, svg_t_tail;
 static double svg_t_realign;   /* the library's iteration two (drop-in build), cumulative */
 static double svg_t_anti;      /* the library's anti-supporting read scan (drop-in build), cumulative */
+/* where the time between the voting step and iteration two goes (SVG_REF_TIMING): from the end of the
+ * last voting run to the anti-supporting read scan (the reference's table merge, core.c:3452), and
+ * from remove_neighbour's end to iteration two (the rewind, core.c:3631-3640) */
+static double svg_t_mark, svg_t_to_anti, svg_t_to_it2;
 static uint64_t *svg_win;       /* svg_win[r] .. svg_win[r+1]: read r's fragile windows in this block */
 
 /* thread 0 (or the only thread): the chunk's reads, the GPU vote (first block's run: every block),
@@ -539,6 +543,7 @@ int do_voting_gpu(global_context_t *gc, thread_context_t *tc)
 	if (!rc) tail_stage(gc, tc, 0, svg_chunk.n);
 	svg_t_tail += miltime() - t0;
 	run_end(gc);
+	svg_t_mark = miltime();
 	return rc ? 1 : 0;
 }
 
@@ -570,6 +575,7 @@ int do_voting_gpu_mt(global_context_t *gc, thread_context_t *tc, int nthreads)
 	if (tid == 0) svg_t_tail += miltime() - t0;
 	const int rc = svg_run_rc;
 	if (tid == 0) run_end(gc);
+	if (tid == 0) svg_t_mark = miltime();
 	return rc ? 1 : 0;
 }
 
@@ -684,8 +690,9 @@ int svg_sam_finish(void)
 	if (svg_sam && (rc = svg_sam_writer_close(svg_sam))) SUBREADprintf("svg_sam_writer_close: %s\n", svg_last_error());
 	svg_sam = NULL;
 	if (getenv("SVG_REF_TIMING"))
-		fprintf(stderr, "SVG_DROPIN_VOTING index_open=%.6f read_chunk=%.6f vote_call=%.6f fragile=%.6f tail=%.6f anti=%.6f realign=%.6f\n",
-		        svg_t_open, svg_t_read, svg_t_vote, svg_t_frag, svg_t_tail, svg_t_anti, svg_t_realign);
+		fprintf(stderr, "SVG_DROPIN_VOTING index_open=%.6f read_chunk=%.6f vote_call=%.6f fragile=%.6f tail=%.6f to_anti=%.6f "
+		        "anti=%.6f to_it2=%.6f realign=%.6f\n",
+		        svg_t_open, svg_t_read, svg_t_vote, svg_t_frag, svg_t_tail, svg_t_to_anti, svg_t_anti, svg_t_to_it2, svg_t_realign);
 	return rc;
 }
 
@@ -1395,6 +1402,7 @@ static int svg_anti_supported(global_context_t *gc)
 int anti_supporting_read_scan(global_context_t *gc)
 {
 	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
+	if (svg_t_mark > 0) { svg_t_to_anti += miltime() - svg_t_mark; svg_t_mark = 0; }
 	if (svg_anti_t) { svg_events_destroy(svg_anti_t); svg_anti_t = NULL; }
 	if (!svg_anti_supported(gc)) return ref_anti_supporting_read_scan(gc);
 	if (ic->total_events < 1) return 0;
@@ -1460,6 +1468,9 @@ void remove_neighbour(global_context_t *gc)
 	svg_events *t = svg_anti_t;
 	svg_anti_t = NULL;
 	if (!svg_anti_supported(gc) || !t || svg_events_count(t) != ic->total_events) {
+		if (getenv("SVG_REF_TIMING"))
+			fprintf(stderr, "SVG_DROPIN_RN reference remove_neighbour (table %p, %lld vs %lld events)\n", (void *)t,
+			        (long long)(t ? svg_events_count(t) : -1), (long long)ic->total_events);
 		if (t) svg_events_destroy(t);
 		ref_remove_neighbour(gc);
 		return;
@@ -1499,11 +1510,13 @@ void remove_neighbour(global_context_t *gc)
 	}
 	free(ev);
 	svg_t_anti += miltime() - t0;
+	svg_t_mark = miltime();
 }
 
 static int svg_iteration_two(global_context_t *gc, thread_context_t *tc)
 {
 	double t0 = miltime();
+	if (svg_t_mark > 0) { svg_t_to_it2 += t0 - svg_t_mark; svg_t_mark = 0; }
 	int rc = svg_it2_setup(gc);
 	if (!rc) rc = svg_it2_events_in(gc);
 	const int ends = 1 + gc->input_reads.is_paired_end_reads;

@@ -76,7 +76,9 @@ def main():
             log("[e2e] ... %.0f s" % (time.time() - t))
     threading.Thread(target=heartbeat, daemon=True).start()
     res, start, phases = {}, {}, {}
-    env = {"SVG_REF_TIMING": "1"}
+    # the reference's phase clocks on; the test harness's vote / event dumps off (tests.dropin.run turns
+    # them on: ~0.6 GB written inside the before-realign window of both programs at 3M reads)
+    env = {"SVG_REF_TIMING": "1", "SVG_REF_DUMP": "", "SVG_REF_EVENTS": ""}
     for kind in kinds:
         binkind = "dropin" if kind == "dropin_refit2" else kind
         kenv = dict(env, SVG_REF_ITER2="1") if kind == "dropin_refit2" else env
@@ -126,7 +128,7 @@ def main():
             "phases_s": phases,
             "phases_note": "the reference's own clocks (read_chunk_circles, core.c:3552-3641), printed by "
                            "oracle/ref_dump_hook.c: load_index, voting, before_realign (anti-support scan + "
-                           "remove_neighbour), realign (iteration two incl. SAM writing)",
+                           "remove_neighbour), realign (iteration two incl. SAM writing); test dumps off",
             "cpu_model": cpu["model"],
             "config": {"genome_mbp": round(g.length / 1e6, 1), "genome": args.genome, "tab_bytes": tab_bytes,
                        "reads": args.reads, "read_len": 100, "mode": "SE, -t 1 (DNA)",
