@@ -1020,6 +1020,20 @@ struct Wave {
 		int sl0[2];
 		sl0[0] = handle_of(0, rs_v, lane);
 		sl0[1] = ENDS == 2 ? handle_of(1, rs_v, lane) : 0;
+		// single end: the handles of used slots 64..255 too, computed once for the six passes below
+		// (slot_of is 29 readlanes; a heavy read's table holds 100-260 used slots)
+		int slh[ENDS == 1 ? 3 : 1];
+		if constexpr (ENDS == 1) {
+#pragma unroll
+			for (int c = 0; c < 3; c++) slh[c] = U[0] > 64 * (c + 1) ? handle_of(0, rs_v, 64 * (c + 1) + lane) : 0;
+		}
+		auto hcache = [&](int e, int f0, int f) __attribute__((always_inline)) -> int {
+			if (f0 == 0) return e ? sl0[1] : sl0[0];
+			if constexpr (ENDS == 1) {
+				if (f0 <= 192) return f0 == 64 ? slh[0] : (f0 == 128 ? slh[1] : slh[2]);
+			}
+			return handle_of(e, rs_v, f);   // all lanes active
+		};
 		for (int e = 0; e < ENDS; e++) {
 			// top-3 distinct over table votes and stored results (update_top_three)
 			int bound = 0x7fffffff;
@@ -1027,7 +1041,7 @@ struct Wave {
 				int best = 0;
 				for (int f0 = 0; f0 < U[e]; f0 += 64) {
 					int f = f0 + lane;
-					int sl = f0 == 0 ? (e ? sl0[1] : sl0[0]) : handle_of(e, rs_v, f);   // all lanes active
+					int sl = hcache(e, f0, f);
 					if (f < U[e]) {
 						uint32_t P, M;
 						int cs_;
@@ -1055,7 +1069,7 @@ struct Wave {
 				if (N < 1 || (top[e][0] - N > p.max_vote_number_cutoff)) break;
 				for (int f0 = 0; f0 < U[e] && ns < p.max_vote_simples; f0 += 64) {
 					int f = f0 + lane;
-					int hd = f0 == 0 ? (e ? sl0[1] : sl0[0]) : handle_of(e, rs_v, f), v = -1;   // all lanes active
+					int hd = hcache(e, f0, f), v = -1;
 					uint32_t P = 0, M = 0;
 					int slot = 0;
 					if (f < U[e]) { ent_h(e, hd, P, M, slot); v = m_votes(M); }
