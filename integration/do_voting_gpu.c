@@ -69,6 +69,23 @@ static svg_index *svg_ix[SVG_MAX_DEV];
 static int svg_nix;
 static double svg_t_open;      /* SVG_REF_TIMING: svg_index_open of every handle (the index files into HBM) */
 static pthread_mutex_t svg_sam_mu_init = PTHREAD_MUTEX_INITIALIZER;   /* one-time setup of the shared state */
+/* the handles are open before the first vote: the drop-in opens them on a thread of its own
+ * (overlapping the first chunk's read, do_voting below); a host that calls svg_attach itself has
+ * them already */
+#ifdef SVG_DROPIN_DO_VOTING
+static int svg_open_join(void);
+#else
+static int svg_open_join(void) { return svg_nix > 0 ? 0 : 1; }
+#endif
+
+typedef struct { const char *prefix; int device; svg_index *ix; int rc; char err[256]; } svg_opener;
+static void *svg_opener_run(void *v)
+{
+	svg_opener *o = v;
+	o->rc = svg_index_open(o->prefix, o->device, &o->ix);
+	if (o->rc) snprintf(o->err, sizeof o->err, "%s", svg_last_error());
+	return NULL;
+}
 
 int svg_attach_devices(global_context_t *gc, const int *devices, int n)
 {
@@ -80,11 +97,29 @@ int svg_attach_devices(global_context_t *gc, const int *devices, int n)
 	}
 	snprintf(prefix, sizeof prefix, "%s", gc->config.index_prefix);
 	const double t0 = miltime();
-	for (k = 0; k < n && !rc; k++) {
-		rc = svg_index_open(prefix, devices[k], &svg_ix[k]);
-		if (rc) SUBREADprintf("GPU voting unavailable on device %d: %s\n", devices[k], svg_last_error());
-		else svg_nix = k + 1;
+	/* one opener thread per device: the .tab's pages are shared in the page cache, each device's
+	 * staging and copies run side by side */
+	svg_opener op[SVG_MAX_DEV];
+	pthread_t th[SVG_MAX_DEV];
+	int started[SVG_MAX_DEV];
+	for (k = 0; k < n; k++) {
+		op[k] = (svg_opener){prefix, devices[k], NULL, 0, ""};
+		started[k] = n > 1 && pthread_create(&th[k], NULL, svg_opener_run, &op[k]) == 0;
+		if (!started[k]) svg_opener_run(&op[k]);
 	}
+	for (k = 0; k < n; k++)
+		if (started[k]) pthread_join(th[k], NULL);
+	for (k = 0; k < n; k++) {
+		if (op[k].rc && !rc) {
+			rc = op[k].rc;
+			SUBREADprintf("GPU voting unavailable on device %d: %s\n", devices[k], op[k].err);
+		}
+	}
+	for (k = 0; k < n; k++) {
+		if (rc) { if (op[k].ix) svg_index_close(op[k].ix); continue; }
+		svg_ix[k] = op[k].ix;
+	}
+	if (!rc) svg_nix = n;
 	svg_t_open += miltime() - t0;
 	return rc;
 }
@@ -429,6 +464,10 @@ static int vote_stage(global_context_t *gc, thread_context_t *tc)
 	double t0 = miltime();
 	rc = read_chunk(gc, tc, ends, c);
 	svg_t_read += miltime() - t0;
+	if (!rc && svg_open_join()) {
+		SUBREADprintf("GPU voting unavailable\n");
+		rc = 1;
+	}
 	/* a multi-block index: the library votes every block (all resident in HBM) in the first
 	 * block's run of read_chunk_circles (core.c:3567-3613); the later runs re-read the chunk
 	 * for the per-block host work */
@@ -1591,27 +1630,60 @@ int do_iteration_two(global_context_t *gc, thread_context_t *tc)
 	return svg_iteration_two(gc, tc);
 }
 
+/*
+ * The handles are opened on a thread of their own at the first voting run, so that loading the
+ * index into HBM (svg_index_open: ~1.9 s for a 3 Gbp index) overlaps the first chunk's read;
+ * vote_stage joins it before the first vote.  SVG_DEVICES=0,1,...: one handle per listed device (a
+ * device may repeat: several replicas on one GPU); else SVG_DEVICE (default 0).
+ */
+static pthread_t svg_open_th;
+static int svg_open_state;            /* 0 not started, 1 running, 2 joined */
+static int svg_open_rc;
+static global_context_t *svg_open_gc;
+
+static void *svg_open_run(void *v)
+{
+	(void)v;
+	global_context_t *gc = svg_open_gc;
+	const char *ds = getenv("SVG_DEVICES"), *d = getenv("SVG_DEVICE");
+	if (ds && ds[0]) {
+		int devs[SVG_MAX_DEV], n = 0;
+		const char *q = ds;
+		while (*q && n < SVG_MAX_DEV) {
+			devs[n++] = atoi(q);
+			while (*q && *q != ',') q++;
+			if (*q == ',') q++;
+		}
+		svg_open_rc = svg_attach_devices(gc, devs, n);
+	} else svg_open_rc = svg_attach(gc, d ? atoi(d) : 0);
+	return NULL;
+}
+
+/* the handles, open (thread 0 of the voting run, before its first vote) */
+static int svg_open_join(void)
+{
+	pthread_mutex_lock(&svg_sam_mu_init);
+	if (svg_open_state == 1) {
+		pthread_join(svg_open_th, NULL);
+		svg_open_state = 2;
+	}
+	const int rc = svg_open_rc;
+	pthread_mutex_unlock(&svg_sam_mu_init);
+	return rc;
+}
+
 int do_voting(global_context_t *gc, thread_context_t *tc)
 {
 	pthread_mutex_lock(&svg_sam_mu_init);
-	int rc = 0;
-	if (!svg_nix) {
-		/* SVG_DEVICES=0,1,...: one handle per listed device (a device may repeat: several replicas on
-		 * one GPU); else SVG_DEVICE (default 0) */
-		const char *ds = getenv("SVG_DEVICES"), *d = getenv("SVG_DEVICE");
-		if (ds && ds[0]) {
-			int devs[SVG_MAX_DEV], n = 0;
-			const char *q = ds;
-			while (*q && n < SVG_MAX_DEV) {
-				devs[n++] = atoi(q);
-				while (*q && *q != ',') q++;
-				if (*q == ',') q++;
-			}
-			rc = svg_attach_devices(gc, devs, n);
-		} else rc = svg_attach(gc, d ? atoi(d) : 0);
+	if (svg_open_state == 0) {
+		svg_open_gc = gc;
+		if (pthread_create(&svg_open_th, NULL, svg_open_run, NULL) == 0) svg_open_state = 1;
+		else {
+			svg_open_run(NULL);
+			svg_open_state = 2;
+		}
 	}
 	pthread_mutex_unlock(&svg_sam_mu_init);
-	if (rc) return 1;
 	if (!tc || gc->config.all_threads < 2) return do_voting_gpu(gc, tc);
 	return do_voting_gpu_mt(gc, tc, gc->config.all_threads);
 }
