@@ -1470,8 +1470,9 @@ int anti_supporting_read_scan(global_context_t *gc)
 	free(ev);
 	svg_t_anti += miltime() - t0;
 	if (rc) {
-		SUBREADprintf("svg anti-supporting read scan: %s\n", svg_last_error());
-		return 1;
+		/* nothing was written back: the reference's own scan on its untouched table */
+		SUBREADprintf("svg anti-supporting read scan: %s (the reference's scan instead)\n", svg_last_error());
+		return ref_anti_supporting_read_scan(gc);
 	}
 	return 0;
 }
