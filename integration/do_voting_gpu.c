@@ -159,11 +159,14 @@ static void svg_fill_params(global_context_t *gc, svg_params *p)
 
 /* the chunk's reads as fetch_next_read_pair hands them to do_voting: text, names, qualities */
 typedef struct {
-	char *text[2], *qual[2], *name[2];
+	char *text[2], *qual[2];
+	char *names[2];                    /* read names back to back, NUL-terminated; read r's at noff[e][r] */
 	uint16_t *len[2];
-	uint64_t *off[2];
-	uint64_t n, cap, bytes[2], bcap[2];
+	uint64_t *off[2], *noff[2];
+	uint64_t n, cap, bytes[2], bcap[2], nbytes[2], ncap[2];
 } svg_chunk_reads;
+
+static inline char *chunk_name(const svg_chunk_reads *c, int e, uint64_t r) { return c->names[e] + c->noff[e][r]; }
 
 static int chunk_push(svg_chunk_reads *c, int e, const char *text, const char *qual, const char *name, int len)
 {
@@ -178,10 +181,16 @@ static int chunk_push(svg_chunk_reads *c, int e, const char *text, const char *q
 	c->off[e][c->n] = c->bytes[e];
 	c->len[e][c->n] = (uint16_t)len;
 	{
-		char *dn = c->name[e] + c->n * (MAX_READ_NAME_LEN + 1);
 		const size_t nl = strnlen(name, MAX_READ_NAME_LEN);
-		memcpy(dn, name, nl);
-		dn[nl] = 0;
+		if (c->nbytes[e] + nl + 1 > c->ncap[e]) {
+			c->ncap[e] = (c->ncap[e] + nl + 1) * 2 + 4096;
+			c->names[e] = realloc(c->names[e], c->ncap[e]);
+			if (!c->names[e]) return -1;
+		}
+		memcpy(c->names[e] + c->nbytes[e], name, nl);
+		c->names[e][c->nbytes[e] + nl] = 0;
+		c->noff[e][c->n] = c->nbytes[e];
+		c->nbytes[e] += nl + 1;
 	}
 	c->bytes[e] += len;
 	return 0;
@@ -191,7 +200,7 @@ static void chunk_free(svg_chunk_reads *c)
 {
 	int e;
 	for (e = 0; e < 2; e++) {
-		free(c->text[e]); free(c->qual[e]); free(c->name[e]); free(c->len[e]); free(c->off[e]);
+		free(c->text[e]); free(c->qual[e]); free(c->names[e]); free(c->len[e]); free(c->off[e]); free(c->noff[e]);
 	}
 }
 
@@ -223,8 +232,8 @@ static int read_chunk(global_context_t *gc, thread_context_t *tc, int ends, svg_
 			for (e = 0; e < ends; e++) {
 				c->len[e] = realloc(c->len[e], c->cap * sizeof(uint16_t));
 				c->off[e] = realloc(c->off[e], c->cap * sizeof(uint64_t));
-				c->name[e] = realloc(c->name[e], c->cap * (MAX_READ_NAME_LEN + 1));
-				if (!c->len[e] || !c->off[e] || !c->name[e]) rc = 1;
+				c->noff[e] = realloc(c->noff[e], c->cap * sizeof(uint64_t));
+				if (!c->len[e] || !c->off[e] || !c->noff[e]) rc = 1;
 			}
 			if (rc) break;
 		}
@@ -529,7 +538,7 @@ static void tail_stage(global_context_t *gc, thread_context_t *tc, uint64_t r0, 
 			if (W->strand) reverse_read(text, rl, gc->config.space_type);
 			memcpy(in, text + W->start, W->length);
 			in[W->length] = 0;
-			fragile_window_events(gc, tc, W, svg_frag.slots, in, c->name[0] + r * (MAX_READ_NAME_LEN + 1));
+			fragile_window_events(gc, tc, W, svg_frag.slots, in, chunk_name(c, 0, r));
 		}
 		if (!gc->is_final_voting_run) continue;
 		/* the final-voting-run block (core.c:3240-3290) */
@@ -543,7 +552,7 @@ static void tail_stage(global_context_t *gc, thread_context_t *tc, uint64_t r0, 
 			memcpy(qual, c->qual[e] + c->off[e][r], rl);
 			text[rl] = qual[rl] = 0;
 			reverse_read(text, rl, gc->config.space_type);
-			char *rn = c->name[e] + r * (MAX_READ_NAME_LEN + 1);
+			char *rn = chunk_name(c, e, r);
 			int b;
 			for (b = 0; b < gc->config.multi_best_reads; b++) {
 				mapping_result_t *cur = _global_retrieve_alignment_ptr(gc, r, e, b);
