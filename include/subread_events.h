@@ -115,6 +115,16 @@ int svg_events_add_batch2(svg_events *t, const svg_genome_arrays *g, const svg_p
                           uint64_t first_read, svg_mapping_result *out, const svg_subjunc_result *jout,
                           const uint16_t *big_margin, const svg_fragile_result *frag);
 
+/*
+ * The events of the fragile junction-voting windows of ONE index block -- what a run of the
+ * reference's block loop other than the last adds (core_fragile_junction_voting in do_voting,
+ * core.c:3138-3142, for every read of the chunk; core-junction.c:5211-5419): every window of
+ * `frag` (all of block `block`, reads of this batch), in order.  The final run's part is
+ * svg_events_add_batch2's (given only the last block's windows).
+ */
+int svg_events_add_windows(svg_events *t, const svg_genome_arrays *g, const svg_params *p, const svg_event_params *ep,
+                           const svg_reads *r1, const svg_reads *r2, const svg_fragile_result *frag, int block);
+
 /* Merge `n` tables (in order) into `dst` (created empty by the caller): the sort-and-sum of
  * finalise_indel_and_junction_thread.  Also call it with n = 1 on a single table: the merged
  * table is sorted by (small side, large side, indel length) as the reference's is. */
@@ -141,6 +151,19 @@ int svg_events_remove_neighbour(svg_events *t);
 /* Append n events (e.g. a table kept from an earlier chunk, or the reference's own table) to t,
  * each entered in its sides' site lists in order as put_new_event does (core-indel.c:1385). */
 int svg_events_load(svg_events *t, const svg_event *ev, int64_t n);
+
+/*
+ * Append n events exactly as a host's own event table holds them: the events (event ids in t
+ * continue from its current count) WITHOUT entering them in site lists, then the site lists as
+ * given -- list s is coordinate pos[s]'s, with entries ids[s * 9 .. s * 9 + cap[s] - 1] (event id
+ * + 1 within ev, 0 ends the list) and room for cap[s] entries (1..9).  This is the state of the
+ * reference's event_entry_table whatever made it: put_new_event's lists (room 9, a put keeps a 0
+ * after the last entry), sort_junction_entry_table's (room = entries, core-indel.c:897-906, so no
+ * put fits), remove_neighbour's compactions (core-indel.c:573-593).  The event searches and puts of
+ * svg_events_add_batch2 / svg_events_add_windows then see the lists the reference's would.
+ */
+int svg_events_load_sites(svg_events *t, const svg_event *ev, int64_t n, const uint32_t *pos, const uint32_t *ids,
+                          const uint8_t *cap, int64_t n_sites);
 
 int64_t svg_events_count(const svg_events *t);
 int     svg_events_get(const svg_events *t, svg_event *out);   /* svg_events_count() entries */

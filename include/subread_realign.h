@@ -136,8 +136,8 @@ int svg_realign_chunk(svg_realign *ra, const svg_fragment_reads *reads, svg_mapp
                       svg_sam_writer *sink, svg_realign_emit_fn emit, void *emit_arg, int threads,
                       svg_realign_stats *stats);
 
-/* contig table of a genome image (for SAM headers): n, names and lengths (read_offsets deltas
- * minus the padding, as write_sam_headers prints them) */
+/* contig table of a genome image (for SAM headers): n, names and lengths as write_sam_headers
+ * prints them in @SQ LN (FETCH_SEQ_LEN, core.c:3841: read_offsets delta + 16 - 2 * padding) */
 int svg_genome_arrays_contigs(const svg_genome_arrays *g, uint32_t *n, const char **names, uint32_t *lengths);
 
 /*

@@ -50,6 +50,19 @@ int  svg_sam_writer_put(svg_sam_writer *w, int64_t fragment, int location, int a
  * round trip.  A producer that owns a run of fragments (svg_realign_chunk's workers take blocks
  * of them) puts the run this way.  Empty text is allowed (fragments that write nothing). */
 int  svg_sam_writer_put_block(svg_sam_writer *w, int64_t first, int64_t count, const char *text, size_t len);
+/*
+ * BAM output (the reference's default; SamBam_writer_add_read, sambam-file.c:1704-1797): the same
+ * ordered sink over binary records.  `file` is the BAM file's FILE* after the writer that made it
+ * wrote the header blocks (SamBam_writer_finish_header, core.c:3870); `paired`: two records per
+ * location (the pair), else one; `level`: the deflate level (the reference's Z_BEST_SPEED, 1).
+ * Producers put svg_bam_format records -- per location the record of each end, locations in order.
+ * The records leave as BGZF blocks cut where the reference's single ordered stream cuts them
+ * (after a location that takes the block past 55000 bytes), each deflated by the thread that cut
+ * it; a partial block carries over to the next chunk and is written by svg_sam_writer_close, which
+ * does not write the BAM end-of-file block (the BAM writer that owns the file does, when it closes).
+ */
+int  svg_sam_writer_open_bam(void *file, int paired, int level, svg_sam_writer **out);
+int  svg_sam_writer_is_bam(const svg_sam_writer *w);
 /* fragments put but not yet written (waiting for an earlier one) */
 int64_t svg_sam_writer_pending(svg_sam_writer *w);
 /* 1 once a write came up short (the reference's output_sam_is_full, core.c:1869-1871) */
@@ -74,6 +87,17 @@ typedef struct svg_sam_record {
 /* Appends the record's line to buf (cap bytes); returns its length, or a negative SVG_E_ARG when
  * it does not fit (nothing is guaranteed about buf then). */
 int64_t svg_sam_format(const svg_sam_record *r, char *buf, size_t cap);
+
+/* The record in BAM binary form, byte for byte as SamBam_writer_add_read builds it from the same
+ * fields (block size, refID, pos - 1, bin / MAPQ / name length, flag / CIGAR op count, l_seq,
+ * next refID, pnext - 1, tlen, name, CIGAR ops, 4-bit bases, qualities - 33, tags as
+ * SamBam_compress_additional encodes them).  refid / next_refid: the contigs' indexes in the BAM
+ * header (the index's contig order; -1 for '*'); read_len: l_seq, the read's length (the text
+ * and quality hold that many bytes).  One difference: a text with a NUL byte inside encodes up to
+ * the NUL, as the reference's does, and the rest of its 4-bit field is zero here where the
+ * reference's record carries whatever its stream buffer held at that place.  Returns the bytes
+ * written, or SVG_E_ARG when cap is too small. */
+int64_t svg_bam_format(const svg_sam_record *r, int32_t refid, int32_t next_refid, int32_t read_len, char *buf, size_t cap);
 
 #ifdef __cplusplus
 }

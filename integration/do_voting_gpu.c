@@ -26,12 +26,17 @@
  * fragile junction voting windows (core_fragile_junction_voting, core.c:3138-3142 ->
  * core-junction.c:5151-5422: gehash_go_q windows, select_best_vote, the best matching halves,
  * the donor test) from the GPU in the same block-0 run (svg_fragile_batch, every block's
- * windows).  The per-read host work of do_voting then runs in do_voting's order with the
- * reference's own functions:
- *   - fragile windows -> events (fragile_window_events: core_dynamic_align,
- *     local_add_indel_event, search_event / put_new_event, core-junction.c:5211-5419), each
- *     index block's windows in that block's run;
- *   - the final voting run: find_new_indels / find_new_junctions per record (core.c:3240-3290).
+ * windows).  The per-read host work of do_voting then runs in do_voting's order in the library
+ * (include/subread_events.h), each thread's slice of the chunk into that thread's event table:
+ *   - fragile windows -> events (core-junction.c:5211-5419), each index block's windows in that
+ *     block's run (svg_events_add_windows);
+ *   - the final voting run: find_new_indels / find_new_junctions per record (core.c:3240-3290),
+ *     after the read's last-block windows (svg_events_add_batch2).
+ * The library's table starts as an exact copy of the run's table (events and site lists,
+ * svg_events_load_sites) and its changes come back into it (event_to_ref, put_new_event).  The
+ * reference's functions (fragile_window_events_ref, tail_ref) stay for what the library does not
+ * cover, and every stage says which implementation ran (SVG_DROPIN_STAGES at exit;
+ * SVG_REQUIRE_LIBRARY=1 makes a use of the reference's function an error).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -46,6 +51,7 @@
 #include "input-files.h"
 #include "gene-algorithms.h"
 #include "subread_vote.h"
+#include "subread_realign.h"
 
 /* defined in core.c (non-static there, not declared in a header) */
 int fetch_next_read_pair(global_context_t *global_context, thread_context_t *thread_context, gene_input_t *ginp1,
@@ -59,6 +65,44 @@ int locate_current_value_index(global_context_t *global_context, thread_context_
 int has_better_mapping(global_context_t *global_context, thread_context_t *thread_context,
                        subread_read_number_t current_read_number, int is_second_read, int this_aln_id);
 int find_subread_end(int len, int TOTAL_SUBREADS, int subread);   /* input-files.c:1371 */
+void set_insertion_sequence(global_context_t *gc, thread_context_t *tc, char **binary_bases, char *read_text,
+                            int insertions);                     /* core-indel.c:1479 */
+
+/*
+ * Which implementation answered each stage (printed at exit by svg_sam_finish as one
+ * SVG_DROPIN_STAGES line): the library -- the GPU vote and fragile windows, the host-C event stage,
+ * anti-supporting read scan, remove_neighbour and iteration two -- or the reference's own function
+ * this binding falls back to for a configuration the library does not cover.  With
+ * SVG_REQUIRE_LIBRARY=1 a fallback ends the run at once (exit status 3) with its reason.
+ */
+enum { ST_VOTE, ST_FRAGILE, ST_EVENTS, ST_ANTI, ST_RN, ST_IT2, ST_N };
+static const char *const svg_stage_name[ST_N] = {"vote", "fragile", "events", "anti_support", "remove_neighbour", "iteration_two"};
+static long svg_stage_n[ST_N][2];   /* [stage][0: library, 1: the reference's function] */
+
+static void svg_stages_print(FILE *fp)
+{
+	fprintf(fp, "SVG_DROPIN_STAGES");
+	for (int k = 0; k < ST_N; k++)
+		fprintf(fp, " %s=library:%ld,reference:%ld", svg_stage_name[k], __atomic_load_n(&svg_stage_n[k][0], __ATOMIC_RELAXED),
+		        __atomic_load_n(&svg_stage_n[k][1], __ATOMIC_RELAXED));
+	fprintf(fp, "\n");
+}
+
+/* one run of stage `st`: by the library (why == NULL) or by the reference's function, for `why` */
+static void svg_stage(int st, const char *why)
+{
+	__atomic_fetch_add(&svg_stage_n[st][why ? 1 : 0], 1, __ATOMIC_RELAXED);
+	if (!why) return;
+	const char *req = getenv("SVG_REQUIRE_LIBRARY");
+	if (getenv("SVG_REF_TIMING") || (req && req[0] == '1'))
+		fprintf(stderr, "SVG_DROPIN_FALLBACK %s: the reference's function (%s)\n", svg_stage_name[st], why);
+	if (req && req[0] == '1') {
+		fprintf(stderr, "SVG_REQUIRE_LIBRARY=1: stage %s fell back to the reference's function: %s\n", svg_stage_name[st], why);
+		svg_stages_print(stderr);
+		fflush(NULL);
+		_exit(3);
+	}
+}
 
 /* The handles: svg_ix[0 .. svg_nix-1], one per device (svg_attach_devices), each with a full index
  * replica in its HBM.  The reads of a chunk are independent, so handle k votes the k-th contiguous
@@ -267,6 +311,10 @@ static void *svg_share_run(void *v)
 	return NULL;
 }
 
+/* the big-margin records of the chunk as the vote wrote them (read, end, SVG_BIG_MARGIN_WORDS), kept
+ * for the event stage of the final run; NULL without big-margin filtering */
+static uint16_t *svg_bm;
+
 /* 2. the chunk's packed reads voted into the bigtable: one call, or with several handles one
  * contiguous range of reads per handle, each from its own host thread */
 static int vote_chunk(global_context_t *gc, int ends, const svg_chunk_reads *c)
@@ -347,18 +395,20 @@ static int vote_chunk(global_context_t *gc, int ends, const svg_chunk_reads *c)
 				       sizeof(uint16_t) * words);
 	}
 	for (e = 0; e < 2; e++) { free(bases[e]); free(xmask[e]); free(starts[e]); }
-	free(bm);
+	free(svg_bm);
+	svg_bm = bm;
 	return rc;
 }
 
 /*
- * The events of one fragile-voting window that svg_fragile_batch voted on the GPU: the tail of
- * core_fragile_junction_voting (core-junction.c:5211-5419) with the reference's own
- * core_dynamic_align / local_add_indel_event / search_event / put_new_event.  `in` is the
- * window's text (NUL-terminated), as core_fragile_junction_voting's InBuff.
+ * The reference-function fallback of the event stage for one fragile-voting window that
+ * svg_fragile_batch voted on the GPU: the tail of core_fragile_junction_voting
+ * (core-junction.c:5211-5419) with the reference's own core_dynamic_align / local_add_indel_event /
+ * search_event / put_new_event.  `in` is the window's text (NUL-terminated), as
+ * core_fragile_junction_voting's InBuff.  (The library's is svg_events_add_windows / _add_batch2.)
  */
-static void fragile_window_events(global_context_t *gc, thread_context_t *tc, const svg_fragile_window *W,
-                                  const svg_fragile_slot *slots, char *in, char *rname)
+static void fragile_window_events_ref(global_context_t *gc, thread_context_t *tc, const svg_fragile_window *W,
+                                      const svg_fragile_slot *slots, char *in, char *rname)
 {
 	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
 	indel_thread_context_t *itc = tc ? (indel_thread_context_t *)tc->module_thread_contexts[MODULE_INDEL_ID] : NULL;
@@ -463,6 +513,9 @@ static double svg_t_anti;      /* the library's anti-supporting read scan (drop-
 static double svg_t_mark, svg_t_to_anti, svg_t_to_it2;
 static uint64_t *svg_win;       /* svg_win[r] .. svg_win[r+1]: read r's fragile windows in this block */
 
+static const char *svg_ev_why;
+static const char *svg_events_unsupported(global_context_t *gc);
+
 /* thread 0 (or the only thread): the chunk's reads, the GPU vote (first block's run: every block),
  * the fragile windows, and the per-read index of this block's windows */
 static int vote_stage(global_context_t *gc, thread_context_t *tc)
@@ -473,7 +526,10 @@ static int vote_stage(global_context_t *gc, thread_context_t *tc)
 	double t0 = miltime();
 	rc = read_chunk(gc, tc, ends, c);
 	svg_t_read += miltime() - t0;
-	if (!rc && svg_open_join()) {
+	/* the handles' opener thread is joined whatever the read returned (it may be inside HIP
+	 * initialisation or an upload; nothing may leave with it running) */
+	const int open_rc = svg_open_join();
+	if (!rc && open_rc) {
 		SUBREADprintf("GPU voting unavailable\n");
 		rc = 1;
 	}
@@ -484,6 +540,7 @@ static int vote_stage(global_context_t *gc, thread_context_t *tc)
 		t0 = miltime();
 		rc = vote_chunk(gc, ends, c);
 		svg_t_vote += miltime() - t0;
+		if (!rc) svg_stage(ST_VOTE, NULL);
 		t0 = miltime();
 		/* fragile junction voting of every block, on the GPU (subjunc reads > 160 bp) */
 		svg_fragile_free(&svg_frag);
@@ -493,9 +550,12 @@ static int vote_stage(global_context_t *gc, thread_context_t *tc)
 			svg_reads a1 = {c->text[0], c->off[0], c->len[0], c->n}, a2 = {c->text[1], c->off[1], c->len[1], c->n};
 			rc = svg_fragile_batch(svg_ix[0], &p, &a1, ends == 2 ? &a2 : NULL, &svg_frag);
 			if (rc) SUBREADprintf("svg_fragile_batch: %s\n", svg_last_error());
+			else svg_stage(ST_FRAGILE, NULL);
 		}
 		svg_t_frag += miltime() - t0;
 	}
+	/* the event stage of this run: the library's, unless the configuration is one it does not cover */
+	svg_ev_why = svg_events_unsupported(gc);
 	/* this block's fragile windows are in (read, strand, end, window) order: read r's are
 	 * svg_win[r] .. svg_win[r+1]-1 */
 	free(svg_win);
@@ -512,10 +572,10 @@ static int vote_stage(global_context_t *gc, thread_context_t *tc)
 	return rc;
 }
 
-/* do_voting's per-read host work for reads [r0, r1) of the chunk, in its order, into tc's event
- * tables (the reference's threads each fill their own, merged by
- * finalise_indel_and_junction_thread, core.c:3452) */
-static void tail_stage(global_context_t *gc, thread_context_t *tc, uint64_t r0, uint64_t r1)
+/* the reference-function fallback of the event stage: do_voting's per-read host work for reads
+ * [r0, r1) of the chunk, in its order, into tc's event tables (the reference's threads each fill
+ * their own, merged by finalise_indel_and_junction_thread, core.c:3452) */
+static void tail_stage_ref(global_context_t *gc, thread_context_t *tc, uint64_t r0, uint64_t r1)
 {
 	const svg_chunk_reads *c = &svg_chunk;
 	int ends = 1 + gc->input_reads.is_paired_end_reads, e;
@@ -538,7 +598,7 @@ static void tail_stage(global_context_t *gc, thread_context_t *tc, uint64_t r0, 
 			if (W->strand) reverse_read(text, rl, gc->config.space_type);
 			memcpy(in, text + W->start, W->length);
 			in[W->length] = 0;
-			fragile_window_events(gc, tc, W, svg_frag.slots, in, chunk_name(c, 0, r));
+			fragile_window_events_ref(gc, tc, W, svg_frag.slots, in, chunk_name(c, 0, r));
 		}
 		if (!gc->is_final_voting_run) continue;
 		/* the final-voting-run block (core.c:3240-3290) */
@@ -574,13 +634,263 @@ static void tail_stage(global_context_t *gc, thread_context_t *tc, uint64_t r0, 
 	}
 }
 
+
+/* chromosome_event_t <-> svg_event: every field but the inserted bases' pointer and the id */
+static void event_to_svg(const chromosome_event_t *e, svg_event *o)
+{
+	memset(o, 0, sizeof *o);
+	o->small_side = e->event_small_side;
+	o->large_side = e->event_large_side;
+	o->indel_length = e->indel_length;
+	o->junction_flanking_left = e->junction_flanking_left;
+	o->junction_flanking_right = e->junction_flanking_right;
+	o->indel_at_junction = e->indel_at_junction;
+	o->is_negative_strand = e->is_negative_strand;
+	o->is_strand_jumped = e->is_strand_jumped;
+	o->is_donor_found_or_annotation = e->is_donor_found_or_annotation;
+	o->small_side_increasing_coordinate = e->small_side_increasing_coordinate;
+	o->large_side_increasing_coordinate = e->large_side_increasing_coordinate;
+	o->connected_next_event_distance = e->connected_next_event_distance;
+	o->connected_previous_event_distance = e->connected_previous_event_distance;
+	o->supporting_reads = e->supporting_reads;
+	o->anti_supporting_reads = e->anti_supporting_reads;
+	o->final_counted_reads = e->final_counted_reads;
+	o->final_reads_mismatches = e->final_reads_mismatches;
+	o->event_type = e->event_type;
+	o->critical_read_id = e->critical_read_id;
+	o->event_quality = e->event_quality;
+	o->critical_supporting_reads = e->critical_supporting_reads;
+}
+
+static void event_to_ref(const svg_event *o, chromosome_event_t *e)
+{
+	e->event_small_side = o->small_side;
+	e->event_large_side = o->large_side;
+	e->indel_length = o->indel_length;
+	e->junction_flanking_left = o->junction_flanking_left;
+	e->junction_flanking_right = o->junction_flanking_right;
+	e->indel_at_junction = o->indel_at_junction;
+	e->is_negative_strand = o->is_negative_strand;
+	e->is_strand_jumped = o->is_strand_jumped;
+	e->is_donor_found_or_annotation = o->is_donor_found_or_annotation;
+	e->small_side_increasing_coordinate = o->small_side_increasing_coordinate;
+	e->large_side_increasing_coordinate = o->large_side_increasing_coordinate;
+	e->connected_next_event_distance = o->connected_next_event_distance;
+	e->connected_previous_event_distance = o->connected_previous_event_distance;
+	e->supporting_reads = o->supporting_reads;
+	e->anti_supporting_reads = o->anti_supporting_reads;
+	e->final_counted_reads = o->final_counted_reads;
+	e->final_reads_mismatches = o->final_reads_mismatches;
+	e->event_type = o->event_type;
+	e->critical_read_id = o->critical_read_id;
+	e->event_quality = o->event_quality;
+	e->critical_supporting_reads = o->critical_supporting_reads;
+}
+
+/* the reference's value arrays and contig table, wrapped without a copy (every block is loaded
+ * before the first voting run, core.c:3553-3558): the event stage and iteration two read them */
+static svg_genome_arrays *svg_gen;
+
+static int svg_gen_setup(global_context_t *gc)
+{
+	if (svg_gen) return 0;
+	svg_value_block blk[100];
+	int nb = gc->index_block_number, b;
+	if (nb < 1 || nb > 100) return SVG_E_ARG;
+	for (b = 0; b < nb; b++) {
+		gene_value_index_t *v = &gc->all_value_indexes[b];
+		blk[b].values = v->values;
+		blk[b].start_point = v->start_point;
+		blk[b].length = v->length;
+		blk[b].start_base_offset = v->start_base_offset;
+		blk[b].values_bytes = v->values_bytes;
+	}
+	gene_offset_t *ct = &gc->chromosome_table;
+	return svg_genome_arrays_wrap(blk, nb, ct->read_offsets, ct->read_names, MAX_CHROMOSOME_NAME_LEN, (uint32_t)ct->total_offsets,
+	                              ct->padding, 1, &svg_gen);
+}
+
+/* svg_ev_why: why the library cannot run this chunk's event stage (NULL: it can); decided once per
+ * run by thread 0 (vote_stage) so that every thread takes the same path */
+
+static const char *svg_events_unsupported(global_context_t *gc)
+{
+	const char *env = getenv("SVG_REF_EVENTSTAGE");
+	if (env && env[0] == '1') return "SVG_REF_EVENTSTAGE=1";
+	if (gc->config.space_type != GENE_SPACE_BASE) return "colour space";
+	if (gc->config.do_fusion_detection || gc->config.do_long_del_detection) return "fusion / long-deletion detection";
+	if (!gc->config.use_dynamic_programming_indel || gc->config.extending_search_indels) return "indel search other than dynamic programming";
+	if (gc->config.multi_best_reads > 3) return "more than 3 records per read end";
+	/* (svg_event keeps 40 inserted bases; an insertion is at most -I long) */
+	if (gc->config.max_indel_length > 40) return "insertions may exceed 40 bases (-I > 40)";
+	if (svg_gen_setup(gc)) return "the genome arrays could not be wrapped";
+	return NULL;
+}
+
+/* the event table this run's thread adds to: its own (the reference's threads each fill one,
+ * merged by finalise_indel_and_junction_thread, core.c:3452) or, with one thread, the global one */
+typedef struct { HashTable *tab; unsigned int *total; } run_table;
+
+static run_table run_table_of(global_context_t *gc, thread_context_t *tc)
+{
+	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
+	indel_thread_context_t *itc = tc ? (indel_thread_context_t *)tc->module_thread_contexts[MODULE_INDEL_ID] : NULL;
+	run_table T = {itc ? itc->event_entry_table : ic->event_entry_table, itc ? &itc->total_events : &ic->total_events};
+	return T;
+}
+
+static chromosome_event_t *run_space(global_context_t *gc, thread_context_t *tc)
+{
+	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
+	indel_thread_context_t *itc = tc ? (indel_thread_context_t *)tc->module_thread_contexts[MODULE_INDEL_ID] : NULL;
+	return itc ? itc->event_space_dynamic : ic->event_space_dynamic;
+}
+
+/* the run's table as the library's: its events and every id list of its entry table, as they are */
+static int table_in(global_context_t *gc, thread_context_t *tc, svg_events **out)
+{
+	run_table T = run_table_of(gc, tc);
+	const chromosome_event_t *space = run_space(gc, tc);
+	const int64_t n = *T.total, ns = T.tab->numOfElements;
+	svg_event *ev = calloc((size_t)(n ? n : 1), sizeof(svg_event));
+	uint32_t *pos = malloc(sizeof(uint32_t) * (size_t)(ns ? ns : 1)), *ids = calloc((size_t)(ns ? ns : 1) * 9, sizeof(uint32_t));
+	uint8_t *cap = malloc((size_t)(ns ? ns : 1));
+	int rc = ev && pos && ids && cap ? 0 : SVG_E_NOMEM;
+	int64_t i, k = 0;
+	for (i = 0; !rc && i < n; i++) event_to_svg(space + i, &ev[i]);
+	for (i = 0; !rc && i < T.tab->numOfBuckets; i++)
+		for (KeyValuePair *kv = T.tab->bucketArray[i]; kv && !rc; kv = kv->next) {
+			const unsigned int *L = kv->value;
+			const unsigned int c = L[0] & 0x0fffffff;
+			if (k >= ns || c < 1 || c > 9) { rc = SVG_E_ARG; break; }
+			pos[k] = (uint32_t)(uintptr_t)kv->key;
+			cap[k] = (uint8_t)c;
+			for (unsigned int j = 0; j < c; j++) {
+				ids[k * 9 + j] = L[1 + j];
+				if (!L[1 + j]) break;
+			}
+			k++;
+		}
+	svg_events *t = NULL;
+	if (!rc) rc = svg_events_create(&t);
+	if (!rc) rc = svg_events_load_sites(t, ev, n, pos, ids, cap, k);
+	if (rc && t) { svg_events_destroy(t); t = NULL; }
+	free(ev); free(pos); free(ids); free(cap);
+	*out = t;
+	return rc;
+}
+
+/* the library's table back into the run's: the events it had get their (updated) fields, the
+ * new ones are added in order as local_add_indel_event / put_new_event add them
+ * (core-indel.c:1498-1569, 1385-1419) -- the library put them into the same id lists the same way */
+static int table_out(global_context_t *gc, thread_context_t *tc, const svg_events *t, int64_t n0)
+{
+	run_table T = run_table_of(gc, tc);
+	const int64_t n = svg_events_count(t);
+	svg_event *ev = malloc(sizeof(svg_event) * (size_t)(n ? n : 1));
+	if (!ev) return SVG_E_NOMEM;
+	int rc = svg_events_get(t, ev);
+	/* (checked before anything is written: a failure leaves the run's table as it was) */
+	for (int64_t i = n0; !rc && i < n; i++)
+		if (ev[i].event_type == CHRO_EVENT_TYPE_INDEL && ev[i].indel_length < 0 && -ev[i].indel_length > ev[i].inserted_len) rc = SVG_E_ARG;
+	chromosome_event_t *space = run_space(gc, tc);
+	for (int64_t i = 0; !rc && i < n0; i++) event_to_ref(&ev[i], space + i);
+	for (int64_t i = n0; !rc && i < n; i++) {
+		const int no = (int)(*T.total)++;
+		space = reallocate_event_space(gc, tc, no);
+		chromosome_event_t *e = space + no;
+		memset(e, 0, sizeof *e);
+		event_to_ref(&ev[i], e);
+		if (e->event_type == CHRO_EVENT_TYPE_INDEL && e->indel_length < 0) {
+			char ins[MAX_INSERTION_LENGTH + 1];
+			const int L = -e->indel_length;
+			memcpy(ins, ev[i].inserted_bases, (size_t)L);
+			ins[L] = 0;
+			set_insertion_sequence(gc, tc, &e->inserted_bases, ins, L);
+		}
+		put_new_event(T.tab, e, no);
+	}
+	free(ev);
+	return rc;
+}
+
+/* the library's event stage for reads [r0, r1) of the chunk: this block's fragile windows of those
+ * reads and, in the final run, their tails (include/subread_events.h); NULL, or why it did not run
+ * (the run's table is then as it was) */
+static const char *tail_stage_lib(global_context_t *gc, thread_context_t *tc, uint64_t r0, uint64_t r1)
+{
+	static __thread char why[300];
+	const svg_chunk_reads *c = &svg_chunk;
+	const int ends = 1 + gc->input_reads.is_paired_end_reads, final = gc->is_final_voting_run;
+	svg_params p;
+	svg_fill_params(gc, &p);
+	svg_event_params ep;
+	svg_event_params_default(&ep);
+	ep.dp_penalty_create_gap = gc->config.DP_penalty_create_gap;
+	ep.dp_penalty_extend_gap = gc->config.DP_penalty_extend_gap;
+	ep.dp_match_score = gc->config.DP_match_score;
+	ep.dp_mismatch_penalty = gc->config.DP_mismatch_penalty;
+	ep.report_multi_mapping_reads = gc->config.report_multi_mapping_reads;
+	ep.quality_base = gc->config.phred_score_format == FASTQ_PHRED64 ? 'B' : '#';   /* read_quality_score, gene-algorithms.c:138 */
+	ep.maximise_sensitivity_indel = gc->config.maximise_sensitivity_indel;
+	svg_reads R[2], Q[2];
+	const int ftype = gc->input_reads.first_read_file.file_type, quals = ftype != GENE_INPUT_FASTA && ftype != GENE_INPUT_GZIP_FASTA;
+	for (int e = 0; e < ends; e++) {
+		R[e] = (svg_reads){c->text[e], c->off[e] + r0, c->len[e] + r0, r1 - r0};
+		Q[e] = (svg_reads){c->qual[e], c->off[e] + r0, c->len[e] + r0, r1 - r0};
+	}
+	/* this block's windows of these reads, numbered from r0 */
+	svg_fragile_result fr = {0, svg_frag.n_slots, NULL, svg_frag.slots};
+	const uint64_t w0 = svg_win[r0], w1 = svg_win[r1];
+	if (w1 > w0) {
+		fr.windows = malloc(sizeof(svg_fragile_window) * (size_t)(w1 - w0));
+		if (!fr.windows) return "out of memory";
+		memcpy(fr.windows, svg_frag.windows + w0, sizeof(svg_fragile_window) * (size_t)(w1 - w0));
+		for (uint64_t w = 0; w < w1 - w0; w++) fr.windows[w].read -= (uint32_t)r0;
+		fr.n_windows = w1 - w0;
+	}
+	if (!final && !fr.n_windows) return NULL;   /* nothing this run adds for these reads */
+	svg_events *t = NULL;
+	int rc = table_in(gc, tc, &t);
+	const int64_t n0 = rc ? 0 : svg_events_count(t);
+	if (!rc && !final)
+		rc = svg_events_add_windows(t, svg_gen, &p, &ep, &R[0], ends == 2 ? &R[1] : NULL, &fr, gc->current_index_block_number);
+	else if (!rc) {
+		const uint64_t per = (uint64_t)ends * (uint64_t)gc->config.multi_best_reads;
+		svg_mapping_result *out = (svg_mapping_result *)_global_retrieve_alignment_ptr(gc, 0, 0, 0) + r0 * per;
+		const svg_subjunc_result *jout = p.do_breakpoint_detection ? (const svg_subjunc_result *)_global_retrieve_subjunc_ptr(gc, 0, 0, 0) + r0 * per : NULL;
+		const uint16_t *bm = svg_bm ? svg_bm + r0 * (uint64_t)ends * SVG_BIG_MARGIN_WORDS : NULL;
+		rc = svg_events_add_batch2(t, svg_gen, &p, &ep, &R[0], ends == 2 ? &R[1] : NULL, quals ? &Q[0] : NULL,
+		                           ends == 2 && quals ? &Q[1] : NULL, r0, out, jout, bm, p.do_breakpoint_detection ? &fr : NULL);
+	}
+	if (!rc) rc = table_out(gc, tc, t, n0);
+	if (rc) snprintf(why, sizeof why, "library event stage failed (%d): %s", rc, svg_last_error());
+	svg_events_destroy(t);
+	free(fr.windows);
+	return rc ? why : NULL;
+}
+
+/* do_voting's per-read host work for reads [r0, r1) of the chunk: the library's, or the reference's
+ * functions where it does not run */
+static void tail_stage(global_context_t *gc, thread_context_t *tc, uint64_t r0, uint64_t r1)
+{
+	const char *why = svg_ev_why;
+	if (!why) why = tail_stage_lib(gc, tc, r0, r1);
+	svg_stage(ST_EVENTS, why);
+	if (why) tail_stage_ref(gc, tc, r0, r1);
+}
+
 static void run_end(global_context_t *gc)
 {
 	chunk_free(&svg_chunk);
 	memset(&svg_chunk, 0, sizeof svg_chunk);
 	free(svg_win);
 	svg_win = NULL;
-	if (gc->is_final_voting_run) svg_fragile_free(&svg_frag);
+	if (gc->is_final_voting_run) {
+		svg_fragile_free(&svg_frag);
+		free(svg_bm);
+		svg_bm = NULL;
+	}
 }
 
 /* one thread: the whole run */
@@ -639,6 +949,7 @@ int do_voting_gpu_mt(global_context_t *gc, thread_context_t *tc, int nthreads)
 #include "subread_sam.h"
 
 static svg_sam_writer *svg_sam;
+static SamBam_Writer *svg_bam_w;       /* the BAM writer whose file svg_sam writes (BAM output) */
 static pthread_mutex_t svg_sam_mu = PTHREAD_MUTEX_INITIALIZER;
 
 void add_buffered_fragment_svg(global_context_t *gc, thread_context_t *tc, subread_read_number_t pair_number,
@@ -735,8 +1046,12 @@ int svg_sam_finish(void)
 	int rc = 0;
 	/* a fragment never put (or a short write) fails the run as the reference's output_sam_is_full
 	 * does (destroy_global_context, core.c:4270-4275: no output file, exit status 1) */
+	const int bam = svg_sam && svg_sam_writer_is_bam(svg_sam);
 	if (svg_sam && (rc = svg_sam_writer_close(svg_sam))) SUBREADprintf("svg_sam_writer_close: %s\n", svg_last_error());
 	svg_sam = NULL;
+	/* (the BAM writer closes the file after this: its end-of-file block follows our last block) */
+	if (bam && svg_bam_w) svg_bam_w->current_BAM_pos = ftello(svg_bam_w->bam_fp);
+	svg_stages_print(stderr);
 	if (getenv("SVG_REF_TIMING"))
 		fprintf(stderr, "SVG_DROPIN_VOTING index_open=%.6f read_chunk=%.6f vote_call=%.6f fragile=%.6f tail=%.6f to_anti=%.6f "
 		        "anti=%.6f to_it2=%.6f realign=%.6f\n",
@@ -1313,37 +1628,30 @@ void add_buffered_fragment(global_context_t *gc, thread_context_t *tc, subread_r
 int ref_do_iteration_two(global_context_t *gc, thread_context_t *tc);
 void print_in_box(int line_width, int is_boundary, int options, char *pattern, ...);
 
-static svg_genome_arrays *svg_it2_g;
 static svg_realign *svg_it2;
 
-static int svg_it2_supported(global_context_t *gc)
+/* why iteration two of this chunk is the reference's (NULL: the library's) */
+static const char *svg_it2_unsupported(global_context_t *gc)
 {
 	const char *e = getenv("SVG_REF_ITER2");
-	if (e && e[0] == '1') return 0;
-	return !gc->config.is_BAM_output && gc->config.space_type == GENE_SPACE_BASE && !gc->config.convert_color_to_base &&
-	       !gc->config.do_fusion_detection && !gc->config.do_long_del_detection && !gc->exonic_region_bitmap &&
-	       !gc->config.scRNA_input_mode && !gc->config.do_big_margin_filtering_for_reads &&
-	       gc->input_reads.first_read_file.file_type != GENE_INPUT_BCL && svg_rc.complete == 1 &&
-	       (subread_read_number_t)svg_rc.n == gc->processed_reads_in_chunk &&
-	       !memcmp(&svg_rc.start1, &gc->current_circle_start_position_file1, sizeof svg_rc.start1);
+	if (e && e[0] == '1') return "SVG_REF_ITER2=1";
+	if (gc->config.is_BAM_output && gc->config.sort_reads_by_coordinates) return "BAM output sorted by coordinate";
+	if (gc->config.space_type != GENE_SPACE_BASE || gc->config.convert_color_to_base) return "colour space";
+	if (gc->config.do_fusion_detection || gc->config.do_long_del_detection) return "fusion / long-deletion detection";
+	if (gc->exonic_region_bitmap) return "exon scoring from an annotation";
+	if (gc->config.scRNA_input_mode) return "scRNA input";
+	if (gc->config.do_big_margin_filtering_for_reads) return "big-margin read filtering";
+	if (gc->input_reads.first_read_file.file_type == GENE_INPUT_BCL) return "BCL input";
+	if (svg_rc.complete != 1) return "the chunk's read cache is not complete";
+	if ((subread_read_number_t)svg_rc.n != gc->processed_reads_in_chunk) return "the read cache holds another chunk";
+	if (memcmp(&svg_rc.start1, &gc->current_circle_start_position_file1, sizeof svg_rc.start1)) return "the chunk starts elsewhere";
+	return NULL;
 }
 
 static int svg_it2_setup(global_context_t *gc)
 {
 	if (svg_it2) return 0;
-	svg_value_block blk[100];
-	int nb = gc->index_block_number, b;
-	for (b = 0; b < nb; b++) {
-		gene_value_index_t *v = &gc->all_value_indexes[b];
-		blk[b].values = v->values;
-		blk[b].start_point = v->start_point;
-		blk[b].length = v->length;
-		blk[b].start_base_offset = v->start_base_offset;
-		blk[b].values_bytes = v->values_bytes;
-	}
-	gene_offset_t *ct = &gc->chromosome_table;
-	int rc = svg_genome_arrays_wrap(blk, nb, ct->read_offsets, ct->read_names, MAX_CHROMOSOME_NAME_LEN, (uint32_t)ct->total_offsets,
-	                                ct->padding, 1, &svg_it2_g);
+	int rc = svg_gen_setup(gc);
 	if (rc) return rc;
 	svg_realign_params p;
 	memset(&p, 0, sizeof p);
@@ -1375,9 +1683,7 @@ static int svg_it2_setup(global_context_t *gc)
 		memcpy(p.read_group_id, gc->config.read_group_id, rg);
 		p.read_group_id[rg] = 0;
 	}
-	rc = svg_realign_create(svg_it2_g, &p, &svg_it2);
-	if (rc) { svg_genome_arrays_close(svg_it2_g); svg_it2_g = NULL; }
-	return rc;
+	return svg_realign_create(svg_gen, &p, &svg_it2);
 }
 
 /* chromosome_event_t -> svg_event: the fields iteration two and the anti-supporting read scan
@@ -1452,8 +1758,14 @@ int anti_supporting_read_scan(global_context_t *gc)
 	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
 	if (svg_t_mark > 0) { svg_t_to_anti += miltime() - svg_t_mark; svg_t_mark = 0; }
 	if (svg_anti_t) { svg_events_destroy(svg_anti_t); svg_anti_t = NULL; }
-	if (!svg_anti_supported(gc)) return ref_anti_supporting_read_scan(gc);
-	if (ic->total_events < 1) return 0;
+	if (!svg_anti_supported(gc)) {
+		svg_stage(ST_ANTI, "configuration (SVG_REF_ANTI=1, fusion / long-deletion detection, colour space, -B > 3 or scRNA)");
+		return ref_anti_supporting_read_scan(gc);
+	}
+	if (ic->total_events < 1) {
+		svg_stage(ST_ANTI, NULL);
+		return 0;
+	}
 	const double t0 = miltime();
 	int64_t n, i;
 	int rc = 0;
@@ -1480,9 +1792,13 @@ int anti_supporting_read_scan(global_context_t *gc)
 	svg_t_anti += miltime() - t0;
 	if (rc) {
 		/* nothing was written back: the reference's own scan on its untouched table */
-		SUBREADprintf("svg anti-supporting read scan: %s (the reference's scan instead)\n", svg_last_error());
+		char why[300];
+		snprintf(why, sizeof why, "library error %d: %s", rc, svg_last_error());
+		SUBREADprintf("svg anti-supporting read scan: %s (the reference's scan instead)\n", why);
+		svg_stage(ST_ANTI, why);
 		return ref_anti_supporting_read_scan(gc);
 	}
+	svg_stage(ST_ANTI, NULL);
 	return 0;
 }
 
@@ -1516,10 +1832,15 @@ void remove_neighbour(global_context_t *gc)
 	indel_context_t *ic = (indel_context_t *)gc->module_contexts[MODULE_INDEL_ID];
 	svg_events *t = svg_anti_t;
 	svg_anti_t = NULL;
+	if (!t && svg_anti_supported(gc) && ic->total_events < 1) {   /* (an empty table: nothing to remove) */
+		svg_stage(ST_RN, NULL);
+		return;
+	}
 	if (!svg_anti_supported(gc) || !t || svg_events_count(t) != ic->total_events) {
-		if (getenv("SVG_REF_TIMING"))
-			fprintf(stderr, "SVG_DROPIN_RN reference remove_neighbour (table %p, %lld vs %lld events)\n", (void *)t,
-			        (long long)(t ? svg_events_count(t) : -1), (long long)ic->total_events);
+		char why[200];
+		snprintf(why, sizeof why, "%s (library table %s, %lld vs %lld events)", svg_anti_supported(gc) ? "no library table" : "configuration",
+		         t ? "present" : "absent", (long long)(t ? svg_events_count(t) : -1), (long long)ic->total_events);
+		svg_stage(ST_RN, why);
 		if (t) svg_events_destroy(t);
 		ref_remove_neighbour(gc);
 		return;
@@ -1532,9 +1853,13 @@ void remove_neighbour(global_context_t *gc)
 	svg_events_destroy(t);
 	if (rc) {
 		free(ev);
+		char why[300];
+		snprintf(why, sizeof why, "library error %d: %s", rc, svg_last_error());
+		svg_stage(ST_RN, why);
 		ref_remove_neighbour(gc);   /* the table is untouched: the reference decides */
 		return;
 	}
+	svg_stage(ST_RN, NULL);
 	HashTable *event_table = ic->event_entry_table;
 	chromosome_event_t *event_space = ic->event_space_dynamic;
 	for (int64_t no = 0; no < n; no++) {
@@ -1592,8 +1917,20 @@ static int svg_iteration_two(global_context_t *gc, thread_context_t *tc)
 	}
 	svg_sam_writer *sink = NULL;
 	if (!rc) {
+		/* SAM: the ordered sink on output_sam_fp.  BAM (the default output): the same sink in BAM mode
+		 * on the BAM file, whose blocks are cut where the reference's ordered stream (-T 1 or
+		 * --keepReadOrder, writer id -1, core.c:1859-1865,2144-2151) cuts them; without
+		 * --keepReadOrder the reference's threads write unordered blocks (core.c:1849-1853), and the
+		 * ordered stream holds the same records */
 		pthread_mutex_lock(&svg_sam_mu);
-		if (!svg_sam && svg_sam_writer_open(gc->output_sam_fp, &svg_sam)) rc = SVG_E_IO;
+		if (!svg_sam) {
+			if (gc->config.is_BAM_output) {
+				svg_bam_w = gc->output_bam_writer;
+				rc = svg_sam_writer_open_bam(svg_bam_w->bam_fp, gc->input_reads.is_paired_end_reads, 1, &svg_sam);
+			}
+			else rc = svg_sam_writer_open(gc->output_sam_fp, &svg_sam);
+			if (rc) rc = SVG_E_IO;
+		}
 		if (!rc) {
 			rc = svg_sam_writer_begin_chunk(svg_sam, (int64_t)n);
 			gc->last_written_fragment_number = -2;
@@ -1635,7 +1972,9 @@ static int svg_iteration_two(global_context_t *gc, thread_context_t *tc)
 
 int do_iteration_two(global_context_t *gc, thread_context_t *tc)
 {
-	if (!svg_it2_supported(gc)) return ref_do_iteration_two(gc, tc);
+	const char *why = svg_it2_unsupported(gc);
+	if (!tc || tc->thread_id == 0) svg_stage(ST_IT2, why);
+	if (why) return ref_do_iteration_two(gc, tc);
 	if (tc && tc->thread_id != 0) return 0;
 	return svg_iteration_two(gc, tc);
 }

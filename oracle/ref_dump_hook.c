@@ -202,3 +202,20 @@ int __wrap_anti_supporting_read_scan(global_context_t *gc)
 	if (ef && ef[0]) dump_events(gc, ef);
 	return rc;
 }
+
+/*
+ * SVG_REF_READS_PER_CHUNK=N (tests only; the stock dump binary and the drop-ins alike): the
+ * aligner's chunk size -- reads_per_chunk, 20M / multi_best (/ 2 for pairs) after
+ * load_global_context (core.c:4091-4094) -- set to N in the first init_bigtable_results
+ * (core.c:3837), before the bigtable is sized from it (core-bigtable.c:84-90).  A small test input
+ * then runs as several read chunks, so the event table, the expected-TLEN estimate and the output
+ * stream cross chunk boundaries (clean_context_after_chunk, core.c:3463-3478) as they do in a
+ * run of more than 6.7M reads.
+ */
+int __real_init_bigtable_results(global_context_t *gc, int is_rewinding);
+int __wrap_init_bigtable_results(global_context_t *gc, int is_rewinding)
+{
+	const char *e = getenv("SVG_REF_READS_PER_CHUNK");
+	if (!is_rewinding && e && atol(e) > 0) gc->config.reads_per_chunk = atol(e);
+	return __real_init_bigtable_results(gc, is_rewinding);
+}

@@ -40,9 +40,11 @@ EXPORTS = [
     "svg_event_params_default", "svg_genome_arrays_open", "svg_genome_arrays_close", "svg_events_create",
     "svg_events_destroy", "svg_events_add_batch", "svg_events_merge", "svg_events_count", "svg_events_get",
     "svg_events_anti_support", "svg_events_add_batch2", "svg_events_remove_neighbour", "svg_events_load",
-    # SAM emission (include/subread_sam.h)
+    "svg_events_add_windows", "svg_events_load_sites",
+    # SAM / BAM emission (include/subread_sam.h)
     "svg_sam_writer_open", "svg_sam_writer_close", "svg_sam_writer_begin_chunk", "svg_sam_writer_put",
     "svg_sam_writer_pending", "svg_sam_writer_failed", "svg_sam_format", "svg_sam_writer_put_block",
+    "svg_sam_writer_open_bam", "svg_sam_writer_is_bam", "svg_bam_format",
     # iteration two (include/subread_realign.h)
     "svg_realign_params_default", "svg_realign_create", "svg_realign_destroy", "svg_realign_set_events",
     "svg_realign_get_events", "svg_realign_set_tlen_state", "svg_realign_get_tlen_state", "svg_realign_chunk",
@@ -168,6 +170,8 @@ def lib():
         L.svg_genome_arrays_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
         L.svg_genome_arrays_open.restype = i32
         L.svg_genome_arrays_close.argtypes = [vp]
+        L.svg_genome_arrays_contigs.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), vp, vp]
+        L.svg_genome_arrays_contigs.restype = i32
         L.svg_events_create.argtypes = [ctypes.POINTER(vp)]
         L.svg_events_create.restype = i32
         L.svg_events_destroy.argtypes = [vp]
@@ -246,6 +250,15 @@ class GenomeArrays:
         h = ctypes.c_void_p()
         _check(lib().svg_genome_arrays_open(str(prefix).encode(), ctypes.byref(h)), "svg_genome_arrays_open")
         self.h = h
+
+    def contigs(self):
+        """[(name, length)] as write_sam_headers' @SQ lines give them (svg_genome_arrays_contigs)."""
+        n = ctypes.c_uint32()
+        _check(lib().svg_genome_arrays_contigs(self.h, ctypes.byref(n), None, None), "svg_genome_arrays_contigs")
+        names = (ctypes.c_char_p * max(1, n.value))()
+        lens = (ctypes.c_uint32 * max(1, n.value))()
+        _check(lib().svg_genome_arrays_contigs(self.h, ctypes.byref(n), names, lens), "svg_genome_arrays_contigs")
+        return [(names[i].decode(), int(lens[i])) for i in range(n.value)]
 
     def close(self):
         if getattr(self, "h", None):

@@ -4,8 +4,10 @@
  * finalise_indel_and_junction_thread (core-indel.c:1012-1141).  See include/subread_events.h.
  *
  * Event table: a growable array of events plus an open-addressing map from a coordinate to
- * the ids of the events that have it as small or large side -- at most 8 per coordinate,
- * like put_new_event's id lists (EVENT_ENTRIES_INIT_SIZE, core-indel.c:1385-1419).
+ * the ids of the events that have it as small or large side -- an id list of put_new_event's
+ * shape (core-indel.c:1385-1419): room for 9 entries (EVENT_ENTRIES_INIT_SIZE), of which a put
+ * fills at most 8 (it keeps a 0 after the last); a list given by svg_events_load_sites may have
+ * less room (sort_junction_entry_table sizes its lists to their entries, core-indel.c:897-906).
  */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -17,7 +19,7 @@
 #include "subread_events.h"
 #include "svg_internal.h"
 
-#define EV_PER_SITE        8          /* id slots of an id list (EVENT_ENTRIES_INIT_SIZE - 1) */
+#define EV_PER_SITE        9          /* entries of an id list (EVENT_ENTRIES_INIT_SIZE, MAX_EVENT_ENTRIES_PER_SITE) */
 #define MAX_INDEL_SECT     7          /* MAX_INDEL_SECTIONS: the loop bound of find_new_indels */
 #define LONG_READ          160        /* EXON_LONG_READ_LENGTH */
 #define MAX_INSERTION      200        /* MAX_INSERTION_LENGTH */
@@ -93,7 +95,8 @@ int svg_genome_arrays_contigs(const svg_genome_arrays *g, uint32_t *n, const cha
 	*n = g->n_chr;
 	for (uint32_t c = 0; c < g->n_chr; c++) {
 		if (names) names[c] = g->chr_name + (size_t)c * SVG_CHR_NAME_LEN;
-		if (lengths) lengths[c] = g->chr_end[c] - (c ? g->chr_end[c - 1] : 0) - (uint32_t)g->padding;
+		/* FETCH_SEQ_LEN, core.c:3841 (write_sam_headers' @SQ LN): read_offsets delta + 16 - 2 * padding */
+		if (lengths) lengths[c] = g->chr_end[c] - (c ? g->chr_end[c - 1] : 0) + 16u - 2u * (uint32_t)g->padding;
 	}
 	return 0;
 }
@@ -335,7 +338,9 @@ static int contig_of(const svg_genome_arrays *g, uint32_t linear)
 }
 
 /* ------------------------------------------------------------------ event table */
-typedef struct { uint32_t key; uint32_t ids[EV_PER_SITE]; } site_t;   /* ids: event id + 1, 0 = end */
+/* ids: event id + 1, 0 = end; cap: the list's room (id_list[0]) -- searches read up to cap entries,
+ * a put takes the first 0 among the first cap - 1 */
+typedef struct { uint32_t key; uint32_t cap; uint32_t ids[EV_PER_SITE]; } site_t;
 
 struct svg_events {
 	svg_event *ev;
@@ -404,6 +409,7 @@ static site_t *site_get(svg_events *t, uint32_t key)
 		if (t->site[i].key == key) return &t->site[i];
 		if (!t->site[i].key) {
 			t->site[i].key = key;
+			t->site[i].cap = EV_PER_SITE;
 			t->site_used++;
 			return &t->site[i];
 		}
@@ -430,8 +436,8 @@ static void put_event(svg_events *t, uint64_t id)
 		site_t *st;
 		if (!sides[s]) continue;
 		st = site_get(t, sides[s]);
-		for (k = 0; k < EV_PER_SITE; k++)
-			if (!st->ids[k]) { st->ids[k] = (uint32_t)id + 1; break; }
+		for (k = 0; k + 1 < (int)st->cap; k++)
+			if (!st->ids[k]) { st->ids[k] = (uint32_t)id + 1; st->ids[k + 1] = 0; break; }
 	}
 }
 
@@ -443,7 +449,7 @@ static int search_small(const svg_events *t, uint32_t pos, int types, uint64_t *
 	int k, n = 0;
 	if (pos < 1 || pos > 0xffff0000u) return 0;
 	if (!(st = site_find(t, pos))) return 0;
-	for (k = 0; k < EV_PER_SITE && st->ids[k]; k++) {
+	for (k = 0; k < (int)st->cap && st->ids[k]; k++) {
 		const svg_event *e = &t->ev[st->ids[k] - 1];
 		if (!(e->event_type & types) || e->small_side != pos) continue;
 		ids[n++] = st->ids[k] - 1;
@@ -1107,6 +1113,33 @@ int svg_events_add_batch2(svg_events *t, const svg_genome_arrays *g, const svg_p
 	return 0;
 }
 
+int svg_events_add_windows(svg_events *t, const svg_genome_arrays *g, const svg_params *p, const svg_event_params *ep_in,
+                           const svg_reads *r1, const svg_reads *r2, const svg_fragile_result *fr, int block)
+{
+	svg_event_params epd;
+	const svg_event_params *ep = ep_in;
+	if (!t || !g || !p || !r1 || !fr) { svg_set_error("svg_events_add_windows: NULL argument"); return SVG_E_ARG; }
+	if (block < 0 || block >= g->nblocks) { svg_set_error("svg_events_add_windows: block %d of %d", block, g->nblocks); return SVG_E_ARG; }
+	for (uint64_t i = 0; i < fr->n_windows; i++)
+		if (fr->windows[i].block != (uint32_t)block || fr->windows[i].read >= r1->n_reads || (fr->windows[i].end && !r2) ||
+		    fr->windows[i].first_slot + fr->windows[i].n_slots > fr->n_slots) {
+			svg_set_error("svg_events_add_windows: fragile windows do not match the batch / block");
+			return SVG_E_ARG;
+		}
+	if (!ep) { svg_event_params_default(&epd); ep = &epd; }
+	scratch_t *s = calloc(1, sizeof *s);
+	if (!s) { svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	s->cols = SVG_MAX_READ_LENGTH;
+	s->rows = SVG_MAX_READ_LENGTH + 20;
+	s->dp = malloc(sizeof(int16_t) * (size_t)s->rows * s->cols);
+	s->mask = malloc((size_t)s->rows * s->cols);
+	if (!s->dp || !s->mask) { free(s->dp); free(s->mask); free(s); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+	uint64_t w = 0;
+	fragile_events(t, s, g, p, ep, r1, r2, fr, &w, block, UINT64_MAX);
+	free(s->dp); free(s->mask); free(s);
+	return 0;
+}
+
 int svg_events_add_batch(svg_events *t, const svg_genome_arrays *g, const svg_params *p, const svg_event_params *ep,
                          const svg_reads *r1, const svg_reads *r2, uint64_t first_read, svg_mapping_result *out,
                          const svg_subjunc_result *jout, const uint16_t *big_margin)
@@ -1348,6 +1381,38 @@ int svg_events_load(svg_events *t, const svg_event *ev, int64_t n)
 	return 0;
 }
 
+int svg_events_load_sites(svg_events *t, const svg_event *ev, int64_t n, const uint32_t *pos, const uint32_t *ids,
+                          const uint8_t *cap, int64_t n_sites)
+{
+	if (!t || n < 0 || (n && !ev) || n_sites < 0 || (n_sites && (!pos || !ids || !cap))) {
+		svg_set_error("svg_events_load_sites: bad argument");
+		return SVG_E_ARG;
+	}
+	const uint64_t base = t->n;
+	for (int64_t s = 0; s < n_sites; s++)
+		if (!pos[s] || cap[s] < 1 || cap[s] > EV_PER_SITE || site_find(t, pos[s])) {
+			svg_set_error("svg_events_load_sites: site %lld (coordinate %u, room %u) invalid or given twice", (long long)s,
+			              pos[s], (unsigned)cap[s]);
+			return SVG_E_ARG;
+		}
+	for (int64_t i = 0; i < n; i++) {
+		const uint64_t id = new_event(t);   /* (may move t->ev) */
+		t->ev[id] = ev[i];
+	}
+	for (int64_t s = 0; s < n_sites; s++) {
+		site_t *st = site_get(t, pos[s]);
+		st->cap = cap[s];
+		memset(st->ids, 0, sizeof st->ids);
+		for (int k = 0; k < cap[s]; k++) {
+			const uint32_t v = ids[s * EV_PER_SITE + k];
+			if (!v) break;
+			if (v > (uint64_t)n) { svg_set_error("svg_events_load_sites: site %lld lists event %u of %lld", (long long)s, v, (long long)n); return SVG_E_ARG; }
+			st->ids[k] = (uint32_t)(base + v);
+		}
+	}
+	return 0;
+}
+
 /* ------------------------------------------------------------------ remove_neighbour */
 typedef struct { uint64_t *v; uint64_t n, cap; } idlist_t;
 
@@ -1370,7 +1435,7 @@ static void site_drop(svg_events *t, uint32_t key, uint64_t id)
 	site_t *st = site_find(t, key);
 	if (!st) return;
 	int w = 0, k;
-	for (k = 0; k < EV_PER_SITE && st->ids[k]; k++) {
+	for (k = 0; k < (int)st->cap && st->ids[k]; k++) {
 		if (st->ids[k] - 1 == id) continue;
 		st->ids[w++] = st->ids[k];
 	}

@@ -1350,17 +1350,22 @@ static int write_fragment(const svg_realign *ra, tally_t *T, const out_t *O, tbu
 		sr[e].tags = tags[e];
 	}
 	if (O->sink) {
+		/* SAM lines, or (BAM sink) the records in BAM form: refID = the contig's index in the header,
+		 * the mate's the other end's ('=' and '*' included: '*' is -1) */
+		const int bam = svg_sam_writer_is_bam(O->sink);
 		size_t need = 1024;
 		for (int e = 0; e < ends; e++)
-			need += strlen(name[e]) + strlen(chro[e]) + strlen(cig[e]) + 2 * (size_t)F->len[e] + strlen(tags[e]) + 80;
-		if (tb_reserve(tb, need)) return SVG_E_NOMEM;
-		int64_t n1 = svg_sam_format(&sr[0], tb->buf + tb->len, tb->cap - tb->len);
-		if (n1 < 0) return SVG_E_ARG;
-		tb->len += (size_t)n1;
-		if (ends == 2) {
-			int64_t n2 = svg_sam_format(&sr[1], tb->buf + tb->len, tb->cap - tb->len);
-			if (n2 < 0) return SVG_E_ARG;
-			tb->len += (size_t)n2;
+			need += strlen(name[e]) + strlen(chro[e]) + strlen(cig[e]) + 2 * (size_t)F->len[e] + strlen(tags[e]) + 80 + (bam ? 4 * 96 : 0);
+		if (tb_reserve(tb, need)) { svg_set_error("out of memory"); return SVG_E_NOMEM; }
+		for (int e = 0; e < ends; e++) {
+			const int32_t ref = okv[e] ? (int32_t)rv[e]->chr : -1, mref = okv[1 - e] ? (int32_t)rv[1 - e]->chr : -1;
+			const int64_t n = bam ? svg_bam_format(&sr[e], ref, mref, F->len[e], tb->buf + tb->len, tb->cap - tb->len)
+			                      : svg_sam_format(&sr[e], tb->buf + tb->len, tb->cap - tb->len);
+			if (n < 0) {
+				svg_set_error("svg_realign_chunk: the %s record of fragment %lld does not fit", bam ? "BAM" : "SAM", (long long)pair_number);
+				return SVG_E_ARG;
+			}
+			tb->len += (size_t)n;
 		}
 		return 0;
 	}
@@ -1796,6 +1801,7 @@ typedef struct {
 	worker_t *wk;
 	int64_t *next, end;
 	volatile int *rc;
+	char *err;              /* the first failing worker's svg_last_error() (errors are per thread) */
 } job_t;
 
 #define BLOCK 256
@@ -1809,7 +1815,12 @@ static void *worker_run(void *v)
 		if (b >= j->end) break;
 		const int64_t e = b + BLOCK < j->end ? b + BLOCK : j->end;
 		const int rc = do_fragments(j->ra, j->wk, j->R, j->records, b, e, j->O);
-		if (rc) { __atomic_store_n(j->rc, rc, __ATOMIC_RELAXED); break; }
+		if (rc) {
+			int zero = 0;
+			if (__atomic_compare_exchange_n(j->rc, &zero, rc, 0, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED))
+				snprintf(j->err, 256, "%s", svg_last_error());
+			break;
+		}
 	}
 	return NULL;
 }
@@ -1842,11 +1853,12 @@ int svg_realign_chunk(svg_realign *ra, const svg_fragment_reads *R, svg_mapping_
 	if (!rc && r < (int64_t)R->n) {
 		int64_t next = r;
 		volatile int jrc = 0;
+		char jerr[256] = "";
 		job_t jobs[64];
 		pthread_t th[64];
 		int started = 0;
 		for (int t = 0; t < threads; t++) {
-			jobs[t] = (job_t){ra, R, records, &O, wk[t], &next, (int64_t)R->n, &jrc};
+			jobs[t] = (job_t){ra, R, records, &O, wk[t], &next, (int64_t)R->n, &jrc, jerr};
 			if (t == 0) continue;
 			if (pthread_create(&th[t], NULL, worker_run, &jobs[t])) break;
 			started = t;
@@ -1854,6 +1866,7 @@ int svg_realign_chunk(svg_realign *ra, const svg_fragment_reads *R, svg_mapping_
 		worker_run(&jobs[0]);
 		for (int t = 1; t <= started; t++) pthread_join(th[t], NULL);
 		rc = jrc;
+		if (rc) svg_set_error("%s", jerr);
 	}
 	const double t2 = now_s();
 	/* the counters and the event support of every worker */
@@ -1882,6 +1895,5 @@ int svg_realign_chunk(svg_realign *ra, const svg_fragment_reads *R, svg_mapping_
 	if (svg_get_option("debug") & 16)
 		fprintf(stderr, "svg_realign_chunk: %llu fragments, %d threads: setup+ordered %.4f s (%lld in order), parallel %.4f s, merge %.4f s\n",
 		        (unsigned long long)R->n, threads, t1 - t0, (long long)r, t2 - t1, now_s() - t2);
-	if (rc && rc != SVG_E_NOMEM) svg_set_error("svg_realign_chunk: SAM output failed (error %d)", rc);
 	return rc;
 }

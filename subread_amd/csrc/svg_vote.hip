@@ -2790,8 +2790,13 @@ static int index_open_block(const char *prefix, int block, int device, svg_index
 	int rc = svg_tab_map(fn, x, &first);
 	if (rc) { svg_host_index_free(x); free(h); return rc; }
 	// the .array and the contig table on a thread of their own
+	// (svg_set_error's buffer is per thread: a failure's message comes back with meta_rc)
 	int meta_rc = 0;
-	std::thread meta([&] { meta_rc = svg_host_index_load_meta(prefix, block, x); });
+	char meta_err[256] = "";
+	std::thread meta([&] {
+		meta_rc = svg_host_index_load_meta(prefix, block, x);
+		if (meta_rc) snprintf(meta_err, sizeof meta_err, "%s", svg_last_error());
+	});
 	// the buckets end one byte before the file does (gehash_dump's is_small_table byte)
 	const uint8_t *const last = (const uint8_t *)x->map + x->map_len - 1;
 	uint32_t *bstart = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)x->nb + 1));
@@ -2891,7 +2896,10 @@ static int index_open_block(const char *prefix, int block, int device, svg_index
 	free(bstart);
 	munmap(x->map, x->map_len);
 	x->map = NULL;
-	if (!rc && meta_rc) rc = meta_rc;
+	if (!rc && meta_rc) {
+		rc = meta_rc;
+		svg_set_error("%s", meta_err);
+	}
 	if (rc) { svg_index_close(h); return rc; }
 	const double t1 = now();
 	if ((rc = svg_index_finish_device(h))) { svg_index_close(h); return rc; }

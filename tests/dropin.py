@@ -12,6 +12,7 @@ Binaries (test infrastructure, never part of the product):
 """
 import glob
 import os
+import re
 import subprocess
 
 import numpy as np
@@ -39,14 +40,19 @@ def write_fastq(path, batch):
             f.write(b"@r%d\n" % i + s + b"\n+\n" + q + b"\n")
 
 
-def run(program, kind, index, f1, f2, out, threads=1, extra=(), env=None, timeout=900):
-    args = [binary(program, kind), "-T", str(threads), "-i", index, "-r", f1, "-o", out, "--SAMoutput"]
+def run(program, kind, index, f1, f2, out, threads=1, extra=(), env=None, timeout=900, sam=True):
+    """One run of a reference binary (`kind`); the drop-ins run with SVG_REQUIRE_LIBRARY=1 unless
+    `env` says otherwise, so that a stage falling back to the reference's own function fails the
+    run instead of passing unnoticed (its output would be the stock program's by construction)."""
+    args = [binary(program, kind), "-T", str(threads), "-i", index, "-r", f1, "-o", out] + (["--SAMoutput"] if sam else [])
     if program == 0:
         args += ["-t", "1"]
     if f2:
         args += ["-R", f2]
     args += list(extra)
     e = dict(os.environ, SVG_REF_DUMP=out + ".votes", SVG_REF_EVENTS=out + ".events")
+    if kind.endswith("dropin"):
+        e["SVG_REQUIRE_LIBRARY"] = "1"
     if env:
         e.update(env)
     for p in glob.glob(out + "*"):
@@ -54,6 +60,34 @@ def run(program, kind, index, f1, f2, out, threads=1, extra=(), env=None, timeou
     r = subprocess.run(args, capture_output=True, text=True, env=e, timeout=timeout)
     assert r.returncode == 0, "%s failed (%d):\n%s\n%s" % (kind, r.returncode, r.stdout[-3000:], r.stderr[-3000:])
     return r
+
+
+STAGES = ("vote", "fragile", "events", "anti_support", "remove_neighbour", "iteration_two")
+
+
+def stages(stderr):
+    """The drop-in's SVG_DROPIN_STAGES line: stage -> (runs by the library, runs by the reference's
+    function)."""
+    m = re.findall(r"^SVG_DROPIN_STAGES (.*)$", stderr, re.M)
+    assert len(m) == 1, "no (or several) SVG_DROPIN_STAGES lines in the drop-in's stderr"
+    d = {}
+    for f in m[0].split():
+        k, v = f.split("=")
+        lib, ref = v.split(",")
+        d[k] = (int(lib.split(":")[1]), int(ref.split(":")[1]))
+    assert sorted(d) == sorted(STAGES), d
+    return d
+
+
+def assert_library(stderr, fragile=False):
+    """Every stage of the drop-in run was the library's, each ran at least once (fragile voting only
+    where the case has subjunc reads > 160 bp)."""
+    st = stages(stderr)
+    for k, (lib, ref) in st.items():
+        assert ref == 0, "stage %s ran the reference's function %d times: %s" % (k, ref, st)
+        if k != "fragile" or fragile:
+            assert lib > 0, "stage %s never ran in the library: %s" % (k, st)
+    return st
 
 
 def outputs(out):
@@ -104,14 +138,16 @@ def case_extra(case):
     return extra
 
 
-def check_case(case, index, tmp, kind, threads=1, env=None):
+def check_case(case, index, tmp, kind, threads=1, env=None, stock_env=None):
     """Stock reference vs the drop-in `kind` on a golden case's reads; identical outputs."""
     prog = case.meta["program"]
     f1, f2 = fastq_pair(tmp, case.name, case.r1, case.r2)
     so, do = os.path.join(tmp, case.name + ".stock.sam"), os.path.join(tmp, case.name + "." + kind + ".sam")
-    run(prog, "dump", index, f1, f2, so, threads, case_extra(case))
-    run(prog, kind, index, f1, f2, do, threads, case_extra(case), env=env)
+    run(prog, "dump", index, f1, f2, so, threads, case_extra(case), env=stock_env)
+    r = run(prog, kind, index, f1, f2, do, threads, case_extra(case), env=env)
     rep = compare(so, do)
+    long_sj = prog == 1 and max(int(case.r1.lens.max()), int(case.r2.lens.max()) if case.r2 is not None else 0) > 160
+    rep["stages"] = assert_library(r.stderr, fragile=long_sj) if kind.endswith("dropin") else None
     # the dumped vote records are the golden records of the case (the reference dumps them
     # the same way when the fixtures are made)
     votes = np.fromfile(do + ".votes", dtype=np.uint8)

@@ -262,26 +262,180 @@ def _bam_records(path):
     return b[p:]
 
 
-def test_oracle_dropin_bam_keep_read_order(cache, tmp_path):
-    """BAM output with --keepReadOrder at -T 4: the drop-in keeps the reference's ordered writer
-    path (add_buffered_fragment, core.c:1855-1881; iteration two is the reference's for BAM), so
-    the records come out in read order, identical to the stock aligner's."""
+def _bgzf_blocks(path):
+    """The BGZF blocks of a BAM file, raw, with their inflated contents: [(raw, data)]."""
+    import struct
+    import zlib
+    b = open(path, "rb").read()
+    out, p = [], 0
+    while p < len(b):
+        assert b[p:p + 4] == b"\x1f\x8b\x08\x04", "not a BGZF block at %d" % p
+        bsize = struct.unpack("<H", b[p + 16:p + 18])[0] + 1
+        raw = b[p:p + bsize]
+        out.append((raw, zlib.decompress(raw[18:-8], -15)))
+        p += bsize
+    return out
+
+
+def _bam_blocks_after_header(path):
+    """The raw BGZF blocks that follow the header's (the @PG line in the header holds the program
+    path, so the header blocks differ between the two programs; the record blocks must not)."""
+    import struct
+    blocks = _bgzf_blocks(path)
+    head = b"".join(d for _, d in blocks)
+    lt = struct.unpack("<i", head[4:8])[0]
+    p = 8 + lt
+    nref = struct.unpack("<i", head[p:p + 4])[0]
+    p += 4
+    for _ in range(nref):
+        ln = struct.unpack("<i", head[p:p + 4])[0]
+        p += 4 + ln + 4
+    k, got = 0, 0
+    while got < p:
+        got += len(blocks[k][1])
+        k += 1
+    assert got == p, "the records share a block with the header"
+    return [raw for raw, _ in blocks[k:]]
+
+
+def _bam_record_list(path):
+    """The alignment records of a BAM file, one bytes object each (block_size included)."""
+    import struct
+    b = _bam_records(path)
+    out, p = [], 0
+    while p < len(b):
+        n = struct.unpack("<i", b[p:p + 4])[0]
+        out.append(b[p:p + 4 + n])
+        p += 4 + n
+    return out
+
+
+def _mask_nul_tails(ours, theirs):
+    """Reads holding NUL bytes (the se_gapped_mixed case): SamBam_read2bin encodes a read's bases up
+    to the NUL (sambam-file.c:1460-1476) in a field of l_seq / 2 bytes; the rest of the reference's
+    field is whatever its stream buffer held there, ours is zero.  Both records get that part
+    masked (it starts at the first all-zero byte of our field)."""
+    import struct
+    a, b = bytearray(ours), bytearray(theirs)
+    name_len, ncig = a[12], struct.unpack("<H", a[16:18])[0]
+    l_seq = struct.unpack("<i", a[20:24])[0]
+    s0 = 36 + name_len + 4 * ncig
+    s1 = s0 + (l_seq + 1) // 2
+    z = a.find(b"\x00", s0, s1)
+    if z >= 0:
+        a[z:s1] = bytes(s1 - z)
+        b[z:s1] = bytes(s1 - z)
+    return bytes(a), bytes(b)
+
+
+@pytest.mark.parametrize("name,threads,keep,chunk", [
+    ("pe_gapped_errmut", 4, True, 0),        # --keepReadOrder at -T 4: the reference's ordered stream (writer id -1 / -2)
+    ("pe_gapped_errmut", 1, False, 0),       # -T 1: the same ordered stream (write_single_fragment, core.c:2144-2151)
+    ("pe_gapped_errmut", 1, False, 600),     # four read chunks: an open block crosses each chunk boundary
+    ("sj_pe_gapped_long", 1, False, 0),      # subjunc PE > 160 bp: XS tags, long records
+    ("se_gapped_mixed_n14_I16", 4, True, 0), # single end: every record closes a location
+    ("pe_gapped_errmut", 4, False, 0),       # the default: the reference's threads write unordered blocks
+])
+def test_oracle_dropin_bam_matches_stock(name, threads, keep, chunk, cache, tmp_path):
+    """BAM output (the reference's default, no --SAMoutput) through the library's iteration two and
+    its BAM sink (svg_sam_writer_open_bam, svg_bam_format): with the reference's ordered stream
+    (-T 1, --keepReadOrder) every record block after the header is byte-identical to the stock
+    aligner's -- the same records, cut into the same BGZF blocks, deflated the same way; without
+    --keepReadOrder the stock aligner's threads write their blocks in whatever order they finish, and
+    the records are the same multiset.  VCF / BED identical, every stage the library's."""
+    from tests import dropin
+    c = Case(name)
+    if not have(c.meta["program"], "oracle-dropin"):
+        pytest.skip("reference drop-in binaries not built (make -C oracle dropin)")
+    f1, f2 = dropin.fastq_pair(str(tmp_path), c.name, c.r1, c.r2)
+    pre = cache.get(c.index_key)
+    extra = dropin.case_extra(c) + (["--keepReadOrder"] if keep else [])
+    env = {"SVG_REF_READS_PER_CHUNK": str(chunk)} if chunk else None
+    so, do = str(tmp_path / "stock.bam"), str(tmp_path / "dropin.bam")
+    dropin.run(c.meta["program"], "dump", pre, f1, f2, so, threads, extra, env=env, sam=False)
+    r = dropin.run(c.meta["program"], "oracle-dropin", pre, f1, f2, do, threads, extra, env=env, sam=False)
+    st = dropin.assert_library(r.stderr)
+    if chunk:
+        assert st["iteration_two"][0] >= 4
+    a, b = _bam_record_list(so), _bam_record_list(do)
+    assert len(a) == len(c.r1) * c.ends
+    if "mixed" in name:   # reads with NUL bytes: compare outside the stale part of their 4-bit field
+        pairs = [_mask_nul_tails(y, x) for x, y in zip(a, b)]
+        assert sum(x != y for x, y in zip(a, b)) < len(a) // 10
+        a, b = [t for _, t in pairs], [o for o, _ in pairs]
+    if threads == 1 or keep:
+        assert a == b
+        if "mixed" not in name:
+            assert _bam_blocks_after_header(so) == _bam_blocks_after_header(do)
+    else:
+        assert sorted(a) == sorted(b)
+    for suf in (".indel.vcf", ".junction.bed"):
+        if os.path.exists(so + suf):
+            assert open(so + suf, "rb").read() == open(do + suf, "rb").read(), suf
+
+
+@pytest.mark.parametrize("name,threads,chunk", [
+    ("pe_gapped_errmut", 1, 500),          # one thread: every chunk adds to the global event table (its sorted site lists)
+    ("pe_gapped_errmut", 4, 500),          # per-thread tables merged into the global one, chunk after chunk
+    ("sj_pe_mb_long_gappedM6", 1, 60),     # 4-block index, long subjunc pairs: windows per block, tables across chunks
+    ("se_gapped_mixed_n14_I16", 2, 700),   # -n 14 -I 16, N / IUPAC
+])
+def test_oracle_dropin_several_chunks(name, threads, chunk, cache, tmp_path):
+    """Inputs run as several read chunks (SVG_REF_READS_PER_CHUNK, both programs): the event table,
+    its site lists, the expected-TLEN estimate and the SAM stream cross chunk boundaries as in a run
+    of more than 6.7M reads -- the stock outputs byte for byte, every stage the library's."""
+    c = Case(name)
+    if not have(c.meta["program"], "oracle-dropin"):
+        pytest.skip("reference drop-in binaries not built (make -C oracle dropin)")
+    rep = check_case(c, cache.get(c.index_key), str(tmp_path), "oracle-dropin", threads,
+                     env={"SVG_REF_READS_PER_CHUNK": str(chunk)}, stock_env={"SVG_REF_READS_PER_CHUNK": str(chunk)})
+    assert rep["stages"]["iteration_two"][0] >= 3 and rep["mapped"] > 0
+
+
+@pytest.mark.parametrize("name,threads", [("pe_gapped_errmut", 4), ("sj_pe_gapped_junc", 1)])   # (the stock subjunc's event dump at -T > 1 varies run to run)
+def test_oracle_dropin_third_iteration(name, threads, cache, tmp_path):
+    """-I 20 (> 16: the reference's third iteration, do_iteration_three, core.c:3643-3647, reads the
+    records and flags iteration two leaves): the stock outputs incl. the reassembly FASTA."""
+    from tests import dropin
+    c = Case(name)
+    if not have(c.meta["program"], "oracle-dropin"):
+        pytest.skip("reference drop-in binaries not built (make -C oracle dropin)")
+    f1, f2 = dropin.fastq_pair(str(tmp_path), c.name, c.r1, c.r2)
+    pre = cache.get(c.index_key)
+    so, do = str(tmp_path / "stock.sam"), str(tmp_path / "dropin.sam")
+    dropin.run(c.meta["program"], "dump", pre, f1, f2, so, threads, ["-I", "20"])
+    r = dropin.run(c.meta["program"], "oracle-dropin", pre, f1, f2, do, threads, ["-I", "20"])
+    dropin.assert_library(r.stderr)
+    rep = dropin.compare(so, do)
+    assert ".reassembly.fa" in rep["files"] or c.meta["program"] == 1
+
+
+@pytest.mark.parametrize("env,stage", [({"SVG_REF_ITER2": "1"}, "iteration_two"), ({"SVG_REF_EVENTSTAGE": "1"}, "events"),
+                                        ({"SVG_REF_ANTI": "1"}, "anti_support")])
+def test_oracle_dropin_fallbacks_are_counted(env, stage, cache, tmp_path):
+    """A stage forced onto the reference's own function: the outputs stay the stock program's (by
+    construction), the stage counter says "reference", and SVG_REQUIRE_LIBRARY=1 turns the same run
+    into an error (exit status 3, the stage and the reason on stderr) -- a fallback never passes as
+    the library's work."""
+    import subprocess
     from tests import dropin
     c = Case("pe_gapped_errmut")
     if not have(c.meta["program"], "oracle-dropin"):
         pytest.skip("reference drop-in binaries not built (make -C oracle dropin)")
     f1, f2 = dropin.fastq_pair(str(tmp_path), c.name, c.r1, c.r2)
     pre = cache.get(c.index_key)
-    outs = {}
-    for kind in ("dump", "oracle-dropin"):
-        o = str(tmp_path / (kind + ".bam"))
-        args = [dropin.binary(0, kind), "-T", "4", "-i", pre, "-r", f1, "-R", f2, "-o", o, "-t", "1", "--keepReadOrder"]
-        import subprocess
-        r = subprocess.run(args, capture_output=True, text=True, timeout=900)
-        assert r.returncode == 0, r.stderr[-2000:]
-        outs[kind] = _bam_records(o)
-    assert len(outs["dump"]) > 100000
-    assert outs["dump"] == outs["oracle-dropin"]
+    so, do = str(tmp_path / "stock.sam"), str(tmp_path / "dropin.sam")
+    dropin.run(c.meta["program"], "dump", pre, f1, f2, so, 2)
+    r = dropin.run(c.meta["program"], "oracle-dropin", pre, f1, f2, do, 2, env=dict(env, SVG_REQUIRE_LIBRARY="0"))
+    st = dropin.stages(r.stderr)
+    assert st[stage][1] > 0 and st[stage][0] == 0, st
+    assert st["vote"][1] == 0 and st["vote"][0] > 0
+    dropin.compare(so, do)
+    args = [dropin.binary(0, "oracle-dropin"), "-T", "2", "-i", pre, "-r", f1, "-R", f2, "-o", str(tmp_path / "x.sam"),
+            "--SAMoutput", "-t", "1"]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=900, env=dict(os.environ, SVG_REQUIRE_LIBRARY="1", **env))
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert "SVG_REQUIRE_LIBRARY=1: stage %s fell back" % stage in r.stderr
 
 
 @pytest.mark.parametrize("name,threads", [("pe_gapped_errmut", 1), ("sj_pe_gapped_long", 1), ("sj_pe_mb_long_gappedM6", 1),

@@ -190,3 +190,26 @@ def test_remove_neighbour_matches_reference(name):
     b = before.view(EVENT_DTYPE).reshape(-1)
     keep = want != 0
     assert (got[keep].view(np.uint8) == b[keep].view(np.uint8)).all()
+
+
+def test_genome_arrays_contigs_are_sam_header_lengths(tmp_path):
+    """svg_genome_arrays_contigs gives write_sam_headers' @SQ lengths (FETCH_SEQ_LEN, core.c:3841:
+    read_offsets delta + 16 - 2 * padding): the FASTA's contig lengths for an index the reference's
+    builder layout pads with 1210 bases, and -- where the stock aligner is built -- its own @SQ lines."""
+    import subread_amd as sa
+    from subread_amd.sim import random_genome, simulate_reads
+    from tests import dropin
+    g = random_genome([150_000, 70_001, 33_333, 5_000], 4242)
+    fa, pre = str(tmp_path / "g.fa"), str(tmp_path / "idx")
+    g.write_fasta(fa)
+    sa.build_index(fa, pre, gap=1, force_one_block=True)
+    got = sa.GenomeArrays(pre).contigs()
+    assert got == [(n, len(s)) for n, s in zip(g.names, g.seqs)]
+    if not dropin.have(0, "dump"):
+        return
+    fq = str(tmp_path / "r.fq")
+    dropin.write_fastq(fq, simulate_reads(g, 50, 100, seed=3))
+    out = str(tmp_path / "o.sam")
+    dropin.run(0, "dump", pre, fq, None, out)
+    sq = [l.split(b"\t") for l in open(out, "rb").read().splitlines() if l.startswith(b"@SQ")]
+    assert [(f[1][3:].decode(), int(f[2][3:])) for f in sq] == got

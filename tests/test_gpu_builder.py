@@ -60,3 +60,18 @@ def test_index_open_from_files_equals_built_index(tmp_path):
     assert (a["values"][:a["values_bytes"]] == b["values"][:b["values_bytes"]]).all()
     built.close()
     opened.close()
+
+
+def test_index_open_reports_a_missing_array_file(index_cache, tmp_path):
+    """svg_index_open loads the .array and contig table on a thread of its own; a failure there comes
+    back with its own message (svg_last_error is per thread), not a stale or empty one."""
+    import shutil
+    import subread_amd as sa
+    src = index_cache.get("chr901_gapped")
+    pre = str(tmp_path / "noarray")
+    for suf in (".00.b.tab", ".reads", ".files"):
+        if os.path.exists(src + suf):
+            shutil.copy(src + suf, pre + suf)
+    with pytest.raises(sa.SvgError) as e:
+        sa.VoteIndex(pre, device=0)
+    assert ".array" in str(e.value), str(e.value)

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from tests.common import Case, IndexCache
-from tests.dropin import check_case, compare, fastq_pair, have, run
+from tests.dropin import assert_library, case_extra, check_case, compare, fastq_pair, have, run
 
 pytestmark = pytest.mark.gpu
 
@@ -60,6 +60,25 @@ def test_gpu_dropin_two_handles(name, threads, cache, tmp_path):
     assert rep["mapped"] > 0
 
 
+@pytest.mark.parametrize("name,threads,chunk", [("pe_gapped_errmut", 4, 600), ("sj_pe_gapped_long", 1, 0)])
+def test_gpu_dropin_bam_keep_read_order(name, threads, chunk, cache, tmp_path):
+    """BAM output with --keepReadOrder through the GPU drop-in (library iteration two, BAM sink):
+    the record blocks after the header are byte-identical to the stock aligner's, here also across
+    read chunks (SVG_REF_READS_PER_CHUNK in both programs)."""
+    from tests.test_dropin import _bam_blocks_after_header, _bam_record_list
+    c = Case(name)
+    _need(c.meta["program"])
+    f1, f2 = fastq_pair(str(tmp_path), c.name, c.r1, c.r2)
+    pre = cache.get(c.index_key)
+    env = {"SVG_REF_READS_PER_CHUNK": str(chunk)} if chunk else None
+    so, do = str(tmp_path / "stock.bam"), str(tmp_path / "dropin.bam")
+    extra = case_extra(c) + ["--keepReadOrder"]
+    run(c.meta["program"], "dump", pre, f1, f2, so, threads, extra, env=env, sam=False)
+    assert_library(run(c.meta["program"], "dropin", pre, f1, f2, do, threads, extra, env=env, sam=False).stderr)
+    assert _bam_record_list(so) == _bam_record_list(do)
+    assert _bam_blocks_after_header(so) == _bam_blocks_after_header(do)
+
+
 @pytest.mark.timeout(600)
 def test_gpu_dropin_c2_200k(tmp_path):
     """200k C2 reads (bench.py workload c2's genome and read generator) through the drop-in, -T 8."""
@@ -75,12 +94,19 @@ def test_gpu_dropin_c2_200k(tmp_path):
     f1, _ = fastq_pair(str(tmp_path), "c2", rb, None)
     so, do = str(tmp_path / "c2.stock.sam"), str(tmp_path / "c2.dropin.sam")
     run(0, "dump", pre, f1, None, so, threads=8)
-    run(0, "dropin", pre, f1, None, do, threads=8)
+    assert_library(run(0, "dropin", pre, f1, None, do, threads=8).stderr)
     rep = compare(so, do)
     # the same with two handles (contiguous halves of the chunk)
     do2 = str(tmp_path / "c2.dropin2.sam")
-    run(0, "dropin", pre, f1, None, do2, threads=8, env={"SVG_DEVICES": "0,0"})
+    assert_library(run(0, "dropin", pre, f1, None, do2, threads=8, env={"SVG_DEVICES": "0,0"}).stderr)
     compare(so, do2)
+    # the reference's default output, BAM, unordered at -T 8: the same records
+    from tests.test_dropin import _bam_record_list
+    sb, db = str(tmp_path / "c2.stock.bam"), str(tmp_path / "c2.dropin.bam")
+    run(0, "dump", pre, f1, None, sb, threads=8, sam=False)
+    assert_library(run(0, "dropin", pre, f1, None, db, threads=8, sam=False).stderr)
+    a, b = _bam_record_list(sb), _bam_record_list(db)
+    assert len(a) == 200_000 and sorted(a) == sorted(b)
     votes = np.fromfile(do + ".votes", dtype=np.uint8)
     assert votes.size == 200_000 * 3 * 68
     assert rep["sam_records"] >= 200_000 and rep["mapped"] > 190_000, rep
