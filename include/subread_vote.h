@@ -187,6 +187,11 @@ typedef struct svg_index_info {
  * with the records the earlier ones left (read_chunk_circles, core.c:3567-3613), so a
  * multi-block index gives the reference's records for the same reads. */
 int  svg_index_open(const char *prefix, int device, svg_index **out);
+/* The same for n devices at once (out[k] on devices[k]; a device may repeat: several replicas on
+ * one GPU): the files are read, walked and staged once and every staged run is copied to every
+ * replica -- an 8-GPU node loads the index once instead of eight times.  All or nothing: on an
+ * error no handle is left open. */
+int  svg_index_open_devices(const char *prefix, const int *devices, int n, svg_index **out);
 void svg_index_close(svg_index *idx);
 int  svg_index_get_info(const svg_index *idx, svg_index_info *out);
 

@@ -141,27 +141,22 @@ int svg_attach_devices(global_context_t *gc, const int *devices, int n)
 	}
 	snprintf(prefix, sizeof prefix, "%s", gc->config.index_prefix);
 	const double t0 = miltime();
-	/* one opener thread per device: the .tab's pages are shared in the page cache, each device's
-	 * staging and copies run side by side */
-	svg_opener op[SVG_MAX_DEV];
-	pthread_t th[SVG_MAX_DEV];
-	int started[SVG_MAX_DEV];
-	for (k = 0; k < n; k++) {
-		op[k] = (svg_opener){prefix, devices[k], NULL, 0, ""};
-		started[k] = n > 1 && pthread_create(&th[k], NULL, svg_opener_run, &op[k]) == 0;
-		if (!started[k]) svg_opener_run(&op[k]);
-	}
-	for (k = 0; k < n; k++)
-		if (started[k]) pthread_join(th[k], NULL);
-	for (k = 0; k < n; k++) {
-		if (op[k].rc && !rc) {
-			rc = op[k].rc;
-			SUBREADprintf("GPU voting unavailable on device %d: %s\n", devices[k], op[k].err);
+	if (n == 1) {
+		svg_opener op = {prefix, devices[0], NULL, 0, ""};
+		svg_opener_run(&op);
+		rc = op.rc;
+		if (rc) SUBREADprintf("GPU voting unavailable on device %d: %s\n", devices[0], op.err);
+		else svg_ix[0] = op.ix;
+	} else {
+		/* one replica per device from ONE read of the index files: the .tab is walked and staged once
+		 * and every staged run is copied to every device (svg_index_open_devices) */
+		rc = svg_index_open_devices(prefix, devices, n, svg_ix);
+		if (rc) {
+			SUBREADprintf("GPU voting unavailable on devices");
+			for (k = 0; k < n; k++) SUBREADprintf(" %d", devices[k]);
+			SUBREADprintf(": %s\n", svg_last_error());
+			for (k = 0; k < n; k++) svg_ix[k] = NULL;
 		}
-	}
-	for (k = 0; k < n; k++) {
-		if (rc) { if (op[k].ix) svg_index_close(op[k].ix); continue; }
-		svg_ix[k] = op[k].ix;
 	}
 	if (!rc) svg_nix = n;
 	svg_t_open += miltime() - t0;

@@ -46,6 +46,16 @@ int svo_dropin_index_open(const char *prefix, int device, svg_index **out)
 	return 0;
 }
 
+/* svg_index_open_devices: one restatement index per listed device */
+int svo_dropin_index_open_devices(const char *prefix, const int *devices, int n, svg_index **out)
+{
+	for (int k = 0; k < n; k++) {
+		const int rc = svo_dropin_index_open(prefix, devices[k], &out[k]);
+		if (rc) return rc;
+	}
+	return 0;
+}
+
 /* 2-bit codes + exception mask back to characters with the same base2int code and the same
  * exception status ('.' sorts below 'G' like the code-2 exceptions, 'N' above it) */
 static int unpack(const svg_packed_reads *pk, svg_reads *r, char **seq, uint64_t **off)

@@ -40,7 +40,7 @@ EXPORTS = [
     "svg_event_params_default", "svg_genome_arrays_open", "svg_genome_arrays_close", "svg_events_create",
     "svg_events_destroy", "svg_events_add_batch", "svg_events_merge", "svg_events_count", "svg_events_get",
     "svg_events_anti_support", "svg_events_add_batch2", "svg_events_remove_neighbour", "svg_events_load",
-    "svg_events_add_windows", "svg_events_load_sites",
+    "svg_events_add_windows", "svg_events_load_sites", "svg_index_open_devices",
     # SAM / BAM emission (include/subread_sam.h)
     "svg_sam_writer_open", "svg_sam_writer_close", "svg_sam_writer_begin_chunk", "svg_sam_writer_put",
     "svg_sam_writer_pending", "svg_sam_writer_failed", "svg_sam_format", "svg_sam_writer_put_block",
@@ -83,6 +83,8 @@ def lib():
         L.svg_params_default.argtypes = [vp, i32, i32]
         L.svg_index_open.argtypes = [ctypes.c_char_p, i32, ctypes.POINTER(vp)]
         L.svg_index_open.restype = i32
+        L.svg_index_open_devices.argtypes = [ctypes.c_char_p, vp, i32, vp]
+        L.svg_index_open_devices.restype = i32
         L.svg_index_close.argtypes = [vp]
         L.svg_index_get_info.argtypes = [vp, vp]
         L.svg_vote_batch.argtypes = [vp] * 7
@@ -418,6 +420,15 @@ class VoteIndex:
         info = SvgIndexInfo()
         lib().svg_index_get_info(self.h, ctypes.byref(info))
         self.info = info
+
+    @classmethod
+    def open_devices(cls, prefix, devices):
+        """One replica per listed device from one read of the files (svg_index_open_devices)."""
+        n = len(devices)
+        devs = (ctypes.c_int32 * n)(*devices)
+        hs = (ctypes.c_void_p * n)()
+        _check(lib().svg_index_open_devices(str(prefix).encode(), devs, n, hs), "svg_index_open_devices")
+        return [cls(_handle=ctypes.c_void_p(hs[k])) for k in range(n)]
 
     @classmethod
     def build(cls, fasta, gap=1, memory_mb=8000, force_one_block=True, repeat_threshold=100, device=0,

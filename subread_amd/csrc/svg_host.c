@@ -51,7 +51,7 @@ static struct { const char *name; volatile int64_t value; } g_opts[] = {
 	{"host_threads", 0}, {"host_sub", 0}, {"host_ramp", 1}, {"chunk", 0}, {"overlap", -1},
 	{"lane", 0}, {"lane_unfused", 0}, {"lane_cap", 0},
 	{"no_bcode", 0}, {"no_khash", 0}, {"khash64", 0}, {"no_bline", 0}, {"no_compact", 0}, {"keys_literal", 0},
-	{"wave_cap", -1}, {"wave_static", -1}, {"probe_cap", 0}, {"long_probes", 0},
+	{"wave_cap", -1}, {"wave_static", -1}, {"probe_cap", 0}, {"long_probes", 0}, {"dev_pace", 0},
 	{"debug", 0},   /* bits: 1 vote-path batches, 2 host pipeline, 4 sublong chunks, 8 index load, 16 iteration two */
 };
 #define N_OPTS ((int)(sizeof g_opts / sizeof g_opts[0]))

@@ -32,6 +32,7 @@
 // the cold part (coverage start/end, 21-entry indel recorder) lives in a
 // per-wave HBM scratch that stays L2-resident.  Integer work only: no MFMA.
 #include <hip/hip_runtime.h>
+#include <string>
 #include <vector>
 #include <chrono>
 #include <atomic>
@@ -1035,28 +1036,32 @@ struct Wave {
 			return handle_of(e, rs_v, f);   // all lanes active
 		};
 		for (int e = 0; e < ENDS; e++) {
-			// top-3 distinct over table votes and stored results (update_top_three)
-			int bound = 0x7fffffff;
+			// top-3 distinct over table votes and stored results (update_top_three, core-junction.c:908-922):
+			// one scan -- each lane keeps the three largest distinct votes of its slots, then three wave
+			// maxima, each taking its value off the lanes that hold it (a heavy read's table has 100-260
+			// slots: one pass over them instead of one per rank)
+			int a = 0, b = 0, c = 0;
+			auto ins = [&](int v) __attribute__((always_inline)) {
+				if (v <= c || v == a || v == b) return;
+				if (v > a) { c = b; b = a; a = v; }
+				else if (v > b) { c = b; b = v; }
+				else c = v;
+			};
+			for (int f0 = 0; f0 < U[e]; f0 += 64) {
+				int f = f0 + lane;
+				int sl = hcache(e, f0, f);
+				if (f < U[e]) {
+					uint32_t P, M;
+					int cs_;
+					ent_h(e, sl, P, M, cs_);
+					ins(m_votes(M));
+				}
+			}
+			if (lane < p.multi_best) ins(rec_votes(L->res[e][lane]));
 			for (int t = 0; t < TS; t++) {
-				int best = 0;
-				for (int f0 = 0; f0 < U[e]; f0 += 64) {
-					int f = f0 + lane;
-					int sl = hcache(e, f0, f);
-					if (f < U[e]) {
-						uint32_t P, M;
-						int cs_;
-						ent_h(e, sl, P, M, cs_);
-						int v = m_votes(M);
-						if (v < bound && v > best) best = v;
-					}
-				}
-				if (lane < p.multi_best) {
-					int v = rec_votes(L->res[e][lane]);
-					if (v > 0 && v < bound && v > best) best = v;
-				}
-				best = wave_max(best);
+				const int best = wave_max(a);
 				top[e][t] = best;
-				bound = best;
+				if (a == best) { a = b; b = c; c = 0; }
 			}
 		}
 		STAMP(8);
@@ -2773,22 +2778,54 @@ static bool tab_walk(const uint8_t *first, const uint8_t *last, uint32_t nb, uin
 	return p == last;
 }
 
-static int index_open_block(const char *prefix, int block, int device, svg_index **out)
+// a second handle's copy of the host side of block `src` (the .array image, contig table, counts)
+static int host_meta_copy(const svg_host_index *src, svg_host_index *dst)
 {
-	*out = NULL;
-	svg_index *h = (svg_index *)calloc(1, sizeof(svg_index));
-	if (!h) { svg_set_error("out of memory"); return SVG_E_NOMEM; }
-	h->device = device;
-	h->nblocks = 1;
+	*dst = *src;
+	dst->map = NULL;
+	dst->map_len = 0;
+	dst->bstart = NULL;
+	dst->keys = NULL;
+	dst->vals = NULL;
+	dst->values = NULL;
+	dst->chr_end = NULL;
+	dst->chr_name = NULL;
+	if (src->values && !(dst->values = (uint8_t *)malloc((size_t)src->values_bytes + 8))) return SVG_E_NOMEM;
+	if (src->values) memcpy(dst->values, src->values, (size_t)src->values_bytes + 8);
+	if (src->n_chr) {
+		dst->chr_end = (uint32_t *)malloc(4 * (size_t)src->n_chr);
+		dst->chr_name = (char (*)[200])malloc(200 * (size_t)src->n_chr);
+		if (!dst->chr_end || !dst->chr_name) return SVG_E_NOMEM;
+		memcpy(dst->chr_end, src->chr_end, 4 * (size_t)src->n_chr);
+		memcpy(dst->chr_name, src->chr_name, 200 * (size_t)src->n_chr);
+	}
+	return 0;
+}
+
+// One block of the index into HBM of every device in devs[0..n-1] (one handle each; a device may
+// repeat): the .tab is mapped, walked and gathered into pinned staging runs ONCE, and every run is
+// copied to every handle's arrays (one stream per worker and handle); the .array and contig table
+// are read once and copied to each handle; each handle then builds its device images on a thread of
+// its own.  n = 1 is svg_index_open's single replica.
+static int index_open_block_multi(const char *prefix, int block, const int *devs, int n, svg_index **outs)
+{
+	for (int k = 0; k < n; k++) outs[k] = NULL;
+	std::vector<svg_index *> h(n, (svg_index *)NULL);
+	auto drop_all = [&]() { for (int k = 0; k < n; k++) if (h[k]) { svg_index_close(h[k]); h[k] = NULL; } };
+	for (int k = 0; k < n; k++) {
+		if (!(h[k] = (svg_index *)calloc(1, sizeof(svg_index)))) { drop_all(); svg_set_error("out of memory"); return SVG_E_NOMEM; }
+		h[k]->device = devs[k];
+		h[k]->nblocks = 1;
+	}
 	const bool dbg = (svg_get_option("debug") & 8) != 0;
 	auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
 	const double t0 = now();
-	svg_host_index *x = &h->host;
+	svg_host_index *x = &h[0]->host;
 	char fn[4096];
 	snprintf(fn, sizeof fn, "%s.%02d.b.tab", prefix, block);
 	const uint8_t *first = NULL;
 	int rc = svg_tab_map(fn, x, &first);
-	if (rc) { svg_host_index_free(x); free(h); return rc; }
+	if (rc) { drop_all(); return rc; }
 	// the .array and the contig table on a thread of their own
 	// (svg_set_error's buffer is per thread: a failure's message comes back with meta_rc)
 	int meta_rc = 0;
@@ -2801,9 +2838,12 @@ static int index_open_block(const char *prefix, int block, int device, svg_index
 	const uint8_t *const last = (const uint8_t *)x->map + x->map_len - 1;
 	uint32_t *bstart = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)x->nb + 1));
 	if (!bstart) { rc = SVG_E_NOMEM; svg_set_error("out of memory"); }
-	if (!rc && ((rc = dmalloc(h, &h->d_bstart, 4 * ((size_t)x->nb + 1))) || (rc = dmalloc(h, &h->d_keys, 2 * x->items + 64)) ||
-	            (rc = dmalloc(h, &h->d_vals, 4 * x->items + 64))))
-		;
+	for (int k = 0; k < n && !rc; k++) {
+		if (hipSetDevice(devs[k]) != hipSuccess) { rc = SVG_E_DEVICE; svg_set_error("hipSetDevice(%d) failed", devs[k]); break; }
+		if ((rc = dmalloc(h[k], &h[k]->d_bstart, 4 * ((size_t)x->nb + 1))) || (rc = dmalloc(h[k], &h[k]->d_keys, 2 * x->items + 64)) ||
+		    (rc = dmalloc(h[k], &h[k]->d_vals, 4 * x->items + 64)))
+			break;
+	}
 	double t_walk = 0, t_copy = 0;
 	if (!rc) {
 		if (!tab_walk(first, last, x->nb, bstart, LOAD_WORKERS)) {
@@ -2812,9 +2852,9 @@ static int index_open_block(const char *prefix, int block, int device, svg_index
 		} else {
 			uint64_t cur = 0;
 			for (uint32_t b = 0; b < x->nb; b++) {
-				const uint32_t n = bstart[b];
+				const uint32_t c = bstart[b];
 				bstart[b] = (uint32_t)cur;
-				cur += n;
+				cur += c;
 			}
 			bstart[x->nb] = (uint32_t)cur;
 			if (cur != x->items) { rc = SVG_E_FORMAT; svg_set_error("'%s': bucket sizes do not add up", fn); }
@@ -2837,16 +2877,18 @@ static int index_open_block(const char *prefix, int block, int device, svg_index
 		std::atomic<size_t> next(0);
 		std::atomic<int> werr(0);
 		auto worker = [&]() {
-			hipStream_t st = NULL;
+			std::vector<hipStream_t> st(n, (hipStream_t)NULL);
 			uint8_t *buf[LOAD_BUFS] = {NULL, NULL};
-			hipEvent_t ev[LOAD_BUFS] = {NULL, NULL};
+			std::vector<hipEvent_t> ev((size_t)LOAD_BUFS * n, (hipEvent_t)NULL);
 			bool used[LOAD_BUFS] = {false, false};
-			int k = 0;
-			if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) werr = 1;
+			int kb_ = 0;
+			for (int k = 0; k < n && !werr; k++) {
+				if (hipSetDevice(devs[k]) != hipSuccess || hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess) werr = 1;
+				for (int i = 0; i < LOAD_BUFS && !werr; i++)
+					if (hipEventCreateWithFlags(&ev[i * n + k], hipEventDisableTiming) != hipSuccess) werr = 1;
+			}
 			for (int i = 0; i < LOAD_BUFS && !werr; i++)
-				if (hipHostMalloc((void **)&buf[i], 6 * (size_t)LOAD_ITEMS, hipHostMallocDefault) != hipSuccess ||
-				    hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess)
-					werr = 1;
+				if (hipHostMalloc((void **)&buf[i], 6 * (size_t)LOAD_ITEMS, hipHostMallocDefault | hipHostMallocPortable) != hipSuccess) werr = 1;
 			for (;;) {
 				const size_t jn = next.fetch_add(1);
 				if (jn >= jobs.size() || werr) break;
@@ -2855,41 +2897,55 @@ static int index_open_block(const char *prefix, int block, int device, svg_index
 				if (!cnt) continue;
 				if (cnt > LOAD_ITEMS) {   // one bucket larger than a staging buffer (b1 == b0 + 1): straight from the map
 					const uint8_t *src = first + 8ull * b0 + 6ull * i0 + 8;
-					if (hipMemcpy((uint8_t *)h->d_keys + 2 * i0, src, 2 * cnt, hipMemcpyHostToDevice) != hipSuccess ||
-					    hipMemcpy((uint8_t *)h->d_vals + 4 * i0, src + 2 * cnt, 4 * cnt, hipMemcpyHostToDevice) != hipSuccess)
-						werr = 1;
+					for (int k = 0; k < n && !werr; k++)
+						if (hipSetDevice(devs[k]) != hipSuccess ||
+						    hipMemcpy((uint8_t *)h[k]->d_keys + 2 * i0, src, 2 * cnt, hipMemcpyHostToDevice) != hipSuccess ||
+						    hipMemcpy((uint8_t *)h[k]->d_vals + 4 * i0, src + 2 * cnt, 4 * cnt, hipMemcpyHostToDevice) != hipSuccess)
+							werr = 1;
 					continue;
 				}
-				if (used[k] && hipEventSynchronize(ev[k]) != hipSuccess) { werr = 1; break; }
-				uint8_t *kb = buf[k], *vb = buf[k] + 2 * (size_t)LOAD_ITEMS;
+				if (used[kb_])
+					for (int k = 0; k < n; k++)
+						if (hipEventSynchronize(ev[kb_ * n + k]) != hipSuccess) werr = 1;
+				if (werr) break;
+				uint8_t *kb = buf[kb_], *vb = buf[kb_] + 2 * (size_t)LOAD_ITEMS;
 				for (uint32_t b = b0; b < b1; b++) {
-					const uint64_t n = (uint64_t)bstart[b + 1] - bstart[b], at = (uint64_t)bstart[b] - i0;
-					if (!n) continue;
+					const uint64_t c = (uint64_t)bstart[b + 1] - bstart[b], at = (uint64_t)bstart[b] - i0;
+					if (!c) continue;
 					const uint8_t *src = first + 8ull * b + 6ull * bstart[b] + 8;
-					memcpy(kb + 2 * at, src, 2 * n);
-					memcpy(vb + 4 * at, src + 2 * n, 4 * n);
+					memcpy(kb + 2 * at, src, 2 * c);
+					memcpy(vb + 4 * at, src + 2 * c, 4 * c);
 				}
-				if (hipMemcpyAsync((uint8_t *)h->d_keys + 2 * i0, kb, 2 * cnt, hipMemcpyHostToDevice, st) != hipSuccess ||
-				    hipMemcpyAsync((uint8_t *)h->d_vals + 4 * i0, vb, 4 * cnt, hipMemcpyHostToDevice, st) != hipSuccess ||
-				    hipEventRecord(ev[k], st) != hipSuccess)
-					werr = 1;
-				used[k] = true;
-				k = (k + 1) % LOAD_BUFS;
+				for (int k = 0; k < n && !werr; k++)
+					if (hipSetDevice(devs[k]) != hipSuccess ||
+					    hipMemcpyAsync((uint8_t *)h[k]->d_keys + 2 * i0, kb, 2 * cnt, hipMemcpyHostToDevice, st[k]) != hipSuccess ||
+					    hipMemcpyAsync((uint8_t *)h[k]->d_vals + 4 * i0, vb, 4 * cnt, hipMemcpyHostToDevice, st[k]) != hipSuccess ||
+					    hipEventRecord(ev[kb_ * n + k], st[k]) != hipSuccess)
+						werr = 1;
+				used[kb_] = true;
+				kb_ = (kb_ + 1) % LOAD_BUFS;
 			}
-			if (st) { if (hipStreamSynchronize(st) != hipSuccess) werr = 1; hipStreamDestroy(st); }
-			for (int i = 0; i < LOAD_BUFS; i++) {
-				if (ev[i]) hipEventDestroy(ev[i]);
+			for (int k = 0; k < n; k++)
+				if (st[k]) {
+					hipSetDevice(devs[k]);
+					if (hipStreamSynchronize(st[k]) != hipSuccess) werr = 1;
+					hipStreamDestroy(st[k]);
+				}
+			for (auto e : ev)
+				if (e) hipEventDestroy(e);
+			for (int i = 0; i < LOAD_BUFS; i++)
 				if (buf[i]) hipHostFree(buf[i]);
-			}
 		};
 		std::vector<std::thread> ws;
 		for (int t = 0; t < LOAD_WORKERS; t++) ws.emplace_back(worker);
 		for (auto &w : ws) w.join();
 		if (werr) { rc = SVG_E_DEVICE; svg_set_error("upload of the index to HBM failed"); }
-		if (!rc && hipMemcpy(h->d_bstart, bstart, 4 * ((size_t)x->nb + 1), hipMemcpyHostToDevice) != hipSuccess) {
-			rc = SVG_E_DEVICE;
-			svg_set_error("upload of the index to HBM failed");
-		}
+		for (int k = 0; k < n && !rc; k++)
+			if (hipSetDevice(devs[k]) != hipSuccess ||
+			    hipMemcpy(h[k]->d_bstart, bstart, 4 * ((size_t)x->nb + 1), hipMemcpyHostToDevice) != hipSuccess) {
+				rc = SVG_E_DEVICE;
+				svg_set_error("upload of the index to HBM failed");
+			}
 		t_copy = now() - t0;
 	}
 	meta.join();
@@ -2900,13 +2956,64 @@ static int index_open_block(const char *prefix, int block, int device, svg_index
 		rc = meta_rc;
 		svg_set_error("%s", meta_err);
 	}
-	if (rc) { svg_index_close(h); return rc; }
+	for (int k = 1; k < n && !rc; k++)
+		if ((rc = host_meta_copy(x, &h[k]->host))) svg_set_error("out of memory");
+	if (rc) { drop_all(); return rc; }
 	const double t1 = now();
-	if ((rc = svg_index_finish_device(h))) { svg_index_close(h); return rc; }
+	// each handle's device images (bucket code / key hash, ...), the handles side by side
+	{
+		std::vector<int> frc(n, 0);
+		std::vector<std::string> ferr(n);
+		std::vector<std::thread> ft;
+		for (int k = 0; k < n; k++) {
+			auto fin = [&, k] {
+				frc[k] = svg_index_finish_device(h[k]);
+				if (frc[k]) ferr[k] = svg_last_error();
+			};
+			if (n == 1) fin();
+			else ft.emplace_back(fin);
+		}
+		for (auto &t : ft) t.join();
+		for (int k = 0; k < n && !rc; k++)
+			if (frc[k]) { rc = frc[k]; svg_set_error("%s", ferr[k].c_str()); }
+	}
+	if (rc) { drop_all(); return rc; }
 	if (dbg)
-		fprintf(stderr, "[svg] index block %d: %.2f GB .tab, bucket walk %.3f s, keys/values in HBM %.3f s, .array + contigs %.3f s, "
-		        "device images %.3f s\n", block, (double)x->map_len / 1e9, t_walk, t_copy, t1 - t0, now() - t1);
-	*out = h;
+		fprintf(stderr, "[svg] index block %d: %.2f GB .tab, %d handle(s), bucket walk %.3f s, keys/values in HBM %.3f s, .array + "
+		        "contigs %.3f s, device images %.3f s\n", block, (double)x->map_len / 1e9, n, t_walk, t_copy, t1 - t0, now() - t1);
+	for (int k = 0; k < n; k++) outs[k] = h[k];
+	return 0;
+}
+
+// every block of the index, one replica per listed device (svg_index_open: one device)
+static int index_open_multi(const char *prefix, const int *devs, int n, svg_index **outs)
+{
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { svg_set_error("no HIP device visible"); return SVG_E_DEVICE; }
+	for (int k = 0; k < n; k++)
+		if (devs[k] < 0 || devs[k] >= ndev) { svg_set_error("device %d out of range (%d visible)", devs[k], ndev); return SVG_E_ARG; }
+	HIPCHK(hipSetDevice(devs[0]));
+	const int nb = svg_index_count_blocks(prefix);
+	if (nb < 1) { svg_set_error("index table '%s.00.b.tab' not found", prefix); return SVG_E_IO; }
+	if (nb > SVG_MAX_BLOCKS) { svg_set_error("%d index blocks (at most %d)", nb, SVG_MAX_BLOCKS); return SVG_E_UNSUPPORTED; }
+	int rc = index_open_block_multi(prefix, 0, devs, n, outs);
+	if (rc) return rc;
+	// every block stays resident in HBM (a human index is ~18 GB in all); the vote runs them in order
+	std::vector<svg_index *> bk(n, (svg_index *)NULL);
+	for (int b = 1; b < nb && !rc; b++) {
+		if ((rc = index_open_block_multi(prefix, b, devs, n, bk.data()))) break;
+		for (int k = 0; k < n; k++) {
+			outs[k]->blk[b] = bk[k];
+			bk[k]->stored = 1;
+			outs[k]->device_bytes += bk[k]->device_bytes;
+			outs[k]->nblocks = b + 1;
+		}
+	}
+	if (rc) {
+		for (int k = 0; k < n; k++) { svg_index_close(outs[k]); outs[k] = NULL; }
+		return rc;
+	}
+	for (int k = 0; k < n; k++) outs[k]->nblocks = nb;
 	return 0;
 }
 
@@ -2914,26 +3021,14 @@ extern "C" int svg_index_open(const char *prefix, int device, svg_index **out)
 {
 	if (!prefix || !out) { svg_set_error("svg_index_open: NULL argument"); return SVG_E_ARG; }
 	*out = NULL;
-	int ndev = 0;
-	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { svg_set_error("no HIP device visible"); return SVG_E_DEVICE; }
-	if (device < 0 || device >= ndev) { svg_set_error("device %d out of range (%d visible)", device, ndev); return SVG_E_ARG; }
-	HIPCHK(hipSetDevice(device));
-	const int nb = svg_index_count_blocks(prefix);
-	if (nb < 1) { svg_set_error("index table '%s.00.b.tab' not found", prefix); return SVG_E_IO; }
-	if (nb > SVG_MAX_BLOCKS) { svg_set_error("%d index blocks (at most %d)", nb, SVG_MAX_BLOCKS); return SVG_E_UNSUPPORTED; }
-	svg_index *h;
-	int rc = index_open_block(prefix, 0, device, &h);
-	if (rc) return rc;
-	// every block stays resident in HBM (a human index is ~18 GB in all); the vote runs them in order
-	for (int k = 1; k < nb; k++) {
-		if ((rc = index_open_block(prefix, k, device, &h->blk[k]))) { svg_index_close(h); return rc; }
-		h->blk[k]->stored = 1;
-		h->device_bytes += h->blk[k]->device_bytes;
-		h->nblocks = k + 1;
-	}
-	h->nblocks = nb;
-	*out = h;
-	return 0;
+	return index_open_multi(prefix, &device, 1, out);
+}
+
+extern "C" int svg_index_open_devices(const char *prefix, const int *devices, int n, svg_index **out)
+{
+	if (!prefix || !devices || !out || n < 1 || n > 64) { svg_set_error("svg_index_open_devices: bad argument"); return SVG_E_ARG; }
+	for (int k = 0; k < n; k++) out[k] = NULL;
+	return index_open_multi(prefix, devices, n, out);
 }
 
 extern "C" int svg_index_export(const svg_index *h, uint32_t *bstart, int16_t *keys, uint32_t *vals, uint8_t *values,
@@ -3499,9 +3594,14 @@ static int vote_batch_device(svg_index *h, const svg_params *p, const svg_reads 
 		while (cb.back() < body_end) cb.push_back(cb.back() + chunk < body_end ? cb.back() + chunk : body_end);
 		if (ramp) { cb.push_back(body_end + q2); cb.push_back(n); }
 	}
+	// option dev_pace: the host thread enqueues chunk k only once chunk k-2's wave kernel is done, as
+	// the host pipeline's thread does (it waits on sub-batch i-2 before it queues i): fewer kernels
+	// of later chunks queued behind the running ones
+	const bool pace = overlap && svg_get_option("dev_pace") > 0;
 	for (size_t k = 0; k + 1 < cb.size() && !rc; k++) {
 		const uint64_t c0 = cb[k], cn = cb[k + 1] - cb[k];
 		const int slot = overlap ? (int)(k % (size_t)NS) : 0;
+		if (pace && slot_busy[slot]) HIPCHK(hipEventSynchronize(h->ev_wave[slot]));
 		if (slot_busy[slot]) HIPCHK(hipStreamWaitEvent(st, h->ev_wave[slot], 0));
 		rc = svg_vote_chunk(h, &job, c0, cn, slot, st, st2);
 		if (!rc && overlap) {

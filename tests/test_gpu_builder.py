@@ -75,3 +75,30 @@ def test_index_open_reports_a_missing_array_file(index_cache, tmp_path):
     with pytest.raises(sa.SvgError) as e:
         sa.VoteIndex(pre, device=0)
     assert ".array" in str(e.value), str(e.value)
+
+
+@pytest.mark.parametrize("key", ["chr901_full", "synth4242_gappedM1"])
+def test_index_open_devices_replicas_equal_single_open(key, index_cache):
+    """svg_index_open_devices (the drop-in's several handles): three replicas on device 0 from one
+    read of the files, each array equal to a single svg_index_open's, each voting the golden
+    records (multi-block index included)."""
+    import subread_amd as sa
+    from tests.common import Case, pack_records
+    pre = index_cache.get(key)
+    one = sa.VoteIndex(pre, device=0)
+    reps = sa.VoteIndex.open_devices(pre, [0, 0, 0])
+    a = one.export()
+    for r in reps:
+        assert r.n_blocks == one.n_blocks
+        b = r.export()
+        for f in ("bstart", "keys", "vals", "chr_end"):
+            assert (a[f] == b[f]).all(), f
+        assert (a["values"][:a["values_bytes"]] == b["values"][:b["values_bytes"]]).all()
+    cases = [n for n in ("pe_gapped_errmut", "se_full_errmut", "pe_mb_synth_gappedM1") if Case(n).index_key == key]
+    for name in cases:
+        c = Case(name)
+        for r in reps:
+            out, _, _ = r.vote(c.params, c.r1, c.r2)
+            assert (pack_records(out, None, None) == c.expected).all(), name
+    for r in reps + [one]:
+        r.close()

@@ -1,6 +1,7 @@
 """GPU box: the HBM-resident entry (svg_vote_batch_packed_device) at C3 against the host
 pipeline (svg_vote_batch_packed) in one process, over device-path chunk sizes (option "chunk",
-reads per chunk; 0 = the default 160 MiB of probe records) and ramping, interleaved rounds.
+reads per chunk; 0 = the default 160 MiB of probe records), ramping and host pacing (option
+dev_pace), interleaved rounds.  SETTINGS="host;chunk,ramp[,pace];..."
 -> one line per setting and round (Mreads/s, ms/step)."""
 import os
 import sys
@@ -66,7 +67,9 @@ for rnd in range(int(os.environ.get("ROUNDS", 2))):
         else:
             sa.set_option("chunk", int(s[0]))
             sa.set_option("host_ramp", int(s[1]))
+            sa.set_option("dev_pace", int(s[2]) if len(s) > 2 else 0)
             dt = timed(device)
             sa.set_option("chunk", 0)
             sa.set_option("host_ramp", 1)
+            sa.set_option("dev_pace", 0)
         print("round %d %-16s %.1f Mreads/s %.2f ms/step" % (rnd, "/".join(s), n / dt / 1e6, dt * 1e3), flush=True)

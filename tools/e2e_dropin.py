@@ -40,6 +40,10 @@ def main():
     ap.add_argument("--gpu-build", action="store_true", help="write the index files with the GPU builder "
                     "(svg_index_build_mem + save_prefix; the same bytes as the CPU builder, minutes faster at 3 Gbp)")
     ap.add_argument("--no-startup", action="store_true", help="skip the one-read runs (fixed cost) of each binary")
+    ap.add_argument("--bam", action="store_true", help="the reference's default output, BAM (no --SAMoutput)")
+    ap.add_argument("--keep-order", action="store_true", help="--keepReadOrder (BAM: the ordered stream, compared byte for byte)")
+    ap.add_argument("--devices", default="0,0,0,0,0,0,0,0",
+                    help="SVG_DEVICES of the kind dropin_dev (default: eight replicas on device 0)")
     args = ap.parse_args()
     kinds = args.kinds.split(",")
     import subread_amd as sa
@@ -79,18 +83,24 @@ def main():
     # the reference's phase clocks on; the test harness's vote / event dumps off (tests.dropin.run turns
     # them on: ~0.6 GB written inside the before-realign window of both programs at 3M reads)
     env = {"SVG_REF_TIMING": "1", "SVG_REF_DUMP": "", "SVG_REF_EVENTS": ""}
+    suffix = ".bam" if args.bam else ".sam"
+    extra = ["--keepReadOrder"] if args.keep_order else []
     for kind in kinds:
-        binkind = "dropin" if kind == "dropin_refit2" else kind
-        kenv = dict(env, SVG_REF_ITER2="1") if kind == "dropin_refit2" else env
+        binkind = "dropin" if kind in ("dropin_refit2", "dropin_dev") else kind
+        # (the drop-in's stages must all be the library's, SVG_REQUIRE_LIBRARY=1 -- but for the run that
+        # asks for the reference's iteration two on purpose)
+        kenv = dict(env, SVG_REF_ITER2="1", SVG_REQUIRE_LIBRARY="0") if kind == "dropin_refit2" else dict(env)
+        if kind == "dropin_dev":   # the same drop-in with one replica per listed device
+            kenv["SVG_DEVICES"] = args.devices
         # the fixed cost first (index load(s), voting space, output files): the same program on one read
-        out = os.path.join(wd, "one_%s.sam" % kind)
+        out = os.path.join(wd, "one_%s%s" % (kind, suffix))
         ts = time.perf_counter()
         if not args.no_startup:
-            dropin.run(0, binkind, pre, fq1, None, out, threads=T, timeout=1500, env=kenv)
+            dropin.run(0, binkind, pre, fq1, None, out, threads=T, extra=extra, timeout=1500, env=kenv, sam=not args.bam)
         start[kind] = time.perf_counter() - ts
-        out = os.path.join(wd, "out_%s.sam" % kind)
+        out = os.path.join(wd, "out_%s%s" % (kind, suffix))
         ts = time.perf_counter()
-        r = dropin.run(0, binkind, pre, fq, None, out, threads=T, timeout=1500, env=kenv)
+        r = dropin.run(0, binkind, pre, fq, None, out, threads=T, extra=extra, timeout=1500, env=kenv, sam=not args.bam)
         res[kind] = time.perf_counter() - ts
         phases[kind] = parse_phases(r.stderr)
         log("[e2e] %s: %.1f s (%.1f s on one read) phases %s" % (kind, res[kind], start[kind], phases[kind]))
@@ -98,9 +108,21 @@ def main():
     same = None
     if len(kinds) >= 2:
         for k in kinds[1:]:
-            dropin.compare(os.path.join(wd, "out_%s.sam" % kinds[0]), os.path.join(wd, "out_%s.sam" % k))
+            a, b = os.path.join(wd, "out_%s%s" % (kinds[0], suffix)), os.path.join(wd, "out_%s%s" % (k, suffix))
+            if args.bam:
+                # BAM: the records (byte for byte in order with --keepReadOrder or -T 1, else as a multiset:
+                # the stock aligner's threads write their blocks unordered), and the VCF
+                from tests.test_dropin import _bam_record_list, _bam_blocks_after_header
+                ra, rb_ = _bam_record_list(a), _bam_record_list(b)
+                if args.keep_order or T == 1:
+                    assert ra == rb_ and _bam_blocks_after_header(a) == _bam_blocks_after_header(b), "BAM differs (%s)" % k
+                else:
+                    assert len(ra) == len(rb_) and sorted(ra) == sorted(rb_), "BAM records differ (%s)" % k
+                assert open(a + ".indel.vcf", "rb").read() == open(b + ".indel.vcf", "rb").read(), "VCF differs (%s)" % k
+            else:
+                dropin.compare(a, b)
         same = True
-        log("[e2e] SAM / VCF byte-identical (%s)" % ", ".join(kinds))
+        log("[e2e] %s / VCF identical (%s)" % ("BAM records" if args.bam else "SAM", ", ".join(kinds)))
     if len(kinds) == 1:
         k = kinds[0]
         line = {"metric": "end-to-end subread-align phases", "kind": k, "seconds": round(res[k], 2),
@@ -125,6 +147,10 @@ def main():
             "dropin_refit2": ({"seconds": round(res["dropin_refit2"], 2),
                                "note": "the same drop-in with the reference's own iteration two (SVG_REF_ITER2=1)"}
                               if "dropin_refit2" in res else None),
+            "dropin_dev": ({"seconds": round(res["dropin_dev"], 2), "svg_devices": args.devices,
+                            "note": "the same drop-in with one index replica per SVG_DEVICES entry, each chunk's reads "
+                                    "split among them (svg_index_open_devices: one read of the files)"}
+                           if "dropin_dev" in res else None),
             "phases_s": phases,
             "phases_note": "the reference's own clocks (read_chunk_circles, core.c:3552-3641), printed by "
                            "oracle/ref_dump_hook.c: load_index, voting, before_realign (anti-support scan + "
@@ -132,6 +158,8 @@ def main():
             "cpu_model": cpu["model"],
             "config": {"genome_mbp": round(g.length / 1e6, 1), "genome": args.genome, "tab_bytes": tab_bytes,
                        "reads": args.reads, "read_len": 100, "mode": "SE, -t 1 (DNA)",
+                       "output": ("BAM" if args.bam else "SAM") + (", --keepReadOrder" if args.keep_order else ""),
+                       "svg_devices_of_dropin_dev": args.devices if "dropin_dev" in kinds else None,
                        "index": "full one-block files (our builder, md5-identical to subread-buildindex -F -B)"}}
     print(json.dumps(line), flush=True)
     if args.out:
@@ -151,6 +179,9 @@ def parse_phases(stderr):
     v = re.findall(r"SVG_DROPIN_VOTING (.*)", stderr)
     if v:
         d["voting_split"] = dict((kv.split("=")[0], round(float(kv.split("=")[1]), 3)) for kv in v[-1].split())
+    st = re.findall(r"SVG_DROPIN_STAGES (.*)", stderr)
+    if st:
+        d["stages"] = st[-1]
     return d
 
 
