@@ -1040,6 +1040,7 @@ struct Wave {
 			// one scan -- each lane keeps the three largest distinct votes of its slots, then three wave
 			// maxima, each taking its value off the lanes that hold it (a heavy read's table has 100-260
 			// slots: one pass over them instead of one per rank)
+#ifndef SVG_AB_TOPK3   // (A/B only: the three-pass version)
 			int a = 0, b = 0, c = 0;
 			auto ins = [&](int v) __attribute__((always_inline)) {
 				if (v <= c || v == a || v == b) return;
@@ -1063,6 +1064,30 @@ struct Wave {
 				top[e][t] = best;
 				if (a == best) { a = b; b = c; c = 0; }
 			}
+#else
+			int bound = 0x7fffffff;
+			for (int t = 0; t < TS; t++) {
+				int best = 0;
+				for (int f0 = 0; f0 < U[e]; f0 += 64) {
+					int f = f0 + lane;
+					int sl = hcache(e, f0, f);
+					if (f < U[e]) {
+						uint32_t P, M;
+						int cs_;
+						ent_h(e, sl, P, M, cs_);
+						int v = m_votes(M);
+						if (v < bound && v > best) best = v;
+					}
+				}
+				if (lane < p.multi_best) {
+					int v = rec_votes(L->res[e][lane]);
+					if (v > 0 && v < bound && v > best) best = v;
+				}
+				best = wave_max(best);
+				top[e][t] = best;
+				bound = best;
+			}
+#endif
 		}
 		STAMP(8);
 		// candidate lists (simples)
@@ -1535,7 +1560,14 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 {
 	extern __shared__ __align__(16) uint8_t lds_raw[];
 	typedef WaveLDS<ENDS, MAXL, MAXP, SJ> LT;
+	// wave-uniform values are made scalar (readfirstlane) so that the wave's pointers and its read
+	// loop state live in SGPRs: in VGPRs they were the first things spilled around run_read (12
+	// scratch stores per read in the 80-VGPR single-end build)
+#ifndef SVG_AB_VLOOP
+	const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#else
 	const int wib = threadIdx.x >> 6;
+#endif
 	const uint64_t gw = (uint64_t)blockIdx.x * WPB + wib;
 	const uint64_t nw = (uint64_t)gridDim.x * WPB;
 	Wave<ENDS, MAXL, MAXP, SJ> W;
@@ -1565,20 +1597,28 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	auto grab = [&]() -> uint64_t {   // a dynamic position, synchronously (twice per wave at most)
 		uint32_t a = 0;
 		if (lane_id() == 0) a = atomicAdd(kp.work, 1u);
-		return n_static + (uint64_t)(uint32_t)__shfl((int)a, 0);
+		return n_static + (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)a, 0));
+	};
+	auto uni = [](uint64_t v) -> uint64_t {   // a wave-uniform 64-bit value, scalar
+#ifndef SVG_AB_VLOOP   // (A/B only: the loop state in VGPRs)
+		return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+		       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+#else
+		return v;
+#endif
 	};
 	auto dyn_after = [&](uint64_t p) { return kp.idx && p + nw >= n_static; };   // p's successor is dynamic
 	uint64_t i = !kp.idx || gw < n_static ? gw : (n ? grab() : n);
 	uint64_t in = i >= n ? n : (dyn_after(i) ? grab() : i + nw);
-	uint64_t r = i < n ? (kp.idx ? kp.idx[i] : i) : 0;
+	uint64_t r = uni(i < n ? (kp.idx ? kp.idx[i] : i) : 0);
 	if (i < n) { W.prefetch_text(r); W.prefetch_recs(r); }
 	while (i < n) {
 		const bool dyn = in < n && dyn_after(in);
 		uint32_t nxt = 0;
 		if (dyn && lane_id() == 0) nxt = atomicAdd(kp.work, 1u);   // consumed after this read
-		const uint64_t rn = in < n ? (kp.idx ? kp.idx[in] : in) : kp.n_reads;
+		const uint64_t rn = uni(in < n ? (kp.idx ? kp.idx[in] : in) : kp.n_reads);
 		W.run_read(r, rn);
-		const uint64_t in2 = in >= n ? n : (dyn ? n_static + (uint64_t)(uint32_t)__shfl((int)nxt, 0) : in + nw);
+		const uint64_t in2 = in >= n ? n : (dyn ? n_static + (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)nxt, 0)) : in + nw);
 		i = in;
 		r = rn;
 		in = in2;

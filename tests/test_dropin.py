@@ -377,7 +377,7 @@ def test_oracle_dropin_bam_matches_stock(name, threads, keep, chunk, cache, tmp_
 @pytest.mark.parametrize("name,threads,chunk", [
     ("pe_gapped_errmut", 1, 500),          # one thread: every chunk adds to the global event table (its sorted site lists)
     ("pe_gapped_errmut", 4, 500),          # per-thread tables merged into the global one, chunk after chunk
-    ("sj_pe_mb_long_gappedM6", 1, 60),     # 4-block index, long subjunc pairs: windows per block, tables across chunks
+    ("sj_pe_mb_long_gappedM6", 1, 150),    # 4-block index, long subjunc pairs: windows per block, tables across chunks
     ("se_gapped_mixed_n14_I16", 2, 700),   # -n 14 -I 16, N / IUPAC
 ])
 def test_oracle_dropin_several_chunks(name, threads, chunk, cache, tmp_path):

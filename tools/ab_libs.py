@@ -2,7 +2,8 @@
 """Interleaved A/B of two builds of libsubread_amd (GPU box): both libraries loaded in one
 process, one index in HBM per library, bench.py's host step alternated A, B, A, B, ... so that
 box-to-box and run-to-run drift hits both equally.  For compile-time knobs (make variant V=...).
-Usage: ab_libs.py WORKLOAD ROUNDS LIB_A LIB_B   (WORKLOAD c3 | c5pe)"""
+Usage: ab_libs.py WORKLOAD ROUNDS LIB_A LIB_B [LIB_C ...]   (WORKLOAD c3 | c5pe); every library's
+records are compared with the first's."""
 import ctypes
 import os
 import sys
@@ -18,7 +19,7 @@ from subread_amd.sim import random_genome, simulate_reads, simulate_pairs, c3_le
 
 
 def main():
-    wl, rounds, la, lb = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    wl, rounds, paths = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
     g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))
     if wl == "c5pe":
         n, L = 12_500_000, 100
@@ -47,25 +48,32 @@ def main():
             pinned(n * ends * 3, SUBJUNC_DTYPE).reshape(n, ends, 3) if sj else None,
             pinned(n * ends * BIG_MARGIN_WORDS, np.uint16).reshape(n, ends, BIG_MARGIN_WORDS) if sj else None)
     libs, ixs = [], []
-    for path in (la, lb):
+    for path in paths:
         sa._lib = None
         sa.LIB_PATH = path
         libs.append(sa.lib())
         ixs.append(sa.VoteIndex.build_genome(g, gap=1, memory_mb=8000, force_one_block=True, device=0))
-    times = [[], []]
-    for k in range(2):
+    L = len(paths)
+    times = [[] for _ in range(L)]
+    same = [True] * L
+    first = None
+    for k in range(L):   # warm-up, and each library's records against the first's
         sa._lib = libs[k]
         ixs[k].vote_packed(p, pk1, pk2, bufs=bufs)
+        if k == 0:
+            first = [b.copy() if b is not None else None for b in bufs]
+        else:
+            same[k] = all((x is None) or bool((x.view(np.uint8) == y.view(np.uint8)).all()) for x, y in zip(first, bufs))
     for _ in range(rounds):
-        for k in range(2):
+        for k in range(L):
             sa._lib = libs[k]
             t = time.perf_counter()
             ixs[k].vote_packed(p, pk1, pk2, bufs=bufs)
             times[k].append((time.perf_counter() - t) * 1e3)
-    for k, path in enumerate((la, lb)):
+    for k, path in enumerate(paths):
         t = np.array(times[k])
-        print("%-48s median %7.1f ms/step (%s)  %.1f Mreads/s" % (os.path.basename(path), np.median(t),
-              " ".join("%.1f" % x for x in t), n * ends / np.median(t) / 1e3), flush=True)
+        print("%-48s median %7.1f ms/step (%s)  %.1f Mreads/s  records %s" % (os.path.basename(path), np.median(t),
+              " ".join("%.1f" % x for x in t), n * ends / np.median(t) / 1e3, "identical" if same[k] else "DIFFERENT"), flush=True)
 
 
 if __name__ == "__main__":

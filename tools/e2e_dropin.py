@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--gpu-build", action="store_true", help="write the index files with the GPU builder "
                     "(svg_index_build_mem + save_prefix; the same bytes as the CPU builder, minutes faster at 3 Gbp)")
     ap.add_argument("--no-startup", action="store_true", help="skip the one-read runs (fixed cost) of each binary")
+    ap.add_argument("--reuse", action="store_true", help="keep index files already in --workdir (the same --genome)")
     ap.add_argument("--bam", action="store_true", help="the reference's default output, BAM (no --SAMoutput)")
     ap.add_argument("--keep-order", action="store_true", help="--keepReadOrder (BAM: the ordered stream, compared byte for byte)")
     ap.add_argument("--devices", default="0,0,0,0,0,0,0,0",
@@ -59,7 +60,9 @@ def main():
     else:
         g = random_genome(c3_lengths(args.mbp * 1_000_000), 3000, repeats=(args.mbp * 300, 300, 200, 0.12))
     fa, pre = os.path.join(wd, "g.fa"), os.path.join(wd, "g_full")
-    if args.gpu_build:
+    if args.reuse and os.path.exists(pre + ".00.b.tab") and os.path.exists(pre + ".reads"):
+        log("[e2e] reusing the index files in %s" % wd)
+    elif args.gpu_build:
         ix = sa.VoteIndex.build_genome(g, gap=1, memory_mb=8000, force_one_block=True, device=0, save_prefix=pre)
         ix.close()
     else:
