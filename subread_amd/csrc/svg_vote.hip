@@ -554,6 +554,7 @@ struct Wave {
 			if (v != 0xff) items_v = v;
 		}
 		for (int o = 32; o; o >>= 1) { const int t = __shfl_xor(nv, o); nv = t > nv ? t : nv; }
+		nv = __builtin_amdgcn_readfirstlane(nv);
 		if (max_vote[E] < nv) max_vote[E] = nv;
 		wsync();
 		return ballot(dep);
@@ -1040,7 +1041,6 @@ struct Wave {
 			// one scan -- each lane keeps the three largest distinct votes of its slots, then three wave
 			// maxima, each taking its value off the lanes that hold it (a heavy read's table has 100-260
 			// slots: one pass over them instead of one per rank)
-#ifndef SVG_AB_TOPK3   // (A/B only: the three-pass version)
 			int a = 0, b = 0, c = 0;
 			auto ins = [&](int v) __attribute__((always_inline)) {
 				if (v <= c || v == a || v == b) return;
@@ -1064,30 +1064,6 @@ struct Wave {
 				top[e][t] = best;
 				if (a == best) { a = b; b = c; c = 0; }
 			}
-#else
-			int bound = 0x7fffffff;
-			for (int t = 0; t < TS; t++) {
-				int best = 0;
-				for (int f0 = 0; f0 < U[e]; f0 += 64) {
-					int f = f0 + lane;
-					int sl = hcache(e, f0, f);
-					if (f < U[e]) {
-						uint32_t P, M;
-						int cs_;
-						ent_h(e, sl, P, M, cs_);
-						int v = m_votes(M);
-						if (v < bound && v > best) best = v;
-					}
-				}
-				if (lane < p.multi_best) {
-					int v = rec_votes(L->res[e][lane]);
-					if (v > 0 && v < bound && v > best) best = v;
-				}
-				best = wave_max(best);
-				top[e][t] = best;
-				bound = best;
-			}
-#endif
 		}
 		STAMP(8);
 		// candidate lists (simples)
@@ -1366,7 +1342,7 @@ struct Wave {
 				if (lane == 0) atomicOr(kp->err, 2u);
 				len = 0;
 			}
-			t_len[e] = len;
+			t_len[e] = __builtin_amdgcn_readfirstlane(len);   // (uniform: the read's offsets / probe counts stay scalar)
 			if constexpr (!SJ) continue;   // the vote step itself never reads the text
 			const char *seq = e ? kp->seq2 : kp->seq1;
 			const uint64_t o = e ? kp->off2[r] : kp->off1[r];
@@ -1563,11 +1539,7 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 	// wave-uniform values are made scalar (readfirstlane) so that the wave's pointers and its read
 	// loop state live in SGPRs: in VGPRs they were the first things spilled around run_read (12
 	// scratch stores per read in the 80-VGPR single-end build)
-#ifndef SVG_AB_VLOOP
 	const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#else
-	const int wib = threadIdx.x >> 6;
-#endif
 	const uint64_t gw = (uint64_t)blockIdx.x * WPB + wib;
 	const uint64_t nw = (uint64_t)gridDim.x * WPB;
 	Wave<ENDS, MAXL, MAXP, SJ> W;
@@ -1600,12 +1572,8 @@ __global__ void __launch_bounds__(64 * WPB, OCC) vote_kernel(KParams kp)
 		return n_static + (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)a, 0));
 	};
 	auto uni = [](uint64_t v) -> uint64_t {   // a wave-uniform 64-bit value, scalar
-#ifndef SVG_AB_VLOOP   // (A/B only: the loop state in VGPRs)
 		return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
 		       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
-#else
-		return v;
-#endif
 	};
 	auto dyn_after = [&](uint64_t p) { return kp.idx && p + nw >= n_static; };   // p's successor is dynamic
 	uint64_t i = !kp.idx || gw < n_static ? gw : (n ? grab() : n);

@@ -54,6 +54,7 @@ def main():
     cpu = cpu_info()
     T = args.threads or cpu["usable_cpus"]
     wd = args.workdir or tempfile.mkdtemp(prefix="svg_e2e_")
+    os.makedirs(wd, exist_ok=True)
     t0 = time.time()
     if args.genome == "c3":   # bench.py's c3 workload genome
         g = random_genome(c3_lengths(), 3000, repeats=(1_000_000, 300, 200, 0.12))

@@ -116,6 +116,18 @@ def main():
     torch.cuda.synchronize()
     t = time.perf_counter() - t
     print("%s device: %d reads x %d ends, %.1f ms/step, %.1f Mreads/s" % (wl, n, ends, t / steps * 1e3, n * ends * steps / t / 1e6))
+    # the same per-launch HIP-event record as the host mode's (one more step)
+    ix.set_timing(True)
+    t1 = time.perf_counter()
+    step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter() - t1
+    kt = ix.kernel_timing()
+    ix.set_timing(False)
+    import json
+    print(json.dumps({"kernel_record": {k: {"ms": round(ms, 4), "launches": nl} for k, (ms, nl) in kt.items() if nl},
+                      "timed_step_ms": round(t / steps * 1e3, 3), "record_step_ms": round(t1 * 1e3, 3),
+                      "workload": wl, "reads": n * ends, "mode": "device", "options": opts}), flush=True)
 
 
 if __name__ == "__main__":
