@@ -1042,12 +1042,12 @@ struct Wave {
 			// maxima, each taking its value off the lanes that hold it (a heavy read's table has 100-260
 			// slots: one pass over them instead of one per rank)
 			int a = 0, b = 0, c = 0;
-			auto ins = [&](int v) __attribute__((always_inline)) {
-				if (v <= c || v == a || v == b) return;
-				if (v > a) { c = b; b = a; a = v; }
-				else if (v > b) { c = b; b = v; }
-				else c = v;
-			};
+			// (branch-free: one max / min bubble step per place -- the if-chain was lowered to a
+			// dynamically indexed private array, i.e. scratch)
+#define TOP3_INS(v_) do { const int v = (v_); \
+				if (v > c && v != a && v != b) { \
+					const int t1 = a < v ? a : v, t2 = b < t1 ? b : t1; \
+					a = a > v ? a : v; b = b > t1 ? b : t1; c = c > t2 ? c : t2; } } while (0)
 			for (int f0 = 0; f0 < U[e]; f0 += 64) {
 				int f = f0 + lane;
 				int sl = hcache(e, f0, f);
@@ -1055,10 +1055,11 @@ struct Wave {
 					uint32_t P, M;
 					int cs_;
 					ent_h(e, sl, P, M, cs_);
-					ins(m_votes(M));
+					TOP3_INS(m_votes(M));
 				}
 			}
-			if (lane < p.multi_best) ins(rec_votes(L->res[e][lane]));
+			if (lane < p.multi_best) TOP3_INS(rec_votes(L->res[e][lane]));
+#undef TOP3_INS
 			for (int t = 0; t < TS; t++) {
 				const int best = wave_max(a);
 				top[e][t] = best;
