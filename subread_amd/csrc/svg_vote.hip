@@ -228,13 +228,20 @@ struct Wave {
 	int cur_strand;
 
 	__device__ __forceinline__ static int rd(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+	// a per-end register array read at a run-time end (PE top-K / junction search): a select, since
+	// one dynamic index puts the whole Wave object -- and the kernel's KParams copy -- in scratch
+	template <class T> __device__ __forceinline__ static T end_sel(const T (&a)[2], int e)
+	{
+		const T a0 = a[0], a1 = a[1];   // (values, not `e ? a[1] : a[0]`: that is a select of two addresses)
+		return e ? a1 : a0;
+	}
 
 	// ---------------------------------------------------------------- probe offset of probe p
 	__device__ __forceinline__ int probe_off(int e, int p) const
 	{
 		int gap = kp->ix.gap;
 		int k = p / gap, x = p - k * gap;
-		int off = (int)(((int64_t)rc.step[e] * k) >> 16);
+		int off = (int)(((int64_t)end_sel(rc.step, e) * k) >> 16);
 		if (gap > 1) off -= off % gap - x;
 		return off;
 	}
@@ -243,7 +250,7 @@ struct Wave {
 	__device__ __forceinline__ int sub_off(int e, int kP1, int x) const
 	{
 		const int gap = kp->ix.gap;
-		int off = (int)(((int64_t)rc.step[e] * (kP1 - 1)) >> 16);
+		int off = (int)(((int64_t)end_sel(rc.step, e) * (kP1 - 1)) >> 16);
 		if (gap > 1) off -= off % gap - x;
 		return off;
 	}
@@ -251,13 +258,13 @@ struct Wave {
 	__device__ __forceinline__ uint32_t slot_cw(int e, int slot, uint32_t M) const
 	{
 		const int ce = sub_off(e, m_last(M), m_x(M)) + 16;
-		const int cs = m_spilled(M) ? (int)(cold_slot(cold[e], slot)[0] & 0xffffu) : sub_off(e, m_first(M), m_fx(M));
+		const int cs = m_spilled(M) ? (int)(cold_slot(end_sel(cold, e), slot)[0] & 0xffffu) : sub_off(e, m_first(M), m_fx(M));
 		return (uint32_t)(uint16_t)cs | ((uint32_t)(uint16_t)ce << 16);
 	}
 	// indel recorder entry i of a slot (meta M)
 	__device__ __forceinline__ int slot_rec(int e, int slot, uint32_t M, int i) const
 	{
-		if (m_spilled(M)) return cold_rec(cold_slot(cold[e], slot), i);
+		if (m_spilled(M)) return cold_rec(cold_slot(end_sel(cold, e), slot), i);
 		return i == 0 ? m_first(M) : (i == 1 ? m_last(M) : 0);
 	}
 
@@ -634,7 +641,7 @@ struct Wave {
 	}
 
 	// ---------------------------------------------------------------- record helpers
-	__device__ void rec_zero(uint32_t *r) { if (lane_id() < 17) r[lane_id()] = 0; }
+	__device__ __forceinline__ void rec_zero(uint32_t *r) { if (lane_id() < 17) r[lane_id()] = 0; }
 
 	// ---------------------------------------------------------------- table entries for top-K
 	// An entry handle h is a table slot, or for PE end 0 an index into the compacted list.
@@ -656,7 +663,7 @@ struct Wave {
 	}
 
 	// PE: end 0's used slots, in flattened row order, to the compact list (all lanes active)
-	__device__ void compact_end0()
+	__device__ __forceinline__ void compact_end0()
 	{
 		const int lane = lane_id();
 		int mine = lane < ROWS ? items_v : 0;
@@ -696,7 +703,7 @@ struct Wave {
 		if (lane < 11) r[MR_REC / 4 + lane] = (uint32_t)(uint16_t)rv_lo | ((uint32_t)(uint16_t)rv_hi << 16);
 		if (lane == 0) {
 			r[0] = P;
-			r[2] = (uint32_t)(uint16_t)m_votes(M) | ((uint32_t)(uint16_t)rc.applied[e] << 16);
+			r[2] = (uint32_t)(uint16_t)m_votes(M) | ((uint32_t)(uint16_t)end_sel(rc.applied, e) << 16);
 			r[3] = (uint32_t)(uint8_t)(int8_t)(nrec > 0 ? last_ind : 0) << 8;   // noninf 0, indels
 			r[15] = cw;      // confident_coverage_start | confident_coverage_end << 16
 			r[16] = 0;
@@ -790,7 +797,7 @@ struct Wave {
 		const svg_params &p = kp->p;
 		const int lane = lane_id();
 		const char *read = L->text[e][cur_strand];
-		const int rl = rc.rl[e];
+		const int rl = end_sel(rc.rl, e);
 		const bool need_donor = p.check_donor_at_junctions != 0;
 		const int allow = p.more_accurate_fusions ? 0 : 1;
 		const int mid = (gs + ge) / 2, n = ge - gs;
@@ -894,13 +901,13 @@ struct Wave {
 		const int Mv = m_votes(MM);
 		const uint32_t mw = slot_cw(e, ms, MM);
 		const int Mcs = (int)(mw & 0xffff), Mce = (int)(mw >> 16);
-		const int rl = rc.rl[e];
+		const int rl = end_sel(rc.rl, e);
 		int Jv = 0, Jcs = 0, Jce = 0, Jsplit = 0, Jnormal = 0, Jdio = 0;
 		// long reads (core-junction.c, curr_read_len > EXON_LONG_READ_LENGTH): the indel offsets
 		// accumulated over each half's indel recorder shift the smaller half's donor tests
 		int major_ind = 0;
 		if (rl > 160 && m_spilled(MM)) {   // an unspilled recorder is (first, last, 0): offset 0
-			const uint32_t *mcs = cold_slot(cold[e], ms);
+			const uint32_t *mcs = cold_slot(end_sel(cold, e), ms);
 			for (int kx = 0; kx < SVG_MAX_INDEL_SECTIONS; kx++) {
 				if (!cold_rec(mcs, kx * 3)) break;
 				major_ind += cold_rec(mcs, kx * 3 + 2);
@@ -953,7 +960,7 @@ struct Wave {
 				int minor_ind = 0, lio = 0;
 				if (rl > 160) {
 					const uint32_t Mb = (uint32_t)rd((int)MMv, b);
-					const uint32_t *ncs = cold_slot(cold[e], rd(sl, b));
+					const uint32_t *ncs = cold_slot(end_sel(cold, e), rd(sl, b));
 					for (int kx = 0; kx < SVG_MAX_INDEL_SECTIONS && m_spilled(Mb); kx++) {
 						if (!cold_rec(ncs, kx * 3)) break;
 						minor_ind += cold_rec(ncs, kx * 3 + 2);
@@ -999,7 +1006,7 @@ struct Wave {
 	}
 
 	// ---------------------------------------------------------------- phase K
-	__device__ void topk(int strand)
+	__device__ __forceinline__ void topk(int strand)
 	{
 		const svg_params &p = kp->p;
 		const int lane = lane_id();
@@ -1131,7 +1138,6 @@ struct Wave {
 			// all valid pairs, keep the first 3 by (score desc, pair order asc)
 			int n0 = nsimp[0], n1 = nsimp[1];
 			int npairs = n0 * n1;
-			int bs[3] = {-1, -1, -1}, bidx[3] = {0x7fffffff, 0x7fffffff, 0x7fffffff};
 			// each simple located once (up to 64 x 64 pairs would locate both ends of every pair)
 			for (int e = 0; e < 2; e++) {
 				if (lane < nsimp[e]) {
@@ -1176,32 +1182,34 @@ struct Wave {
 					else { ls2 = sc; li2 = q; }
 				}
 			}
+			// the wave's first three pairs as scalars (no arrays: a dynamically indexed one lives in scratch)
+			int s0 = -1, s1 = -1, s2 = -1, q0 = 0, q1 = 0, q2 = 0, nfound = 0;
+#pragma unroll
 			for (int r = 0; r < 3; r++) {
 				const int m = wave_max(ls0);
 				if (m < 0) break;
 				const int qi = wave_min(ls0 == m ? li0 : 0x7fffffff);
-				bs[r] = m; bidx[r] = qi;
+				if (r == 0) { s0 = m; q0 = qi; } else if (r == 1) { s1 = m; q1 = qi; } else { s2 = m; q2 = qi; }
+				nfound++;
 				if (li0 == qi) { ls0 = ls1; li0 = li1; ls1 = ls2; li1 = li2; ls2 = -1; li2 = 0x7fffffff; }
 			}
-			for (int t = 0; t < 3 && t < p.max_vote_combinations; t++)
-				if (bs[t] >= 0) ncomb++;
-			int ci[3], cj[3], cs3[3];
-			for (int t = 0; t < ncomb; t++) { ci[t] = bidx[t] / n1; cj[t] = bidx[t] % n1; cs3[t] = bs[t]; }
-			// merge_sort -> selection sort ascending by score (core.c:4716-4729), unstable
-			for (int i = 0; i < ncomb - 1; i++) {
-				int mj = i;
-				for (int j = i + 1; j < ncomb; j++) if (cs3[mj] - cs3[j] > 0) mj = j;
-				if (i != mj) {
-					int t1 = ci[i], t2 = cj[i], t3 = cs3[i];
-					ci[i] = ci[mj]; cj[i] = cj[mj]; cs3[i] = cs3[mj];
-					ci[mj] = t1; cj[mj] = t2; cs3[mj] = t3;
-				}
+			ncomb = nfound < p.max_vote_combinations ? nfound : (p.max_vote_combinations > 0 ? p.max_vote_combinations : 0);
+			// merge_sort -> selection sort ascending by score (core.c:4716-4729), unstable: position 0
+			// takes the first strictly smaller of positions 1, 2, then position 1 the smaller of 1, 2
+			{
+				int mj = 0, sm = s0;
+				if (ncomb > 1 && sm - s1 > 0) { mj = 1; sm = s1; }
+				if (ncomb > 2 && sm - s2 > 0) mj = 2;
+				if (mj == 1) { int t = s0; s0 = s1; s1 = t; t = q0; q0 = q1; q1 = t; }
+				else if (mj == 2) { int t = s0; s0 = s2; s2 = t; t = q0; q0 = q2; q2 = t; }
+				if (ncomb > 2 && s1 - s2 > 0) { int t = s1; s1 = s2; s2 = t; t = q1; q1 = q2; q2 = t; }
 			}
 			if (ncomb > 0) {
 				for (int e = 0; e < 2; e++) {
 					for (int i = ncomb - 1; i >= 0; i--) {
 						if (cur[e] >= p.multi_best) break;
-						int si = e ? cj[i] : ci[i];
+						const int qq = i == 0 ? q0 : (i == 1 ? q1 : q2);
+						const int si = e ? qq % n1 : qq / n1;
 						uint32_t ps = L->simp_pos[e][si];
 						bool ex = false;
 						for (int j = 0; j < cur[e]; j++) if (rec_pos(L->tmp[e][j]) == ps) ex = true;
@@ -1245,7 +1253,7 @@ struct Wave {
 	}
 
 	// write simple si of end e as tmp record slot c
-	__device__ void emit(int e, int si, int c, int rs_v, int U)
+	__device__ __forceinline__ void emit(int e, int si, int c, int rs_v, int U)
 	{
 		int sl = L->simp_slot[e][si];
 		if (sl & 0x8000) {
@@ -1275,7 +1283,7 @@ struct Wave {
 	{
 		const int size = kp->p.big_margin_record_size;   // 0..2 (no records) or 3, 6, 9
 		if (size < 3) return;
-		const int lane = lane_id(), ns = size / 3, rl = rc.rl[e];
+		const int lane = lane_id(), ns = size / 3, rl = end_sel(rc.rl, e);
 		const int rs = (int)(cw & 0xffff), re = (int)(cw >> 16);
 		const uint32_t pay = cur_strand ? (uint32_t)(uint16_t)(rl - re) | ((uint32_t)(uint16_t)(rl - rs) << 16)
 		                                : (uint32_t)(uint16_t)rs | ((uint32_t)(uint16_t)re << 16);
@@ -1314,7 +1322,7 @@ struct Wave {
 
 	// voting of one end for one strand: init_gene_vote + subread loop + shift-indel round
 	template <int E>
-	__device__ void vote_end(int strand)
+	__device__ __forceinline__ void vote_end(int strand)
 	{
 		nshift[E] = 0;
 		if (rc.np[E] == 0) { table_reset<E>(); return; }
@@ -1333,7 +1341,7 @@ struct Wave {
 	uint32_t tw[ENDS][WPL];
 	int t_shift[ENDS], t_len[ENDS];
 
-	__device__ void prefetch_text(uint64_t r)
+	__device__ __forceinline__ void prefetch_text(uint64_t r)
 	{
 		const int lane = lane_id();
 		for (int e = 0; e < ENDS; e++) {
@@ -1365,7 +1373,7 @@ struct Wave {
 	uint2 trec[PRE_RECS ? RPL : 1];
 	uint64_t t_r;
 
-	__device__ void prefetch_recs(uint64_t r)
+	__device__ __forceinline__ void prefetch_recs(uint64_t r)
 	{
 		t_r = r;
 		if constexpr (PRE_RECS) {
@@ -1384,7 +1392,7 @@ struct Wave {
 		return sd ? kp->precs[(uint64_t)i * sd + r] : kp->precs[r * (uint64_t)(ENDS * 2 * kp->nps) + i];
 	}
 
-	__device__ void stage_probes()
+	__device__ __forceinline__ void stage_probes()
 	{
 		const int nps = kp->nps, per = ENDS * 2 * nps;
 #pragma unroll
@@ -1404,7 +1412,7 @@ struct Wave {
 	}
 
 	// prefetched words -> LDS staging (the vote table, free at this point) -> both strands
-	__device__ void stage_text()
+	__device__ __forceinline__ void stage_text()
 	{
 		const svg_params &p = kp->p;
 		const int lane = lane_id();
@@ -1428,7 +1436,7 @@ struct Wave {
 		wsync();
 	}
 
-	__device__ void run_read(uint64_t r, uint64_t r_next)
+	__device__ __forceinline__ void run_read(uint64_t r, uint64_t r_next)
 	{
 		const svg_params &p = kp->p;
 		const int lane = lane_id();
@@ -1494,8 +1502,8 @@ struct Wave {
 				vote_end<1>(strand);
 			}
 			STAMP(3);
-			if (ENDS == 2) topk(strand);
-			else if (max_vote[0] >= p.min_votes_first) topk(strand);
+			// (one call site: a second one kept topk out of line, and the wave's state in scratch)
+			if (ENDS == 2 || max_vote[0] >= p.min_votes_first) topk(strand);
 			else if (rec_votes(L->res[0][0]) < 1) {
 				if (lane == 0) {
 					uint32_t *r0 = L->res[0][0];

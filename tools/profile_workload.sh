@@ -12,3 +12,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $out/fetch -o run -- python3 too
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $out/write -o run -- python3 tools/prof_run.py $wl 1 $mode > $out/write.log 2>&1
 python3 tools/prof_kernels.py $out/summary --trace $out/trace --fetch $out/fetch --write $out/write --steps $steps --warmup 1 \
   --reads $reads --workload $wl --cmd "python3 tools/prof_run.py $wl STEPS $mode"
+# the rocprofv3 databases exceed what gpurun copies back (64 MiB): keep the summary only
+[ "${KEEP_DB:-0}" = 1 ] || rm -rf $out/trace $out/fetch $out/write
