@@ -92,7 +92,7 @@ struct WaveLDS {
 	int16_t simp_chr[ENDS == 2 ? 2 : 1][ENDS == 2 ? MAXS : 1];   //     its chromosome, -1 where locate fails
 	uint16_t bm[SJ ? ENDS : 1][10];
 	uint8_t rnew[32];                     // batch mode: new row occupancy (0xff = unchanged)
-	alignas(16) uint32_t bkv[64];         // batch mode: the chunk's kv, for broadcast reads
+	alignas(16) unsigned long long btab[32];   // batch mode: lane masks of the chunk's candidates by kv bin, then by row
 	uint8_t gwin[SJ ? 2 : 1][SJ ? 64 : 4];   // subjunc donor windows of the .array
 	char text[SJ ? ENDS : 1][2][SJ ? MAXL : 4];   // strand 0 / strand 1 (reverse_read) form, donor scoring only
 };
@@ -451,24 +451,23 @@ struct Wave {
 		int nmatch = 0, tslot = -1, td = 1;
 		uint32_t tM = 0u;
 		if (act) {
-			// four slots per LDS round trip
-			const int tot = n0 + np_ + nm;
-			for (int q0 = 0; q0 < tot && nmatch < 2; q0 += 4) {
-				int at[4];
-				uint2 e[4];
+			// the three rows in scan order, four consecutive slots of a row per LDS round trip (the
+			// reads past a row's used slots are masked; the index is clamped to the table)
 #pragma unroll
-				for (int k = 0; k < 4; k++) {
-					const int q = q0 + k < tot ? q0 + k : tot - 1;
-					const uint32_t row = q < n0 ? r0 : (q < n0 + np_ ? rp : rm);
-					at[k] = (int)row * PSTR + (q < n0 ? q : (q < n0 + np_ ? q - n0 : q - n0 - np_));
-					e[k] = L->pm[at[k]];
-				}
+			for (int sg = 0; sg < 3; sg++) {
+				const int cnt = sg == 0 ? n0 : (sg == 1 ? np_ : nm);
+				const int base = (int)(sg == 0 ? r0 : (sg == 1 ? rp : rm)) * PSTR;
+				for (int q = 0; q < cnt && nmatch < 2; q += 4) {
+					uint2 e[4];
 #pragma unroll
-				for (int k = 0; k < 4; k++) {
-					const int d = (int)(kv - e[k].x);
-					if (q0 + k < tot && d >= -tol && d <= tol) {
-						if (!nmatch) { tslot = at[k]; tM = e[k].y; td = d; }
-						nmatch++;
+					for (int k = 0; k < 4; k++) e[k] = L->pm[min(base + q + k, NSLOT - 1)];
+#pragma unroll
+					for (int k = 0; k < 4; k++) {
+						const int d = (int)(kv - e[k].x);
+						if (q + k < cnt && (uint32_t)(d + tol) <= (uint32_t)(2 * tol)) {
+							if (!nmatch) { tslot = base + q + k; tM = e[k].y; td = d; }
+							nmatch++;
+						}
 					}
 				}
 			}
@@ -477,32 +476,41 @@ struct Wave {
 		const bool bcand = act && nmatch == 1 && td == 0 && !m_spilled(tM) && kP1 > m_last(tM);
 		// chunk neighbours: eqm = the candidates with this kv (this lane included), nbfar = one at
 		// 0 < |d| <= 2*tol.  A B candidate's slot position is its kv, so its group (the chunk's
-		// votes on the slot) is eqm; kv broadcast from LDS, four per read
-		L->bkv[lane] = kv;
+		// votes on the slot) is eqm.  The candidates go into a 62-entry table of lane masks by kv bin
+		// (bins of 2^sb >= 2*tol positions, so a candidate within 2*tol is in the same or an adjacent
+		// bin, bins counted modulo 2^(32-sb) as the distance test wraps modulo 2^32), and each lane
+		// tests only the candidates of its three bins' entries -- a few, where testing all m against
+		// all m cost ~100 instructions per 4.  Entries 0-31 are btab, 32-61 the vote table's unused
+		// 25th slot of each row (the row stride is 25, a row holds at most 24)
+		const int sb = tol < 1 ? 0 : 32 - __clz(2 * tol - 1);
+		const uint32_t bin = sb < 32 ? kv >> sb : 0u, bmask = sb < 32 ? 0xffffffffu >> sb : 0u;
+		auto nb_ent = [&](uint32_t b) -> unsigned long long * {
+			const uint32_t h = (b & bmask) % 62u;
+			return h < 32u ? &L->btab[h] : reinterpret_cast<unsigned long long *>(&L->pm[(int)(h - 32u) * PSTR + SPACE]);
+		};
+		if (lane < 62) *nb_ent((uint32_t)lane) = 0ull;   // (bmask >= 63: sb <= 26, tol < 2^25)
 		wsync();
+		if (act) atomicOr(nb_ent(bin), 1ull << lane);
+		wsync();
+		unsigned long long near = act ? (*nb_ent(bin - 1u) | *nb_ent(bin) | *nb_ent(bin + 1u)) & ~(1ull << lane) : 0ull;
 		bool nbfar = false;
-		unsigned long long eqm = 0;
-		for (int j = 0; j < m; j += 4) {
-			const uint4 q = *reinterpret_cast<const uint4 *>(&L->bkv[j]);
-#pragma unroll
-			for (int k = 0; k < 4; k++) {
-				const uint32_t kj = k == 0 ? q.x : (k == 1 ? q.y : (k == 2 ? q.z : q.w));
-				if (j + k < m) {
-					const bool eq = kj == kv;
-					nbfar = nbfar || (!eq && kj - kv + (uint32_t)(2 * tol) <= (uint32_t)(4 * tol));
-					if (eq) eqm |= 1ull << (j + k);
-				}
+		unsigned long long eqm = act ? 1ull << lane : 0ull;
+		while (ballot(near != 0ull)) {   // (every lane takes part in the shuffle)
+			const int j = near ? __ffsll((long long)near) - 1 : lane;
+			const uint32_t kj = (uint32_t)__shfl((int)kv, j);
+			if (near) {
+				if (kj == kv) eqm |= 1ull << j;
+				else if (kj - kv + (uint32_t)(2 * tol) <= (uint32_t)(4 * tol)) nbfar = true;
+				near &= near - 1ull;
 			}
 		}
-		// same = the chunk's candidates of this lane's row, one ballot per distinct row
-		unsigned long long same = 0, rem = ballot(act);
-		while (rem) {
-			const int l = __ffsll((long long)rem) - 1;
-			const uint32_t rv = (uint32_t)rd((int)r0, l);
-			const unsigned long long mk = ballot(act && r0 == rv);
-			if (act && r0 == rv) same = mk;
-			rem &= ~mk;
-		}
+		// same = the chunk's candidates of this lane's row: the table again, by row
+		wsync();
+		if (lane < 32) L->btab[lane] = 0ull;
+		wsync();
+		if (act) atomicOr(&L->btab[r0], 1ull << lane);
+		wsync();
+		const unsigned long long same = act ? L->btab[r0] : 0ull;
 		// a B group settles when all of it are B candidates with distinct kP1 (non-decreasing in
 		// chunk order: compare with the previous member) and nothing else is within 2*tol
 		const unsigned long long below = eqm & ((1ull << lane) - 1ull);
