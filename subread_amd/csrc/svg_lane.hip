@@ -554,8 +554,11 @@ __device__ int ldonor(const LParams &lp, const uint32_t *rc, int rl, uint32_t le
 
 // (waves_per_eu 4: the subjunc variant needs 154 VGPRs unconstrained, i.e. 3 waves/SIMD; capped at
 // 128 it spills 48 B/lane and the C5 lane kernel runs 3.6 -> 2.5 ms per 1M reads)
+#ifndef SVG_LANE_WPE
+#define SVG_LANE_WPE 4
+#endif
 template <int K, int NPF, bool SJ>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) lane_kernel(LParams lp)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SVG_LANE_WPE))) lane_kernel(LParams lp)
 {
 	extern __shared__ __align__(16) uint8_t lds_raw[];
 	const uint32_t gw = blockIdx.x, nw = gridDim.x;

@@ -3351,7 +3351,7 @@ static int launch_vote(svg_index *h, KParams &kp, hipStream_t st, int npmax, boo
 #define SVG_WAVE_CAP 6   // C3: 317 (uncapped, 10) -> 328 Mreads/s; 4 and 3 starve the wave kernel
 #endif
 #ifndef SVG_SE_OCC
-#define SVG_SE_OCC 6   // 80 VGPRs: the wave kernel shares the CUs with the next chunk's probe / lane kernels (C3: OCC 4 139, 5 116, 6 108, 8 134 ms/step)
+#define SVG_SE_OCC 7   // 72 VGPRs: the wave kernel shares the CUs with the next chunk's probe / lane kernels (round 3, C3: OCC 4 139, 5 116, 6 108, 8 134 ms/step; round 6 after the batch-mode table: 6 92.3, 7 89.0)
 #endif
 	return npmax <= 32 ? launch_t<1, 256, 32, 2, SVG_SE_OCC, false>(h, kp, st) : launch_t<1, 256, 64, 2, SVG_SE_OCC, false>(h, kp, st);
 }
