@@ -3,7 +3,10 @@
 process, one index in HBM per library, bench.py's host step alternated A, B, A, B, ... so that
 box-to-box and run-to-run drift hits both equally.  For compile-time knobs (make variant V=...).
 Usage: ab_libs.py WORKLOAD ROUNDS LIB_A LIB_B [LIB_C ...]   (WORKLOAD c3 | c5pe); every library's
-records are compared with the first's."""
+records are compared with the first's.  LIB@name=value,name=value sets library options (svg_set_option)
+before each of that library's steps -- give the same build under two file names to compare options.
+Compare two libraries at a time, in both orders: with five indexes in one process the first one
+measured several percent off in one run (profiles/r06/r6r)."""
 import ctypes
 import os
 import sys
@@ -47,8 +50,11 @@ def main():
     bufs = (pinned(n * ends * 3, MAPPING_DTYPE).reshape(n, ends, 3),
             pinned(n * ends * 3, SUBJUNC_DTYPE).reshape(n, ends, 3) if sj else None,
             pinned(n * ends * BIG_MARGIN_WORDS, np.uint16).reshape(n, ends, BIG_MARGIN_WORDS) if sj else None)
-    libs, ixs = [], []
-    for path in paths:
+    libs, ixs, opts = [], [], []
+    for k, spec in enumerate(paths):
+        path, _, o = spec.partition("@")
+        paths[k] = path
+        opts.append([(kv.split("=")[0], int(kv.split("=")[1])) for kv in o.split(",") if kv])
         sa._lib = None
         sa.LIB_PATH = path
         libs.append(sa.lib())
@@ -57,8 +63,13 @@ def main():
     times = [[] for _ in range(L)]
     same = [True] * L
     first = None
-    for k in range(L):   # warm-up, and each library's records against the first's
+    def use(k):
         sa._lib = libs[k]
+        for name, v in opts[k]:
+            sa.set_option(name, v)
+
+    for k in range(L):   # warm-up, and each library's records against the first's
+        use(k)
         ixs[k].vote_packed(p, pk1, pk2, bufs=bufs)
         if k == 0:
             first = [b.copy() if b is not None else None for b in bufs]
@@ -66,12 +77,13 @@ def main():
             same[k] = all((x is None) or bool((x.view(np.uint8) == y.view(np.uint8)).all()) for x, y in zip(first, bufs))
     for _ in range(rounds):
         for k in range(L):
-            sa._lib = libs[k]
+            use(k)
             t = time.perf_counter()
             ixs[k].vote_packed(p, pk1, pk2, bufs=bufs)
             times[k].append((time.perf_counter() - t) * 1e3)
     for k, path in enumerate(paths):
         t = np.array(times[k])
+        path = path + ("@" + ",".join("%s=%d" % o for o in opts[k]) if opts[k] else "")
         print("%-48s median %7.1f ms/step (%s)  %.1f Mreads/s  records %s" % (os.path.basename(path), np.median(t),
               " ".join("%.1f" % x for x in t), n * ends / np.median(t) / 1e3, "identical" if same[k] else "DIFFERENT"), flush=True)
 
