@@ -240,6 +240,7 @@ struct Wave {
 	__device__ __forceinline__ int probe_off(int e, int p) const
 	{
 		int gap = kp->ix.gap;
+		if (gap == 1) return (int)(((int64_t)end_sel(rc.step, e) * p) >> 16);   // full index: no division (gap is uniform)
 		int k = p / gap, x = p - k * gap;
 		int off = (int)(((int64_t)end_sel(rc.step, e) * k) >> 16);
 		if (gap > 1) off -= off % gap - x;
@@ -495,14 +496,14 @@ struct Wave {
 		unsigned long long near = act ? (*nb_ent(bin - 1u) | *nb_ent(bin) | *nb_ent(bin + 1u)) & ~(1ull << lane) : 0ull;
 		bool nbfar = false;
 		unsigned long long eqm = act ? 1ull << lane : 0ull;
-		while (ballot(near != 0ull)) {   // (every lane takes part in the shuffle)
-			const int j = near ? __ffsll((long long)near) - 1 : lane;
+		while (ballot(near != 0ull)) {   // (every lane takes part in the shuffle; no branches inside)
+			const bool has = near != 0ull;
+			const int j = has ? __ffsll((long long)near) - 1 : lane;
 			const uint32_t kj = (uint32_t)__shfl((int)kv, j);
-			if (near) {
-				if (kj == kv) eqm |= 1ull << j;
-				else if (kj - kv + (uint32_t)(2 * tol) <= (uint32_t)(4 * tol)) nbfar = true;
-				near &= near - 1ull;
-			}
+			const bool eq = has && kj == kv;
+			nbfar = nbfar || (has && !eq && kj - kv + (uint32_t)(2 * tol) <= (uint32_t)(4 * tol));
+			eqm |= eq ? 1ull << j : 0ull;
+			near &= near - 1ull;   // (0 stays 0)
 		}
 		// same = the chunk's candidates of this lane's row: the table again, by row
 		wsync();
@@ -606,7 +607,7 @@ struct Wave {
 			const uint32_t mid = L->pmid[E][s][p];
 			item = j < fwd ? mid + j : mid - 1 - (j - fwd);
 			off = probe_off(E, p);
-			kP1 = p / gap + 1;
+			kP1 = (gap == 1 ? p : p / gap) + 1;
 			return false;
 		};
 		uint32_t nitem = 0, nval = 0;
